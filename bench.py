@@ -1,0 +1,220 @@
+"""Benchmark: GCN SpMM aggregation (the BASELINE.json metric) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2|ns] [--feat F]
+
+One "step" = one full GCN neighbour aggregation Y = A_hat . X + b over the
+whole (per-rank) graph -- the op that replaces torch.spmm(adj, support) + bias
+at GCN/GCN.py:43-45 -- with X and the CSR adjacency already resident in HBM.
+
+Workloads (synthetic R-MAT, SURVEY.md section 8(d) recipe, reference GCN
+normalisation):
+  cfg2  BASELINE configs[1]: 1M nodes / 10M directed edges (nnz 20,073,500), F=128
+  ns    north star: 10M nodes / 100M edges (nnz 206,948,698), F=128
+With --gpus N > 1 (torchrun, one process per GPU, RCCL) the graph grows with N
+(weak scaling: N x the per-GPU graph) and is edge-cut N ways by contiguous
+nnz-balanced row blocks; each step exchanges halo feature rows with an RCCL
+all-to-all-v and runs the interior SpMM concurrently on a second stream.
+
+Rank 0 prints ONE JSON line (value = aggregated edges/s over all ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "aggregated edges/sec + achieved HBM GB/s, GCN SpMM feat_dim=128 @1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+WORKLOADS = {
+    "cfg2": dict(nodes=1_000_000, edges=10_000_000,
+                 name="GCN SpMM, RMAT 1M nodes / 10M edges (BASELINE configs[1])"),
+    "ns": dict(nodes=10_000_000, edges=100_000_000,
+               name="GCN SpMM, RMAT 10M nodes / 100M edges (north star)"),
+}
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(nnz: int, n_rows: int, feat: int) -> int:
+    """SpMM algorithmic bytes: per edge 4 col + 4 val + 4F gathered row;
+    per output row 8 rowptr + 4F written row."""
+    return nnz * (8 + 4 * feat) + n_rows * (8 + 4 * feat)
+
+
+def build_graph(nodes: int, edges: int, dev, rank: int, world: int):
+    from graphneuralnetwork_amd.preprocess import gcn_normalized_csr
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    t0 = time.time()
+    if world > 1:
+        # rank 0 draws the edge list (numpy recipe), every rank receives it over RCCL
+        if rank == 0:
+            s, d = rmat_edges(nodes, edges, 0)
+            buf = torch.from_numpy(np.stack([s, d])).to(dev)
+        else:
+            buf = torch.empty((2, edges), dtype=torch.int64, device=dev)
+        dist.broadcast(buf, 0)
+        s, d = buf[0], buf[1]
+    else:
+        s, d = rmat_edges(nodes, edges, 0)
+    log(f"[bench] rmat edges ready in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    g = gcn_normalized_csr(s, d, nodes, device=dev)
+    torch.cuda.synchronize(dev)
+    log(f"[bench] normalized CSR nnz={g.nnz} in {time.time() - t0:.1f}s")
+    return g
+
+
+def cpu_baseline(g, X, feat: int):
+    """Oracle C restatement of the reference SpMM timed on this host's cores (rank 0, N=1)."""
+    from oracle import c_oracle
+    threads = int(os.environ.get("GNN_CPU_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+    c_oracle.set_threads(threads)
+    rowptr = g.rowptr.cpu().numpy()
+    col = g.col.cpu().numpy()
+    val = g.val.cpu().numpy()
+    Xn = X.cpu().numpy()
+    c_oracle.spmm_csr(rowptr, col, val, Xn, None, 0, min(g.n_rows, 20000))  # warm-up
+    times = []
+    t_budget = time.perf_counter()
+    for _ in range(5):
+        t0 = time.perf_counter()
+        c_oracle.spmm_csr(rowptr, col, val, Xn)
+        times.append(time.perf_counter() - t0)
+        if time.perf_counter() - t_budget > 20:
+            break
+    t = statistics.median(times)
+    return {"value": g.nnz / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"full graph ({g.n_rows} rows, nnz {g.nnz}, F={feat}), oracle/spmm_oracle.c "
+                      f"OpenMP double-accumulation SpMM, median of {len(times)} runs",
+            "seconds_per_step": t}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--feat", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd.ops import spmm_forward
+    _lib.load()
+
+    wl = WORKLOADS[args.workload]
+    nodes, edges = wl["nodes"] * world, wl["edges"] * world
+    F = args.feat
+    g = build_graph(nodes, edges, dev, rank, world)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    bias = torch.randn(F, device=dev, generator=gen)
+
+    if world == 1:
+        X = torch.randn(g.n_cols, F, device=dev, generator=gen)
+        Y = torch.empty(g.n_rows, F, device=dev)
+        step = lambda: spmm_forward(g, X, bias, out=Y)  # noqa: E731
+        rows_local, nnz_local = g.n_rows, g.nnz
+        bytes_local = algorithmic_bytes(nnz_local, rows_local, F)
+        halo_rows = 0
+    else:
+        from graphneuralnetwork_amd.distributed import EdgeCutSpmm, build_partition
+        part = build_partition(g, rank, world)
+        X = torch.randn(part.n_own, F, device=dev, generator=gen)
+        runner = EdgeCutSpmm(part, F, dev)
+        step = lambda: runner(X, bias)  # noqa: E731
+        rows_local, nnz_local = part.n_own, part.nnz
+        bytes_local = algorithmic_bytes(nnz_local, rows_local, F)
+        halo_rows = part.n_halo
+        del g
+        torch.cuda.empty_cache()
+
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    per_step = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                for _ in range(args.steps)]
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for a, b in per_step:
+        a.record(stream)
+        step()
+        b.record(stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    step_ms = [a.elapsed_time(b) for a, b in per_step]
+    elapsed = torch.tensor([max(wall, gpu_ms / 1e3)], dtype=torch.float64, device=dev)
+    tot_nnz = torch.tensor([nnz_local], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot_nnz, op=dist.ReduceOp.SUM)
+    T = float(elapsed.item())
+    ms_per_step = T / args.steps * 1e3
+    value = float(tot_nnz.item()) * args.steps / T
+    kern_ms = statistics.mean(step_ms)
+    achieved = bytes_local / (kern_ms / 1e3) / 1e9
+
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (R-MAT a=.57 b=.19 c=.19 d=.05, seed 0, reference GCN normalisation; "
+                    "X ~ N(0,1))",
+            "config": {"workload": wl["name"], "nodes": nodes, "directed_edges": edges,
+                       "nnz": int(tot_nnz.item()), "feat_dim": F, "global_batch": nodes,
+                       "parallelism": f"edge-cut{world}" if world > 1 else "single-gpu",
+                       "nnz_rank0": nnz_local, "halo_rows_rank0": halo_rows},
+            "achieved_GBps": achieved,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "kernel": "spmm_csr_kernel (+ spmm_fixup_kernel), per-step HIP events",
+                         "algorithmic_bytes_per_launch": bytes_local,
+                         "avg_launch_ms": kern_ms, "min_launch_ms": min(step_ms)},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                res["cpu_baseline"] = cpu_baseline(g, X, F)
+            except Exception as e:  # the baseline is reported, never the target
+                res["cpu_baseline"] = {"value": None, "error": repr(e)}
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,90 @@
+"""ctypes binding of libgnn_mi355x.so (the C-ABI in include/gnn_mi355x.h).
+
+This is the Python-side FFI the reference's modules call into: plain device
+pointers (``tensor.data_ptr()``), sizes and the current HIP stream handle go
+across; nothing else.  The library is loaded lazily and only after ``torch``
+(so that it binds to the HIP runtime torch already loaded).  There is no CPU
+fallback: if the library is missing every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must be imported before the HIP library is dlopen'ed)
+
+from . import build as _build
+
+_lock = threading.Lock()
+_lib: ctypes.CDLL | None = None
+
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_u32 = ctypes.c_uint32
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); must match include/gnn_mi355x.h exactly.
+SIGNATURES: dict[str, tuple] = {
+    "gnn_version": (ctypes.c_int, []),
+    "gnn_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "gnn_spmm_csr_f32": (ctypes.c_int, [
+        _vp, _vp, _vp, _i64,            # rowptr, col, val, n_rows
+        _vp, _i64, _i64,                # x, ldx, feat
+        _vp, _vp, _i64,                 # bias, y, ldy
+        _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
+        _vp, _vp, _i64, _vp,            # long_row, long_seg_ptr, n_long, partial
+        _u32, _vp]),                    # flags, stream
+    "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
+    "gnn_spmm_plan_count": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
+    "gnn_spmm_plan_fill": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+}
+
+EPI_RELU = 1
+EPI_ELU = 2
+
+
+def library_path() -> Path:
+    return _build.LIB_PATH
+
+
+def load(build_if_missing: bool = False) -> ctypes.CDLL:
+    """dlopen libgnn_mi355x.so and bind every C-ABI symbol (raises if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = library_path()
+        if not path.exists():
+            if not build_if_missing:
+                raise RuntimeError(
+                    f"{path} is missing: build it with `python -m graphneuralnetwork_amd.build` "
+                    "(the MI355X aggregation ops have no CPU fallback)")
+            _build.build()
+        lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def error_string(code: int) -> str:
+    return load().gnn_error_string(int(code)).decode()
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        raise RuntimeError(f"{what} failed with code {code}: {error_string(code)}")
+
+
+def ptr(t) -> int | None:
+    """Device address of a tensor (None for an absent optional operand)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

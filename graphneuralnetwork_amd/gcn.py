@@ -1,0 +1,73 @@
+"""Drop-in GCN modules (reference: GCN/GCN.py).
+
+Same class names, constructor arguments, parameter names/shapes
+(``gcn_blocks.gcn{i}.dense.weight`` [out, in], ``gcn_blocks.gcn{i}.bias`` [out])
+and ``forward(X, adj)`` signature as the reference, so reference checkpoints
+load unchanged.  ``GCN_Model.forward`` dispatches on the class-name string
+exactly like GCN/GCN.py:23, which is why the layer class keeps the name
+``Graph_conv_layer``.
+
+The aggregation ``torch.spmm(adj, support) + bias`` (GCN/GCN.py:43-45) runs
+as ONE gfx950 kernel launch (CSR SpMM with the bias fused into its epilogue);
+the feature transform ``support = dense(X)`` stays an MFMA GEMM (hipBLASLt via
+torch).  ``adj`` may be the reference's sparse COO tensor, a sparse CSR
+tensor, a dense tensor or a prebuilt ``CsrGraph``; the CSR form is cached on
+the adjacency tensor.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from .graph import as_csr
+from .ops import spmm
+
+
+class GCN_Model(nn.Module):
+    """GCN/GCN.py:5-27."""
+
+    def __init__(self, num_features, num_hidden, num_classes, num_layers, dropout, **kwargs):
+        super().__init__(**kwargs)
+        self.gcn_blocks = nn.Sequential()
+        for i in range(num_layers):
+            if i == 0:
+                self.gcn_blocks.add_module(f'gcn{i}', Graph_conv_layer(num_features, num_hidden))
+                self.gcn_blocks.add_module(f'relu{i}', nn.ReLU())
+                self.gcn_blocks.add_module(f'dropout{i}', nn.Dropout(dropout))
+            elif i == num_layers - 1:
+                self.gcn_blocks.add_module(f'gcn{i}', Graph_conv_layer(num_hidden, num_classes))
+            else:
+                self.gcn_blocks.add_module(f'gcn{i}', Graph_conv_layer(num_hidden, num_hidden))
+                self.gcn_blocks.add_module(f'relu{i}', nn.ReLU())
+                self.gcn_blocks.add_module(f'dropout{i}', nn.Dropout(dropout))
+
+    def forward(self, X, adj):
+        for gcn_block in self.gcn_blocks:
+            if gcn_block._get_name() == 'Graph_conv_layer':
+                X = gcn_block(X, adj)
+            else:
+                X = gcn_block(X)
+        return X
+
+
+class Graph_conv_layer(nn.Module):
+    """GCN/GCN.py:30-52: support = X W^T ; out = A_hat support + bias (one HIP launch)."""
+
+    def __init__(self, in_features, out_features, is_bias=True, **kwargs):
+        super().__init__(**kwargs)
+        self.in_features = in_features
+        self.out_features = out_features
+        self.dense = nn.Linear(in_features, out_features, bias=False)
+        if is_bias:
+            self.bias = nn.Parameter(torch.zeros(out_features))
+        else:
+            self.register_parameter('bias', None)
+
+    def forward(self, X_input, adj):
+        support = self.dense(X_input)
+        return spmm(as_csr(adj), support, self.bias)
+
+    def __repr__(self):
+        return self.__class__.__name__ + ' (' \
+               + str(self.in_features) + ' -> ' \
+               + str(self.out_features) + ')'

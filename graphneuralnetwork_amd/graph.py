@@ -1,0 +1,187 @@
+"""CSR graphs and row-split plans resident in HBM.
+
+The reference hands its aggregation ops three adjacency forms:
+
+* GCN: a torch sparse COO fp32 tensor, int64 indices, *uncoalesced*, built by
+  ``sparse_mx_to_torch_sparse_tensor`` (GCN/data_utils.py:63-70);
+* GAT (dense layer): a dense [N, N] tensor whose entries ``> 0`` are edges
+  (GAT/models/layers.py:29, GAT/data_utils.py:85);
+* GAT (sparse layer): the same dense tensor, edges = ``adj.nonzero()``
+  (GAT/models/layers.py:98).
+
+All of them become one ``CsrGraph`` (rowptr int64 [N+1], col int32 [nnz],
+val fp32 [nnz]) on the device, built once and cached on the adjacency tensor
+object (keyed by the tensor's version counter, so an in-place edit rebuilds
+it).  Duplicate COO entries are kept as separate edges: the SpMM sums them,
+exactly as ``torch.spmm`` does on an uncoalesced tensor.
+
+Power-law rows (degree > ``seg_len``) get a ``RowSplitPlan`` built on the
+device by the C-ABI (``gnn_spmm_plan_*``); it is cached per ``seg_len``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib
+
+# Segment size for long rows: ~128 KiB of gathered feature bytes per wavefront.
+SEG_BYTES = 128 * 1024
+MIN_SEG_LEN = 128
+
+
+def seg_len_for(feat: int) -> int:
+    return max(MIN_SEG_LEN, SEG_BYTES // max(1, 4 * feat))
+
+
+@dataclass
+class RowSplitPlan:
+    seg_len: int
+    seg_row: torch.Tensor      # int32 [n_seg]
+    seg_begin: torch.Tensor    # int64 [n_seg]
+    long_row: torch.Tensor     # int32 [n_long]
+    long_seg_ptr: torch.Tensor  # int32 [n_long + 1]
+
+    @property
+    def n_seg(self) -> int:
+        return int(self.seg_row.numel())
+
+    @property
+    def n_long(self) -> int:
+        return int(self.long_row.numel())
+
+
+@dataclass
+class CsrGraph:
+    """Adjacency in CSR: row = output node, col = gathered node (torch.spmm orientation)."""
+
+    rowptr: torch.Tensor  # int64 [n_rows + 1]
+    col: torch.Tensor     # int32 [nnz]
+    val: torch.Tensor     # fp32 [nnz]
+    n_rows: int
+    n_cols: int
+    _plans: dict = field(default_factory=dict, repr=False)
+    _transpose: "CsrGraph | None" = field(default=None, repr=False)
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.numel())
+
+    @property
+    def device(self) -> torch.device:
+        return self.rowptr.device
+
+    def validate(self) -> None:
+        assert self.rowptr.dtype == torch.int64 and self.rowptr.numel() == self.n_rows + 1
+        assert self.col.dtype == torch.int32 and self.val.dtype == torch.float32
+        assert self.col.numel() == self.val.numel()
+        assert self.rowptr.is_contiguous() and self.col.is_contiguous() and self.val.is_contiguous()
+
+    # ------------------------------------------------------------------ plans
+    def plan(self, seg_len: int) -> RowSplitPlan:
+        """Row-split plan for this graph (device-built once per seg_len, then cached)."""
+        p = self._plans.get(seg_len)
+        if p is None:
+            p = _build_plan(self, seg_len)
+            self._plans[seg_len] = p
+        return p
+
+    def transpose(self) -> "CsrGraph":
+        """CSR of A^T (used by the SpMM backward: dX = A^T dY)."""
+        if self._transpose is None:
+            rows = torch.repeat_interleave(
+                torch.arange(self.n_rows, device=self.device, dtype=torch.int64),
+                self.rowptr[1:] - self.rowptr[:-1])
+            self._transpose = from_coo(self.col.to(torch.int64), rows, self.val,
+                                       self.n_cols, self.n_rows)
+        return self._transpose
+
+    def to(self, device) -> "CsrGraph":
+        return CsrGraph(self.rowptr.to(device), self.col.to(device), self.val.to(device),
+                        self.n_rows, self.n_cols)
+
+
+def _build_plan(g: CsrGraph, seg_len: int) -> RowSplitPlan:
+    lib = _lib.load()
+    dev = g.device
+    stream = _lib.stream_handle(dev)
+    nbytes = int(lib.gnn_spmm_plan_scratch_bytes(g.n_rows))
+    scratch = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dev)
+    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    _lib.check(lib.gnn_spmm_plan_count(g.rowptr.data_ptr(), g.n_rows, seg_len, counts.data_ptr(),
+                                       scratch.data_ptr(), stream), "gnn_spmm_plan_count")
+    n_long, n_seg = (int(v) for v in counts.cpu().tolist())  # one host round-trip per graph
+    seg_row = torch.empty(n_seg, dtype=torch.int32, device=dev)
+    seg_begin = torch.empty(n_seg, dtype=torch.int64, device=dev)
+    long_row = torch.empty(n_long, dtype=torch.int32, device=dev)
+    long_seg_ptr = torch.empty(n_long + 1, dtype=torch.int32, device=dev)
+    _lib.check(lib.gnn_spmm_plan_fill(g.rowptr.data_ptr(), g.n_rows, seg_len, _lib.ptr(seg_row),
+                                      _lib.ptr(seg_begin), _lib.ptr(long_row),
+                                      long_seg_ptr.data_ptr(), scratch.data_ptr(), stream),
+               "gnn_spmm_plan_fill")
+    return RowSplitPlan(seg_len, seg_row, seg_begin, long_row, long_seg_ptr)
+
+
+# ---------------------------------------------------------------- builders
+def from_coo(row: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n_rows: int,
+             n_cols: int) -> CsrGraph:
+    """CSR from COO triplets (any order, duplicates kept), rows stably sorted."""
+    row = row.to(torch.int64)
+    if row.numel() and (int(row.min()) < 0 or int(row.max()) >= n_rows
+                        or int(col.min()) < 0 or int(col.max()) >= n_cols):
+        raise IndexError("COO index out of range for the adjacency shape")
+    order = torch.argsort(row, stable=True)
+    counts = torch.bincount(row, minlength=n_rows)
+    rowptr = torch.zeros(n_rows + 1, dtype=torch.int64, device=row.device)
+    torch.cumsum(counts, 0, out=rowptr[1:])
+    g = CsrGraph(rowptr, col[order].to(torch.int32).contiguous(),
+                 val[order].to(torch.float32).contiguous(), n_rows, n_cols)
+    return g
+
+
+def from_dense(adj: torch.Tensor, predicate: str) -> CsrGraph:
+    """CSR of a dense [N, M] adjacency; edges where ``adj > 0`` ('positive') or ``adj != 0`` ('nonzero')."""
+    if predicate == "positive":
+        mask = adj > 0
+    elif predicate == "nonzero":
+        mask = adj != 0
+    else:
+        raise ValueError(predicate)
+    idx = mask.nonzero()  # row-major order
+    return from_coo(idx[:, 0], idx[:, 1], adj[mask], adj.shape[0], adj.shape[1])
+
+
+def from_torch_sparse(adj: torch.Tensor) -> CsrGraph:
+    if adj.layout == torch.sparse_coo:
+        idx = adj._indices()
+        return from_coo(idx[0], idx[1], adj._values(), adj.shape[0], adj.shape[1])
+    if adj.layout == torch.sparse_csr:
+        return CsrGraph(adj.crow_indices().to(torch.int64).contiguous(),
+                        adj.col_indices().to(torch.int32).contiguous(),
+                        adj.values().to(torch.float32).contiguous(), adj.shape[0], adj.shape[1])
+    raise TypeError(f"unsupported sparse layout {adj.layout}")
+
+
+def as_csr(adj, predicate: str = "nonzero") -> CsrGraph:
+    """The CsrGraph of a reference adjacency (cached on the tensor object)."""
+    if isinstance(adj, CsrGraph):
+        return adj
+    if not isinstance(adj, torch.Tensor) or adj.dim() != 2:
+        raise TypeError("adj must be a 2-D torch tensor (dense, sparse COO or sparse CSR) or a CsrGraph")
+    key = (predicate if adj.layout == torch.strided else "sparse", adj._version, adj.device)
+    cache = getattr(adj, "_gnn_csr_cache", None)
+    if cache is not None and key in cache:
+        return cache[key]
+    if adj.layout == torch.strided:
+        g = from_dense(adj, predicate)
+    else:
+        g = from_torch_sparse(adj)
+    if cache is None:
+        cache = {}
+        try:
+            adj._gnn_csr_cache = cache
+        except (AttributeError, RuntimeError):
+            return g
+    cache[key] = g
+    return g

@@ -1,0 +1,64 @@
+"""Reference GCN adjacency preprocessing, on the device.
+
+Restates the reference pipeline that feeds the SpMM
+(GCN/data_utils.py:32-35 symmetrise, :78 ``+ sp.eye``, :54-60
+``normalize_adj``, :63-70 fp32 COO) as sort/unique passes over int64 edge keys
+resident in HBM, so a 100M-edge graph is prepared in seconds instead of the
+reference's scipy minutes:
+
+    A      = coo(ones(E), (src, dst))   duplicates summed        (:32-33)
+    A_sym  = elementwise max(A, A^T)                             (:35)
+    A_til  = A_sym + I                  float64                  (:78)
+    d      = rowsum(A_til)^-1/2, inf -> 0                        (:55-57)
+    A_hat[i, j] = (A_til[j, i] * d[i]) * d[j]  -> fp32           (:60, :65)
+
+The structure is bit-exact with the reference and the values are computed in
+float64 then rounded to fp32 exactly like scipy does (checked against the
+reference-generated fixtures in tests/test_preprocess.py).
+"""
+from __future__ import annotations
+
+import torch
+
+from .graph import CsrGraph
+
+
+def gcn_normalized_csr(src, dst, n: int, device=None) -> CsrGraph:
+    """CSR of D^-1/2 (A_sym + I)^T D^-1/2 for a directed edge list (src -> dst)."""
+    src = torch.as_tensor(src, dtype=torch.int64, device=device)
+    dst = torch.as_tensor(dst, dtype=torch.int64, device=device)
+    dev = src.device
+    if src.numel() and (int(src.min()) < 0 or int(src.max()) >= n or int(dst.min()) < 0
+                        or int(dst.max()) >= n):
+        raise IndexError("edge endpoint out of range")
+    # A: duplicate edges summed (counts are exact in the reference's fp32)
+    key, cnt = torch.unique(src * n + dst, return_counts=True)
+    r, c = key // n, key % n
+    del src, dst
+    # A_sym = max(A, A^T)
+    k2 = torch.cat([key, c * n + r])
+    v2 = torch.cat([cnt, cnt]).to(torch.float64)
+    del key, cnt, r, c
+    key, inv = torch.unique(k2, return_inverse=True)
+    w = torch.zeros(key.numel(), dtype=torch.float64, device=dev)
+    w.scatter_reduce_(0, inv, v2, reduce="amax", include_self=False)
+    del k2, v2, inv
+    # + I (float64)
+    diag = torch.arange(n, dtype=torch.int64, device=dev) * (n + 1)
+    k3 = torch.cat([key, diag])
+    v3 = torch.cat([w, torch.ones(n, dtype=torch.float64, device=dev)])
+    del key, w, diag
+    key, inv = torch.unique(k3, return_inverse=True)
+    w = torch.zeros(key.numel(), dtype=torch.float64, device=dev).index_add_(0, inv, v3)
+    del k3, v3, inv
+    r, c = key // n, key % n
+    del key
+    rowsum = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, r, w)
+    d = rowsum.pow(-0.5)
+    d[torch.isinf(d)] = 0.0
+    # transpose: output row = c, gathered col = r
+    val = ((w * d[c]) * d[r]).to(torch.float32)
+    order = torch.argsort(c * n + r)
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(torch.bincount(c, minlength=n), 0, out=rowptr[1:])
+    return CsrGraph(rowptr, r[order].to(torch.int32).contiguous(), val[order].contiguous(), n, n)

@@ -1,0 +1,93 @@
+/*
+ * gnn_mi355x.h -- C-ABI of the MI355X (gfx950) message-passing aggregation library
+ * (libgnn_mi355x.so, built from graphneuralnetwork_amd/csrc/ *.hip).
+ *
+ * Every entry point:
+ *   - takes plain device pointers, sizes and a hipStream_t passed as `void*`
+ *     (NULL = the null stream); no torch / C++ types cross this boundary;
+ *   - never allocates device memory and never synchronises the host: buffers
+ *     (outputs, workspaces) are owned and preallocated by the caller;
+ *   - enqueues its kernels on `stream` and returns 0 on success, a positive
+ *     hipError_t on a launch/runtime failure, or a negative GNN_E_* code when an
+ *     argument is rejected before anything is launched. It never throws.
+ *
+ * Layout conventions (DESIGN.md "Data layout in HBM"):
+ *   CSR graph   rowptr int64 [n_rows+1], col int32 [nnz], val fp32 [nnz]
+ *               (row = destination/output node, col = source/gathered node,
+ *               exactly torch.spmm(adj, X)'s orientation: Y[i] = sum_j adj[i,j] X[j]).
+ *   features    fp32 row-major, row stride `ld*` in elements (ld >= feat).
+ *
+ * Each function names the reference call site it replaces (file:line under
+ * kaddly/GraphNeuralNetwork).
+ */
+#ifndef GNN_MI355X_H_
+#define GNN_MI355X_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes (negative = argument rejected, nothing launched) ---- */
+#define GNN_OK 0
+#define GNN_E_ARG (-1)        /* null pointer / negative size / bad stride          */
+#define GNN_E_ALIGN (-2)      /* a pointer is not aligned as the layout requires    */
+#define GNN_E_UNSUPPORTED (-3) /* shape outside what the library implements         */
+
+/* ---- epilogue flags ---- */
+#define GNN_EPI_RELU 1u /* y = max(y, 0) after the bias add                          */
+#define GNN_EPI_ELU 2u  /* y = y > 0 ? y : expm1(y)   (F.elu, alpha = 1)             */
+
+/* Library version, e.g. 100 for 0.1.0. */
+int gnn_version(void);
+
+/* Human-readable text for a return code of this library (GNN_E_* or hipError_t). */
+const char* gnn_error_string(int code);
+
+/*
+ * GCN aggregation: Y[r, :] = sum_{e in row r} val[e] * X[col[e], :] (+ bias) (epilogue)
+ *
+ * Replaces `torch.spmm(adj, support)` + `output + self.bias` at
+ * GCN/GCN.py:43-45 (Graph_conv_layer.forward).
+ *
+ * Rows whose degree exceeds `seg_len` are "long rows": they are not reduced by
+ * one wavefront but split into segments of at most `seg_len` edges described by
+ * a row-split plan (gnn_spmm_plan_* below). Pass n_seg = 0 / n_long = 0 and
+ * seg_len = INT64_MAX-like value when the graph has no long rows.
+ *
+ *   seg_row[n_seg], seg_begin[n_seg] : owning row and first edge of every segment
+ *                                      (segment s ends at min(seg_begin+seg_len, rowptr[row+1]))
+ *   long_row[n_long]                 : the long rows
+ *   long_seg_ptr[n_long+1]           : segments of long_row[i] are [long_seg_ptr[i], long_seg_ptr[i+1])
+ *   partial[n_seg * feat]            : fp32 workspace for per-segment partial rows
+ * flags: GNN_EPI_* ; bias may be NULL.
+ */
+int gnn_spmm_csr_f32(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
+                     const float* x, int64_t ldx, int64_t feat, const float* bias, float* y,
+                     int64_t ldy, int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin,
+                     int64_t n_seg, const int32_t* long_row, const int32_t* long_seg_ptr,
+                     int64_t n_long, float* partial, uint32_t flags, void* stream);
+
+/*
+ * Row-split plan for gnn_spmm_csr_f32 / gnn_gat_csr_f32 (built once per graph).
+ *
+ * gnn_spmm_plan_count: counts long rows (degree > seg_len) and their segments.
+ *   Writes two int64 counters into `counts_dev` (device memory, [2]:
+ *   n_long, n_seg). The caller reads them back once (this is the only
+ *   host round-trip of a plan and happens once per graph, never per forward).
+ * gnn_spmm_plan_fill: fills seg_row / seg_begin / long_row / long_seg_ptr for the
+ *   counts above. `scratch` needs gnn_spmm_plan_scratch_bytes(n_rows) bytes.
+ */
+int64_t gnn_spmm_plan_scratch_bytes(int64_t n_rows);
+int gnn_spmm_plan_count(const int64_t* rowptr, int64_t n_rows, int64_t seg_len,
+                        int64_t* counts_dev, void* scratch, void* stream);
+int gnn_spmm_plan_fill(const int64_t* rowptr, int64_t n_rows, int64_t seg_len, int32_t* seg_row,
+                       int64_t* seg_begin, int32_t* long_row, int32_t* long_seg_ptr,
+                       void* scratch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GNN_MI355X_H_ */

@@ -1,0 +1,254 @@
+"""CPU ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+A plain-numpy restatement of the reference (kaddly/GraphNeuralNetwork) algorithm
+for the GCN / GAT / GraphSAGE aggregation path, used as the *checker* of the
+HIP kernels.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import it; the product package
+(``graphneuralnetwork_amd``) never does and has no CPU fallback.
+
+Parity pinning: the restatement is checked against golden vectors produced by
+running the reference's own Python code in this container
+(``tests/golden/make_golden.py`` -> ``tests/golden/*.npz``;
+``tests/test_oracle_golden.py``).  All arithmetic is float64 (the reference is
+fp32 except for the adjacency normalisation, which the reference itself does
+in float64 before casting to fp32 at GCN/data_utils.py:65).
+
+Every function cites the reference lines it restates.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# ----------------------------------------------------------------- graph prep
+
+
+def coalesce_counts(src: np.ndarray, dst: np.ndarray, n: int):
+    """COO edge list -> unique (row, col, count) sorted row-major.
+
+    Restates ``sp.coo_matrix((np.ones(E), (e0, e1)))`` followed by the implicit
+    duplicate summation of its first CSR conversion (GCN/data_utils.py:32-35).
+    """
+    key = src.astype(np.int64) * n + dst.astype(np.int64)
+    uk, cnt = np.unique(key, return_counts=True)
+    return (uk // n).astype(np.int64), (uk % n).astype(np.int64), cnt.astype(np.float64)
+
+
+def symmetrize_max(row, col, w, n: int):
+    """A_sym = A + A^T.multiply(A^T > A) - A.multiply(A^T > A)  (GCN/data_utils.py:35).
+
+    For non-negative A this is the element-wise maximum of A and A^T.
+    Returns unique (row, col, value) sorted row-major.
+    """
+    r = np.concatenate([row, col])
+    c = np.concatenate([col, row])
+    v = np.concatenate([w, w])
+    key = r * n + c
+    order = np.lexsort((-v, key))  # per key, largest value first
+    key, v = key[order], v[order]
+    first = np.ones(key.size, dtype=bool)
+    first[1:] = key[1:] != key[:-1]
+    key, v = key[first], v[first]
+    return key // n, key % n, v
+
+
+def add_self_loops(row, col, val, n: int):
+    """adj + sp.eye(N)  (GCN/data_utils.py:78): adds 1.0 on the diagonal (float64)."""
+    key = np.concatenate([row * n + col, np.arange(n, dtype=np.int64) * (n + 1)])
+    v = np.concatenate([val.astype(np.float64), np.ones(n)])
+    uk, inv = np.unique(key, return_inverse=True)
+    out = np.zeros(uk.size)
+    np.add.at(out, inv, v)
+    return uk // n, uk % n, out
+
+
+def normalize_adj(row, col, val, n: int):
+    """A_hat = (A D^-1/2)^T D^-1/2 = D^-1/2 A^T D^-1/2  (GCN/data_utils.py:54-60).
+
+    D = rowsum(A) in float64, d^-1/2 with inf -> 0.  Entry (i, j) of the result
+    is (A[j, i] * d[i]) * d[j]; returned as (row, col, float64 value) sorted
+    row-major (row = output node i).
+    """
+    rowsum = np.zeros(n)
+    np.add.at(rowsum, row, val)
+    with np.errstate(divide="ignore"):
+        d = np.power(rowsum, -0.5)
+    d[np.isinf(d)] = 0.0
+    # transpose: entry (i=col, j=row) = (val * d[col]) * d[row]
+    r_t, c_t = col, row
+    v_t = (val * d[col]) * d[row]
+    order = np.lexsort((c_t, r_t))
+    return r_t[order], c_t[order], v_t[order]
+
+
+def gcn_adjacency(src: np.ndarray, dst: np.ndarray, n: int):
+    """Full reference pipeline C3 -> +I -> C2 -> fp32 (GCN/data_utils.py:27-36,54-70,78,85).
+
+    Returns CSR (rowptr int64, col int32, val float32).
+    """
+    r, c, w = coalesce_counts(src, dst, n)
+    r, c, w = symmetrize_max(r, c, w, n)
+    r, c, w = add_self_loops(r, c, w, n)
+    r, c, w = normalize_adj(r, c, w, n)
+    return coo_to_csr(r, c, w.astype(np.float32), n)
+
+
+def coo_to_csr(row, col, val, n_rows: int):
+    """Stable row sort of COO triplets (duplicates kept)."""
+    row = np.asarray(row, dtype=np.int64)
+    order = np.argsort(row, kind="stable")
+    rowptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(np.bincount(row, minlength=n_rows), out=rowptr[1:])
+    return rowptr, np.asarray(col)[order].astype(np.int32), np.asarray(val)[order]
+
+
+# ---------------------------------------------------------------------- GCN
+
+
+def spmm_csr(rowptr, col, val, x, bias=None):
+    """Y = A X (+ bias), float64 accumulation  (torch.spmm at GCN/GCN.py:43, + bias :45)."""
+    x = np.asarray(x, dtype=np.float64)
+    n_rows = rowptr.size - 1
+    contrib = np.asarray(val, dtype=np.float64)[:, None] * x[np.asarray(col, dtype=np.int64)]
+    y = np.zeros((n_rows, x.shape[1]))
+    deg = np.diff(rowptr)
+    nz = deg > 0
+    if contrib.shape[0]:
+        y[nz] = np.add.reduceat(contrib, rowptr[:-1][nz], axis=0)
+    if bias is not None:
+        y = y + np.asarray(bias, dtype=np.float64)
+    return y
+
+
+def gcn_layer(rowptr, col, val, x, weight, bias):
+    """Graph_conv_layer.forward (GCN/GCN.py:41-47): spmm(A, X W^T) + b."""
+    support = np.asarray(x, np.float64) @ np.asarray(weight, np.float64).T
+    return spmm_csr(rowptr, col, val, support, bias)
+
+
+def gcn_model(rowptr, col, val, x, weights, biases):
+    """GCN_Model.forward in eval mode (GCN/GCN.py:21-27): gcn -> relu (-> dropout=id) -> ... -> gcn."""
+    h = np.asarray(x, np.float64)
+    for i, (w, b) in enumerate(zip(weights, biases)):
+        h = gcn_layer(rowptr, col, val, h, w, b)
+        if i != len(weights) - 1:
+            h = np.maximum(h, 0.0)
+    return h
+
+
+# ---------------------------------------------------------------------- GAT
+
+
+def _leaky(x, alpha):
+    return np.where(x > 0, x, alpha * x)
+
+
+def _elu(x):
+    return np.where(x > 0, x, np.expm1(np.minimum(x, 0)))
+
+
+def gat_dense_head(h, adj_dense, W, a, alpha, concat):
+    """GraphAttentionLayer.forward, eval mode (GAT/models/layers.py:22-37).
+
+    e_ij = LeakyReLU(a[:F].Wh_i + a[F:].Wh_j); masked where adj <= 0 with -9e15;
+    row softmax; h' = att . Wh; ELU if concat.  A row with no edge degenerates
+    to a uniform average over all N rows (every logit is -9e15).
+    """
+    Wh = np.asarray(h, np.float64) @ np.asarray(W, np.float64)
+    F = Wh.shape[1]
+    a = np.asarray(a, np.float64).reshape(-1)
+    el = Wh @ a[:F]
+    er = Wh @ a[F:]
+    e = _leaky(el[:, None] + er[None, :], alpha)
+    e = np.where(np.asarray(adj_dense) > 0, e, -9e15)
+    e = e - e.max(axis=1, keepdims=True)
+    p = np.exp(e)
+    att = p / p.sum(axis=1, keepdims=True)
+    out = att @ Wh
+    return _elu(out) if concat else out
+
+
+def gat_sparse_head(h, adj_dense, W, a, alpha, concat):
+    """SpGraphAttentionLayer.forward, eval mode (GAT/models/layers.py:94-131).
+
+    edges = adj.nonzero(); edge_e = exp(-LeakyReLU(a.[Wh_i || Wh_j])) (no max
+    subtraction, as the reference); h' = (sum_j edge_e Wh_j) / (sum_j edge_e);
+    a row without edges gives 0/0 = NaN (the reference then fails its
+    ``assert not isnan``); ELU if concat.
+    """
+    Wh = np.asarray(h, np.float64) @ np.asarray(W, np.float64)
+    F = Wh.shape[1]
+    a = np.asarray(a, np.float64).reshape(-1)
+    ii, jj = np.nonzero(np.asarray(adj_dense))
+    s = Wh[ii] @ a[:F] + Wh[jj] @ a[F:]
+    ee = np.exp(-_leaky(s, alpha))
+    n = Wh.shape[0]
+    rowsum = np.zeros(n)
+    np.add.at(rowsum, ii, ee)
+    acc = np.zeros_like(Wh)
+    np.add.at(acc, ii, ee[:, None] * Wh[jj])
+    with np.errstate(invalid="ignore", divide="ignore"):
+        out = acc / rowsum[:, None]
+    return _elu(out) if concat else out
+
+
+def gat_model(h, adj_dense, heads, out_head, alpha, sparse: bool):
+    """GATBase.forward, eval mode (GAT/models/GAT.py:14-18): concat heads -> out_att -> ELU."""
+    f = gat_sparse_head if sparse else gat_dense_head
+    x = np.concatenate([f(h, adj_dense, W, a, alpha, True) for W, a in heads], axis=1)
+    W, a = out_head
+    return _elu(f(x, adj_dense, W, a, alpha, False))
+
+
+# ---------------------------------------------------------------- GraphSAGE
+
+
+def aggregator(neigh_feat, agg_func="MEAN"):
+    """Aggregator (GraphSAGE/graph_utils.py:4-11).
+
+    MEAN -> mean over dim 1 (float64 here); MAX -> argmax over dim 1 as int64:
+    first maximal position, a NaN counts as the maximum (torch.argmax rule).
+    """
+    x = np.asarray(neigh_feat)
+    if agg_func == "MEAN":
+        return x.astype(np.float64).mean(axis=1)
+    if agg_func == "MAX":
+        nan = np.isnan(x)
+        arg = np.argmax(np.where(nan, -np.inf, x), axis=1)
+        has_nan = nan.any(axis=1)
+        first_nan = np.argmax(nan, axis=1)
+        return np.where(has_nan, first_nan, arg).astype(np.int64)
+    raise RuntimeError("unknown agg_func")
+
+
+def sage_layer(self_feats, agg_feats, weight, gcn=False):
+    """SageLayer.forward (GraphSAGE/GraphSAGE.py:15-20): relu(W . cat[self, agg])."""
+    agg = np.asarray(agg_feats, np.float64)
+    comb = agg if gcn else np.concatenate([np.asarray(self_feats, np.float64), agg], axis=1)
+    return np.maximum(comb @ np.asarray(weight, np.float64).T, 0.0)
+
+
+def graphsage_forward(center_feats, center_nodes_map, neigh_feats, neigh_nodes_map, weights,
+                      agg_func="MEAN", gcn=False, dense=None):
+    """GraphSAGE.forward, supervised branch (GraphSAGE/GraphSAGE.py:42-53)."""
+    num_layers = len(weights)
+    cf = np.asarray(center_feats, np.float64)
+    nf = np.asarray(neigh_feats, np.float64)
+    feats = None
+    for i, w in enumerate(weights):
+        agg = aggregator(nf, agg_func)
+        feats = sage_layer(cf, agg, w, gcn)
+        if i != num_layers - 1:
+            cm = np.asarray(center_nodes_map[i])
+            nm = np.asarray(neigh_nodes_map[i])
+            cf = feats[cm[cm != -1]]
+            nf = feats[nm[nm[:, 0] != -1, :]]
+    classes = None
+    if dense is not None:
+        Wd, bd = dense
+        classes = feats @ np.asarray(Wd, np.float64).T + np.asarray(bd, np.float64)
+    return feats, classes
+
+
+def sage_gather_aggregate(table, idx, agg_func="MEAN"):
+    """Fused gather + Aggregator: Aggregator(embedding(table, idx)) (GraphSAGE/GraphSAGE.py:47-49 + graph_utils.py:6,8)."""
+    return aggregator(np.asarray(table)[np.asarray(idx)], agg_func)

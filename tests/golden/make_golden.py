@@ -1,0 +1,322 @@
+"""Generate the golden vectors in tests/golden/ by running the REFERENCE code.
+
+Run in the build container only (needs /root/reference, read-only):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+For each model family a fresh subprocess puts the reference directory on
+sys.path, imports the reference modules (no bytecode is written), builds small
+seeded synthetic inputs in the reference's own formats, runs the reference
+forward passes on CPU and stores inputs + outputs as compressed .npz
+fixtures.  Nothing from the reference is copied: only data is written.
+Parameters are drawn from a small dyadic grid (k/64) so the fixtures compress
+well and are exactly representable in fp32.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+REF = Path("/root/reference")
+
+
+def _q(rng, shape, scale=64, lim=64):
+    """Dyadic random values k/scale, k in [-lim, lim]."""
+    return (rng.integers(-lim, lim + 1, size=shape) / scale).astype(np.float32)
+
+
+def _set_params(module, rng, scale=64, lim=48):
+    import torch
+    with torch.no_grad():
+        for p in module.parameters():
+            p.copy_(torch.from_numpy(_q(rng, tuple(p.shape), scale, lim)))
+
+
+# ----------------------------------------------------------------------- GCN
+def _write_cora(d: Path, rng, n=2708, n_feat=1433, n_cls=7, n_cites=5429):
+    ids = rng.choice(np.arange(10_000, 10_000 + 20 * n), size=n, replace=False)
+    labels = [f"Class_{c}" for c in rng.integers(0, n_cls, size=n)]
+    with open(d / "cora.content", "w") as f:
+        for i in range(n):
+            row = np.zeros(n_feat, dtype=np.int64)
+            row[rng.choice(n_feat, size=int(rng.integers(5, 30)), replace=False)] = 1
+            f.write(f"{ids[i]}\t" + "\t".join(map(str, row)) + f"\t{labels[i]}\n")
+    # power-law-ish cites: a few hubs, duplicates allowed, no self cites needed
+    w = 1.0 / np.arange(1, n + 1) ** 0.8
+    w /= w.sum()
+    src = rng.choice(n, size=n_cites, p=w)
+    dst = rng.integers(0, n, size=n_cites)
+    with open(d / "cora.cites", "w") as f:
+        for s, t in zip(src, dst):
+            f.write(f"{ids[s]}\t{ids[t]}\n")
+    return ids, src, dst
+
+
+def part_gcn():
+    sys.path.insert(0, str(REF / "GCN"))
+    import torch
+    import data_utils as du  # reference GCN/data_utils.py
+    import scipy.sparse as sp
+    from GCN import GCN_Model, Graph_conv_layer  # reference GCN/GCN.py
+
+    torch.manual_seed(0)
+    rng = np.random.default_rng(0)
+    out = {}
+    # -- cfg1: Cora-format synthetic through the full reference loader + model
+    with tempfile.TemporaryDirectory() as td:
+        d = Path(td)
+        ids, src, dst = _write_cora(d, rng)
+        adj, features, labels, *_ = du.load_cora(data_dir=str(d) + "/", dataset="cora")
+    model = GCN_Model(features.shape[1], num_hidden=128, num_classes=7, num_layers=2, dropout=0.5)
+    _set_params(model, rng, lim=16)
+    model.eval()
+    with torch.no_grad():
+        logits = model(features, adj)
+    sd = model.state_dict()
+    fnz = features.nonzero().numpy()
+    idx = adj._indices().numpy()
+    np.savez_compressed(
+        HERE / "gcn_cora.npz",
+        edges=np.stack([src, dst], 1).astype(np.int32),  # node indices (file order)
+        adj_row=idx[0].astype(np.int32), adj_col=idx[1].astype(np.int32),
+        adj_val=adj._values().numpy(), n=np.int64(features.shape[0]),
+        feat_row=fnz[:, 0].astype(np.int32), feat_col=fnz[:, 1].astype(np.int16),
+        feat_val=features[fnz[:, 0], fnz[:, 1]].numpy(), n_feat=np.int64(features.shape[1]),
+        w0=sd["gcn_blocks.gcn0.dense.weight"].numpy(), b0=sd["gcn_blocks.gcn0.bias"].numpy(),
+        w1=sd["gcn_blocks.gcn1.dense.weight"].numpy(), b1=sd["gcn_blocks.gcn1.bias"].numpy(),
+        logits=logits.numpy(), state_keys=np.array(list(sd.keys())))
+    print("gcn_cora.npz", logits.shape)
+
+    # -- SpMM graphs through the reference preprocessing + Graph_conv_layer (W = I)
+    def ref_adj(n, s, t):
+        feats = np.zeros((n, 3), dtype=object)
+        feats[:, 0] = np.arange(n).astype(str)
+        feats[:, 1] = "1"
+        feats[:, 2] = "c"
+        node2idx = {i: i for i in range(n)}
+        edges_un = np.stack([s, t], 1).astype(np.int32)
+        _, _, a = du.preprocess_data(feats, edges_un, node2idx)
+        a = du.normalize_adj(a + sp.eye(a.shape[0]))
+        return du.sparse_mx_to_torch_sparse_tensor(a)
+
+    cases = []
+    # g1: duplicates, a 600-edge hub, isolated nodes
+    n = 1000
+    s = rng.integers(0, 900, size=4000)
+    t = rng.integers(0, 900, size=4000)
+    s = np.concatenate([s, np.zeros(600, np.int64), s[:300]])      # hub 0 + 300 duplicates
+    t = np.concatenate([t, rng.choice(900, 600, replace=False), t[:300]])
+    cases.append(("g1", n, s, t, [7, 64]))
+    # g2: RMAT (survey recipe, scale 12) folded onto 3000 nodes
+    scale, ne = 12, 24000
+    r2 = np.random.default_rng(2)
+    rs = np.zeros(ne, np.int64)
+    cs = np.zeros(ne, np.int64)
+    for b in range(scale):
+        u = r2.random(ne)
+        v = r2.random(ne)
+        rb = u > 0.57 + 0.19
+        cb = np.where(rb, v < 0.05 / (0.19 + 0.05), v < 0.19 / (0.57 + 0.19))
+        rs |= rb.astype(np.int64) << b
+        cs |= cb.astype(np.int64) << b
+    cases.append(("g2", 3000, rs % 3000, cs % 3000, [128, 256]))
+    # g3: tiny, every node isolated except a chain
+    cases.append(("g3", 257, np.arange(0, 100), np.arange(1, 101), [1, 5, 33]))
+    arrays = {}
+    for name, n, s, t, feats in cases:
+        A = ref_adj(n, s, t)
+        i = A._indices().numpy()
+        arrays[f"{name}_n"] = np.int64(n)
+        arrays[f"{name}_edges"] = np.stack([s, t], 1).astype(np.int32)
+        arrays[f"{name}_row"] = i[0].astype(np.int32)
+        arrays[f"{name}_col"] = i[1].astype(np.int32)
+        arrays[f"{name}_val"] = A._values().numpy()
+        deg = np.bincount(i[0], minlength=n)
+        check = np.unique(np.concatenate([rng.choice(n, size=min(n, 192), replace=False),
+                                          np.argsort(-deg)[:8], np.nonzero(deg <= 1)[0][:8]]))
+        for F in feats:
+            layer = Graph_conv_layer(F, F)
+            with torch.no_grad():
+                layer.dense.weight.copy_(torch.eye(F))
+                layer.bias.copy_(torch.from_numpy(_q(rng, (F,), 16, 16)))
+            X = (rng.integers(-16, 17, size=(n, F)) / 8).astype(np.float32)
+            with torch.no_grad():
+                Y = layer(torch.from_numpy(X), A).numpy()
+            arrays[f"{name}_F{F}_xq"] = (X * 8).astype(np.int8)
+            arrays[f"{name}_F{F}_bias"] = layer.bias.detach().numpy()
+            arrays[f"{name}_F{F}_rows"] = check.astype(np.int32)
+            arrays[f"{name}_F{F}_y"] = Y[check]
+        print(name, n, A._nnz(), feats)
+    arrays["cases"] = np.array([c[0] for c in cases])
+    arrays["feats"] = np.array([",".join(map(str, c[4])) for c in cases])
+    np.savez_compressed(HERE / "gcn_spmm.npz", **arrays)
+
+
+# ----------------------------------------------------------------------- GAT
+def part_gat():
+    import importlib.util
+    import torch
+    spec = importlib.util.spec_from_file_location("ref_gat_layers", REF / "GAT/models/layers.py")
+    L = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(L)
+    torch.manual_seed(0)
+    rng = np.random.default_rng(3)
+    N, Fin, H, Fh, C, alpha = 512, 64, 8, 8, 7, 0.2
+    # adjacency: symmetric, self loops, positive normalised-looking values
+    s = rng.integers(0, N, 3000)
+    t = rng.integers(0, N, 3000)
+    A = np.zeros((N, N), np.float32)
+    A[s, t] = 1
+    A[t, s] = 1
+    A[np.arange(N), np.arange(N)] = 1
+    A[5, :] = 0
+    A[5, 5] = 1                            # a degree-1 row
+    A[7, :50] = 1                          # a hub-ish row
+    A = A * (rng.integers(1, 5, (N, N)) / 4).astype(np.float32)
+    h = _q(rng, (N, Fin), 32, 32)
+    adj = torch.from_numpy(A)
+    ht = torch.from_numpy(h)
+    out = {"adj_row": None}
+    for kind, cls in (("dense", L.GraphAttentionLayer), ("sparse", L.SpGraphAttentionLayer)):
+        heads = [cls(Fin, Fh, dropout=0.6, alpha=alpha, concat=True) for _ in range(H)]
+        out_att = cls(Fh * H, C, dropout=0.6, alpha=alpha, concat=False)
+        for m in heads + [out_att]:
+            _set_params(m, rng, 64, 40)
+            m.eval()
+        with torch.no_grad():
+            head0 = heads[0](ht, adj)
+            x = torch.cat([m(ht, adj) for m in heads], dim=1)       # GAT/models/GAT.py:16
+            logits = torch.nn.functional.elu(out_att(x, adj))       # GAT/models/GAT.py:18
+        out[f"{kind}_W"] = np.stack([m.W.detach().numpy() for m in heads])
+        out[f"{kind}_a"] = np.stack([m.a.detach().numpy().reshape(-1) for m in heads])
+        out[f"{kind}_outW"] = out_att.W.detach().numpy()
+        out[f"{kind}_outa"] = out_att.a.detach().numpy().reshape(-1)
+        out[f"{kind}_head0"] = head0.numpy()
+        out[f"{kind}_concat"] = x.numpy()
+        out[f"{kind}_logits"] = logits.numpy()
+        print("gat", kind, logits.shape)
+    # dense-vs-nonzero edge sets: a matrix with negative entries, one head each
+    An = A.copy()
+    An[np.arange(0, N, 3), np.arange(1, N, 3)[: len(range(0, N, 3))]] = -0.5
+    adjn = torch.from_numpy(An)
+    dl = L.GraphAttentionLayer(Fin, Fh, dropout=0.0, alpha=alpha, concat=True)
+    sl = L.SpGraphAttentionLayer(Fin, Fh, dropout=0.0, alpha=alpha, concat=True)
+    for m in (dl, sl):
+        _set_params(m, rng, 64, 40)
+        m.eval()
+    with torch.no_grad():
+        out["neg_dense_out"] = dl(ht, adjn).numpy()
+        out["neg_sparse_out"] = sl(ht, adjn).numpy()
+    out["neg_dense_W"], out["neg_dense_a"] = dl.W.detach().numpy(), dl.a.detach().numpy().reshape(-1)
+    out["neg_sparse_W"], out["neg_sparse_a"] = sl.W.detach().numpy(), sl.a.detach().numpy().reshape(-1)
+    # isolated row: dense gives a uniform average, sparse raises (NaN assert)
+    Ai = A.copy()
+    Ai[9, :] = 0
+    with torch.no_grad():
+        out["iso_dense_out"] = dl(ht, torch.from_numpy(Ai)).numpy()
+        try:
+            sl(ht, torch.from_numpy(Ai))
+            out["iso_sparse_raises"] = np.int64(0)
+        except AssertionError:
+            out["iso_sparse_raises"] = np.int64(1)
+    nz = np.nonzero(A)
+    out.pop("adj_row")
+    out.update(adj_row=nz[0].astype(np.int32), adj_col=nz[1].astype(np.int32), adj_val=A[nz],
+               neg_row=np.nonzero(An)[0].astype(np.int32), neg_col=np.nonzero(An)[1].astype(np.int32),
+               neg_val=An[np.nonzero(An)], h=h, n=np.int64(N), alpha=np.float64(alpha),
+               iso_row=np.int64(9))
+    np.savez_compressed(HERE / "gat.npz", **out)
+
+
+# ----------------------------------------------------------------- GraphSAGE
+def part_sage():
+    sys.path.insert(0, str(REF / "GraphSAGE"))
+    import random
+    from collections import defaultdict
+    import torch
+    import data_utils as du  # reference GraphSAGE/data_utils.py
+    from GraphSAGE import GraphSAGE  # reference GraphSAGE/GraphSAGE.py
+    from graph_utils import Aggregator  # reference GraphSAGE/graph_utils.py
+
+    random.seed(0)
+    torch.manual_seed(0)
+    rng = np.random.default_rng(5)
+    N, F, Hd, K, B = 200, 32, 16, 5, 16
+    adj_lists = defaultdict(set)
+    for i in range(N):  # ring (deg >= 2) + random chords + a hub
+        adj_lists[i].add((i + 1) % N)
+        adj_lists[(i + 1) % N].add(i)
+    for s, t in rng.integers(0, N, (300, 2)):
+        if s != t:
+            adj_lists[int(s)].add(int(t))
+            adj_lists[int(t)].add(int(s))
+    for t in range(1, 60):
+        adj_lists[0].add(t)
+        adj_lists[t].add(0)
+    feat = _q(rng, (N, F), 16, 32)
+    feat_list = feat.tolist()
+    out = {"feat": feat}
+    batch_nodes = [int(v) for v in rng.choice(N, B, replace=False)]
+    labels = [int(v) for v in rng.integers(0, 3, B)]
+    for tag, agg, gcn in (("mean", "MEAN", False), ("max", "MAX", False), ("gcn", "MEAN", True)):
+        col = du.collate_fn(adj_lists, feat_list, 2, K, gcn, False)
+        X, y = col(list(zip(batch_nodes, labels)))
+        net = GraphSAGE(2, F, Hd, gcn, agg_func=agg, Unsupervised=False, class_size=3)
+        _set_params(net, rng, 64, 24)
+        net.eval()
+        with torch.no_grad():
+            emb, logits = net(*X, None, None, None, None, None)
+            agg0 = Aggregator(X[2], agg)
+        out[f"{tag}_center_feats"] = X[0].numpy()
+        out[f"{tag}_nodes_map"] = X[1].numpy()
+        out[f"{tag}_neigh_feats"] = X[2].numpy()
+        out[f"{tag}_neigh_map"] = X[3].numpy()
+        out[f"{tag}_agg0"] = agg0.numpy()
+        for k, v in net.state_dict().items():
+            out[f"{tag}_sd_{k}"] = v.numpy()
+        out[f"{tag}_emb"] = emb.numpy()
+        out[f"{tag}_logits"] = logits.numpy()
+        print("sage", tag, emb.shape, X[2].shape)
+    # unsupervised branch (GraphSAGE.py:54-61): contexts + negatives
+    col = du.collate_fn(adj_lists, feat_list, 2, K, False, True)
+    data = []
+    for v in batch_nodes[:6]:
+        ctx = random.choices(list(adj_lists[v]), k=2)
+        neg = [int(x) for x in rng.choice(N, 3, replace=False)]
+        data.append((v, ctx, neg))
+    X, y = col(data)
+    net = GraphSAGE(2, F, Hd, False, agg_func="MEAN", Unsupervised=True)
+    _set_params(net, rng, 64, 24)
+    net.eval()
+    with torch.no_grad():
+        emb, scores = net(*X, y.shape)
+    for i, t in enumerate(X):
+        out[f"unsup_X{i}"] = t.numpy()
+    out["unsup_shape"] = np.array(y.shape)
+    for k, v in net.state_dict().items():
+        out[f"unsup_sd_{k}"] = v.numpy()
+    out["unsup_emb"] = emb.numpy()
+    out["unsup_scores"] = scores.numpy()
+    np.savez_compressed(HERE / "sage.npz", **out)
+    print("sage unsup", emb.shape, scores.shape)
+
+
+PARTS = {"gcn": part_gcn, "gat": part_gat, "sage": part_sage}
+
+if __name__ == "__main__":
+    sys.dont_write_bytecode = True
+    if len(sys.argv) > 2 and sys.argv[1] == "--part":
+        PARTS[sys.argv[2]]()
+        sys.exit(0)
+    if not REF.exists():
+        sys.exit("the reference is not mounted at /root/reference: fixtures cannot be regenerated")
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", PYTHONHASHSEED="0")
+    for p in (sys.argv[1:] or list(PARTS)):
+        subprocess.run([sys.executable, __file__, "--part", p], check=True, env=env,
+                       cwd=tempfile.gettempdir())

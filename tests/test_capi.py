@@ -1,0 +1,68 @@
+"""The C-ABI library: loads, exports every symbol include/gnn_mi355x.h declares,
+and rejects bad arguments before launching anything (no GPU needed)."""
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "gnn_mi355x.h"
+
+
+def header_functions():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"\b(gnn_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from graphneuralnetwork_amd import _lib
+    return _lib.load(build_if_missing=True)
+
+
+def test_header_symbols_exported(lib):
+    from graphneuralnetwork_amd import _lib
+    names = header_functions()
+    assert names, "no functions parsed from the header"
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in gnn_mi355x.h but not exported"
+    assert set(names) == set(_lib.SIGNATURES), "ctypes SIGNATURES out of sync with the header"
+
+
+def test_exports_are_c_abi():
+    import subprocess
+    from graphneuralnetwork_amd import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.library_path())],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (gnn_\w+)", out))
+    assert set(header_functions()) <= exported
+
+
+def test_error_strings_and_version(lib):
+    from graphneuralnetwork_amd import _lib
+    assert lib.gnn_version() >= 100
+    assert "invalid argument" in _lib.error_string(-1)
+    assert "unsupported" in _lib.error_string(-3) or "not supported" in _lib.error_string(-3)
+
+
+def test_argument_rejection_without_launch(lib):
+    # null pointers / negative sizes -> GNN_E_ARG before anything reaches the device
+    rc = lib.gnn_spmm_csr_f32(None, None, None, 10, None, 4, 4, None, None, 4, 8, None, None, 0,
+                              None, None, 0, None, 0, None)
+    assert rc == -1
+    rc = lib.gnn_spmm_csr_f32(None, None, None, -1, None, 4, 4, None, None, 4, 8, None, None, 0,
+                              None, None, 0, None, 0, None)
+    assert rc == -1
+    assert lib.gnn_spmm_plan_count(None, 10, 4, None, None, None) == -1
+    assert lib.gnn_spmm_plan_scratch_bytes(-5) < 0
+    assert lib.gnn_spmm_plan_scratch_bytes(10_000_000) > 0
+
+
+def test_ops_refuse_cpu_tensors():
+    import torch
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.ops import spmm_forward
+    g = CsrGraph(torch.zeros(3, dtype=torch.int64), torch.zeros(0, dtype=torch.int32),
+                 torch.zeros(0), 2, 2)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        spmm_forward(g, torch.zeros(2, 4))
