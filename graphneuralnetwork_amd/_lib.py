@@ -38,6 +38,25 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
     "gnn_spmm_plan_count": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gnn_spmm_plan_fill": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gnn_gat_logits_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64,
+                                          _vp]),
+    "gnn_gat_csr_f32": (ctypes.c_int, [
+        _vp, _vp, _i64,                 # rowptr, col, n_rows
+        _vp, _i64, _i64, _i64,          # wh, ldw, heads, fh
+        _vp, _vp, _i64,                 # el, er, lde
+        ctypes.c_float, _i32, _vp,      # negative_slope, mode, empty_row_fill
+        ctypes.c_float, ctypes.c_uint64,  # dropout_p, dropout_seed
+        _vp, _i64,                      # out, ldo
+        _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
+        _vp, _vp, _i64, _vp,            # long_row, long_seg_ptr, n_long, partial
+        _u32, _vp]),                    # flags, stream
+    "gnn_col_mean_scratch_bytes": (_i64, [_i64, _i64]),
+    "gnn_col_mean_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
+    "gnn_sage_aggregate_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _i64,
+                                              _vp]),
+    "gnn_sage_gather_aggregate_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
+                                                     _i32, _vp, _i64, _vp, _vp]),
+    "gnn_gather_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
 }
 
 EPI_RELU = 1

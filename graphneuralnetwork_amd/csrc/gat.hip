@@ -1,0 +1,503 @@
+// gat.hip -- GAT edge-softmax + neighbour aggregation on gfx950, all heads in one pass.
+//
+// Replaces, per attention layer, the reference's
+//   dense  GraphAttentionLayer.forward   GAT/models/layers.py:22-37
+//          (N x N a_input, LeakyReLU, mask adj > 0 with -9e15, softmax(dim=1), att @ Wh, ELU)
+//   sparse SpGraphAttentionLayer.forward GAT/models/layers.py:94-131
+//          (edge_h gather/cat, exp(-LeakyReLU(a.edge_h)), two COO spmm's, div, ELU)
+// and the per-head Python loop + torch.cat of GAT/models/GAT.py:16.
+//
+// Inputs are the projected features Wh [N, H*Fh] (one MFMA GEMM for all heads)
+// and the per-node attention logits el = a_src.Wh_i, er = a_dst.Wh_j [N, H]
+// (gnn_gat_logits_f32). Per output row i the kernel streams the row's edges once:
+//
+//   phase A (lane = edge, 64 edges per chunk): s_ijh = LeakyReLU(el_ih + er_jh);
+//     dense : online softmax -- chunk max per head by a wave reduction, running
+//             max m_h, rescale of the lane-local denominators and of acc;
+//     sparse: p = exp(-s) with NO max subtraction (bit-for-bit the reference's
+//             arithmetic, including its overflow to inf / NaN);
+//     p[e][h] goes to a 64 x HP LDS tile private to the wave.
+//   phase B (lanes = features): acc[f] += p[e][head(f)] * Wh[col_e][f] with the
+//     same wide-gather geometry as the SpMM (EPI edge slots x LPR lanes x VW).
+//   epilogue: slot reduction, out = acc / l[head(f)] (+ ELU), one store per row.
+//
+// Dropout (training mode) is applied to the numerator weights only -- exactly
+// where both reference layers apply it (after softmax / after the rowsum) --
+// with a counter-based hash RNG keyed by (seed, edge, head).
+// Power-law rows are split into segments like the SpMM; a segment emits
+// (acc, l, m) and the fix-up merges segments with the standard log-sum-exp rule.
+#include "common.hpp"
+
+namespace gnn {
+
+constexpr int kGatBlock = 256;
+constexpr int kGatWaves = kGatBlock / kWave;
+constexpr int kMaxHeads = 8;  // heads per launch; more heads are split by the host
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 1; m < kWave; m <<= 1) v = fmaxf(v, __shfl_xor(v, m, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 1; m < kWave; m <<= 1) v += __shfl_xor(v, m, kWave);
+  return v;
+}
+
+__device__ __forceinline__ uint32_t hash3(uint64_t seed, int64_t edge, int head) {
+  uint32_t h = static_cast<uint32_t>(seed) ^ (static_cast<uint32_t>(seed >> 32) * 0x27d4eb2fu);
+  h ^= static_cast<uint32_t>(edge) * 0x9e3779b9u;
+  h ^= static_cast<uint32_t>(static_cast<uint64_t>(edge) >> 32) * 0x85ebca6bu;
+  h ^= static_cast<uint32_t>(head) * 0xc2b2ae35u;
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+struct GatParams {
+  const int64_t* rowptr;
+  const int32_t* col;
+  int64_t n_rows;
+  const float* wh;
+  int64_t ldw;
+  int64_t feat;  // H * Fh of this head group
+  int64_t fh;
+  const float* el;
+  const float* er;
+  int64_t lde;
+  int heads;
+  float slope;
+  const float* empty_fill;
+  float drop_p;
+  float drop_scale;
+  uint64_t drop_seed;
+  int head0;  // global index of this group's first head (dropout stream)
+  float* out;
+  int64_t ldo;
+  int64_t seg_len;
+  const int32_t* seg_row;
+  const int64_t* seg_begin;
+  int64_t n_seg;
+  int64_t seg_waves;
+  const int32_t* long_row;
+  const int32_t* long_seg_ptr;
+  int64_t n_long;
+  float* partial;  // per segment: [feat acc][heads l][heads m]
+  int64_t ldp;
+  uint32_t flags;
+};
+
+template <int VW, int LPR, int NCH, int HP, bool SPARSE, int U>
+__global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
+  constexpr int EPI = kWave / LPR;
+  __shared__ float p_lds[kGatWaves][kWave * HP];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x >> 6;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kGatWaves + wid;
+  const int sub = lane & (LPR - 1);
+  const int grp = lane / LPR;
+
+  int64_t row, beg, end;
+  bool is_seg = false;
+  if (wave < P.seg_waves) {
+    if (wave >= P.n_seg) return;
+    row = P.seg_row[wave];
+    beg = P.seg_begin[wave];
+    end = min(beg + P.seg_len, P.rowptr[row + 1]);
+    is_seg = true;
+  } else {
+    row = wave - P.seg_waves;
+    if (row >= P.n_rows) return;
+    beg = P.rowptr[row];
+    end = P.rowptr[row + 1];
+    if (end - beg > P.seg_len) return;
+  }
+
+  float eli[HP], m[HP], lsum[HP];
+#pragma unroll
+  for (int h = 0; h < HP; ++h) {
+    eli[h] = h < P.heads ? P.el[row * P.lde + h] : 0.f;
+    m[h] = SPARSE ? 0.f : -INFINITY;
+    lsum[h] = 0.f;
+  }
+  // head of each feature vector this lane owns (Fh % VW == 0 on the vector path)
+  int hid[NCH];
+  typename Vec<VW>::T acc[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+    hid[ch] = f < P.feat ? static_cast<int>(f / P.fh) : 0;
+    acc[ch] = vzero<VW>();
+  }
+  float* pw = p_lds[wid];
+
+  for (int64_t base = beg; base < end; base += kWave) {
+    const int n = static_cast<int>(min(static_cast<int64_t>(kWave), end - base));
+    const bool live = lane < n;
+    const int c = live ? P.col[base + lane] : 0;
+    // ---- phase A: logits and unnormalised weights, lane = edge
+    float p[HP];
+#pragma unroll
+    for (int h = 0; h < HP; ++h) {
+      float lg = -INFINITY;
+      if (live && h < P.heads) {
+        const float s = eli[h] + P.er[static_cast<int64_t>(c) * P.lde + h];
+        const float x = s > 0.f ? s : P.slope * s;
+        lg = SPARSE ? -x : x;
+      }
+      p[h] = lg;
+    }
+    if (!SPARSE) {
+      float scl[HP];
+#pragma unroll
+      for (int h = 0; h < HP; ++h) {
+        const float mn = fmaxf(m[h], wave_max(p[h]));
+        scl[h] = __expf(m[h] - mn);  // 0 on the first chunk (m = -inf), uniform across lanes
+        m[h] = mn;
+        p[h] = live ? __expf(p[h] - mn) : 0.f;
+        lsum[h] = lsum[h] * scl[h] + p[h];
+      }
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        float sc = scl[0];
+#pragma unroll
+        for (int h = 1; h < HP; ++h)
+          if (h == hid[ch]) sc = scl[h];
+        acc[ch] *= sc;
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < HP; ++h) {
+        p[h] = live ? expf(p[h]) : 0.f;
+        lsum[h] += p[h];
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < HP; ++h) pw[lane * HP + h] = p[h];
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- phase B: weighted gather of neighbour rows, lanes = features
+    for (int k = 0; k < n; k += EPI * U) {
+      typename Vec<VW>::T xv[U][NCH];
+      float w[U][NCH];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = k + u * EPI + grp;
+        const int src = e & (kWave - 1);
+        const int ce = __shfl(c, src, kWave);
+        const float* xr = P.wh + static_cast<int64_t>(ce) * P.ldw;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+          const bool ok = e < n && f < P.feat;
+          xv[u][ch] = ok ? vload<VW>(xr + f) : vzero<VW>();
+          float wv = ok ? pw[src * HP + hid[ch]] : 0.f;
+          if (P.drop_p > 0.f && ok) {
+            const uint32_t r = hash3(P.drop_seed, base + e, P.head0 + hid[ch]);
+            wv = (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f
+                                                                                 : wv * P.drop_scale;
+          }
+          w[u][ch] = wv;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) acc[ch] += w[u][ch] * xv[u][ch];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // ---- epilogue
+#pragma unroll
+  for (int mm = LPR; mm < kWave; mm <<= 1) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) acc[ch] += shfl_xor_f(acc[ch], mm);
+  }
+#pragma unroll
+  for (int h = 0; h < HP; ++h) lsum[h] = wave_sum(lsum[h]);
+
+  if (is_seg) {
+    float* pr = P.partial + wave * P.ldp;
+    if (lane < LPR) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+        if (f < P.feat) vstore<VW>(pr + f, acc[ch]);
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int h = 0; h < HP; ++h) {
+        if (h < P.heads) {
+          pr[P.feat + h] = lsum[h];
+          pr[P.feat + P.heads + h] = m[h];
+        }
+      }
+    }
+    return;
+  }
+  if (lane >= LPR) return;
+  const bool empty = end == beg;
+  float* orow = P.out + row * P.ldo;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+    if (f >= P.feat) continue;
+    float l = lsum[0];
+#pragma unroll
+    for (int h = 1; h < HP; ++h)
+      if (h == hid[ch]) l = lsum[h];
+    typename Vec<VW>::T r;
+    if (!SPARSE && empty) {
+      r = P.empty_fill ? vload<VW>(P.empty_fill + f) : typename Vec<VW>::T(NAN);
+    } else {
+      r = acc[ch] / l;  // sparse, no edge: 0/0 = NaN like the reference
+    }
+#pragma unroll
+    for (int i = 0; i < VW; ++i) vset(r, i, act_apply(vget(r, i), P.flags));
+    vstore<VW>(orow + f, r);
+  }
+}
+
+// Merge the (acc, l, m) partial states of each long row (log-sum-exp rule; m = 0 for sparse).
+template <int VW, int LPR, int NCH, bool SPARSE>
+__global__ __launch_bounds__(kGatBlock) void gat_fixup_kernel(GatParams P) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kGatWaves + (threadIdx.x >> 6);
+  if (i >= P.n_long || lane >= LPR) return;
+  const int sub = lane;
+  const int32_t s0 = P.long_seg_ptr[i], s1 = P.long_seg_ptr[i + 1];
+  const int64_t row = P.long_row[i];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+    if (f >= P.feat) continue;
+    const int h = static_cast<int>(f / P.fh);
+    float M = SPARSE ? 0.f : -INFINITY;
+    if (!SPARSE)
+      for (int32_t s = s0; s < s1; ++s) M = fmaxf(M, P.partial[s * P.ldp + P.feat + P.heads + h]);
+    typename Vec<VW>::T a = vzero<VW>();
+    float l = 0.f;
+    for (int32_t s = s0; s < s1; ++s) {
+      const float* pr = P.partial + static_cast<int64_t>(s) * P.ldp;
+      const float sc = SPARSE ? 1.f : __expf(pr[P.feat + P.heads + h] - M);
+      a += sc * vload<VW>(pr + f);
+      l += sc * pr[P.feat + h];
+    }
+    typename Vec<VW>::T r = a / l;
+#pragma unroll
+    for (int k = 0; k < VW; ++k) vset(r, k, act_apply(vget(r, k), P.flags));
+    vstore<VW>(P.out + row * P.ldo + f, r);
+  }
+}
+
+template <int VW, int LPR, int NCH, int HP, bool SPARSE>
+static void launch_gat(const GatParams& P, hipStream_t s) {
+  constexpr int U = NCH >= 2 ? 1 : 2;
+  const int64_t seg_blocks = (P.n_seg + kGatWaves - 1) / kGatWaves;
+  const int64_t row_blocks = (P.n_rows + kGatWaves - 1) / kGatWaves;
+  GatParams Q = P;
+  Q.seg_waves = seg_blocks * kGatWaves;
+  if (seg_blocks + row_blocks > 0)
+    hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U>),
+                       dim3(static_cast<unsigned>(seg_blocks + row_blocks)), dim3(kGatBlock), 0, s,
+                       Q);
+  if (P.n_long > 0)
+    hipLaunchKernelGGL((gat_fixup_kernel<VW, LPR, NCH, SPARSE>),
+                       dim3(static_cast<unsigned>((P.n_long + kGatWaves - 1) / kGatWaves)),
+                       dim3(kGatBlock), 0, s, Q);
+}
+
+template <int VW, int HP, bool SPARSE>
+static int dispatch_gat_lpr(const GatParams& P, hipStream_t s) {
+  const int64_t nv = (P.feat + VW - 1) / VW;
+  if (nv <= 64) {
+    switch (next_pow2_le64(nv)) {
+      case 1: launch_gat<VW, 1, 1, HP, SPARSE>(P, s); break;
+      case 2: launch_gat<VW, 2, 1, HP, SPARSE>(P, s); break;
+      case 4: launch_gat<VW, 4, 1, HP, SPARSE>(P, s); break;
+      case 8: launch_gat<VW, 8, 1, HP, SPARSE>(P, s); break;
+      case 16: launch_gat<VW, 16, 1, HP, SPARSE>(P, s); break;
+      case 32: launch_gat<VW, 32, 1, HP, SPARSE>(P, s); break;
+      default: launch_gat<VW, 64, 1, HP, SPARSE>(P, s); break;
+    }
+  } else if (nv <= 128) {
+    launch_gat<VW, 64, 2, HP, SPARSE>(P, s);
+  } else if (nv <= 256) {
+    launch_gat<VW, 64, 4, HP, SPARSE>(P, s);
+  } else {
+    return GNN_E_UNSUPPORTED;
+  }
+  return launch_status();
+}
+
+template <int VW, bool SPARSE>
+static int dispatch_gat(const GatParams& P, hipStream_t s) {
+  if (P.heads <= 1) return dispatch_gat_lpr<VW, 1, SPARSE>(P, s);
+  if (P.heads <= 2) return dispatch_gat_lpr<VW, 2, SPARSE>(P, s);
+  if (P.heads <= 4) return dispatch_gat_lpr<VW, 4, SPARSE>(P, s);
+  return dispatch_gat_lpr<VW, 8, SPARSE>(P, s);
+}
+
+// el[n, h] = sum_f Wh[n, h*fh + f] * a_src[h*fh + f]; er likewise with a_dst.
+__global__ __launch_bounds__(256) void gat_logits_kernel(const float* __restrict__ wh, int64_t ldw,
+                                                         int64_t n_rows, int64_t heads, int64_t fh,
+                                                         const float* __restrict__ a_src,
+                                                         const float* __restrict__ a_dst,
+                                                         float* __restrict__ el,
+                                                         float* __restrict__ er, int64_t lde) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= n_rows * heads) return;
+  const int64_t n = t / heads, h = t % heads;
+  const float* x = wh + n * ldw + h * fh;
+  const float* as = a_src + h * fh;
+  const float* ad = a_dst + h * fh;
+  float sl = 0.f, sr = 0.f;
+  for (int64_t f = 0; f < fh; ++f) {
+    const float v = x[f];
+    sl = fmaf(v, as[f], sl);
+    sr = fmaf(v, ad[f], sr);
+  }
+  el[n * lde + h] = sl;
+  er[n * lde + h] = sr;
+}
+
+// out[f] = mean over rows of x[:, f] (double accumulation; two passes, deterministic).
+constexpr int kMeanRows = 4096;
+__global__ __launch_bounds__(256) void col_sum_partial_kernel(const float* __restrict__ x,
+                                                              int64_t ldx, int64_t n_rows,
+                                                              int64_t feat,
+                                                              double* __restrict__ part) {
+  const int64_t f = static_cast<int64_t>(blockIdx.y) * blockDim.x + threadIdx.x;
+  if (f >= feat) return;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kMeanRows;
+  const int64_t r1 = min(r0 + kMeanRows, n_rows);
+  double s = 0.0;
+  for (int64_t r = r0; r < r1; ++r) s += static_cast<double>(x[r * ldx + f]);
+  part[static_cast<int64_t>(blockIdx.x) * feat + f] = s;
+}
+__global__ __launch_bounds__(256) void col_mean_final_kernel(const double* __restrict__ part,
+                                                             int64_t nblk, int64_t n_rows,
+                                                             int64_t feat, float* __restrict__ out) {
+  const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (f >= feat) return;
+  double s = 0.0;
+  for (int64_t b = 0; b < nblk; ++b) s += part[b * feat + f];
+  out[f] = static_cast<float>(s / static_cast<double>(n_rows));
+}
+
+}  // namespace gnn
+
+using namespace gnn;
+
+extern "C" int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t heads,
+                                  int64_t fh, const float* a_src, const float* a_dst, float* el,
+                                  float* er, int64_t lde, void* stream) {
+  if (n_rows < 0 || heads < 1 || fh < 1 || ldw < heads * fh || lde < heads) return GNN_E_ARG;
+  if (n_rows == 0) return GNN_OK;
+  if (!wh || !a_src || !a_dst || !el || !er) return GNN_E_ARG;
+  const int64_t total = n_rows * heads;
+  hipLaunchKernelGGL(gat_logits_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256),
+                     0, static_cast<hipStream_t>(stream), wh, ldw, n_rows, heads, fh, a_src, a_dst,
+                     el, er, lde);
+  return launch_status();
+}
+
+extern "C" int64_t gnn_col_mean_scratch_bytes(int64_t n_rows, int64_t feat) {
+  if (n_rows < 0 || feat < 0) return GNN_E_ARG;
+  return ((n_rows + kMeanRows - 1) / kMeanRows) * feat * static_cast<int64_t>(sizeof(double));
+}
+
+extern "C" int gnn_col_mean_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t feat,
+                                float* out, void* scratch, void* stream) {
+  if (n_rows < 1 || feat < 1 || ldx < feat || !x || !out || !scratch) return GNN_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t nblk = (n_rows + kMeanRows - 1) / kMeanRows;
+  if (nblk > 0x7fffffffLL || (feat + 255) / 256 > 65535) return GNN_E_UNSUPPORTED;
+  double* part = static_cast<double*>(scratch);
+  hipLaunchKernelGGL(col_sum_partial_kernel,
+                     dim3(static_cast<unsigned>(nblk), static_cast<unsigned>((feat + 255) / 256)),
+                     dim3(256), 0, s, x, ldx, n_rows, feat, part);
+  hipLaunchKernelGGL(col_mean_final_kernel, dim3(static_cast<unsigned>((feat + 255) / 256)),
+                     dim3(256), 0, s, part, nblk, n_rows, feat, out);
+  return launch_status();
+}
+
+extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                               const float* wh, int64_t ldw, int64_t heads, int64_t fh,
+                               const float* el, const float* er, int64_t lde, float negative_slope,
+                               int32_t mode, const float* empty_row_fill, float dropout_p,
+                               uint64_t dropout_seed, float* out, int64_t ldo, int64_t seg_len,
+                               const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
+                               const int32_t* long_row, const int32_t* long_seg_ptr,
+                               int64_t n_long, float* partial, uint32_t flags, void* stream) {
+  if (n_rows < 0 || heads < 1 || fh < 1 || seg_len < 1 || n_seg < 0 || n_long < 0) return GNN_E_ARG;
+  if (mode != 0 && mode != 1) return GNN_E_ARG;
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return GNN_E_ARG;
+  if (flags & ~(GNN_EPI_RELU | GNN_EPI_ELU)) return GNN_E_ARG;
+  if (n_rows == 0) return GNN_OK;
+  const int64_t feat_all = heads * fh;
+  if (!rowptr || !wh || !el || !er || !out || ldw < feat_all || ldo < feat_all || lde < heads)
+    return GNN_E_ARG;
+  if (n_rows > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
+  if ((n_seg > 0 || n_long > 0) &&
+      (!seg_row || !seg_begin || !long_row || !long_seg_ptr || !partial || n_seg == 0 || n_long == 0))
+    return GNN_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // partial row layout per segment: [heads*fh acc | heads l | heads m] of the WHOLE layer;
+  // each head group writes its own slice (the host allocates ldp = heads*fh + 2*heads).
+  const int64_t ldp = feat_all + 2 * heads;
+  const int64_t groups = (heads + kMaxHeads - 1) / kMaxHeads;
+  for (int64_t g = 0; g < groups; ++g) {
+    const int64_t h0 = g * kMaxHeads;
+    const int64_t hg = heads - h0 < kMaxHeads ? heads - h0 : kMaxHeads;
+    GatParams P{};
+    P.rowptr = rowptr;
+    P.col = col;
+    P.n_rows = n_rows;
+    P.feat = hg * fh;
+    P.fh = fh;
+    P.wh = wh + h0 * fh;
+    P.ldw = ldw;
+    P.el = el + h0;
+    P.er = er + h0;
+    P.lde = lde;
+    P.heads = static_cast<int>(hg);
+    P.slope = negative_slope;
+    P.empty_fill = empty_row_fill ? empty_row_fill + h0 * fh : nullptr;
+    P.drop_p = dropout_p;
+    P.drop_scale = dropout_p > 0.f ? 1.0f / (1.0f - dropout_p) : 1.0f;
+    P.drop_seed = dropout_seed;
+    P.head0 = static_cast<int>(h0);
+    P.out = out + h0 * fh;
+    P.ldo = ldo;
+    P.seg_len = seg_len;
+    P.seg_row = seg_row;
+    P.seg_begin = seg_begin;
+    P.n_seg = n_seg;
+    P.long_row = long_row;
+    P.long_seg_ptr = long_seg_ptr;
+    P.n_long = n_long;
+    // group slice of the partial rows: acc at h0*fh, l/m stored right after the slice's feat
+    P.partial = partial ? partial + g * (kMaxHeads * fh + 2 * kMaxHeads) : nullptr;
+    P.ldp = ldp;  // same row stride for every group
+    P.flags = flags;
+    const bool vec4 = (fh % 4 == 0) && (ldw % 4 == 0) && (ldo % 4 == 0) && aligned_to(P.wh, 16) &&
+                      aligned_to(P.out, 16) &&
+                      (P.empty_fill == nullptr || aligned_to(P.empty_fill, 16)) &&
+                      (P.partial == nullptr || (aligned_to(P.partial, 16) && ldp % 4 == 0));
+    int rc;
+    if (mode == 1)
+      rc = vec4 ? dispatch_gat<4, true>(P, s) : dispatch_gat<1, true>(P, s);
+    else
+      rc = vec4 ? dispatch_gat<4, false>(P, s) : dispatch_gat<1, false>(P, s);
+    if (rc != GNN_OK) return rc;
+  }
+  return GNN_OK;
+}

@@ -1,0 +1,188 @@
+"""Drop-in GAT modules (reference: GAT/models/layers.py, GAT/models/GAT.py).
+
+Same class names, constructor arguments, parameter shapes/initialisation and
+``forward(h, adj)`` signatures as the reference:
+
+* ``GraphAttentionLayer``   -- W [in, out] xavier_uniform(gain 1.414), a [2*out, 1]
+  (layers.py:6-40); edges are ``adj > 0``; softmax attention.
+* ``SpGraphAttentionLayer`` -- W [in, out] xavier_normal(gain 1.414), a [1, 2*out]
+  (layers.py:72-134); edges are ``adj.nonzero()``; exp(-LeakyReLU) weights
+  with no max subtraction, exactly the reference arithmetic (incl. its NaN
+  assert for edgeless rows).
+* ``GAT`` / ``SpGAT`` (GAT.py:7-38) -- ``attentions.AttentionHead{i}`` + ``out_att``
+  state_dict keys.  The reference module cannot even be imported (GAT.py:4
+  imports the missing ``models.HAN``); these are usable.
+
+Where the reference materialises an N x N x 2F tensor per head (dense) or
+E x 2F per head (sparse) and loops over heads in Python, here every
+attention layer is: one GEMM for all heads (X @ [W_1 | ... | W_H], hipBLASLt
+MFMA), one HIP launch for the attention logits, one HIP launch for the fused
+edge-softmax + aggregation (+ ELU) over the CSR adjacency.  ``adj`` may be the
+reference's dense tensor, a torch sparse tensor or a ``CsrGraph``.
+
+Forward only: autograd through these layers is not implemented yet
+(backward kernels are the next row of the plan); a forward with gradients
+enabled on trainable parameters raises.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .graph import as_csr
+from .ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_logits
+
+# The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
+# (layers.py:102,109,119,124).  Kept on by default for identical error
+# behaviour; each check is one device reduction + host sync.
+SPARSE_NAN_CHECK = True
+
+
+def _no_autograd(module: nn.Module) -> None:
+    if torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters()):
+        raise NotImplementedError(
+            f"{type(module).__name__}: the MI355X GAT path is forward-only for now; run it under "
+            "torch.no_grad() / torch.inference_mode() or freeze its parameters")
+
+
+def _dropout_seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+class _AttentionBase(nn.Module):
+    MODE = GAT_DENSE
+    PREDICATE = "positive"
+
+    def _a_parts(self):
+        a = self.a.reshape(-1)
+        F_ = self.out_features
+        return a[:F_], a[F_:]
+
+    def _aggregate(self, Wh, adj, heads, fh, a_src, a_dst, activation, dropout_p):
+        g = as_csr(adj, self.PREDICATE)
+        el, er = gat_logits(Wh, heads, fh, a_src, a_dst)
+        p = dropout_p if self.training else 0.0
+        out = gat_aggregate(g, Wh, el, er, heads, fh, self.alpha, self.MODE, activation,
+                            dropout_p=p, seed=_dropout_seed() if p > 0 else 0)
+        if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
+            assert not torch.isnan(out).any()
+        return out
+
+    def forward(self, h, adj, activation: str | None = "__concat__"):
+        _no_autograd(self)
+        if activation == "__concat__":
+            activation = "elu" if self.concat else None
+        Wh = torch.mm(h, self.W)
+        if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
+            assert not torch.isnan(Wh).any()
+        a_src, a_dst = self._a_parts()
+        return self._aggregate(Wh, adj, 1, self.out_features, a_src, a_dst, activation,
+                               self._drop_p())
+
+    def __repr__(self):
+        return self.__class__.__name__ + ' (' + str(self.in_features) + ' -> ' + str(self.out_features) + ')'
+
+
+class GraphAttentionLayer(_AttentionBase):
+    """GAT/models/layers.py:6-40 (dense attention, edges = adj > 0)."""
+
+    MODE = GAT_DENSE
+    PREDICATE = "positive"
+
+    def __init__(self, in_features, out_features, dropout, alpha, concat=True, **kwargs):
+        super().__init__(**kwargs)
+        self.dropout = dropout
+        self.in_features = in_features
+        self.out_features = out_features
+        self.alpha = alpha
+        self.concat = concat
+        self.W = nn.Parameter(torch.empty(size=(in_features, out_features)))
+        nn.init.xavier_uniform_(self.W.data, gain=1.414)
+        self.a = nn.Parameter(torch.empty(size=(2 * out_features, 1)))
+        nn.init.xavier_uniform_(self.a.data, gain=1.414)
+        self.leakyrelu = nn.LeakyReLU(self.alpha)
+
+    def _drop_p(self):
+        return float(self.dropout)
+
+
+class SpGraphAttentionLayer(_AttentionBase):
+    """GAT/models/layers.py:72-134 (sparse attention, edges = adj.nonzero())."""
+
+    MODE = GAT_SPARSE
+    PREDICATE = "nonzero"
+
+    def __init__(self, in_features, out_features, dropout, alpha, concat=True):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.alpha = alpha
+        self.concat = concat
+        self.W = nn.Parameter(torch.zeros(size=(in_features, out_features)))
+        nn.init.xavier_normal_(self.W.data, gain=1.414)
+        self.a = nn.Parameter(torch.zeros(size=(1, 2 * out_features)))
+        nn.init.xavier_normal_(self.a.data, gain=1.414)
+        self.dropout = nn.Dropout(dropout)
+        self.leakyrelu = nn.LeakyReLU(self.alpha)
+
+    def _drop_p(self):
+        return float(self.dropout.p)
+
+
+class GATBase(nn.Module):
+    """GAT/models/GAT.py:7-18: dropout -> concat(heads) -> dropout -> ELU(out_att)."""
+
+    def __init__(self, dropout, **kwargs):
+        super().__init__(**kwargs)
+        self.dropout = dropout
+        self.attentions = nn.ModuleList()
+        self.out_att = None
+
+    def _heads(self, x, adj):
+        heads = list(self.attentions)
+        first = heads[0]
+        uniform = all(type(m) is type(first) and m.concat and m.alpha == first.alpha
+                      and m.out_features == first.out_features
+                      and m._drop_p() == first._drop_p() for m in heads)
+        if not uniform:
+            return torch.cat([att(x, adj) for att in heads], dim=1)
+        for m in heads:
+            _no_autograd(m)
+        fh = first.out_features
+        W = torch.cat([m.W for m in heads], dim=1)          # [in, H*fh]
+        Wh = torch.mm(x, W)                                  # one MFMA GEMM for all heads
+        if first.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
+            assert not torch.isnan(Wh).any()
+        parts = [m._a_parts() for m in heads]
+        a_src = torch.cat([p[0] for p in parts])
+        a_dst = torch.cat([p[1] for p in parts])
+        return first._aggregate(Wh, adj, len(heads), fh, a_src, a_dst, "elu", first._drop_p())
+
+    def forward(self, x, adj):
+        x = F.dropout(x, self.dropout, training=self.training)
+        x = self._heads(x, adj)
+        x = F.dropout(x, self.dropout, training=self.training)
+        return self.out_att(x, adj, activation="elu")  # F.elu(out_att(x)) fused (concat=False)
+
+
+class GAT(GATBase):
+    """GAT/models/GAT.py:21-28 (dense version)."""
+
+    def __init__(self, nfeat, nhid, nclass, dropout, alpha, nheads, **kwargs):
+        super().__init__(dropout, **kwargs)
+        for i in range(nheads):
+            self.attentions.add_module(f'AttentionHead{i}',
+                                       GraphAttentionLayer(nfeat, nhid, dropout=dropout, alpha=alpha, concat=True))
+        self.out_att = GraphAttentionLayer(nhid * nheads, nclass, dropout=dropout, alpha=alpha, concat=False)
+
+
+class SpGAT(GATBase):
+    """GAT/models/GAT.py:31-38 (sparse version)."""
+
+    def __init__(self, nfeat, nhid, nclass, dropout, alpha, nheads, **kwargs):
+        super().__init__(dropout, **kwargs)
+        for i in range(nheads):
+            self.attentions.add_module(f'AttentionHead{i}',
+                                       SpGraphAttentionLayer(nfeat, nhid, dropout=dropout, alpha=alpha, concat=True))
+        self.out_att = SpGraphAttentionLayer(nhid * nheads, nclass, dropout=dropout, alpha=alpha, concat=False)

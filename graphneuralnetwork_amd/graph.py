@@ -72,6 +72,14 @@ class CsrGraph:
     def device(self) -> torch.device:
         return self.rowptr.device
 
+    def has_empty_rows(self) -> bool:
+        """Whether some row has no edge (one device reduction, cached)."""
+        v = self._plans.get("_has_empty")
+        if v is None:
+            v = bool(((self.rowptr[1:] - self.rowptr[:-1]) == 0).any())
+            self._plans["_has_empty"] = v
+        return v
+
     def validate(self) -> None:
         assert self.rowptr.dtype == torch.int64 and self.rowptr.numel() == self.n_rows + 1
         assert self.col.dtype == torch.int32 and self.val.dtype == torch.float32
@@ -152,31 +160,61 @@ def from_dense(adj: torch.Tensor, predicate: str) -> CsrGraph:
     return from_coo(idx[:, 0], idx[:, 1], adj[mask], adj.shape[0], adj.shape[1])
 
 
-def from_torch_sparse(adj: torch.Tensor) -> CsrGraph:
+def _edge_mask(val: torch.Tensor, predicate: str):
+    if predicate == "all":
+        return None
+    if predicate == "positive":
+        return val > 0
+    if predicate == "nonzero":
+        return val != 0
+    raise ValueError(predicate)
+
+
+def from_torch_sparse(adj: torch.Tensor, predicate: str = "all") -> CsrGraph:
+    """CSR of a torch sparse COO/CSR tensor; ``predicate`` filters stored entries
+    ('all' keeps every stored entry, as torch.spmm uses them)."""
     if adj.layout == torch.sparse_coo:
+        if predicate != "all":  # edge-set semantics (GAT): one edge per (i, j)
+            adj = adj.coalesce()
         idx = adj._indices()
-        return from_coo(idx[0], idx[1], adj._values(), adj.shape[0], adj.shape[1])
-    if adj.layout == torch.sparse_csr:
-        return CsrGraph(adj.crow_indices().to(torch.int64).contiguous(),
-                        adj.col_indices().to(torch.int32).contiguous(),
-                        adj.values().to(torch.float32).contiguous(), adj.shape[0], adj.shape[1])
-    raise TypeError(f"unsupported sparse layout {adj.layout}")
+        row, col, val = idx[0], idx[1], adj._values()
+    elif adj.layout == torch.sparse_csr:
+        crow = adj.crow_indices().to(torch.int64)
+        val = adj.values()
+        mask = _edge_mask(val, predicate)
+        if mask is None:
+            return CsrGraph(crow.contiguous(), adj.col_indices().to(torch.int32).contiguous(),
+                            val.to(torch.float32).contiguous(), adj.shape[0], adj.shape[1])
+        row = torch.repeat_interleave(torch.arange(adj.shape[0], device=crow.device),
+                                      crow[1:] - crow[:-1])
+        col = adj.col_indices()
+    else:
+        raise TypeError(f"unsupported sparse layout {adj.layout}")
+    mask = _edge_mask(val, predicate)
+    if mask is not None:
+        row, col, val = row[mask], col[mask], val[mask]
+    return from_coo(row, col, val, adj.shape[0], adj.shape[1])
 
 
-def as_csr(adj, predicate: str = "nonzero") -> CsrGraph:
-    """The CsrGraph of a reference adjacency (cached on the tensor object)."""
+def as_csr(adj, predicate: str = "all") -> CsrGraph:
+    """The CsrGraph of a reference adjacency (cached on the tensor object).
+
+    predicate: which entries are edges -- 'all' (every stored entry of a sparse
+    tensor / every nonzero of a dense one: torch.spmm semantics), 'positive'
+    (adj > 0: dense GAT layer), 'nonzero' (adj != 0: sparse GAT layer).
+    """
     if isinstance(adj, CsrGraph):
         return adj
     if not isinstance(adj, torch.Tensor) or adj.dim() != 2:
         raise TypeError("adj must be a 2-D torch tensor (dense, sparse COO or sparse CSR) or a CsrGraph")
-    key = (predicate if adj.layout == torch.strided else "sparse", adj._version, adj.device)
+    key = (predicate, adj._version, adj.device)
     cache = getattr(adj, "_gnn_csr_cache", None)
     if cache is not None and key in cache:
         return cache[key]
     if adj.layout == torch.strided:
-        g = from_dense(adj, predicate)
+        g = from_dense(adj, "nonzero" if predicate == "all" else predicate)
     else:
-        g = from_torch_sparse(adj)
+        g = from_torch_sparse(adj, predicate)
     if cache is None:
         cache = {}
         try:

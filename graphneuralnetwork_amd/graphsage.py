@@ -1,0 +1,160 @@
+"""Drop-in GraphSAGE modules (reference: GraphSAGE/GraphSAGE.py, GraphSAGE/graph_utils.py).
+
+Same names, constructor arguments, 9-argument ``forward`` and state_dict keys
+(``sage_blocks.sage_layer{i}.weight.weight`` [H, 2F or F], ``dense.weight`` /
+``dense.bias``) as the reference.
+
+Hot path on gfx950:
+
+* ``Aggregator`` (graph_utils.py:4-11) -> one HIP launch (mean, or torch.argmax's
+  int64 first-max indices, bit-exact);
+* the re-gathers of GraphSAGE.py:47-49 (``torch.embedding(feats, map)`` followed
+  by the next layer's ``Aggregator``) -> ONE fused gather-aggregate launch that
+  never materialises the [M, k, H] neighbour tensor, plus one row-gather
+  launch for the centre rows;
+* ``SageLayer``'s ``Linear(cat[self, agg])`` -> two accumulating MFMA GEMMs on
+  the two halves of W (no concatenated copy).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .ops import gather_rows, sage_aggregate, sage_gather_aggregate
+
+
+class _MeanAgg(torch.autograd.Function):
+    """Pre-gathered MEAN with autograd (d neigh = d out / k broadcast over k)."""
+
+    @staticmethod
+    def forward(ctx, neigh):
+        ctx.k = neigh.shape[1]
+        return sage_aggregate(neigh, "MEAN")
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g / ctx.k).unsqueeze(1).expand(-1, ctx.k, -1)
+
+
+class _GatherMeanAgg(torch.autograd.Function):
+    """Fused gather + MEAN with autograd w.r.t. the table (scatter of d out / k)."""
+
+    @staticmethod
+    def forward(ctx, table, idx):
+        ctx.save_for_backward(idx)
+        ctx.n = table.shape[0]
+        return sage_gather_aggregate(table, idx, "MEAN")
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        k = idx.shape[1]
+        gt = torch.zeros((ctx.n, g.shape[1]), dtype=g.dtype, device=g.device)
+        gt.index_add_(0, idx.reshape(-1), (g / k).repeat_interleave(k, dim=0))
+        return gt, None
+
+
+class _GatherRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx):
+        ctx.save_for_backward(idx)
+        ctx.n = x.shape[0]
+        return gather_rows(x, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        gx = torch.zeros((ctx.n, g.shape[1]), dtype=g.dtype, device=g.device)
+        gx.index_add_(0, idx, g)
+        return gx, None
+
+
+def Aggregator(neigh_feat, agg_func='MEAN'):
+    """GraphSAGE/graph_utils.py:4-11 on the device ('MEAN' -> fp32, 'MAX' -> int64 argmax)."""
+    if agg_func == 'MEAN' and torch.is_grad_enabled() and neigh_feat.requires_grad:
+        return _MeanAgg.apply(neigh_feat)
+    return sage_aggregate(neigh_feat, agg_func)
+
+
+def _gather_aggregate(table, idx, agg_func):
+    if agg_func == 'MEAN' and torch.is_grad_enabled() and table.requires_grad:
+        return _GatherMeanAgg.apply(table, idx)
+    return sage_gather_aggregate(table, idx, agg_func)
+
+
+def _gather(x, idx):
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _GatherRows.apply(x, idx)
+    return gather_rows(x, idx)
+
+
+class SageLayer(nn.Module):
+    """GraphSAGE/GraphSAGE.py:7-20: relu(W . cat[self, agg]) (or relu(W . agg) in gcn mode)."""
+
+    def __init__(self, input_size, output_size, gcn=False, **kwargs):
+        super().__init__(**kwargs)
+        self.input_size = input_size
+        self.output_size = output_size
+        self.gcn = gcn
+        self.weight = nn.Linear(self.input_size if self.gcn else 2 * self.input_size, self.output_size, bias=False)
+
+    def forward(self, self_feats, aggregate_feats):
+        W = self.weight.weight
+        if self.gcn:  # the reference feeds the aggregate straight into Linear (int64 argmax fails there too)
+            return F.relu(self.weight(aggregate_feats))
+        if aggregate_feats.dtype != torch.float32:  # MAX mode: argmax indices promote like torch.cat
+            aggregate_feats = aggregate_feats.to(torch.float32)
+        if self_feats.dtype != torch.float32:
+            self_feats = self_feats.to(torch.float32)
+        n = self.input_size
+        # cat([self, agg]) @ W^T == self @ W[:, :n]^T + agg @ W[:, n:]^T (no concat copy)
+        out = torch.addmm(F.linear(self_feats, W[:, :n]), aggregate_feats, W[:, n:].t())
+        return F.relu(out)
+
+
+class GraphSAGE(nn.Module):
+    """GraphSAGE/GraphSAGE.py:23-61 with the same 9-argument forward."""
+
+    def __init__(self, num_layers, input_size, out_size, gcn=False, agg_func='MEAN', Unsupervised=True, class_size=None,
+                 **kwargs):
+        super().__init__(**kwargs)
+        self.num_layers = num_layers
+        self.gcn = gcn
+        self.agg_func = agg_func
+        self.sage_blocks = nn.Sequential()
+        for index in range(0, num_layers):
+            layer_size = out_size if index != 0 else input_size
+            self.sage_blocks.add_module('sage_layer' + str(index), SageLayer(layer_size, out_size, gcn=self.gcn))
+        self.Unsupervised = Unsupervised
+        if not Unsupervised:
+            self.dense = nn.Linear(out_size, class_size)
+
+    def forward(self, center_feats_data, center_nodes_map, center_neigh_feats_data, center_neigh_nodes_map,
+                contexts_negatives_feats_data, contexts_negatives_nodes_map, contexts_negatives_neigh_feats_data,
+                contexts_negatives_neigh_nodes_map, contexts_negatives_shape):
+        if contexts_negatives_feats_data is None:
+            pending = None  # (table, index map) of a fused gather-aggregate
+            feats_data = None
+            for i, block in enumerate(self.sage_blocks):
+                if pending is None:
+                    aggregator_feats_data = Aggregator(center_neigh_feats_data, self.agg_func)
+                else:
+                    aggregator_feats_data = _gather_aggregate(pending[0], pending[1], self.agg_func)
+                feats_data = block(center_feats_data, aggregator_feats_data)
+                if i != self.num_layers - 1:
+                    cm = center_nodes_map[i]
+                    nm = center_neigh_nodes_map[i]
+                    center_feats_data = _gather(feats_data, cm[cm != -1])
+                    pending = (feats_data, nm[nm[:, 0] != -1, :])
+            classes = None
+            if not self.Unsupervised:
+                classes = self.dense(feats_data)
+            return feats_data, classes
+        center_feats_data, _ = self(center_feats_data, center_nodes_map, center_neigh_feats_data,
+                                    center_neigh_nodes_map, None, None, None, None, None)
+        contexts_negatives_feats_data, _ = self(contexts_negatives_feats_data, contexts_negatives_nodes_map,
+                                                contexts_negatives_neigh_feats_data,
+                                                contexts_negatives_neigh_nodes_map, None, None, None, None, None)
+        contexts_negatives_feats_data = contexts_negatives_feats_data.reshape(*contexts_negatives_shape, -1)
+        return center_feats_data, torch.bmm(center_feats_data.unsqueeze(1), contexts_negatives_feats_data.permute(0, 2, 1))

@@ -92,3 +92,170 @@ def spmm(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None) -> torc
     if torch.is_grad_enabled() and (x.requires_grad or (bias is not None and bias.requires_grad)):
         return _SpmmFn.apply(x, bias, g)
     return spmm_forward(g, x, bias)
+
+
+# ---------------------------------------------------------------------- GAT
+GAT_DENSE = 0   # GraphAttentionLayer   (GAT/models/layers.py:22-37)
+GAT_SPARSE = 1  # SpGraphAttentionLayer (GAT/models/layers.py:94-131)
+
+
+def gat_logits(wh: torch.Tensor, heads: int, fh: int, a_src: torch.Tensor,
+               a_dst: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """el[n,h] = a_src[h].Wh[n,h], er[n,h] = a_dst[h].Wh[n,h] (one HIP launch)."""
+    _require_device(wh, a_src, a_dst)
+    wh = _rows_f32(wh, "Wh")
+    n = wh.shape[0]
+    if wh.shape[1] != heads * fh or a_src.numel() != heads * fh or a_dst.numel() != heads * fh:
+        raise ValueError("Wh / attention vectors do not match heads * fh")
+    el = torch.empty((n, heads), dtype=torch.float32, device=wh.device)
+    er = torch.empty((n, heads), dtype=torch.float32, device=wh.device)
+    lib = _lib.load()
+    _lib.check(lib.gnn_gat_logits_f32(wh.data_ptr(), wh.stride(0), n, heads, fh,
+                                      a_src.contiguous().data_ptr(), a_dst.contiguous().data_ptr(),
+                                      el.data_ptr(), er.data_ptr(), heads,
+                                      _lib.stream_handle(wh.device)), "gnn_gat_logits_f32")
+    return el, er
+
+
+def col_mean(x: torch.Tensor) -> torch.Tensor:
+    """Mean over rows (double accumulation) -- the dense GAT layer's edgeless-row output."""
+    _require_device(x)
+    x = _rows_f32(x, "x")
+    lib = _lib.load()
+    scratch = torch.empty(max(8, int(lib.gnn_col_mean_scratch_bytes(x.shape[0], x.shape[1]))),
+                          dtype=torch.uint8, device=x.device)
+    out = torch.empty(x.shape[1], dtype=torch.float32, device=x.device)
+    _lib.check(lib.gnn_col_mean_f32(x.data_ptr(), x.stride(0), x.shape[0], x.shape[1],
+                                    out.data_ptr(), scratch.data_ptr(),
+                                    _lib.stream_handle(x.device)), "gnn_col_mean_f32")
+    return out
+
+
+def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tensor, heads: int,
+                  fh: int, negative_slope: float, mode: int, activation: str | None = None,
+                  dropout_p: float = 0.0, seed: int = 0, seg_len: int | None = None,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+    """Fused edge-softmax + neighbour aggregation for all heads (one HIP launch + fix-up)."""
+    _require_device(g.rowptr, wh, el, er, out)
+    wh = _rows_f32(wh, "Wh")
+    n = g.n_rows
+    if wh.shape[0] != g.n_cols or wh.shape[1] != heads * fh:
+        raise ValueError("Wh must be [n_cols, heads * fh]")
+    if g.n_rows != g.n_cols:
+        raise ValueError("GAT attention needs a square adjacency")
+    el = el.contiguous()
+    er = er.contiguous()
+    if el.shape != (n, heads) or er.shape != (n, heads):
+        raise ValueError("el / er must be [N, heads]")
+    feat = heads * fh
+    if out is None:
+        out = torch.empty((n, feat), dtype=torch.float32, device=wh.device)
+    if n == 0:
+        return out
+    fill = None
+    if mode == GAT_DENSE and g.has_empty_rows():
+        fill = col_mean(wh)
+    plan = g.plan(seg_len if seg_len is not None else seg_len_for(feat))
+    partial = None
+    if plan.n_seg:
+        partial = torch.empty((plan.n_seg, feat + 2 * heads), dtype=torch.float32,
+                              device=wh.device)
+    lib = _lib.load()
+    rc = lib.gnn_gat_csr_f32(
+        g.rowptr.data_ptr(), g.col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
+        el.data_ptr(), er.data_ptr(), heads, float(negative_slope), int(mode), _lib.ptr(fill),
+        float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), out.stride(0),
+        plan.seg_len, _lib.ptr(plan.seg_row), _lib.ptr(plan.seg_begin), plan.n_seg,
+        _lib.ptr(plan.long_row), plan.long_seg_ptr.data_ptr(), plan.n_long, _lib.ptr(partial),
+        _ACT_FLAGS[activation], _lib.stream_handle(wh.device))
+    _lib.check(rc, "gnn_gat_csr_f32")
+    return out
+
+
+# ---------------------------------------------------------------- GraphSAGE
+SAGE_MODES = {"MEAN": 0, "MAX": 1}
+
+
+def _sage_out(M, F, mode, dev):
+    dt = torch.float32 if mode == 0 else torch.int64
+    return torch.empty((M, F), dtype=dt, device=dev)
+
+
+def sage_aggregate(neigh: torch.Tensor, agg_func: str = "MEAN") -> torch.Tensor:
+    """Aggregator over a pre-gathered [M, k, F] tensor (GraphSAGE/graph_utils.py:4-11)."""
+    if agg_func not in SAGE_MODES:
+        print('请选择合适的聚合函数')  # the reference's message before its bare raise
+        raise RuntimeError(f"unknown agg_func {agg_func!r}")
+    _require_device(neigh)
+    if neigh.dtype != torch.float32 or neigh.dim() != 3:
+        raise TypeError("neigh_feat must be float32 [M, k, F]")
+    if neigh.stride(2) != 1:
+        neigh = neigh.contiguous()
+    M, k, F = neigh.shape
+    mode = SAGE_MODES[agg_func]
+    if k == 0:
+        if mode == 1:
+            raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
+        return torch.full((M, F), float("nan"), device=neigh.device)
+    out = _sage_out(M, F, mode, neigh.device)
+    lib = _lib.load()
+    _lib.check(lib.gnn_sage_aggregate_f32(neigh.data_ptr(), neigh.stride(1), neigh.stride(0), M, k,
+                                          F, mode, out.data_ptr(), F,
+                                          _lib.stream_handle(neigh.device)),
+               "gnn_sage_aggregate_f32")
+    return out
+
+
+def _check_err(err: torch.Tensor, what: str) -> None:
+    if int(err.item()) != 0:
+        raise IndexError(f"{what}: index out of range in self")
+
+
+def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str = "MEAN",
+                          check: bool = True) -> torch.Tensor:
+    """Aggregator(torch.embedding(table, idx)) fused: [M, k] int64 indices into table [n, F]."""
+    if agg_func not in SAGE_MODES:
+        raise RuntimeError(f"unknown agg_func {agg_func!r}")
+    _require_device(table, idx)
+    table = _rows_f32(table, "table")
+    if idx.dim() != 2:
+        raise ValueError("idx must be [M, k]")
+    idx = idx.to(torch.int64)
+    if idx.stride(1) != 1:
+        idx = idx.contiguous()
+    M, k = idx.shape
+    F = table.shape[1]
+    mode = SAGE_MODES[agg_func]
+    if k == 0:
+        if mode == 1:
+            raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
+        return torch.full((M, F), float("nan"), device=table.device)
+    out = _sage_out(M, F, mode, table.device)
+    err = torch.zeros(1, dtype=torch.int32, device=table.device)
+    lib = _lib.load()
+    _lib.check(lib.gnn_sage_gather_aggregate_f32(
+        table.data_ptr(), table.stride(0), table.shape[0], idx.data_ptr(), idx.stride(0), M, k, F,
+        mode, out.data_ptr(), F, err.data_ptr(), _lib.stream_handle(table.device)),
+        "gnn_sage_gather_aggregate_f32")
+    if check:
+        _check_err(err, "sage_gather_aggregate")
+    return out
+
+
+def gather_rows(x: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = None,
+                check: bool = True) -> torch.Tensor:
+    """out[i] = x[idx[i]] (torch.embedding semantics, one HIP launch)."""
+    _require_device(x, idx, out)
+    x = _rows_f32(x, "x")
+    idx = idx.to(torch.int64).contiguous().view(-1)
+    n, F = idx.numel(), x.shape[1]
+    if out is None:
+        out = torch.empty((n, F), dtype=torch.float32, device=x.device)
+    err = torch.zeros(1, dtype=torch.int32, device=x.device)
+    lib = _lib.load()
+    _lib.check(lib.gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0], idx.data_ptr(), n, F,
+                                       out.data_ptr(), out.stride(0), err.data_ptr(),
+                                       _lib.stream_handle(x.device)), "gnn_gather_rows_f32")
+    if check:
+        _check_err(err, "gather_rows")
+    return out

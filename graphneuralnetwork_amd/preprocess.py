@@ -43,17 +43,21 @@ def gcn_normalized_csr(src, dst, n: int, device=None) -> CsrGraph:
     w = torch.zeros(key.numel(), dtype=torch.float64, device=dev)
     w.scatter_reduce_(0, inv, v2, reduce="amax", include_self=False)
     del k2, v2, inv
-    # + I (float64)
+    # + I (float64): every key is unique on both sides, so plain scatters (no atomics)
     diag = torch.arange(n, dtype=torch.int64, device=dev) * (n + 1)
-    k3 = torch.cat([key, diag])
-    v3 = torch.cat([w, torch.ones(n, dtype=torch.float64, device=dev)])
-    del key, w, diag
-    key, inv = torch.unique(k3, return_inverse=True)
-    w = torch.zeros(key.numel(), dtype=torch.float64, device=dev).index_add_(0, inv, v3)
-    del k3, v3, inv
-    r, c = key // n, key % n
-    del key
-    rowsum = torch.zeros(n, dtype=torch.float64, device=dev).index_add_(0, r, w)
+    merged = torch.unique(torch.cat([key, diag]))
+    w3 = torch.zeros(merged.numel(), dtype=torch.float64, device=dev)
+    w3[torch.searchsorted(merged, key)] = w
+    pd = torch.searchsorted(merged, diag)
+    w3[pd] = w3[pd] + 1.0
+    del key, w, diag, pd
+    r, c = merged // n, merged % n
+    del merged
+    # rowsum(A_til): keys are row-major sorted -> one segmented sum per row
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(torch.bincount(r, minlength=n), 0, out=offs[1:])
+    rowsum = torch.segment_reduce(w3, "sum", offsets=offs)
+    w = w3
     d = rowsum.pow(-0.5)
     d[torch.isinf(d)] = 0.0
     # transpose: output row = c, gathered col = r

@@ -86,6 +86,83 @@ int gnn_spmm_plan_fill(const int64_t* rowptr, int64_t n_rows, int64_t seg_len, i
                        int64_t* seg_begin, int32_t* long_row, int32_t* long_seg_ptr,
                        void* scratch, void* stream);
 
+/*
+ * GAT attention logits for all heads: el[n,h] = a_src[h,:] . Wh[n, h*fh:(h+1)*fh],
+ * er[n,h] = a_dst[h,:] . Wh[n, h*fh:(h+1)*fh]  (a_src/a_dst: [heads*fh]).
+ *
+ * Replaces the a-products of GAT/models/layers.py:25-26 (dense: a[:F] pairs with
+ * the row node, a[F:] with the column node) and :105-108 (sparse: a[:, :F] / a[:, F:]).
+ */
+int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t heads, int64_t fh,
+                       const float* a_src, const float* a_dst, float* el, float* er, int64_t lde,
+                       void* stream);
+
+/*
+ * GAT edge-softmax + neighbour aggregation over CSR, all heads in one pass:
+ *   out[i, h*fh+f] = act( sum_{j in row i} p_ijh * Wh[j, h*fh+f] / sum_j p_ijh )
+ * mode 0 (dense layer, GAT/models/layers.py:22-37):
+ *     p_ijh = exp(LeakyReLU(el_ih + er_jh) - max_j(...))   -- softmax(dim=1)
+ *     rows with no edge -> empty_row_fill[h*fh+f] (the reference's uniform
+ *     average over all N rows; NULL -> NaN)
+ * mode 1 (sparse layer, GAT/models/layers.py:94-131):
+ *     p_ijh = exp(-LeakyReLU(el_ih + er_jh))  -- no max subtraction (reference arithmetic)
+ *     rows with no edge -> 0/0 = NaN (the reference then fails its isnan assert)
+ * dropout_p > 0 (training) drops numerator weights with a hash RNG keyed by
+ * (dropout_seed, edge, head) and rescales by 1/(1-p), as F.dropout does.
+ * Long rows use the row-split plan of gnn_spmm_plan_* with
+ * partial[n_seg * (heads*fh + 2*heads)].  flags: GNN_EPI_ELU for concat=True.
+ */
+int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows, const float* wh,
+                    int64_t ldw, int64_t heads, int64_t fh, const float* el, const float* er,
+                    int64_t lde, float negative_slope, int32_t mode, const float* empty_row_fill,
+                    float dropout_p, uint64_t dropout_seed, float* out, int64_t ldo,
+                    int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin,
+                    int64_t n_seg, const int32_t* long_row, const int32_t* long_seg_ptr,
+                    int64_t n_long, float* partial, uint32_t flags, void* stream);
+
+/*
+ * Column mean of x[n_rows, feat] (double accumulation, deterministic): the dense
+ * GAT layer's output for an edgeless row (uniform softmax over all N nodes,
+ * GAT/models/layers.py:29-32). scratch: gnn_col_mean_scratch_bytes(n_rows, feat).
+ */
+int64_t gnn_col_mean_scratch_bytes(int64_t n_rows, int64_t feat);
+int gnn_col_mean_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t feat, float* out,
+                     void* scratch, void* stream);
+
+/* ---- GraphSAGE aggregation modes ---- */
+#define GNN_SAGE_MEAN 0   /* torch.mean(neigh_feat, dim=1)               -> fp32 out  */
+#define GNN_SAGE_ARGMAX 1 /* torch.argmax(neigh_feat, dim=1): first max,
+                             NaN counts as the maximum                   -> int64 out */
+
+/*
+ * GraphSAGE Aggregator over a pre-gathered neighbour tensor
+ *   neigh[m, j, f] at neigh + m*ld_m + j*ld_k + f   (m < M, j < k, f < feat)
+ * Replaces Aggregator(neigh_feat, agg_func) at GraphSAGE/graph_utils.py:4-11.
+ * out: fp32 [M, ldo] (MEAN) or int64 [M, ldo] (ARGMAX). k == 0 -> GNN_E_UNSUPPORTED.
+ */
+int gnn_sage_aggregate_f32(const float* neigh, int64_t ld_k, int64_t ld_m, int64_t M, int64_t k,
+                           int64_t feat, int32_t mode, void* out, int64_t ldo, void* stream);
+
+/*
+ * Fused gather + Aggregator: out[m] = Aggregator(table[idx[m, 0..k)]) without
+ * materialising the [M, k, feat] tensor the reference builds with
+ * torch.embedding (GraphSAGE/GraphSAGE.py:47-49 + graph_utils.py:6,8).
+ * idx int64 [M, ldi]; an index outside [0, n_table) sets *err_flag (device int32,
+ * OR-ed with 1) and is skipped -- the caller raises IndexError like torch.embedding.
+ */
+int gnn_sage_gather_aggregate_f32(const float* table, int64_t ldt, int64_t n_table,
+                                  const int64_t* idx, int64_t ldi, int64_t M, int64_t k,
+                                  int64_t feat, int32_t mode, void* out, int64_t ldo,
+                                  int32_t* err_flag, void* stream);
+
+/*
+ * Row gather out[i, :] = x[idx[i], :] (torch.embedding at GraphSAGE/GraphSAGE.py:47-48;
+ * also packs halo send buffers for the multi-GPU edge-cut). Out-of-range index ->
+ * *err_flag |= 1, row skipped.
+ */
+int gnn_gather_rows_f32(const float* x, int64_t ldx, int64_t n_x, const int64_t* idx, int64_t n,
+                        int64_t feat, float* out, int64_t ldo, int32_t* err_flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

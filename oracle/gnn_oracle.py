@@ -252,3 +252,46 @@ def graphsage_forward(center_feats, center_nodes_map, neigh_feats, neigh_nodes_m
 def sage_gather_aggregate(table, idx, agg_func="MEAN"):
     """Fused gather + Aggregator: Aggregator(embedding(table, idx)) (GraphSAGE/GraphSAGE.py:47-49 + graph_utils.py:6,8)."""
     return aggregator(np.asarray(table)[np.asarray(idx)], agg_func)
+
+
+def gat_csr(rowptr, col, wh, el, er, heads, fh, slope, sparse: bool, empty_fill=None):
+    """Edge-list form of both GAT layers for H heads at once, float64.
+
+    dense  (layers.py:25-32): out_i = sum_j softmax_j(LeakyReLU(el_i + er_j)) Wh_j,
+           edgeless row -> ``empty_fill`` (the uniform average over all rows);
+    sparse (layers.py:105-122): out_i = sum_j exp(-LeakyReLU(.)) Wh_j / sum_j exp(-LeakyReLU(.)).
+    Wh [N, H*fh]; el, er [N, H].  No activation.
+    """
+    wh = np.asarray(wh, np.float64).reshape(-1, heads, fh)
+    el = np.asarray(el, np.float64)
+    er = np.asarray(er, np.float64)
+    n = rowptr.size - 1
+    rows = np.repeat(np.arange(n), np.diff(rowptr))
+    col = np.asarray(col, np.int64)
+    s = _leaky(el[rows] + er[col], slope)                     # [E, H]
+    if sparse:
+        p = np.exp(-s)
+    else:
+        mx = np.full((n, heads), -np.inf)
+        np.maximum.at(mx, rows, s)
+        p = np.exp(s - mx[rows])
+    den = np.zeros((n, heads))
+    np.add.at(den, rows, p)
+    num = np.zeros((n, heads, fh))
+    np.add.at(num, rows, p[:, :, None] * wh[col])
+    with np.errstate(invalid="ignore", divide="ignore"):
+        out = num / den[:, :, None]
+    out = out.reshape(n, heads * fh)
+    if not sparse:
+        empty = np.diff(rowptr) == 0
+        if empty.any():
+            fill = wh.reshape(n, -1).mean(0) if empty_fill is None else empty_fill
+            out[empty] = fill
+    return out
+
+
+def gat_logits(wh, heads, fh, a_src, a_dst):
+    """el = a_src . Wh_i, er = a_dst . Wh_j per head (layers.py:25-26, :105-108)."""
+    w = np.asarray(wh, np.float64).reshape(-1, heads, fh)
+    return (w * np.asarray(a_src, np.float64).reshape(heads, fh)).sum(-1), \
+           (w * np.asarray(a_dst, np.float64).reshape(heads, fh)).sum(-1)

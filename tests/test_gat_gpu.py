@@ -1,0 +1,141 @@
+"""GAT fused edge-softmax + aggregation on the GPU vs the reference's golden vectors and the oracle.
+
+Tolerance: fp32 within 1e-4 relative (atol scaled by max |out|)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gnn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def close(a, b, rtol=1e-4):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    scale = max(1.0, float(np.nanmax(np.abs(b)))) if b.size else 1.0
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=2e-5 * scale)
+
+
+def _dense(g, prefix, n):
+    A = np.zeros((n, n), np.float32)
+    A[g[f"{prefix}_row"], g[f"{prefix}_col"]] = g[f"{prefix}_val"]
+    return A
+
+
+def _load_heads(model, g, kind):
+    sd = {}
+    H = g[f"{kind}_W"].shape[0]
+    for i in range(H):
+        sd[f"attentions.AttentionHead{i}.W"] = torch.from_numpy(g[f"{kind}_W"][i])
+        a = g[f"{kind}_a"][i]
+        sd[f"attentions.AttentionHead{i}.a"] = torch.from_numpy(a.reshape(-1, 1) if kind == "dense" else a.reshape(1, -1))
+    sd["out_att.W"] = torch.from_numpy(g[f"{kind}_outW"])
+    a = g[f"{kind}_outa"]
+    sd["out_att.a"] = torch.from_numpy(a.reshape(-1, 1) if kind == "dense" else a.reshape(1, -1))
+    model.load_state_dict(sd, strict=True)
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse"])
+@pytest.mark.parametrize("adj_form", ["dense", "sparse_coo"])
+def test_golden_gat_models(golden, dev, kind, adj_form):
+    from graphneuralnetwork_amd.gat import GAT, SpGAT
+    g = golden("gat")
+    n = int(g["n"])
+    A = torch.from_numpy(_dense(g, "adj", n))
+    adj = A.to(dev) if adj_form == "dense" else A.to_sparse().to(dev)
+    model = (GAT if kind == "dense" else SpGAT)(64, 8, 7, 0.6, float(g["alpha"]), 8)
+    _load_heads(model, g, kind)
+    model.to(dev).eval()
+    h = torch.from_numpy(g["h"]).to(dev)
+    with torch.no_grad():
+        logits = model(h, adj).cpu().numpy()
+        head0 = model.attentions.AttentionHead0(h, adj).cpu().numpy()
+    close(head0, g[f"{kind}_head0"])
+    close(logits, g[f"{kind}_logits"])
+
+
+def test_golden_edge_predicates_and_isolated_rows(golden, dev):
+    from graphneuralnetwork_amd.gat import GraphAttentionLayer, SpGraphAttentionLayer
+    g = golden("gat")
+    n = int(g["n"])
+    alpha = float(g["alpha"])
+    h = torch.from_numpy(g["h"]).to(dev)
+    dl = GraphAttentionLayer(64, 8, 0.0, alpha, True)
+    sl = SpGraphAttentionLayer(64, 8, 0.0, alpha, True)
+    dl.load_state_dict({"W": torch.from_numpy(g["neg_dense_W"]),
+                        "a": torch.from_numpy(g["neg_dense_a"].reshape(-1, 1))})
+    sl.load_state_dict({"W": torch.from_numpy(g["neg_sparse_W"]),
+                        "a": torch.from_numpy(g["neg_sparse_a"].reshape(1, -1))})
+    dl.to(dev).eval()
+    sl.to(dev).eval()
+    An = torch.from_numpy(_dense(g, "neg", n)).to(dev)
+    with torch.no_grad():
+        close(dl(h, An).cpu().numpy(), g["neg_dense_out"])   # edges: adj > 0
+        close(sl(h, An).cpu().numpy(), g["neg_sparse_out"])  # edges: adj != 0
+        Ai = _dense(g, "adj", n)
+        Ai[int(g["iso_row"]), :] = 0
+        Ai = torch.from_numpy(Ai).to(dev)
+        close(dl(h, Ai).cpu().numpy(), g["iso_dense_out"])   # uniform average row
+        with pytest.raises(AssertionError):                  # reference: NaN assert
+            sl(h, Ai)
+
+
+def _rand_csr(n, e, seed, hub=0):
+    rng = np.random.default_rng(seed)
+    s = np.concatenate([rng.integers(0, n, e), np.full(hub, 1)])
+    d = np.concatenate([rng.integers(0, n, e), rng.integers(0, n, hub)])
+    key = np.unique(s * n + d)
+    rowptr, col, _ = O.coo_to_csr(key // n, key % n, np.ones(key.size, np.float32), n)
+    return rowptr, col
+
+
+@pytest.mark.parametrize("heads,fh", [(8, 8), (1, 7), (3, 5), (4, 16), (12, 4), (2, 64), (1, 200)])
+@pytest.mark.parametrize("sparse", [False, True])
+@pytest.mark.parametrize("seg_len", [None, 40])
+def test_gat_aggregate_vs_oracle(dev, heads, fh, sparse, seg_len):
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_logits
+    n = 1500
+    rowptr, col = _rand_csr(n, 12 * n, heads * 100 + fh, hub=900)
+    rng = np.random.default_rng(fh)
+    wh = (rng.standard_normal((n, heads * fh)) * 0.5).astype(np.float32)
+    a_s = (rng.standard_normal(heads * fh) * 0.3).astype(np.float32)
+    a_d = (rng.standard_normal(heads * fh) * 0.3).astype(np.float32)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.ones(col.size, device=dev), n, n)
+    whd = torch.from_numpy(wh).to(dev)
+    el, er = gat_logits(whd, heads, fh, torch.from_numpy(a_s).to(dev), torch.from_numpy(a_d).to(dev))
+    el_o, er_o = O.gat_logits(wh, heads, fh, a_s, a_d)
+    close(el.cpu().numpy(), el_o)
+    close(er.cpu().numpy(), er_o)
+    out = gat_aggregate(g, whd, el, er, heads, fh, 0.2, GAT_SPARSE if sparse else GAT_DENSE,
+                        seg_len=seg_len).cpu().numpy()
+    ref = O.gat_csr(rowptr, col, wh, el.cpu().numpy(), er.cpu().numpy(), heads, fh, 0.2, sparse)
+    close(out, ref)
+
+
+def test_gat_dropout_is_seeded_and_unbiased(dev):
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.ops import GAT_DENSE, gat_aggregate
+    n, heads, fh = 400, 2, 8
+    rowptr, col = _rand_csr(n, 200 * n, 3)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.ones(col.size, device=dev), n, n)
+    wh = torch.ones(n, heads * fh, device=dev)
+    el = torch.zeros(n, heads, device=dev)
+    er = torch.zeros(n, heads, device=dev)
+    a = gat_aggregate(g, wh, el, er, heads, fh, 0.2, GAT_DENSE, dropout_p=0.5, seed=7)
+    b = gat_aggregate(g, wh, el, er, heads, fh, 0.2, GAT_DENSE, dropout_p=0.5, seed=7)
+    c = gat_aggregate(g, wh, el, er, heads, fh, 0.2, GAT_DENSE, dropout_p=0.5, seed=8)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    # uniform attention over ~200 edges, inverted dropout keeps the expectation at 1
+    assert abs(float(a.mean()) - 1.0) < 0.02
+
+
+def test_gat_forward_only_guard(dev):
+    from graphneuralnetwork_amd.gat import GraphAttentionLayer
+    layer = GraphAttentionLayer(8, 4, 0.0, 0.2).to(dev)
+    adj = torch.eye(5, device=dev)
+    with pytest.raises(NotImplementedError):
+        layer(torch.randn(5, 8, device=dev), adj)

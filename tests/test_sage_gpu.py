@@ -1,0 +1,109 @@
+"""GraphSAGE aggregation on the GPU vs the reference's golden vectors and the oracle.
+
+MEAN: fp32 within 1e-4 relative; MAX (torch.argmax int64 indices): bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gnn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def close(a, b, rtol=1e-4):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    scale = max(1.0, float(np.nanmax(np.abs(b)))) if b.size else 1.0
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=1e-5 * scale)
+
+
+def _sd(g, tag):
+    p = f"{tag}_sd_"
+    return {k[len(p):]: torch.from_numpy(v) for k, v in g.items() if k.startswith(p)}
+
+
+@pytest.mark.parametrize("tag,agg,gcn", [("mean", "MEAN", False), ("max", "MAX", False),
+                                         ("gcn", "MEAN", True)])
+def test_golden_graphsage_supervised(golden, dev, tag, agg, gcn):
+    from graphneuralnetwork_amd.graphsage import Aggregator, GraphSAGE
+    g = golden("sage")
+    F = g["feat"].shape[1]
+    net = GraphSAGE(2, F, 16, gcn, agg_func=agg, Unsupervised=False, class_size=3)
+    net.load_state_dict(_sd(g, tag), strict=True)
+    net.to(dev).eval()
+    X = [torch.from_numpy(g[f"{tag}_{k}"]).to(dev)
+         for k in ("center_feats", "nodes_map", "neigh_feats", "neigh_map")]
+    with torch.no_grad():
+        agg0 = Aggregator(X[2], agg).cpu().numpy()
+        emb, logits = net(*X, None, None, None, None, None)
+    if agg == "MAX":
+        assert agg0.dtype == np.int64
+        np.testing.assert_array_equal(agg0, g[f"{tag}_agg0"])
+    else:
+        close(agg0, g[f"{tag}_agg0"])
+    close(emb.cpu().numpy(), g[f"{tag}_emb"])
+    close(logits.cpu().numpy(), g[f"{tag}_logits"])
+
+
+def test_golden_graphsage_unsupervised(golden, dev):
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    g = golden("sage")
+    F = g["feat"].shape[1]
+    net = GraphSAGE(2, F, 16, False, agg_func="MEAN", Unsupervised=True)
+    net.load_state_dict(_sd(g, "unsup"), strict=True)
+    net.to(dev).eval()
+    X = [torch.from_numpy(g[f"unsup_X{i}"]).to(dev) for i in range(8)]
+    with torch.no_grad():
+        emb, scores = net(*X, tuple(int(v) for v in g["unsup_shape"]))
+    close(emb.cpu().numpy(), g["unsup_emb"])
+    close(scores.cpu().numpy(), g["unsup_scores"])
+
+
+@pytest.mark.parametrize("F", [1, 7, 32, 100, 128, 256, 600, 2050])
+@pytest.mark.parametrize("k", [1, 3, 10, 25, 70])
+def test_pregathered_mean_and_argmax(dev, F, k):
+    from graphneuralnetwork_amd.ops import sage_aggregate
+    rng = np.random.default_rng(F * 100 + k)
+    M = 300 if F < 1000 else 40
+    x = (rng.integers(-6, 7, size=(M, k, F)) / 4).astype(np.float32)  # many ties
+    x[0, min(1, k - 1), 0] = np.nan
+    if k > 2:
+        x[1, 2, : min(F, 3)] = np.nan
+        x[1, k - 1, : min(F, 3)] = np.nan
+    xd = torch.from_numpy(x).to(dev)
+    close(sage_aggregate(xd, "MEAN").cpu().numpy()[2:], O.aggregator(x, "MEAN")[2:])
+    got = sage_aggregate(xd, "MAX").cpu().numpy()
+    np.testing.assert_array_equal(got, O.aggregator(x, "MAX"))
+    np.testing.assert_array_equal(got, torch.argmax(torch.from_numpy(x), dim=1).numpy())
+
+
+@pytest.mark.parametrize("F", [16, 128, 300])
+def test_fused_gather_aggregate(dev, F):
+    from graphneuralnetwork_amd.ops import gather_rows, sage_gather_aggregate
+    rng = np.random.default_rng(F)
+    n, M, k = 5000, 2000, 10
+    table = (rng.integers(-8, 9, size=(n, F)) / 8).astype(np.float32)
+    idx = rng.integers(0, n, size=(M, k))
+    td = torch.from_numpy(table).to(dev)
+    idd = torch.from_numpy(idx).to(dev)
+    close(sage_gather_aggregate(td, idd, "MEAN").cpu().numpy(), O.sage_gather_aggregate(table, idx, "MEAN"))
+    np.testing.assert_array_equal(sage_gather_aggregate(td, idd, "MAX").cpu().numpy(),
+                                  O.sage_gather_aggregate(table, idx, "MAX"))
+    np.testing.assert_array_equal(gather_rows(td, idd[:, 0]).cpu().numpy(), table[idx[:, 0]])
+
+
+def test_out_of_range_indices_raise(dev):
+    from graphneuralnetwork_amd.ops import gather_rows, sage_gather_aggregate
+    t = torch.zeros(10, 8, device=dev)
+    with pytest.raises(IndexError):
+        sage_gather_aggregate(t, torch.tensor([[1, 10]], device=dev))
+    with pytest.raises(IndexError):
+        gather_rows(t, torch.tensor([-1], device=dev))
+
+
+def test_mean_backward(dev):
+    from graphneuralnetwork_amd.graphsage import Aggregator
+    x = torch.randn(5, 4, 3, device=dev, requires_grad=True)
+    y = Aggregator(x, "MEAN")
+    y.backward(torch.ones_like(y))
+    assert torch.allclose(x.grad, torch.full_like(x, 0.25))
