@@ -60,13 +60,15 @@ def build_graph(nodes: int, edges: int, dev, rank: int, world: int):
     from graphneuralnetwork_amd.rmat import rmat_edges
     t0 = time.time()
     if world > 1:
-        # rank 0 draws the edge list (numpy recipe), every rank receives it over RCCL
+        # rank 0 draws the edge list (numpy recipe), every rank receives it (RCCL broadcast)
+        bdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
         if rank == 0:
             s, d = rmat_edges(nodes, edges, 0)
-            buf = torch.from_numpy(np.stack([s, d])).to(dev)
+            buf = torch.from_numpy(np.stack([s, d])).to(bdev)
         else:
-            buf = torch.empty((2, edges), dtype=torch.int64, device=dev)
+            buf = torch.empty((2, edges), dtype=torch.int64, device=bdev)
         dist.broadcast(buf, 0)
+        buf = buf.to(dev)
         s, d = buf[0], buf[1]
     else:
         s, d = rmat_edges(nodes, edges, 0)
@@ -111,6 +113,10 @@ def main():
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo = multi-rank rehearsal (host-staged exchange), never for numbers")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC traffic summary (tools/pmc_traffic.py); default profiles/traffic_<workload>_F<feat>.json")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,10 +124,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = int(os.environ.get("GNN_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from graphneuralnetwork_amd import _lib
     from graphneuralnetwork_amd.ops import spmm_forward
@@ -147,6 +157,9 @@ def main():
         X = torch.randn(part.n_own, F, device=dev, generator=gen)
         runner = EdgeCutSpmm(part, F, dev)
         step = lambda: runner(X, bias)  # noqa: E731
+        log(f"[bench] rank0 partition: rows {part.n_own} nnz {part.nnz} (interior "
+            f"{part.interior.nnz}, halo {part.halo.nnz}) halo rows {part.n_halo} send rows "
+            f"{part.send_idx.numel()}")
         rows_local, nnz_local = part.n_own, part.nnz
         bytes_local = algorithmic_bytes(nnz_local, rows_local, F)
         halo_rows = part.n_halo
@@ -188,6 +201,14 @@ def main():
     kern_ms = statistics.mean(step_ms)
     achieved = bytes_local / (kern_ms / 1e3) / 1e9
 
+    traffic = None
+    tpath = Path(args.traffic_json) if args.traffic_json else \
+        ROOT / "profiles" / f"traffic_{args.workload}_F{F}.json"
+    if world == 1 and tpath.exists():
+        try:
+            traffic = json.loads(tpath.read_text())
+        except ValueError:
+            traffic = None
     if rank == 0:
         res = {
             "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
@@ -201,7 +222,11 @@ def main():
                        "nnz_rank0": nnz_local, "halo_rows_rank0": halo_rows},
             "achieved_GBps": achieved,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                         "traffic": traffic["traffic_bytes"] if traffic else None,
+                         "traffic_source": (str(tpath.relative_to(ROOT)) + ": rocprofv3 --pmc "
+                                            "FETCH_SIZE x2 + WRITE_SIZE of this command")
+                         if traffic else None,
                          "kernel": "spmm_csr_kernel (+ spmm_fixup_kernel), per-step HIP events",
                          "algorithmic_bytes_per_launch": bytes_local,
                          "avg_launch_ms": kern_ms, "min_launch_ms": min(step_ms)},

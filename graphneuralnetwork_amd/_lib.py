@@ -61,6 +61,7 @@ SIGNATURES: dict[str, tuple] = {
 
 EPI_RELU = 1
 EPI_ELU = 2
+EPI_ACCUMULATE = 4
 
 
 def library_path() -> Path:

@@ -95,8 +95,9 @@ __device__ __forceinline__ void store_row(float* __restrict__ out, const float* 
     const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
     if (f >= feat) continue;
     typename Vec<VW>::T r = acc[ch];
+    if (flags & GNN_EPI_ACCUMULATE) r += vload<VW>(out + f);
     if (bias != nullptr) r += vload<VW>(bias + f);
-    if (flags != 0) {
+    if (flags & (GNN_EPI_RELU | GNN_EPI_ELU)) {
 #pragma unroll
       for (int i = 0; i < VW; ++i) vset(r, i, act_apply(vget(r, i), flags));
     }
@@ -252,7 +253,7 @@ extern "C" int gnn_spmm_csr_f32(const int64_t* rowptr, const int32_t* col, const
       (seg_row == nullptr || seg_begin == nullptr || long_row == nullptr ||
        long_seg_ptr == nullptr || partial == nullptr || n_long == 0 || n_seg == 0))
     return GNN_E_ARG;
-  if (flags & ~(GNN_EPI_RELU | GNN_EPI_ELU)) return GNN_E_ARG;
+  if (flags & ~(GNN_EPI_RELU | GNN_EPI_ELU | GNN_EPI_ACCUMULATE)) return GNN_E_ARG;
 
   const bool vec4 = (feat % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) && aligned_to(x, 16) &&
                     aligned_to(y, 16) && (bias == nullptr || aligned_to(bias, 16)) &&

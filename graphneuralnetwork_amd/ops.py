@@ -33,8 +33,11 @@ def _rows_f32(x: torch.Tensor, name: str) -> torch.Tensor:
 
 def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
                  activation: str | None = None, out: torch.Tensor | None = None,
-                 seg_len: int | None = None) -> torch.Tensor:
+                 seg_len: int | None = None, accumulate: bool = False) -> torch.Tensor:
     """Y = A.X (+ bias) (act) with A in CSR -- the GCN aggregation (GCN/GCN.py:43-45).
+
+    ``accumulate=True`` adds into ``out`` (Y = out + A.X ...): the halo pass of
+    the multi-GPU edge-cut aggregation.
 
     ``seg_len`` overrides the long-row threshold (rows with more edges are split
     across wavefronts); by default it is sized from the feature width.
@@ -52,19 +55,24 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
         out = torch.empty((g.n_rows, feat), dtype=torch.float32, device=x.device)
     elif out.shape != (g.n_rows, feat) or out.stride(1) != 1 or out.dtype != torch.float32:
         raise ValueError("out must be float32 [n_rows, features] with unit column stride")
+    if accumulate and out is None:
+        raise ValueError("accumulate=True needs `out`")
     if g.n_rows == 0 or feat == 0:
         return out
     plan = g.plan(seg_len if seg_len is not None else seg_len_for(feat))
     partial = None
     if plan.n_seg:
         partial = torch.empty((plan.n_seg, feat), dtype=torch.float32, device=x.device)
+    if x.numel() == 0:  # no column to gather from (e.g. an empty halo): never read
+        x = torch.empty((1, feat), dtype=torch.float32, device=x.device)
     lib = _lib.load()
     rc = lib.gnn_spmm_csr_f32(
         g.rowptr.data_ptr(), g.col.data_ptr(), g.val.data_ptr(), g.n_rows,
         x.data_ptr(), x.stride(0), feat, _lib.ptr(bias), out.data_ptr(), out.stride(0),
         plan.seg_len, _lib.ptr(plan.seg_row), _lib.ptr(plan.seg_begin), plan.n_seg,
         _lib.ptr(plan.long_row), plan.long_seg_ptr.data_ptr(), plan.n_long, _lib.ptr(partial),
-        _ACT_FLAGS[activation], _lib.stream_handle(x.device))
+        _ACT_FLAGS[activation] | (_lib.EPI_ACCUMULATE if accumulate else 0),
+        _lib.stream_handle(x.device))
     _lib.check(rc, "gnn_spmm_csr_f32")
     return out
 

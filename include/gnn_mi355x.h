@@ -38,6 +38,8 @@ extern "C" {
 /* ---- epilogue flags ---- */
 #define GNN_EPI_RELU 1u /* y = max(y, 0) after the bias add                          */
 #define GNN_EPI_ELU 2u  /* y = y > 0 ? y : expm1(y)   (F.elu, alpha = 1)             */
+#define GNN_EPI_ACCUMULATE 4u /* SpMM only: y = y_old + A.X (+ bias) (act) -- second pass
+                                 of a split (interior + halo) aggregation             */
 
 /* Library version, e.g. 100 for 0.1.0. */
 int gnn_version(void);

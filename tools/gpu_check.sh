@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU-box session: gpu tests, bench, rocprofv3 kernel-trace summary.
+# One GPU-box session. Usage: tools/gpu_check.sh <mode>...   modes: tests bench bench_ns prof pmc
 # Each GPU step has its own time limit; a crash/timeout (exit >1) ends the script.
 set -u
 OUT=${OUT:-gpurun_out}
@@ -11,17 +11,19 @@ step() {  # step <name> <timeout> <cmd...>
   timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"
-  tail -n 25 "$OUT/$name.log"
+  tail -n ${TAILN:-25} "$OUT/$name.log"
   if [ $rc -gt 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-MODE=${1:-all}
-if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
-fi
-if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  step bench 600 python bench.py --steps 20 --warmup 5
-fi
-if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-  step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
-fi
+for MODE in "$@"; do
+  case $MODE in
+    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    testsk) step pytest_gpu_k 900 python -m pytest tests -m gpu -q -p no:cacheprovider -k "${K:-spmm}" ;;
+    bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench_ns) step bench_ns 900 python bench.py --steps 20 --warmup 5 --workload ns ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
+         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    *) echo "unknown mode $MODE"; exit 2 ;;
+  esac
+done
