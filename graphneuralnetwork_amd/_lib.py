@@ -57,6 +57,8 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_sage_gather_aggregate_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
                                                      _i32, _vp, _i64, _vp, _vp]),
     "gnn_gather_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
+    "gnn_sample_neighbors": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, ctypes.c_uint64, _vp,
+                                            _vp, _vp]),
 }
 
 EPI_RELU = 1

@@ -1,0 +1,88 @@
+// sample.hip -- GraphSAGE neighbour sampling on gfx950 (the "next" row of SURVEY 8f).
+//
+// Restates get_layer_adj_nodes' per-node draw (GraphSAGE/data_utils.py:89-94):
+//   deg >  k : random.sample(neighs, k)   -- k distinct neighbours (no replacement)
+//   deg <= k : random.choices(neighs, k)  -- k draws with replacement
+//   deg == 0 : the reference raises IndexError (random.choices of an empty list)
+// for a whole frontier at once, one thread per frontier node, with a
+// counter-based hash RNG keyed by (seed, node, draw) instead of CPython's
+// Mersenne Twister (the reference sampler is unseeded, so only the
+// distribution -- not the exact draw -- is reproducible).
+// Without replacement uses Robert Floyd's algorithm: k iterations, each a
+// uniform draw and a membership test against the <= k picks so far.
+#include "common.hpp"
+
+namespace gnn {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// uniform integer in [0, n) (n < 2^32 on this path; Lemire's multiply-shift)
+__device__ __forceinline__ int64_t uniform_below(uint64_t seed, int64_t node, int64_t draw, int64_t n) {
+  const uint64_t r = mix64(seed ^ mix64(static_cast<uint64_t>(node) * 0x100000001b3ull +
+                                        static_cast<uint64_t>(draw)));
+  if (n <= 0xffffffffll) return static_cast<int64_t>(((r >> 32) * static_cast<uint64_t>(n)) >> 32);
+  return static_cast<int64_t>(r % static_cast<uint64_t>(n));
+}
+
+constexpr int kMaxFanout = 256;
+
+__global__ __launch_bounds__(256) void sample_kernel(const int64_t* __restrict__ rowptr,
+                                                     const int32_t* __restrict__ col,
+                                                     int64_t n_graph,
+                                                     const int64_t* __restrict__ nodes, int64_t n,
+                                                     int64_t k, uint64_t seed,
+                                                     int64_t* __restrict__ out,
+                                                     int32_t* __restrict__ err) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t v = nodes[i];
+  int64_t* o = out + i * k;
+  if (v < 0 || v >= n_graph) {
+    atomicOr(err, 2);
+    for (int64_t j = 0; j < k; ++j) o[j] = -1;
+    return;
+  }
+  const int64_t b = rowptr[v];
+  const int64_t deg = rowptr[v + 1] - b;
+  if (deg == 0) {
+    atomicOr(err, 1);
+    for (int64_t j = 0; j < k; ++j) o[j] = -1;
+    return;
+  }
+  if (deg <= k) {  // random.choices: k independent draws
+    for (int64_t j = 0; j < k; ++j) o[j] = col[b + uniform_below(seed, v, j, deg)];
+    return;
+  }
+  // random.sample: Floyd -- positions chosen so far live in o[] (as offsets, then mapped)
+  int64_t cnt = 0;
+  for (int64_t j = deg - k; j < deg; ++j) {
+    const int64_t t = uniform_below(seed, v, j, j + 1);
+    bool seen = false;
+    for (int64_t q = 0; q < cnt; ++q) seen |= (o[q] == t);
+    o[cnt++] = seen ? j : t;
+  }
+  for (int64_t j = 0; j < k; ++j) o[j] = col[b + o[j]];
+}
+
+}  // namespace gnn
+
+using namespace gnn;
+
+extern "C" int gnn_sample_neighbors(const int64_t* rowptr, const int32_t* col, int64_t n_graph,
+                                    const int64_t* nodes, int64_t n, int64_t k, uint64_t seed,
+                                    int64_t* out, int32_t* err_flag, void* stream) {
+  if (n < 0 || k < 0 || n_graph < 0 || k > kMaxFanout) return GNN_E_ARG;
+  if (n == 0 || k == 0) return GNN_OK;
+  if (!rowptr || !col || !nodes || !out || !err_flag) return GNN_E_ARG;
+  const int64_t blocks = (n + 255) / 256;
+  if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
+  hipLaunchKernelGGL(sample_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), rowptr, col, n_graph, nodes, n, k, seed, out,
+                     err_flag);
+  return launch_status();
+}

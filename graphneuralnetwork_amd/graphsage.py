@@ -17,11 +17,25 @@ Hot path on gfx950:
 """
 from __future__ import annotations
 
+from typing import NamedTuple
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 from .ops import gather_rows, sage_aggregate, sage_gather_aggregate
+
+
+class Gathered(NamedTuple):
+    """A feature tensor given as (table, index): ``table[index]`` without materialising it.
+
+    Accepted by ``GraphSAGE.forward`` in place of the pre-gathered
+    ``center_feats_data`` ([M] index) / ``center_neigh_feats_data`` ([M, k] index)
+    the reference's collate_fn builds with torch.embedding
+    (GraphSAGE/data_utils.py:161-162); see ``sampler.sample_batch``.
+    """
+    table: torch.Tensor
+    index: torch.Tensor
 
 
 class _MeanAgg(torch.autograd.Function):
@@ -72,6 +86,8 @@ class _GatherRows(torch.autograd.Function):
 
 def Aggregator(neigh_feat, agg_func='MEAN'):
     """GraphSAGE/graph_utils.py:4-11 on the device ('MEAN' -> fp32, 'MAX' -> int64 argmax)."""
+    if isinstance(neigh_feat, Gathered):
+        return _gather_aggregate(neigh_feat.table, neigh_feat.index, agg_func)
     if agg_func == 'MEAN' and torch.is_grad_enabled() and neigh_feat.requires_grad:
         return _MeanAgg.apply(neigh_feat)
     return sage_aggregate(neigh_feat, agg_func)
@@ -136,6 +152,8 @@ class GraphSAGE(nn.Module):
         if contexts_negatives_feats_data is None:
             pending = None  # (table, index map) of a fused gather-aggregate
             feats_data = None
+            if isinstance(center_feats_data, Gathered):
+                center_feats_data = _gather(center_feats_data.table, center_feats_data.index)
             for i, block in enumerate(self.sage_blocks):
                 if pending is None:
                     aggregator_feats_data = Aggregator(center_neigh_feats_data, self.agg_func)

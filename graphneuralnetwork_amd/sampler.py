@@ -1,0 +1,98 @@
+"""Device-side GraphSAGE mini-batch sampling (reference: GraphSAGE/data_utils.py:82-162).
+
+The reference's ``collate_fn`` samples on the host with Python sets and
+``random``, needs one fanout for every layer (its maps are stacked with
+``torch.tensor``) and materialises every neighbour feature row with
+``torch.embedding``.  Here the frontier of a batch is built on the device:
+
+    nb0  = sample(adj, seeds, fanouts[0])             # [B, k0]   (gnn_sample_neighbors)
+    S1   = unique(seeds ++ nb0)                        # layer-0 centre nodes (sorted ids)
+    nb1  = sample(adj, S1, fanouts[1])                 # [|S1|, k1] global ids
+    maps = positions of seeds / nb0 inside S1          # the reference's -1-free index maps
+
+and the batch is handed to ``GraphSAGE.forward`` as ``Gathered`` (table, index)
+pairs, so no [M, k, F] neighbour tensor is ever written: the layer-0
+aggregation gathers straight from the feature table (gnn_sage_gather_aggregate_f32).
+Per-hop fanouts ([25, 10]) are supported.  The reference's set iteration order
+and Mersenne-Twister draws are not reproduced (it is unseeded); the sampled
+distribution is (tests/test_sampler_gpu.py).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .graph import CsrGraph
+from .graphsage import Gathered
+
+
+def sample_neighbors(adj: CsrGraph, nodes: torch.Tensor, k: int, seed: int = 0) -> torch.Tensor:
+    """[len(nodes), k] int64 sampled neighbour ids (random.sample / random.choices rule)."""
+    if not adj.rowptr.is_cuda:
+        raise RuntimeError("sampling runs on the ROCm device only (no CPU fallback)")
+    nodes = nodes.to(device=adj.device, dtype=torch.int64).contiguous()
+    out = torch.empty((nodes.numel(), k), dtype=torch.int64, device=adj.device)
+    err = torch.zeros(1, dtype=torch.int32, device=adj.device)
+    lib = _lib.load()
+    _lib.check(lib.gnn_sample_neighbors(adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.n_rows,
+                                        nodes.data_ptr(), nodes.numel(), k,
+                                        int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(),
+                                        err.data_ptr(), _lib.stream_handle(adj.device)),
+               "gnn_sample_neighbors")
+    e = int(err.item())
+    if e & 2:
+        raise IndexError("sample_neighbors: node id out of range")
+    if e & 1:  # random.choices(list(set()), k) in the reference
+        raise IndexError("Cannot choose from an empty sequence")
+    return out
+
+
+@dataclass
+class SampledBatch:
+    seeds: torch.Tensor        # [B] global ids
+    frontier: torch.Tensor     # S1 [M] global ids (sorted), layer-0 centres
+    frontier_nbrs: torch.Tensor  # [M, k1] global ids (index the feature table)
+    center_map: torch.Tensor   # [B] positions of the seeds in S1
+    neigh_map: torch.Tensor    # [B, k0] positions of the seeds' neighbours in S1
+
+    @property
+    def sampled_edges(self) -> int:
+        return int(self.frontier_nbrs.numel() + self.neigh_map.numel())
+
+    def forward_args(self, table: torch.Tensor):
+        """The 4 leading arguments of GraphSAGE.forward (supervised branch)."""
+        return (Gathered(table, self.frontier), [self.center_map],
+                Gathered(table, self.frontier_nbrs), [self.neigh_map])
+
+
+def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int = 0,
+                 gcn: bool = False) -> SampledBatch:
+    """Two-layer frontier for ``seeds`` (fanouts[0] for the seeds, fanouts[1] for S1)."""
+    if len(fanouts) != 2:
+        raise NotImplementedError("two-layer sampling (the reference's num_layers=2 runs)")
+    seeds = seeds.to(device=adj.device, dtype=torch.int64)
+    nb0 = sample_neighbors(adj, seeds, fanouts[0], seed)
+    if gcn:  # the reference appends the node itself (data_utils.py:95-96)
+        nb0 = torch.cat([nb0, seeds[:, None]], dim=1)
+    s1 = torch.unique(torch.cat([seeds, nb0.reshape(-1)]))
+    nb1 = sample_neighbors(adj, s1, fanouts[1], seed + 1)
+    if gcn:
+        nb1 = torch.cat([nb1, s1[:, None]], dim=1)
+    return SampledBatch(seeds, s1, nb1, torch.searchsorted(s1, seeds),
+                        torch.searchsorted(s1, nb0))
+
+
+def symmetric_adjacency(src, dst, n: int, device=None) -> CsrGraph:
+    """Undirected neighbour lists without self-loops (the reference's ``adj_lists`` of sets,
+    GraphSAGE/data_utils.py:30-38) as a CSR with ascending neighbours."""
+    s = torch.as_tensor(src, dtype=torch.int64, device=device)
+    d = torch.as_tensor(dst, dtype=torch.int64, device=device)
+    keep = s != d
+    s, d = s[keep], d[keep]
+    key = torch.unique(torch.cat([s * n + d, d * n + s]))
+    r, c = key // n, key % n
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=s.device)
+    torch.cumsum(torch.bincount(r, minlength=n), 0, out=rowptr[1:])
+    return CsrGraph(rowptr, c.to(torch.int32), torch.ones(c.numel(), device=s.device), n, n)

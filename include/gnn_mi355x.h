@@ -165,6 +165,20 @@ int gnn_sage_gather_aggregate_f32(const float* table, int64_t ldt, int64_t n_tab
 int gnn_gather_rows_f32(const float* x, int64_t ldx, int64_t n_x, const int64_t* idx, int64_t n,
                         int64_t feat, float* out, int64_t ldo, int32_t* err_flag, void* stream);
 
+/*
+ * GraphSAGE neighbour sampling for a frontier (GraphSAGE/data_utils.py:89-94):
+ *   out[i, 0..k) = k neighbours of nodes[i] in the CSR (rowptr, col):
+ *     deg >  k: k distinct neighbours (random.sample), Floyd's algorithm;
+ *     deg <= k: k draws with replacement (random.choices);
+ *     deg == 0: row of -1 and *err_flag |= 1 (the reference raises IndexError);
+ *   node id outside [0, n_graph): row of -1, *err_flag |= 2.
+ * Draws come from a counter-based hash RNG keyed by (seed, node, draw): a
+ * frontier is reproducible for a given seed. k <= 256.
+ */
+int gnn_sample_neighbors(const int64_t* rowptr, const int32_t* col, int64_t n_graph,
+                         const int64_t* nodes, int64_t n, int64_t k, uint64_t seed, int64_t* out,
+                         int32_t* err_flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,74 @@
+"""Device neighbour sampler (GraphSAGE/data_utils.py:82-117 semantics) and the
+fused Gathered forward path."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _adj(dev, n=3000, e=20000, seed=0):
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    from graphneuralnetwork_amd.sampler import symmetric_adjacency
+    s, d = rmat_edges(n, e, seed)
+    return symmetric_adjacency(s, d, n, device=dev)
+
+
+def test_sample_rules(dev):
+    from graphneuralnetwork_amd.sampler import sample_neighbors
+    adj = _adj(dev)
+    rowptr = adj.rowptr.cpu().numpy()
+    col = adj.col.cpu().numpy()
+    deg = np.diff(rowptr)
+    nodes = np.nonzero(deg > 0)[0]
+    k = 10
+    out = sample_neighbors(adj, torch.from_numpy(nodes), k, seed=3).cpu().numpy()
+    again = sample_neighbors(adj, torch.from_numpy(nodes), k, seed=3).cpu().numpy()
+    np.testing.assert_array_equal(out, again)
+    for i, v in enumerate(nodes):
+        nb = set(col[rowptr[v]:rowptr[v + 1]].tolist())
+        assert set(out[i].tolist()) <= nb
+        if deg[v] > k:
+            assert len(set(out[i].tolist())) == k  # random.sample: distinct
+    with pytest.raises(IndexError):
+        iso = np.nonzero(deg == 0)[0]
+        if iso.size == 0:
+            raise IndexError("no isolated node in this graph")
+        sample_neighbors(adj, torch.from_numpy(iso[:1]), k)
+
+
+def test_sample_is_uniform(dev):
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.sampler import sample_neighbors
+    deg = 40
+    rowptr = torch.tensor([0, deg], dtype=torch.int64, device=dev)
+    col = torch.arange(deg, dtype=torch.int32, device=dev)
+    g = CsrGraph(rowptr, col, torch.ones(deg, device=dev), 1, deg)
+    nodes = torch.zeros(1, dtype=torch.int64, device=dev)
+    counts = np.zeros(deg)
+    for s in range(400):
+        counts += np.bincount(sample_neighbors(g, nodes, 10, seed=s).cpu().numpy()[0], minlength=deg)
+    expected = 400 * 10 / deg
+    chi2 = ((counts - expected) ** 2 / expected).sum()
+    assert chi2 < 90  # 39 dof: p ~ 1e-5 threshold
+
+
+def test_batch_maps_and_gathered_forward(dev):
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    from graphneuralnetwork_amd.sampler import sample_batch
+    adj = _adj(dev)
+    deg = (adj.rowptr[1:] - adj.rowptr[:-1]).cpu().numpy()
+    seeds = torch.from_numpy(np.nonzero(deg > 0)[0][:64]).to(dev)
+    b = sample_batch(adj, seeds, fanouts=(25, 10), seed=1)
+    assert torch.equal(b.frontier[b.center_map], seeds)
+    assert b.frontier_nbrs.shape == (b.frontier.numel(), 10)
+    assert b.neigh_map.shape == (64, 25)
+    F = 32
+    table = torch.randn(adj.n_rows, F, device=dev)
+    net = GraphSAGE(2, F, 16, False, agg_func="MEAN", Unsupervised=False, class_size=3).to(dev).eval()
+    with torch.no_grad():
+        e1, c1 = net(*b.forward_args(table), None, None, None, None, None)
+        pre = (table[b.frontier], [b.center_map], table[b.frontier_nbrs], [b.neigh_map])
+        e2, c2 = net(*pre, None, None, None, None, None)
+    torch.testing.assert_close(e1, e2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(c1, c2, rtol=1e-5, atol=1e-5)
