@@ -129,8 +129,11 @@ def main():
     dev = torch.device("cuda", dev_index)
     if world > 1:
         if args.backend == "nccl":
+            if os.environ.get("LOCAL_WORLD_SIZE", str(world)) == str(world):
+                os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")  # single node: loopback bootstrap
             dist.init_process_group("nccl", device_id=dev)
         else:
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")  # the box hostname may not resolve
             dist.init_process_group("gloo")
 
     from graphneuralnetwork_amd import _lib

@@ -15,6 +15,23 @@ import torch.multiprocessing as mp
 from oracle import gnn_oracle as O
 
 
+def _collect(procs, q, n, timeout=600):
+    """Results from n workers; fails fast when a worker dies instead of waiting for the timeout."""
+    import queue
+    import time
+    out, t0 = [], time.time()
+    while len(out) < n:
+        try:
+            out.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() - t0 > timeout:
+                for p in procs:
+                    p.kill()
+                raise AssertionError(f"worker failed (exit codes {dead}) or timed out")
+    return out
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -48,7 +65,7 @@ def _graph(n, seed):
 
 
 def _worker(rank, world, port, n, F, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from graphneuralnetwork_amd.distributed import EdgeCutSpmm, build_partition
@@ -73,7 +90,7 @@ def test_edge_cut_matches_single_device(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, F, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in range(world)]
+    res = _collect(procs, q, world, 300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -13,6 +13,23 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 
+def _collect(procs, q, n, timeout=600):
+    """Results from n workers; fails fast when a worker dies instead of waiting for the timeout."""
+    import queue
+    import time
+    out, t0 = [], time.time()
+    while len(out) < n:
+        try:
+            out.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.time() - t0 > timeout:
+                for p in procs:
+                    p.kill()
+                raise AssertionError(f"worker failed (exit codes {dead}) or timed out")
+    return out
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -29,7 +46,7 @@ def _graph(n, dev):
 
 
 def _worker(rank, world, port, n, F, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from graphneuralnetwork_amd.distributed import EdgeCutSpmm, build_partition
@@ -57,7 +74,7 @@ def test_edge_cut_hip_path_matches_single_gpu(dev):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, F, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=600) for _ in range(world))
+    res = sorted(_collect(procs, q, world))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0

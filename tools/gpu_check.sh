@@ -5,6 +5,7 @@ set -u
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+export PYTHONUNBUFFERED=1
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 t=$2; shift 2
   echo "== $name ($(date +%T))"
@@ -18,7 +19,7 @@ step() {  # step <name> <timeout> <cmd...>
 for MODE in "$@"; do
   case $MODE in
     tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
-    testsk) step pytest_gpu_k 900 python -m pytest tests -m gpu -q -p no:cacheprovider -k "${K:-spmm}" ;;
+    testsk) step pytest_gpu_k 900 python -m pytest tests -m gpu -v -p no:cacheprovider -k "${K:-spmm}" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench_ns) step bench_ns 900 python bench.py --steps 20 --warmup 5 --workload ns ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} ;;
