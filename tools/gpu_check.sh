@@ -21,6 +21,8 @@ for MODE in "$@"; do
     tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     testsk) step pytest_gpu_k 900 python -m pytest tests -m gpu -v -p no:cacheprovider -k "${K:-spmm}" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench_gat) step bench_gat 600 python bench.py --steps 20 --warmup 5 --workload cfg3 ;;
+    bench_sage) step bench_sage 900 python bench.py --steps 20 --warmup 5 --workload cfg4 ;;
     bench_ns) step bench_ns 900 python bench.py --steps 20 --warmup 5 --workload ns ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
