@@ -84,7 +84,7 @@ __device__ __forceinline__ void reduce_slots(typename Vec<VW>::T (&acc)[NCH]) {
   }
 }
 
-template <int VW, int LPR, int NCH>
+template <int VW, int LPR, int NCH, bool NT = false>
 __device__ __forceinline__ void store_row(float* __restrict__ out, const float* __restrict__ bias,
                                           int64_t feat, uint32_t flags, int lane,
                                           typename Vec<VW>::T (&acc)[NCH]) {
@@ -101,13 +101,16 @@ __device__ __forceinline__ void store_row(float* __restrict__ out, const float* 
 #pragma unroll
       for (int i = 0; i < VW; ++i) vset(r, i, act_apply(vget(r, i), flags));
     }
-    vstore<VW>(out + f, r);
+    if (NT)
+      __builtin_nontemporal_store(r, reinterpret_cast<typename Vec<VW>::T*>(out + f));
+    else
+      vstore<VW>(out + f, r);
   }
 }
 
 // One launch: waves [0, seg_waves) reduce long-row segments into `partial`,
 // the remaining waves reduce one short row each straight into y.
-template <int VW, int LPR, int NCH, int U>
+template <int VW, int LPR, int NCH, int U, bool NT = false>
 __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, int64_t n_rows, const float* __restrict__ x, int64_t ldx,
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(
   if (end - beg > seg_len) return;  // long row: reduced by segment waves + fix-up
   gather_rows<VW, LPR, NCH, U>(col, val, beg, end, x, ldx, feat, lane, acc);
   reduce_slots<VW, LPR, NCH>(acc);
-  store_row<VW, LPR, NCH>(y + row * ldy, bias, feat, flags, lane, acc);
+  store_row<VW, LPR, NCH, NT>(y + row * ldy, bias, feat, flags, lane, acc);
 }
 
 // y[long_row[i]] = act(sum_{s in segs(i)} partial[s] + bias), segments summed in a fixed order.
@@ -192,15 +195,15 @@ struct SpmmArgs {
   hipStream_t stream;
 };
 
-template <int VW, int LPR, int NCH>
+template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = false>
 static int launch_spmm(const SpmmArgs& a) {
-  constexpr int U = NCH >= 4 ? 1 : (NCH == 2 ? 2 : 4);
+  constexpr int U = U_OVERRIDE ? U_OVERRIDE : (NCH >= 4 ? 1 : (NCH == 2 ? 2 : 4));
   const int64_t seg_blocks = (a.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
   const int64_t row_blocks = (a.n_rows + kWavesPerBlock - 1) / kWavesPerBlock;
   const int64_t blocks = seg_blocks + row_blocks;
   if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   if (blocks > 0) {
-    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U>), dim3(static_cast<unsigned>(blocks)),
+    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBlock), 0, a.stream, a.rowptr, a.col, a.val, a.n_rows, a.x, a.ldx,
                        a.feat, a.bias, a.y, a.ldy, a.seg_len, a.seg_row, a.seg_begin, a.n_seg,
                        seg_blocks * kWavesPerBlock, a.partial, a.ldp, a.flags);
@@ -273,4 +276,29 @@ extern "C" int gnn_spmm_csr_f32(const int64_t* rowptr, const int32_t* col, const
     if (rc != GNN_OK) return rc;
   }
   return GNN_OK;
+}
+
+// ---- developer entry: kernel-variant A/B at one shape (tools/spmm_ab.py) ----
+extern "C" int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* col, const float* val,
+                                        int64_t n_rows, const float* x, int64_t ldx, int64_t feat,
+                                        const float* bias, float* y, int64_t ldy, int64_t seg_len,
+                                        const int32_t* seg_row, const int64_t* seg_begin,
+                                        int64_t n_seg, const int32_t* long_row,
+                                        const int32_t* long_seg_ptr, int64_t n_long,
+                                        float* partial, int32_t variant, void* stream) {
+  if (feat != 128 || ldx % 4 || ldy % 4 || !aligned_to(x, 16) || !aligned_to(y, 16))
+    return GNN_E_UNSUPPORTED;
+  SpmmArgs a{rowptr, col, val, n_rows, x, ldx, feat, bias, y, ldy, seg_len, seg_row, seg_begin,
+             n_seg, long_row, long_seg_ptr, n_long, partial, feat, 0u,
+             static_cast<hipStream_t>(stream)};
+  switch (variant) {
+    case 0: return launch_spmm<4, 32, 1, 4, false>(a);
+    case 1: return launch_spmm<4, 32, 1, 8, false>(a);
+    case 2: return launch_spmm<4, 32, 1, 2, false>(a);
+    case 3: return launch_spmm<4, 32, 1, 4, true>(a);
+    case 4: return launch_spmm<2, 64, 1, 4, false>(a);
+    case 5: return launch_spmm<2, 64, 1, 8, true>(a);
+    case 6: return launch_spmm<4, 32, 1, 8, true>(a);
+    default: return GNN_E_ARG;
+  }
 }

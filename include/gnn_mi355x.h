@@ -179,6 +179,18 @@ int gnn_sample_neighbors(const int64_t* rowptr, const int32_t* col, int64_t n_gr
                          const int64_t* nodes, int64_t n, int64_t k, uint64_t seed, int64_t* out,
                          int32_t* err_flag, void* stream);
 
+/* ---- developer entry (not part of the drop-in surface) ----
+ * gnn_dev_spmm_variant_f32: gnn_spmm_csr_f32 at feat == 128 with a compile-time
+ * kernel variant (0 default U=4; 1 U=8; 2 U=2; 3 non-temporal Y stores;
+ * 4 one edge per instruction (64 lanes x 8 B); 5 = 4 + U=8 + nt stores;
+ * 6 U=8 + nt stores), for interleaved A/B timing (tools/spmm_ab.py). */
+int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* col, const float* val,
+                             int64_t n_rows, const float* x, int64_t ldx, int64_t feat,
+                             const float* bias, float* y, int64_t ldy, int64_t seg_len,
+                             const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
+                             const int32_t* long_row, const int32_t* long_seg_ptr, int64_t n_long,
+                             float* partial, int32_t variant, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
