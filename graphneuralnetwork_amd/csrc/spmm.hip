@@ -143,15 +143,23 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(
   store_row<VW, LPR, NCH, NT>(y + row * ldy, bias, feat, flags, lane, acc);
 }
 
-// y[long_row[i]] = act(sum_{s in segs(i)} partial[s] + bias), segments summed in a fixed order.
-template <int VW, int LPR, int NCH>
+// y[long_row[i]] = act(sum_{s in segs(i)} partial[s] + bias).
+// One workgroup (4 waves x EPI slots) per long row, UF partial-row loads in flight
+// per slot, so a 1,460-segment hub row is not a serial tail; the slot / wave
+// partials are combined in a fixed order (xor tree, then waves 0..3 via LDS):
+// bitwise reproducible.
+template <int VW, int LPR, int NCH, bool NT>
 __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(
     const int32_t* __restrict__ long_row, const int32_t* __restrict__ long_seg_ptr, int64_t n_long,
     const float* __restrict__ partial, int64_t ldp, int64_t feat, const float* __restrict__ bias,
     float* __restrict__ y, int64_t ldy, uint32_t flags) {
   constexpr int EPI = kWave / LPR;
+  constexpr int UF = 4;
+  constexpr int STRIDE = kWavesPerBlock * EPI;
+  __shared__ typename Vec<VW>::T red[kWavesPerBlock][NCH][LPR];
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+  const int wid = threadIdx.x >> 6;
+  const int64_t i = blockIdx.x;
   if (i >= n_long) return;
   const int sub = lane & (LPR - 1);
   const int grp = lane / LPR;
@@ -159,16 +167,42 @@ __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) acc[ch] = vzero<VW>();
   const int32_t s1 = long_seg_ptr[i + 1];
-  for (int32_t s = long_seg_ptr[i] + grp; s < s1; s += EPI) {
-    const float* pr = partial + static_cast<int64_t>(s) * ldp;
+  for (int32_t s0 = long_seg_ptr[i] + wid * EPI + grp; s0 < s1; s0 += UF * STRIDE) {
+    typename Vec<VW>::T v[UF][NCH];
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-      const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
-      if (f < feat) acc[ch] += vload<VW>(pr + f);
+    for (int u = 0; u < UF; ++u) {
+      const int32_t s = s0 + u * STRIDE;
+      const float* pr = partial + static_cast<int64_t>(s) * ldp;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+        v[u][ch] = (s < s1 && f < feat) ? vload<VW>(pr + f) : vzero<VW>();
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UF; ++u) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) acc[ch] += v[u][ch];
     }
   }
   reduce_slots<VW, LPR, NCH>(acc);
-  store_row<VW, LPR, NCH>(y + static_cast<int64_t>(long_row[i]) * ldy, bias, feat, flags, lane, acc);
+  if (lane < LPR) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) red[wid][ch][lane] = acc[ch];
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  if (lane < LPR) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      typename Vec<VW>::T r = red[0][ch][lane];
+#pragma unroll
+      for (int w = 1; w < kWavesPerBlock; ++w) r += red[w][ch][lane];
+      acc[ch] = r;
+    }
+  }
+  store_row<VW, LPR, NCH, NT>(y + static_cast<int64_t>(long_row[i]) * ldy, bias, feat, flags, lane,
+                              acc);
 }
 
 struct SpmmArgs {
@@ -195,7 +229,7 @@ struct SpmmArgs {
   hipStream_t stream;
 };
 
-template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = false>
+template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true>
 static int launch_spmm(const SpmmArgs& a) {
   constexpr int U = U_OVERRIDE ? U_OVERRIDE : (NCH >= 4 ? 1 : (NCH == 2 ? 2 : 4));
   const int64_t seg_blocks = (a.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -209,8 +243,8 @@ static int launch_spmm(const SpmmArgs& a) {
                        seg_blocks * kWavesPerBlock, a.partial, a.ldp, a.flags);
   }
   if (a.n_long > 0) {
-    const int64_t fb = (a.n_long + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL((spmm_fixup_kernel<VW, LPR, NCH>), dim3(static_cast<unsigned>(fb)),
+    const int64_t fb = a.n_long;
+    hipLaunchKernelGGL((spmm_fixup_kernel<VW, LPR, NCH, NT>), dim3(static_cast<unsigned>(fb)),
                        dim3(kBlock), 0, a.stream, a.long_row, a.long_seg_ptr, a.n_long, a.partial,
                        a.ldp, a.feat, a.bias, a.y, a.ldy, a.flags);
   }
@@ -292,7 +326,8 @@ extern "C" int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* co
              n_seg, long_row, long_seg_ptr, n_long, partial, feat, 0u,
              static_cast<hipStream_t>(stream)};
   switch (variant) {
-    case 0: return launch_spmm<4, 32, 1, 4, false>(a);
+    case 0: return launch_spmm<4, 32, 1, 4, true>(a);  // the shipped configuration
+    case 7: return launch_spmm<4, 32, 1, 4, false>(a);
     case 1: return launch_spmm<4, 32, 1, 8, false>(a);
     case 2: return launch_spmm<4, 32, 1, 2, false>(a);
     case 3: return launch_spmm<4, 32, 1, 4, true>(a);

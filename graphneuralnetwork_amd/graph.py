@@ -26,9 +26,10 @@ import torch
 
 from . import _lib
 
-# Segment size for long rows: ~128 KiB of gathered feature bytes per wavefront.
-SEG_BYTES = 128 * 1024
-MIN_SEG_LEN = 128
+# Long-row segment size: ~64 KiB of gathered feature rows per wavefront (A/B on
+# MI355X, tools/spmm_ab.py: 128 edges at F=128 beat 256/512/1024 on the 1M graph).
+SEG_BYTES = 64 * 1024
+MIN_SEG_LEN = 64
 
 
 def seg_len_for(feat: int) -> int:

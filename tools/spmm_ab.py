@@ -17,8 +17,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--rounds", type=int, default=8)
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6")
-    ap.add_argument("--seg-lens", default="128,256,512,1024,4096")
+    ap.add_argument("--variants", default="0,7,1,6")
+    ap.add_argument("--seg-lens", default="64,96,128,192,256,384")
     args = ap.parse_args()
     from graphneuralnetwork_amd import _lib
     from graphneuralnetwork_amd.preprocess import gcn_normalized_csr
@@ -46,8 +46,8 @@ def main():
             variant, stream.cuda_stream)
         _lib.check(rc, "variant")
 
-    configs = [(v, 256) for v in map(int, args.variants.split(","))] + \
-              [(0, sl) for sl in map(int, args.seg_lens.split(",")) if sl != 256]
+    configs = [(v, 128) for v in map(int, args.variants.split(","))] + \
+              [(0, sl) for sl in map(int, args.seg_lens.split(",")) if sl != 128]
     times = {c: [] for c in configs}
     for c in configs:  # correctness + warm-up
         run(*c)
