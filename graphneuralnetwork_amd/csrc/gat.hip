@@ -93,13 +93,14 @@ struct GatParams {
 
 template <int VW, int LPR, int NCH, int HP, bool SPARSE, int U>
 __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
-  constexpr int EPI = kWave / LPR;
-  __shared__ float p_lds[kGatWaves][kWave * HP];
+  constexpr int EPI = kWave / LPR;  // phase B: edges per gather instruction
+  constexpr int EPP = kWave / HP;   // phase A: edges per pass (lane = edge x head)
   const int lane = threadIdx.x & (kWave - 1);
-  const int wid = threadIdx.x >> 6;
-  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kGatWaves + wid;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kGatWaves + (threadIdx.x >> 6);
   const int sub = lane & (LPR - 1);
   const int grp = lane / LPR;
+  const int ah = lane & (HP - 1);  // phase-A head of this lane
+  const int ae = lane / HP;        // phase-A edge slot of this lane
 
   int64_t row, beg, end;
   bool is_seg = false;
@@ -116,15 +117,10 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
     end = P.rowptr[row + 1];
     if (end - beg > P.seg_len) return;
   }
-
-  float eli[HP], m[HP], lsum[HP];
-#pragma unroll
-  for (int h = 0; h < HP; ++h) {
-    eli[h] = h < P.heads ? P.el[row * P.lde + h] : 0.f;
-    m[h] = SPARSE ? 0.f : -INFINITY;
-    lsum[h] = 0.f;
-  }
-  // head of each feature vector this lane owns (Fh % VW == 0 on the vector path)
+  const bool head_ok = ah < P.heads;
+  const float eli = head_ok ? P.el[row * P.lde + ah] : 0.f;
+  float m = SPARSE ? 0.f : -INFINITY;  // running max of head `ah` (uniform over its lanes)
+  float lsum = 0.f;                     // lane-local partial denominator of head `ah`
   int hid[NCH];
   typename Vec<VW>::T acc[NCH];
 #pragma unroll
@@ -133,75 +129,56 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
     hid[ch] = f < P.feat ? static_cast<int>(f / P.fh) : 0;
     acc[ch] = vzero<VW>();
   }
-  float* pw = p_lds[wid];
 
-  for (int64_t base = beg; base < end; base += kWave) {
-    const int n = static_cast<int>(min(static_cast<int64_t>(kWave), end - base));
-    const bool live = lane < n;
-    const int c = live ? P.col[base + lane] : 0;
-    // ---- phase A: logits and unnormalised weights, lane = edge
-    float p[HP];
-#pragma unroll
-    for (int h = 0; h < HP; ++h) {
-      float lg = -INFINITY;
-      if (live && h < P.heads) {
-        const float s = eli[h] + P.er[static_cast<int64_t>(c) * P.lde + h];
-        const float x = s > 0.f ? s : P.slope * s;
-        lg = SPARSE ? -x : x;
-      }
-      p[h] = lg;
+  for (int64_t b = beg; b < end; b += EPP) {
+    const int np = static_cast<int>(min(static_cast<int64_t>(EPP), end - b));
+    // ---- phase A: lane (edge ae, head ah)
+    const bool live = ae < np && head_ok;
+    const int c = ae < np ? P.col[b + ae] : 0;
+    float z = -INFINITY;
+    if (live) {
+      const float sv = eli + P.er[static_cast<int64_t>(c) * P.lde + ah];
+      const float x = sv > 0.f ? sv : P.slope * sv;
+      z = SPARSE ? -x : x;
     }
+    float p, scale = 1.f;
     if (!SPARSE) {
-      float scl[HP];
+      float pm = z;
 #pragma unroll
-      for (int h = 0; h < HP; ++h) {
-        const float mn = fmaxf(m[h], wave_max(p[h]));
-        scl[h] = __expf(m[h] - mn);  // 0 on the first chunk (m = -inf), uniform across lanes
-        m[h] = mn;
-        p[h] = live ? __expf(p[h] - mn) : 0.f;
-        lsum[h] = lsum[h] * scl[h] + p[h];
-      }
+      for (int o = HP; o < kWave; o <<= 1) pm = fmaxf(pm, __shfl_xor(pm, o, kWave));
+      const float mn = fmaxf(m, pm);
+      scale = __expf(m - mn);  // 0 on the first pass (m = -inf)
+      m = mn;
+      p = live ? __expf(z - mn) : 0.f;
+      lsum = lsum * scale + p;
 #pragma unroll
-      for (int ch = 0; ch < NCH; ++ch) {
-        float sc = scl[0];
-#pragma unroll
-        for (int h = 1; h < HP; ++h)
-          if (h == hid[ch]) sc = scl[h];
-        acc[ch] *= sc;
-      }
+      for (int ch = 0; ch < NCH; ++ch) acc[ch] *= __shfl(scale, hid[ch], kWave);
     } else {
-#pragma unroll
-      for (int h = 0; h < HP; ++h) {
-        p[h] = live ? expf(p[h]) : 0.f;
-        lsum[h] += p[h];
-      }
+      p = live ? expf(z) : 0.f;  // the reference's exp(-LeakyReLU), no max subtraction
+      lsum += p;
     }
-#pragma unroll
-    for (int h = 0; h < HP; ++h) pw[lane * HP + h] = p[h];
-    __builtin_amdgcn_wave_barrier();
-
-    // ---- phase B: weighted gather of neighbour rows, lanes = features
-    for (int k = 0; k < n; k += EPI * U) {
+    // ---- phase B: lanes = features, EPI edges per gather instruction
+    for (int k = 0; k < np; k += EPI * U) {
       typename Vec<VW>::T xv[U][NCH];
       float w[U][NCH];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = k + u * EPI + grp;
-        const int src = e & (kWave - 1);
-        const int ce = __shfl(c, src, kWave);
+        const int es = (e < EPP ? e : 0) * HP;
+        const int ce = __shfl(c, es, kWave);
         const float* xr = P.wh + static_cast<int64_t>(ce) * P.ldw;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
           const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
-          const bool ok = e < n && f < P.feat;
+          const bool ok = e < np && f < P.feat;
+          float wv = __shfl(p, es + hid[ch], kWave);
           xv[u][ch] = ok ? vload<VW>(xr + f) : vzero<VW>();
-          float wv = ok ? pw[src * HP + hid[ch]] : 0.f;
           if (P.drop_p > 0.f && ok) {
-            const uint32_t r = hash3(P.drop_seed, base + e, P.head0 + hid[ch]);
+            const uint32_t r = hash3(P.drop_seed, b + e, P.head0 + hid[ch]);
             wv = (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f
                                                                                  : wv * P.drop_scale;
           }
-          w[u][ch] = wv;
+          w[u][ch] = ok ? wv : 0.f;
         }
       }
 #pragma unroll
@@ -210,7 +187,6 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
         for (int ch = 0; ch < NCH; ++ch) acc[ch] += w[u][ch] * xv[u][ch];
       }
     }
-    __builtin_amdgcn_wave_barrier();
   }
 
   // ---- epilogue
@@ -220,7 +196,7 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
     for (int ch = 0; ch < NCH; ++ch) acc[ch] += shfl_xor_f(acc[ch], mm);
   }
 #pragma unroll
-  for (int h = 0; h < HP; ++h) lsum[h] = wave_sum(lsum[h]);
+  for (int o = HP; o < kWave; o <<= 1) lsum += __shfl_xor(lsum, o, kWave);  // per head, all lanes
 
   if (is_seg) {
     float* pr = P.partial + wave * P.ldp;
@@ -231,33 +207,27 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
         if (f < P.feat) vstore<VW>(pr + f, acc[ch]);
       }
     }
-    if (lane == 0) {
-#pragma unroll
-      for (int h = 0; h < HP; ++h) {
-        if (h < P.heads) {
-          pr[P.feat + h] = lsum[h];
-          pr[P.feat + P.heads + h] = m[h];
-        }
-      }
+    if (lane < HP && head_ok) {
+      pr[P.feat + lane] = lsum;
+      pr[P.feat + P.heads + lane] = m;
     }
     return;
   }
-  if (lane >= LPR) return;
   const bool empty = end == beg;
+  float lh[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) lh[ch] = __shfl(lsum, hid[ch], kWave);
+  if (lane >= LPR) return;
   float* orow = P.out + row * P.ldo;
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
     if (f >= P.feat) continue;
-    float l = lsum[0];
-#pragma unroll
-    for (int h = 1; h < HP; ++h)
-      if (h == hid[ch]) l = lsum[h];
     typename Vec<VW>::T r;
     if (!SPARSE && empty) {
       r = P.empty_fill ? vload<VW>(P.empty_fill + f) : typename Vec<VW>::T(NAN);
     } else {
-      r = acc[ch] / l;  // sparse, no edge: 0/0 = NaN like the reference
+      r = acc[ch] / lh[ch];  // sparse, no edge: 0/0 = NaN like the reference
     }
 #pragma unroll
     for (int i = 0; i < VW; ++i) vset(r, i, act_apply(vget(r, i), P.flags));
@@ -299,7 +269,10 @@ __global__ __launch_bounds__(kGatBlock) void gat_fixup_kernel(GatParams P) {
 
 template <int VW, int LPR, int NCH, int HP, bool SPARSE>
 static void launch_gat(const GatParams& P, hipStream_t s) {
-  constexpr int U = NCH >= 2 ? 1 : 2;
+  // phase B covers a pass of 64/HP edges in ceil(EPP/EPI) gather instructions
+  constexpr int EPI = kWave / LPR, EPP = kWave / HP;
+  constexpr int U0 = (EPP + EPI - 1) / EPI;
+  constexpr int U = NCH >= 2 ? 1 : (U0 < 4 ? U0 : 4);
   const int64_t seg_blocks = (P.n_seg + kGatWaves - 1) / kGatWaves;
   const int64_t row_blocks = (P.n_rows + kGatWaves - 1) / kGatWaves;
   GatParams Q = P;

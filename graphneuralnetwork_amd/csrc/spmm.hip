@@ -31,7 +31,7 @@ constexpr int kBlock = 256;                 // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 // acc[ch] += sum_{e in [beg, end)} val[e] * x[col[e]][(ch*LPR + sub)*VW .. +VW)
-template <int VW, int LPR, int NCH, int U>
+template <int VW, int LPR, int NCH, int U, int LOADMODE = 0>
 __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ col,
                                             const float* __restrict__ val, int64_t beg,
                                             int64_t end, const float* __restrict__ x,
@@ -55,14 +55,23 @@ __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ col,
       for (int u = 0; u < U; ++u) {
         const int e = k + u * EPI + grp;
         const int src = e & (kWave - 1);
-        const int ce = __shfl(c, src, kWave);
+        const int craw = __shfl(c, src, kWave);
+        const int ce = LOADMODE == 2 ? (craw & 0x7fffffff) : craw;
         const float we = __shfl(v, src, kWave);
         w[u] = e < n ? we : 0.f;
         const float* xr = x + static_cast<int64_t>(ce) * ldx;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
           const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
-          xv[u][ch] = (e < n && f < feat) ? vload<VW>(xr + f) : vzero<VW>();
+          const bool ok = e < n && f < feat;
+          if (LOADMODE == 0) {
+            xv[u][ch] = ok ? vload<VW>(xr + f) : vzero<VW>();
+          } else {
+            const bool nt = LOADMODE == 1 || craw < 0;
+            typedef typename Vec<VW>::T VT;
+            const VT* pp = reinterpret_cast<const VT*>(xr + f);
+            xv[u][ch] = !ok ? vzero<VW>() : (nt ? __builtin_nontemporal_load(pp) : *pp);
+          }
         }
       }
 #pragma unroll
@@ -110,7 +119,7 @@ __device__ __forceinline__ void store_row(float* __restrict__ out, const float* 
 
 // One launch: waves [0, seg_waves) reduce long-row segments into `partial`,
 // the remaining waves reduce one short row each straight into y.
-template <int VW, int LPR, int NCH, int U, bool NT = false>
+template <int VW, int LPR, int NCH, int U, bool NT = false, int LOADMODE = 0>
 __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, int64_t n_rows, const float* __restrict__ x, int64_t ldx,
@@ -128,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(
     const int32_t row = seg_row[wave];
     const int64_t beg = seg_begin[wave];
     const int64_t end = min(beg + seg_len, rowptr[row + 1]);
-    gather_rows<VW, LPR, NCH, U>(col, val, beg, end, x, ldx, feat, lane, acc);
+    gather_rows<VW, LPR, NCH, U, LOADMODE>(col, val, beg, end, x, ldx, feat, lane, acc);
     reduce_slots<VW, LPR, NCH>(acc);
     store_row<VW, LPR, NCH>(partial + wave * ldp, nullptr, feat, 0u, lane, acc);
     return;
@@ -138,7 +147,7 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(
   const int64_t beg = rowptr[row];
   const int64_t end = rowptr[row + 1];
   if (end - beg > seg_len) return;  // long row: reduced by segment waves + fix-up
-  gather_rows<VW, LPR, NCH, U>(col, val, beg, end, x, ldx, feat, lane, acc);
+  gather_rows<VW, LPR, NCH, U, LOADMODE>(col, val, beg, end, x, ldx, feat, lane, acc);
   reduce_slots<VW, LPR, NCH>(acc);
   store_row<VW, LPR, NCH, NT>(y + row * ldy, bias, feat, flags, lane, acc);
 }
@@ -229,7 +238,7 @@ struct SpmmArgs {
   hipStream_t stream;
 };
 
-template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true>
+template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true, int LOADMODE = 0>
 static int launch_spmm(const SpmmArgs& a) {
   constexpr int U = U_OVERRIDE ? U_OVERRIDE : (NCH >= 4 ? 1 : (NCH == 2 ? 2 : 4));
   const int64_t seg_blocks = (a.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -237,7 +246,7 @@ static int launch_spmm(const SpmmArgs& a) {
   const int64_t blocks = seg_blocks + row_blocks;
   if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   if (blocks > 0) {
-    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT>), dim3(static_cast<unsigned>(blocks)),
+    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT, LOADMODE>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBlock), 0, a.stream, a.rowptr, a.col, a.val, a.n_rows, a.x, a.ldx,
                        a.feat, a.bias, a.y, a.ldy, a.seg_len, a.seg_row, a.seg_begin, a.n_seg,
                        seg_blocks * kWavesPerBlock, a.partial, a.ldp, a.flags);
@@ -328,6 +337,8 @@ extern "C" int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* co
   switch (variant) {
     case 0: return launch_spmm<4, 32, 1, 4, true>(a);  // the shipped configuration
     case 7: return launch_spmm<4, 32, 1, 4, false>(a);
+    case 8: return launch_spmm<4, 32, 1, 4, true, 1>(a);  // every X gather non-temporal
+    case 9: return launch_spmm<4, 32, 1, 4, true, 2>(a);  // col sign bit = cold -> non-temporal
     case 1: return launch_spmm<4, 32, 1, 8, false>(a);
     case 2: return launch_spmm<4, 32, 1, 2, false>(a);
     case 3: return launch_spmm<4, 32, 1, 4, true>(a);

@@ -183,7 +183,9 @@ int gnn_sample_neighbors(const int64_t* rowptr, const int32_t* col, int64_t n_gr
  * gnn_dev_spmm_variant_f32: gnn_spmm_csr_f32 at feat == 128 with a compile-time
  * kernel variant (0 shipped: U=4, non-temporal Y stores; 1 U=8; 2 U=2; 3 = 0;
  * 4 one edge per instruction (64 lanes x 8 B); 5 = 4 + U=8 + nt stores;
- * 6 U=8 + nt stores; 7 U=4 plain stores), for interleaved A/B timing (tools/spmm_ab.py). */
+ * 6 U=8 + nt stores; 7 U=4 plain stores; 8 all X gathers non-temporal;
+ * 9 col sign bit marks cold columns -> non-temporal gathers), for interleaved A/B
+ * timing (tools/spmm_ab.py). */
 int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* col, const float* val,
                              int64_t n_rows, const float* x, int64_t ldx, int64_t feat,
                              const float* bias, float* y, int64_t ldy, int64_t seg_len,

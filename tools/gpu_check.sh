@@ -21,7 +21,7 @@ for MODE in "$@"; do
     tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     testsk) step pytest_gpu_k 900 python -m pytest tests -m gpu -v -p no:cacheprovider -k "${K:-spmm}" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
-    ab) step spmm_ab 900 python tools/spmm_ab.py --workload ${AB_WL:-cfg2} ;;
+    ab) step spmm_ab 900 python tools/spmm_ab.py --workload ${AB_WL:-cfg2} ${AB_ARGS:-} ;;
     bench_gat) step bench_gat 600 python bench.py --steps 20 --warmup 5 --workload cfg3 ;;
     bench_sage) step bench_sage 900 python bench.py --steps 20 --warmup 5 --workload cfg4 ;;
     bench_ns) step bench_ns 900 python bench.py --steps 20 --warmup 5 --workload ns ;;
