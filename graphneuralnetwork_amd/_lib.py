@@ -33,11 +33,14 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _i64, _i64,                # x, ldx, feat
         _vp, _vp, _i64,                 # bias, y, ldy
         _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
-        _vp, _vp, _i64, _vp,            # long_row, long_seg_ptr, n_long, partial
+        _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
+        _vp, _vp, _vp, _i64,            # small_row, small_col, small_val, n_small
+        _vp, _i64, _vp,                 # mid_row, n_mid, partial
         _u32, _vp]),                    # flags, stream
     "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
     "gnn_spmm_plan_count": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
-    "gnn_spmm_plan_fill": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gnn_spmm_plan_fill": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          _vp, _vp, _vp, _vp]),
     "gnn_gat_logits_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64,
                                           _vp]),
     "gnn_gat_csr_f32": (ctypes.c_int, [
@@ -48,7 +51,9 @@ SIGNATURES: dict[str, tuple] = {
         ctypes.c_float, ctypes.c_uint64,  # dropout_p, dropout_seed
         _vp, _i64,                      # out, ldo
         _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
-        _vp, _vp, _i64, _vp,            # long_row, long_seg_ptr, n_long, partial
+        _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
+        _vp, _vp, _i64,                 # small_row, small_col, n_small
+        _vp, _i64, _vp,                 # mid_row, n_mid, partial
         _u32, _vp]),                    # flags, stream
     "gnn_col_mean_scratch_bytes": (_i64, [_i64, _i64]),
     "gnn_col_mean_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
@@ -58,8 +63,8 @@ SIGNATURES: dict[str, tuple] = {
                                                      _i32, _vp, _i64, _vp, _vp]),
     "gnn_gather_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
     "gnn_dev_spmm_variant_f32": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64,
-                                                _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32,
-                                                _vp]),
+                                                _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp,
+                                                _vp, _i64, _vp, _i64, _vp, _i32, _vp]),
     "gnn_sample_neighbors": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, ctypes.c_uint64, _vp,
                                             _vp, _vp]),
 }

@@ -83,6 +83,12 @@ struct GatParams {
   const int64_t* seg_begin;
   int64_t n_seg;
   int64_t seg_waves;
+  const int32_t* mid_row;  // NULL: every row is a mid row (no plan)
+  int64_t n_mid;
+  int64_t mid_waves;
+  const int32_t* small_row;
+  const int32_t* small_col;
+  int64_t n_small;
   const int32_t* long_row;
   const int32_t* long_seg_ptr;
   int64_t n_long;
@@ -90,6 +96,74 @@ struct GatParams {
   int64_t ldp;
   uint32_t flags;
 };
+
+constexpr int kGatSmallUnroll = 4;
+
+// Rows with at most one edge (44 % of the R-MAT rows: the self-loop only), packed
+// EPI x kGatSmallUnroll per wave. One edge j: dense softmax weight exp(z - z) = 1,
+// so out = Wh_j exactly; sparse computes (p * Wh_j) / p with p = exp(-LeakyReLU)
+// like the reference (inf/0 -> NaN preserved). No edge: dense -> empty_fill,
+// sparse -> 0/0 = NaN.
+template <int VW, int LPR, int NCH, bool SPARSE>
+__device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave, int lane) {
+  constexpr int EPI = kWave / LPR;
+  const int sub = lane & (LPR - 1);
+  const int grp = lane / LPR;
+  const int64_t i0 = wave * (EPI * kGatSmallUnroll);
+  typename Vec<VW>::T xv[kGatSmallUnroll][NCH];
+  int64_t rows[kGatSmallUnroll];
+  int cols[kGatSmallUnroll];
+#pragma unroll
+  for (int u = 0; u < kGatSmallUnroll; ++u) {
+    const int64_t i = i0 + u * EPI + grp;
+    const bool ok = i < P.n_small;
+    const int c = ok ? P.small_col[i] : -1;
+    rows[u] = ok ? P.small_row[i] : -1;
+    cols[u] = c;
+    const float* xr = P.wh + static_cast<int64_t>(c < 0 ? 0 : c) * P.ldw;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+      xv[u][ch] = (c >= 0 && f < P.feat) ? vload<VW>(xr + f) : vzero<VW>();
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kGatSmallUnroll; ++u) {
+    if (rows[u] < 0) continue;
+    float* orow = P.out + rows[u] * P.ldo;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+      if (f >= P.feat) continue;
+      typename Vec<VW>::T r;
+      if (cols[u] < 0) {
+        r = (!SPARSE && P.empty_fill) ? vload<VW>(P.empty_fill + f) : typename Vec<VW>::T(NAN);
+      } else if (SPARSE) {
+        const int h = static_cast<int>(f / P.fh);
+        const float sv = P.el[rows[u] * P.lde + h] + P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
+        const float p = expf(-(sv > 0.f ? sv : P.slope * sv));
+        float wv = p;
+        if (P.drop_p > 0.f) {
+          const uint32_t rr = hash3(P.drop_seed, P.rowptr[rows[u]], P.head0 + h);
+          wv = (static_cast<float>(rr >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f
+                                                                                : wv * P.drop_scale;
+        }
+        r = (wv * xv[u][ch]) / p;
+      } else {
+        float wv = 1.f;
+        if (P.drop_p > 0.f) {
+          const int h = static_cast<int>(f / P.fh);
+          const uint32_t rr = hash3(P.drop_seed, P.rowptr[rows[u]], P.head0 + h);
+          wv = (static_cast<float>(rr >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f : P.drop_scale;
+        }
+        r = wv * xv[u][ch];
+      }
+#pragma unroll
+      for (int k = 0; k < VW; ++k) vset(r, k, act_apply(vget(r, k), P.flags));
+      vstore<VW>(orow + f, r);
+    }
+  }
+}
 
 template <int VW, int LPR, int NCH, int HP, bool SPARSE, int U>
 __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
@@ -110,12 +184,15 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
     beg = P.seg_begin[wave];
     end = min(beg + P.seg_len, P.rowptr[row + 1]);
     is_seg = true;
-  } else {
-    row = wave - P.seg_waves;
-    if (row >= P.n_rows) return;
+  } else if (wave < P.seg_waves + P.mid_waves) {
+    const int64_t i = wave - P.seg_waves;
+    if (i >= P.n_mid) return;
+    row = P.mid_row ? P.mid_row[i] : i;
     beg = P.rowptr[row];
     end = P.rowptr[row + 1];
-    if (end - beg > P.seg_len) return;
+  } else {
+    gat_small_rows<VW, LPR, NCH, SPARSE>(P, wave - P.seg_waves - P.mid_waves, lane);
+    return;
   }
   const bool head_ok = ah < P.heads;
   const float eli = head_ok ? P.el[row * P.lde + ah] : 0.f;
@@ -274,13 +351,16 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
   constexpr int U0 = (EPP + EPI - 1) / EPI;
   constexpr int U = NCH >= 2 ? 1 : (U0 < 4 ? U0 : 4);
   const int64_t seg_blocks = (P.n_seg + kGatWaves - 1) / kGatWaves;
-  const int64_t row_blocks = (P.n_rows + kGatWaves - 1) / kGatWaves;
+  const int64_t mid_blocks = (P.n_mid + kGatWaves - 1) / kGatWaves;
+  const int64_t small_waves = (P.n_small + EPI * kGatSmallUnroll - 1) / (EPI * kGatSmallUnroll);
+  const int64_t small_blocks = (small_waves + kGatWaves - 1) / kGatWaves;
   GatParams Q = P;
   Q.seg_waves = seg_blocks * kGatWaves;
-  if (seg_blocks + row_blocks > 0)
+  Q.mid_waves = mid_blocks * kGatWaves;
+  const int64_t blocks = seg_blocks + mid_blocks + small_blocks;
+  if (blocks > 0)
     hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U>),
-                       dim3(static_cast<unsigned>(seg_blocks + row_blocks)), dim3(kGatBlock), 0, s,
-                       Q);
+                       dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), 0, s, Q);
   if (P.n_long > 0)
     hipLaunchKernelGGL((gat_fixup_kernel<VW, LPR, NCH, SPARSE>),
                        dim3(static_cast<unsigned>((P.n_long + kGatWaves - 1) / kGatWaves)),
@@ -409,8 +489,14 @@ extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_
                                uint64_t dropout_seed, float* out, int64_t ldo, int64_t seg_len,
                                const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
                                const int32_t* long_row, const int32_t* long_seg_ptr,
-                               int64_t n_long, float* partial, uint32_t flags, void* stream) {
-  if (n_rows < 0 || heads < 1 || fh < 1 || seg_len < 1 || n_seg < 0 || n_long < 0) return GNN_E_ARG;
+                               int64_t n_long, const int32_t* small_row, const int32_t* small_col,
+                               int64_t n_small, const int32_t* mid_row, int64_t n_mid,
+                               float* partial, uint32_t flags, void* stream) {
+  if (n_rows < 0 || heads < 1 || fh < 1 || seg_len < 1 || n_seg < 0 || n_long < 0 || n_small < 0)
+    return GNN_E_ARG;
+  const bool plan = mid_row != nullptr;
+  if (plan && (n_mid < 0 || n_mid + n_small + n_long > n_rows)) return GNN_E_ARG;
+  if (plan && n_small > 0 && (!small_row || !small_col)) return GNN_E_ARG;
   if (mode != 0 && mode != 1) return GNN_E_ARG;
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return GNN_E_ARG;
   if (flags & ~(GNN_EPI_RELU | GNN_EPI_ELU)) return GNN_E_ARG;
@@ -450,13 +536,18 @@ extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_
     P.head0 = static_cast<int>(h0);
     P.out = out + h0 * fh;
     P.ldo = ldo;
-    P.seg_len = seg_len;
+    P.seg_len = plan ? seg_len : INT64_MAX;  // no plan: every row by one wave
     P.seg_row = seg_row;
     P.seg_begin = seg_begin;
-    P.n_seg = n_seg;
+    P.n_seg = plan ? n_seg : 0;
     P.long_row = long_row;
     P.long_seg_ptr = long_seg_ptr;
-    P.n_long = n_long;
+    P.n_long = plan ? n_long : 0;
+    P.mid_row = mid_row;
+    P.n_mid = plan ? n_mid : n_rows;
+    P.small_row = small_row;
+    P.small_col = small_col;
+    P.n_small = plan ? n_small : 0;
     // group slice of the partial rows: acc at h0*fh, l/m stored right after the slice's feat
     P.partial = partial ? partial + g * (kMaxHeads * fh + 2 * kMaxHeads) : nullptr;
     P.ldp = ldp;  // same row stride for every group

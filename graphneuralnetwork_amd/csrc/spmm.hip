@@ -3,35 +3,69 @@
 // Replaces torch.spmm(adj, support) + bias at GCN/GCN.py:43-45 (reference
 // Graph_conv_layer.forward). The reference reduces an uncoalesced fp32 COO with
 // ATen's serial CPU kernel; here the adjacency is CSR (rowptr int64, col int32,
-// val fp32) and the reduction is one wavefront per output row:
+// val fp32) and rows are reduced by wavefronts according to the row-class plan
+// of plan.hip:
 //
-//   * the wave splits into EPI = 64/LPR "edge slots" of LPR lanes; each slot
-//     gathers one neighbour row per instruction with VW-wide (16 B for fp32x4)
-//     loads, so at F = 128 one wave instruction moves two whole 512-B rows
-//     (1 KiB, the widest coalesced access per instruction on CDNA4);
-//   * the 64 (col, val) pairs of an edge chunk are loaded coalesced once per
-//     chunk and broadcast to the slots with __shfl (ds_bpermute), never
-//     re-read per feature lane;
-//   * U edge-slot loads are issued before the first FMA so every wave keeps
-//     U x NCH x 16 B per lane in flight (latency hiding across ~900-cycle HBM
-//     misses);
-//   * slot partial sums are combined with xor-shuffles in a fixed order, so
-//     results are bitwise reproducible run to run (no float atomics).
-//
-// Power-law graphs: rows whose degree exceeds `seg_len` ("long rows", e.g. the
-// 187k-degree hub of the 10M-node RMAT graph) are cut into seg_len-edge
-// segments reduced by independent waves into a partial buffer, then summed in
-// segment order by a fix-up kernel. Segment waves are dispatched first (low
-// block ids) so the heavy work starts before the short-row tail.
+//   * mid rows (1 < deg <= seg_len): one wavefront per row. The wave splits into
+//     EPI = 64/LPR "edge slots" of LPR lanes; each slot gathers one neighbour row
+//     per instruction with VW-wide (16 B for fp32x4) loads, so at F = 128 one wave
+//     instruction moves two whole 512-B rows (1 KiB, the widest coalesced access
+//     per instruction on CDNA4). The 64 (col, val) pairs of an edge chunk are
+//     loaded coalesced once and broadcast to the slots with __shfl (ds_bpermute);
+//     U slot loads are issued before the first FMA (U x 16 B per lane in flight).
+//   * small rows (deg <= 1, 44% of the rows of the R-MAT graphs: self-loop only):
+//     their (col, val) was resolved by the plan, so one wavefront packs
+//     EPI x kSmallUnroll of them -- every slot gathers a different row -- instead
+//     of spending a whole wave (and a rowptr -> col -> X dependency chain) per row.
+//   * long rows (deg > seg_len, the power-law hubs): cut into seg_len-edge
+//     segments, one wave each, written to a partial buffer and merged by a
+//     fix-up workgroup per row (32 partial loads in flight, fixed order).
+//   * slot partial sums are combined with xor-shuffles in a fixed order and no
+//     float atomics are used anywhere: results are bitwise reproducible.
+//   * the final Y rows are written with non-temporal stores (Y is not re-read by
+//     this kernel; keeping it out of L2/MALL leaves room for hub rows of X:
+//     +1-3 % measured, tools/spmm_ab.py).
+// Segment waves are dispatched first (lowest block ids), then mid rows, then the
+// packed small rows.
 #include "common.hpp"
 
 namespace gnn {
 
 constexpr int kBlock = 256;                 // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kSmallUnroll = 4;             // small rows per slot per wave
+
+struct SpmmParams {
+  const int64_t* rowptr;
+  const int32_t* col;
+  const float* val;
+  int64_t n_rows;
+  const float* x;
+  int64_t ldx;
+  int64_t feat;  // width of this column block
+  const float* bias;
+  float* y;
+  int64_t ldy;
+  int64_t seg_len;
+  const int32_t* seg_row;
+  const int64_t* seg_begin;
+  int64_t n_seg;
+  const int32_t* mid_row;  // NULL: mid rows are all rows 0..n_rows-1 (no plan)
+  int64_t n_mid;
+  const int32_t* small_row;
+  const int32_t* small_col;
+  const float* small_val;
+  int64_t n_small;
+  float* partial;
+  int64_t ldp;
+  uint32_t flags;
+  // launch geometry (wave index boundaries)
+  int64_t seg_waves;
+  int64_t mid_waves;
+};
 
 // acc[ch] += sum_{e in [beg, end)} val[e] * x[col[e]][(ch*LPR + sub)*VW .. +VW)
-template <int VW, int LPR, int NCH, int U, int LOADMODE = 0>
+template <int VW, int LPR, int NCH, int U>
 __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ col,
                                             const float* __restrict__ val, int64_t beg,
                                             int64_t end, const float* __restrict__ x,
@@ -55,23 +89,14 @@ __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ col,
       for (int u = 0; u < U; ++u) {
         const int e = k + u * EPI + grp;
         const int src = e & (kWave - 1);
-        const int craw = __shfl(c, src, kWave);
-        const int ce = LOADMODE == 2 ? (craw & 0x7fffffff) : craw;
+        const int ce = __shfl(c, src, kWave);
         const float we = __shfl(v, src, kWave);
         w[u] = e < n ? we : 0.f;
         const float* xr = x + static_cast<int64_t>(ce) * ldx;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
           const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
-          const bool ok = e < n && f < feat;
-          if (LOADMODE == 0) {
-            xv[u][ch] = ok ? vload<VW>(xr + f) : vzero<VW>();
-          } else {
-            const bool nt = LOADMODE == 1 || craw < 0;
-            typedef typename Vec<VW>::T VT;
-            const VT* pp = reinterpret_cast<const VT*>(xr + f);
-            xv[u][ch] = !ok ? vzero<VW>() : (nt ? __builtin_nontemporal_load(pp) : *pp);
-          }
+          xv[u][ch] = (e < n && f < feat) ? vload<VW>(xr + f) : vzero<VW>();
         }
       }
 #pragma unroll
@@ -93,12 +118,12 @@ __device__ __forceinline__ void reduce_slots(typename Vec<VW>::T (&acc)[NCH]) {
   }
 }
 
-template <int VW, int LPR, int NCH, bool NT = false>
-__device__ __forceinline__ void store_row(float* __restrict__ out, const float* __restrict__ bias,
-                                          int64_t feat, uint32_t flags, int lane,
-                                          typename Vec<VW>::T (&acc)[NCH]) {
-  if (lane >= LPR) return;  // slot 0 holds the reduced row
-  const int sub = lane;
+// Epilogue for one output row held by the LPR lanes `sub` = 0..LPR-1 of a slot.
+template <int VW, int LPR, int NCH, bool NT>
+__device__ __forceinline__ void store_slot_row(float* __restrict__ out,
+                                               const float* __restrict__ bias, int64_t feat,
+                                               uint32_t flags, int sub,
+                                               typename Vec<VW>::T (&acc)[NCH]) {
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
@@ -117,39 +142,66 @@ __device__ __forceinline__ void store_row(float* __restrict__ out, const float* 
   }
 }
 
-// One launch: waves [0, seg_waves) reduce long-row segments into `partial`,
-// the remaining waves reduce one short row each straight into y.
-template <int VW, int LPR, int NCH, int U, bool NT = false, int LOADMODE = 0>
-__global__ __launch_bounds__(kBlock) void spmm_csr_kernel(
-    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, int64_t n_rows, const float* __restrict__ x, int64_t ldx,
-    int64_t feat, const float* __restrict__ bias, float* __restrict__ y, int64_t ldy,
-    int64_t seg_len, const int32_t* __restrict__ seg_row, const int64_t* __restrict__ seg_begin,
-    int64_t n_seg, int64_t seg_waves, float* __restrict__ partial, int64_t ldp, uint32_t flags) {
+template <int VW, int LPR, int NCH, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
+  constexpr int EPI = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+  const int sub = lane & (LPR - 1);
+  const int grp = lane / LPR;
   typename Vec<VW>::T acc[NCH];
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) acc[ch] = vzero<VW>();
 
-  if (wave < seg_waves) {
-    if (wave >= n_seg) return;
-    const int32_t row = seg_row[wave];
-    const int64_t beg = seg_begin[wave];
-    const int64_t end = min(beg + seg_len, rowptr[row + 1]);
-    gather_rows<VW, LPR, NCH, U, LOADMODE>(col, val, beg, end, x, ldx, feat, lane, acc);
+  if (wave < P.seg_waves) {  // ---- long-row segment -> partial row
+    if (wave >= P.n_seg) return;
+    const int32_t row = P.seg_row[wave];
+    const int64_t beg = P.seg_begin[wave];
+    const int64_t end = min(beg + P.seg_len, P.rowptr[row + 1]);
+    gather_rows<VW, LPR, NCH, U>(P.col, P.val, beg, end, P.x, P.ldx, P.feat, lane, acc);
     reduce_slots<VW, LPR, NCH>(acc);
-    store_row<VW, LPR, NCH>(partial + wave * ldp, nullptr, feat, 0u, lane, acc);
+    if (lane < LPR) store_slot_row<VW, LPR, NCH, false>(P.partial + wave * P.ldp, nullptr, P.feat,
+                                                        0u, sub, acc);
     return;
   }
-  const int64_t row = wave - seg_waves;
-  if (row >= n_rows) return;
-  const int64_t beg = rowptr[row];
-  const int64_t end = rowptr[row + 1];
-  if (end - beg > seg_len) return;  // long row: reduced by segment waves + fix-up
-  gather_rows<VW, LPR, NCH, U, LOADMODE>(col, val, beg, end, x, ldx, feat, lane, acc);
-  reduce_slots<VW, LPR, NCH>(acc);
-  store_row<VW, LPR, NCH, NT>(y + row * ldy, bias, feat, flags, lane, acc);
+  if (wave < P.seg_waves + P.mid_waves) {  // ---- one wave per mid row
+    const int64_t i = wave - P.seg_waves;
+    if (i >= P.n_mid) return;
+    const int64_t row = P.mid_row ? P.mid_row[i] : i;
+    gather_rows<VW, LPR, NCH, U>(P.col, P.val, P.rowptr[row], P.rowptr[row + 1], P.x, P.ldx,
+                                 P.feat, lane, acc);
+    reduce_slots<VW, LPR, NCH>(acc);
+    if (lane < LPR) store_slot_row<VW, LPR, NCH, NT>(P.y + row * P.ldy, P.bias, P.feat, P.flags,
+                                                     sub, acc);
+    return;
+  }
+  // ---- packed small rows: EPI x kSmallUnroll rows per wave, one per slot and unroll step
+  const int64_t i0 = (wave - P.seg_waves - P.mid_waves) * (EPI * kSmallUnroll);
+  typename Vec<VW>::T xv[kSmallUnroll][NCH];
+  float w[kSmallUnroll];
+  int64_t rows[kSmallUnroll];
+#pragma unroll
+  for (int u = 0; u < kSmallUnroll; ++u) {
+    const int64_t i = i0 + u * EPI + grp;
+    const bool ok = i < P.n_small;
+    const int c = ok ? P.small_col[i] : -1;
+    rows[u] = ok ? P.small_row[i] : -1;
+    w[u] = c >= 0 ? P.small_val[i] : 0.f;
+    const float* xr = P.x + static_cast<int64_t>(c < 0 ? 0 : c) * P.ldx;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+      xv[u][ch] = (c >= 0 && f < P.feat) ? vload<VW>(xr + f) : vzero<VW>();
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kSmallUnroll; ++u) {
+    if (rows[u] < 0) continue;
+    typename Vec<VW>::T r[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) r[ch] = w[u] * xv[u][ch];
+    store_slot_row<VW, LPR, NCH, NT>(P.y + rows[u] * P.ldy, P.bias, P.feat, P.flags, sub, r);
+  }
 }
 
 // y[long_row[i]] = act(sum_{s in segs(i)} partial[s] + bias).
@@ -200,84 +252,167 @@ __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(
     for (int ch = 0; ch < NCH; ++ch) red[wid][ch][lane] = acc[ch];
   }
   __syncthreads();
-  if (wid != 0) return;
-  if (lane < LPR) {
+  if (wid != 0 || lane >= LPR) return;
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-      typename Vec<VW>::T r = red[0][ch][lane];
+  for (int ch = 0; ch < NCH; ++ch) {
+    typename Vec<VW>::T r = red[0][ch][lane];
 #pragma unroll
-      for (int w = 1; w < kWavesPerBlock; ++w) r += red[w][ch][lane];
-      acc[ch] = r;
-    }
+    for (int w = 1; w < kWavesPerBlock; ++w) r += red[w][ch][lane];
+    acc[ch] = r;
   }
-  store_row<VW, LPR, NCH, NT>(y + static_cast<int64_t>(long_row[i]) * ldy, bias, feat, flags, lane,
-                              acc);
+  store_slot_row<VW, LPR, NCH, NT>(y + static_cast<int64_t>(long_row[i]) * ldy, bias, feat, flags,
+                                   sub, acc);
 }
 
-struct SpmmArgs {
-  const int64_t* rowptr;
-  const int32_t* col;
-  const float* val;
-  int64_t n_rows;
-  const float* x;
-  int64_t ldx;
-  int64_t feat;  // width of this column block
-  const float* bias;
-  float* y;
-  int64_t ldy;
-  int64_t seg_len;
-  const int32_t* seg_row;
-  const int64_t* seg_begin;
-  int64_t n_seg;
+struct SpmmLaunch {
+  SpmmParams p;
   const int32_t* long_row;
   const int32_t* long_seg_ptr;
   int64_t n_long;
-  float* partial;
-  int64_t ldp;
-  uint32_t flags;
   hipStream_t stream;
 };
 
-template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true, int LOADMODE = 0>
-static int launch_spmm(const SpmmArgs& a) {
+template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true>
+static int launch_spmm(const SpmmLaunch& L) {
   constexpr int U = U_OVERRIDE ? U_OVERRIDE : (NCH >= 4 ? 1 : (NCH == 2 ? 2 : 4));
-  const int64_t seg_blocks = (a.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int64_t row_blocks = (a.n_rows + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int64_t blocks = seg_blocks + row_blocks;
+  constexpr int EPI = kWave / LPR;
+  SpmmParams p = L.p;
+  const int64_t seg_blocks = (p.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int64_t mid_blocks = (p.n_mid + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int64_t small_waves = (p.n_small + EPI * kSmallUnroll - 1) / (EPI * kSmallUnroll);
+  const int64_t small_blocks = (small_waves + kWavesPerBlock - 1) / kWavesPerBlock;
+  p.seg_waves = seg_blocks * kWavesPerBlock;
+  p.mid_waves = mid_blocks * kWavesPerBlock;
+  const int64_t blocks = seg_blocks + mid_blocks + small_blocks;
   if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   if (blocks > 0) {
-    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT, LOADMODE>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(kBlock), 0, a.stream, a.rowptr, a.col, a.val, a.n_rows, a.x, a.ldx,
-                       a.feat, a.bias, a.y, a.ldy, a.seg_len, a.seg_row, a.seg_begin, a.n_seg,
-                       seg_blocks * kWavesPerBlock, a.partial, a.ldp, a.flags);
+    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), 0, L.stream, p);
   }
-  if (a.n_long > 0) {
-    const int64_t fb = a.n_long;
-    hipLaunchKernelGGL((spmm_fixup_kernel<VW, LPR, NCH, NT>), dim3(static_cast<unsigned>(fb)),
-                       dim3(kBlock), 0, a.stream, a.long_row, a.long_seg_ptr, a.n_long, a.partial,
-                       a.ldp, a.feat, a.bias, a.y, a.ldy, a.flags);
+  if (L.n_long > 0) {
+    hipLaunchKernelGGL((spmm_fixup_kernel<VW, LPR, NCH, NT>), dim3(static_cast<unsigned>(L.n_long)),
+                       dim3(kBlock), 0, L.stream, L.long_row, L.long_seg_ptr, L.n_long, p.partial,
+                       p.ldp, p.feat, p.bias, p.y, p.ldy, p.flags);
   }
   return launch_status();
 }
 
-// Picks (VW, LPR, NCH) for one column block of width a.feat (<= 64*8*VW).
+// Picks (VW, LPR, NCH) for one column block of width feat (<= 64*8*VW).
 template <int VW>
-static int dispatch_spmm(const SpmmArgs& a) {
-  const int64_t nv = (a.feat + VW - 1) / VW;  // vectors per row
+static int dispatch_spmm(const SpmmLaunch& L) {
+  const int64_t nv = (L.p.feat + VW - 1) / VW;  // vectors per row
   if (nv <= 64) {
     switch (next_pow2_le64(nv)) {
-      case 1: return launch_spmm<VW, 1, 1>(a);
-      case 2: return launch_spmm<VW, 2, 1>(a);
-      case 4: return launch_spmm<VW, 4, 1>(a);
-      case 8: return launch_spmm<VW, 8, 1>(a);
-      case 16: return launch_spmm<VW, 16, 1>(a);
-      case 32: return launch_spmm<VW, 32, 1>(a);
-      default: return launch_spmm<VW, 64, 1>(a);
+      case 1: return launch_spmm<VW, 1, 1>(L);
+      case 2: return launch_spmm<VW, 2, 1>(L);
+      case 4: return launch_spmm<VW, 4, 1>(L);
+      case 8: return launch_spmm<VW, 8, 1>(L);
+      case 16: return launch_spmm<VW, 16, 1>(L);
+      case 32: return launch_spmm<VW, 32, 1>(L);
+      default: return launch_spmm<VW, 64, 1>(L);
     }
   }
-  if (nv <= 128) return launch_spmm<VW, 64, 2>(a);
-  if (nv <= 256) return launch_spmm<VW, 64, 4>(a);
-  return launch_spmm<VW, 64, 8>(a);
+  if (nv <= 128) return launch_spmm<VW, 64, 2>(L);
+  if (nv <= 256) return launch_spmm<VW, 64, 4>(L);
+  return launch_spmm<VW, 64, 8>(L);
+}
+
+static int check_spmm_args(const int64_t* rowptr, int64_t n_rows, const float* x, int64_t ldx,
+                           int64_t feat, float* y, int64_t ldy, int64_t seg_len, int64_t n_seg,
+                           int64_t n_long, int64_t n_small, int64_t n_mid, const int32_t* seg_row,
+                           const int64_t* seg_begin, const int32_t* long_row,
+                           const int32_t* long_seg_ptr, const int32_t* small_row,
+                           const int32_t* small_col, const float* small_val,
+                           const int32_t* mid_row, const float* partial, uint32_t flags) {
+  if (n_rows < 0 || feat < 0 || n_seg < 0 || n_long < 0 || n_small < 0 || seg_len < 1)
+    return GNN_E_ARG;
+  if (rowptr == nullptr || y == nullptr || x == nullptr) return GNN_E_ARG;
+  if (ldx < feat || ldy < feat) return GNN_E_ARG;
+  if (n_rows > 0x7fffffffLL) return GNN_E_UNSUPPORTED;  // int32 column ids / row lists
+  if ((n_seg > 0 || n_long > 0) &&
+      (seg_row == nullptr || seg_begin == nullptr || long_row == nullptr ||
+       long_seg_ptr == nullptr || partial == nullptr || n_long == 0 || n_seg == 0))
+    return GNN_E_ARG;
+  if (n_small > 0 && (small_row == nullptr || small_col == nullptr || small_val == nullptr))
+    return GNN_E_ARG;
+  if (mid_row != nullptr && (n_mid < 0 || n_mid + n_small + n_long > n_rows)) return GNN_E_ARG;
+  if (flags & ~(GNN_EPI_RELU | GNN_EPI_ELU | GNN_EPI_ACCUMULATE)) return GNN_E_ARG;
+  return GNN_OK;
+}
+
+static int run_spmm(SpmmLaunch L, const float* x, const float* bias, float* y, float* partial,
+                    int64_t feat, int variant) {
+  const bool vec4 = (feat % 4 == 0) && (L.p.ldx % 4 == 0) && (L.p.ldy % 4 == 0) &&
+                    aligned_to(x, 16) && aligned_to(y, 16) &&
+                    (bias == nullptr || aligned_to(bias, 16)) &&
+                    (partial == nullptr || aligned_to(partial, 16));
+  if (variant >= 0) {  // developer A/B (feat == 128, vector path only)
+    if (feat != 128 || !vec4) return GNN_E_UNSUPPORTED;
+    L.p.feat = feat;
+    L.p.x = x;
+    L.p.y = y;
+    L.p.bias = bias;
+    L.p.partial = partial;
+    switch (variant) {
+      case 0: return launch_spmm<4, 32, 1, 4, true>(L);  // the shipped configuration
+      case 1: return launch_spmm<4, 32, 1, 8, true>(L);
+      case 2: return launch_spmm<4, 32, 1, 2, true>(L);
+      case 7: return launch_spmm<4, 32, 1, 4, false>(L);
+      default: return GNN_E_ARG;
+    }
+  }
+  const int64_t vw = vec4 ? 4 : 1;
+  const int64_t blk = 64 * 8 * vw;  // widest column block one launch covers
+  for (int64_t c0 = 0; c0 < feat; c0 += blk) {
+    L.p.feat = feat - c0 < blk ? feat - c0 : blk;
+    L.p.x = x + c0;
+    L.p.y = y + c0;
+    L.p.bias = bias ? bias + c0 : nullptr;
+    L.p.partial = partial ? partial + c0 : nullptr;
+    const int rc = vec4 ? dispatch_spmm<4>(L) : dispatch_spmm<1>(L);
+    if (rc != GNN_OK) return rc;
+  }
+  return GNN_OK;
+}
+
+static int spmm_entry(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
+                      const float* x, int64_t ldx, int64_t feat, const float* bias, float* y,
+                      int64_t ldy, int64_t seg_len, const int32_t* seg_row,
+                      const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
+                      const int32_t* long_seg_ptr, int64_t n_long, const int32_t* small_row,
+                      const int32_t* small_col, const float* small_val, int64_t n_small,
+                      const int32_t* mid_row, int64_t n_mid, float* partial, uint32_t flags,
+                      void* stream, int variant) {
+  int rc = check_spmm_args(rowptr, n_rows, x, ldx, feat, y, ldy, seg_len, n_seg, n_long, n_small,
+                           n_mid, seg_row, seg_begin, long_row, long_seg_ptr, small_row, small_col,
+                           small_val, mid_row, partial, flags);
+  if (rc != GNN_OK) return rc;
+  if (n_rows == 0 || feat == 0) return GNN_OK;
+  const bool plan = mid_row != nullptr;
+  SpmmLaunch L{};
+  L.p.rowptr = rowptr;
+  L.p.col = col;
+  L.p.val = val;
+  L.p.n_rows = n_rows;
+  L.p.ldx = ldx;
+  L.p.ldy = ldy;
+  L.p.seg_len = plan ? seg_len : INT64_MAX;  // no plan: every row by one wave
+  L.p.seg_row = seg_row;
+  L.p.seg_begin = seg_begin;
+  L.p.n_seg = plan ? n_seg : 0;
+  L.p.mid_row = mid_row;
+  L.p.n_mid = plan ? n_mid : n_rows;
+  L.p.small_row = small_row;
+  L.p.small_col = small_col;
+  L.p.small_val = small_val;
+  L.p.n_small = plan ? n_small : 0;
+  L.p.ldp = feat;
+  L.p.flags = flags;
+  L.long_row = long_row;
+  L.long_seg_ptr = long_seg_ptr;
+  L.n_long = plan ? n_long : 0;
+  L.stream = static_cast<hipStream_t>(stream);
+  return run_spmm(L, x, bias, y, partial, feat, variant);
 }
 
 }  // namespace gnn
@@ -289,62 +424,27 @@ extern "C" int gnn_spmm_csr_f32(const int64_t* rowptr, const int32_t* col, const
                                 const float* bias, float* y, int64_t ldy, int64_t seg_len,
                                 const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
                                 const int32_t* long_row, const int32_t* long_seg_ptr,
-                                int64_t n_long, float* partial, uint32_t flags, void* stream) {
-  if (n_rows < 0 || feat < 0 || n_seg < 0 || n_long < 0 || seg_len < 1) return GNN_E_ARG;
-  if (n_rows == 0 || feat == 0) return GNN_OK;
-  if (rowptr == nullptr || y == nullptr || x == nullptr) return GNN_E_ARG;
-  if (ldx < feat || ldy < feat) return GNN_E_ARG;
-  if (n_rows > 0x7fffffffLL) return GNN_E_UNSUPPORTED;  // int32 column ids
-  if ((n_seg > 0 || n_long > 0) &&
-      (seg_row == nullptr || seg_begin == nullptr || long_row == nullptr ||
-       long_seg_ptr == nullptr || partial == nullptr || n_long == 0 || n_seg == 0))
-    return GNN_E_ARG;
-  if (flags & ~(GNN_EPI_RELU | GNN_EPI_ELU | GNN_EPI_ACCUMULATE)) return GNN_E_ARG;
-
-  const bool vec4 = (feat % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) && aligned_to(x, 16) &&
-                    aligned_to(y, 16) && (bias == nullptr || aligned_to(bias, 16)) &&
-                    (partial == nullptr || aligned_to(partial, 16));
-  const int64_t vw = vec4 ? 4 : 1;
-  const int64_t blk = 64 * 8 * vw;  // widest column block one launch covers
-  SpmmArgs a{rowptr, col, val, n_rows, x, ldx, 0, bias, y, ldy, seg_len, seg_row, seg_begin,
-             n_seg, long_row, long_seg_ptr, n_long, partial, feat, flags,
-             static_cast<hipStream_t>(stream)};
-  for (int64_t c0 = 0; c0 < feat; c0 += blk) {
-    a.feat = feat - c0 < blk ? feat - c0 : blk;
-    a.x = x + c0;
-    a.y = y + c0;
-    a.bias = bias ? bias + c0 : nullptr;
-    a.partial = partial ? partial + c0 : nullptr;
-    const int rc = vec4 ? dispatch_spmm<4>(a) : dispatch_spmm<1>(a);
-    if (rc != GNN_OK) return rc;
-  }
-  return GNN_OK;
+                                int64_t n_long, const int32_t* small_row, const int32_t* small_col,
+                                const float* small_val, int64_t n_small, const int32_t* mid_row,
+                                int64_t n_mid, float* partial, uint32_t flags, void* stream) {
+  return spmm_entry(rowptr, col, val, n_rows, x, ldx, feat, bias, y, ldy, seg_len, seg_row,
+                    seg_begin, n_seg, long_row, long_seg_ptr, n_long, small_row, small_col,
+                    small_val, n_small, mid_row, n_mid, partial, flags, stream, -1);
 }
 
 // ---- developer entry: kernel-variant A/B at one shape (tools/spmm_ab.py) ----
-extern "C" int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* col, const float* val,
-                                        int64_t n_rows, const float* x, int64_t ldx, int64_t feat,
-                                        const float* bias, float* y, int64_t ldy, int64_t seg_len,
-                                        const int32_t* seg_row, const int64_t* seg_begin,
-                                        int64_t n_seg, const int32_t* long_row,
-                                        const int32_t* long_seg_ptr, int64_t n_long,
+extern "C" int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* col,
+                                        const float* val, int64_t n_rows, const float* x,
+                                        int64_t ldx, int64_t feat, const float* bias, float* y,
+                                        int64_t ldy, int64_t seg_len, const int32_t* seg_row,
+                                        const int64_t* seg_begin, int64_t n_seg,
+                                        const int32_t* long_row, const int32_t* long_seg_ptr,
+                                        int64_t n_long, const int32_t* small_row,
+                                        const int32_t* small_col, const float* small_val,
+                                        int64_t n_small, const int32_t* mid_row, int64_t n_mid,
                                         float* partial, int32_t variant, void* stream) {
-  if (feat != 128 || ldx % 4 || ldy % 4 || !aligned_to(x, 16) || !aligned_to(y, 16))
-    return GNN_E_UNSUPPORTED;
-  SpmmArgs a{rowptr, col, val, n_rows, x, ldx, feat, bias, y, ldy, seg_len, seg_row, seg_begin,
-             n_seg, long_row, long_seg_ptr, n_long, partial, feat, 0u,
-             static_cast<hipStream_t>(stream)};
-  switch (variant) {
-    case 0: return launch_spmm<4, 32, 1, 4, true>(a);  // the shipped configuration
-    case 7: return launch_spmm<4, 32, 1, 4, false>(a);
-    case 8: return launch_spmm<4, 32, 1, 4, true, 1>(a);  // every X gather non-temporal
-    case 9: return launch_spmm<4, 32, 1, 4, true, 2>(a);  // col sign bit = cold -> non-temporal
-    case 1: return launch_spmm<4, 32, 1, 8, false>(a);
-    case 2: return launch_spmm<4, 32, 1, 2, false>(a);
-    case 3: return launch_spmm<4, 32, 1, 4, true>(a);
-    case 4: return launch_spmm<2, 64, 1, 4, false>(a);
-    case 5: return launch_spmm<2, 64, 1, 8, true>(a);
-    case 6: return launch_spmm<4, 32, 1, 8, true>(a);
-    default: return GNN_E_ARG;
-  }
+  if (variant < 0) return GNN_E_ARG;
+  return spmm_entry(rowptr, col, val, n_rows, x, ldx, feat, bias, y, ldy, seg_len, seg_row,
+                    seg_begin, n_seg, long_row, long_seg_ptr, n_long, small_row, small_col,
+                    small_val, n_small, mid_row, n_mid, partial, 0u, stream, variant);
 }

@@ -26,9 +26,11 @@ import torch
 
 from . import _lib
 
-# Long-row segment size: ~64 KiB of gathered feature rows per wavefront (A/B on
-# MI355X, tools/spmm_ab.py: 128 edges at F=128 beat 256/512/1024 on the 1M graph).
-SEG_BYTES = 64 * 1024
+# Long-row segment size: ~96 KiB of gathered feature rows per wavefront. A/B on
+# MI355X (tools/spmm_ab.py, F=128): 192 edges is within 1 % of the best setting on
+# both the 1M-node graph (best 64-192) and the 10M-node graph (best 192-256);
+# 512+ leaves single-wave tails, 64 over-splits the large graph.
+SEG_BYTES = 96 * 1024
 MIN_SEG_LEN = 64
 
 
@@ -38,11 +40,17 @@ def seg_len_for(feat: int) -> int:
 
 @dataclass
 class RowSplitPlan:
+    """Row classes of a CSR graph (plan.hip): small (deg <= 1), mid, long (split)."""
+
     seg_len: int
     seg_row: torch.Tensor      # int32 [n_seg]
     seg_begin: torch.Tensor    # int64 [n_seg]
     long_row: torch.Tensor     # int32 [n_long]
     long_seg_ptr: torch.Tensor  # int32 [n_long + 1]
+    small_row: torch.Tensor    # int32 [n_small]
+    small_col: torch.Tensor    # int32 [n_small] (-1: no edge)
+    small_val: torch.Tensor    # fp32  [n_small]
+    mid_row: torch.Tensor      # int32 [n_mid]
 
     @property
     def n_seg(self) -> int:
@@ -51,6 +59,24 @@ class RowSplitPlan:
     @property
     def n_long(self) -> int:
         return int(self.long_row.numel())
+
+    @property
+    def n_small(self) -> int:
+        return int(self.small_row.numel())
+
+    @property
+    def n_mid(self) -> int:
+        return int(self.mid_row.numel())
+
+    def args(self):
+        """The plan arguments of gnn_spmm_csr_f32 / gnn_gat_csr_f32 (after seg_len)."""
+        from ._lib import ptr
+        return (ptr(self.seg_row), ptr(self.seg_begin), self.n_seg, ptr(self.long_row),
+                self.long_seg_ptr.data_ptr(), self.n_long, ptr(self.small_row),
+                ptr(self.small_col), ptr(self.small_val), self.n_small,
+                # mid_row must be non-NULL whenever a plan is used (NULL = "no plan")
+                self.mid_row.data_ptr() if self.n_mid else self.long_seg_ptr.data_ptr(),
+                self.n_mid)
 
 
 @dataclass
@@ -117,19 +143,30 @@ def _build_plan(g: CsrGraph, seg_len: int) -> RowSplitPlan:
     stream = _lib.stream_handle(dev)
     nbytes = int(lib.gnn_spmm_plan_scratch_bytes(g.n_rows))
     scratch = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dev)
-    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    counts = torch.zeros(4, dtype=torch.int64, device=dev)
     _lib.check(lib.gnn_spmm_plan_count(g.rowptr.data_ptr(), g.n_rows, seg_len, counts.data_ptr(),
                                        scratch.data_ptr(), stream), "gnn_spmm_plan_count")
-    n_long, n_seg = (int(v) for v in counts.cpu().tolist())  # one host round-trip per graph
-    seg_row = torch.empty(n_seg, dtype=torch.int32, device=dev)
+    # one host round-trip per graph
+    n_long, n_seg, n_small, n_mid = (int(v) for v in counts.cpu().tolist())
+    i32 = dict(dtype=torch.int32, device=dev)
+    seg_row = torch.empty(n_seg, **i32)
     seg_begin = torch.empty(n_seg, dtype=torch.int64, device=dev)
-    long_row = torch.empty(n_long, dtype=torch.int32, device=dev)
-    long_seg_ptr = torch.empty(n_long + 1, dtype=torch.int32, device=dev)
-    _lib.check(lib.gnn_spmm_plan_fill(g.rowptr.data_ptr(), g.n_rows, seg_len, _lib.ptr(seg_row),
-                                      _lib.ptr(seg_begin), _lib.ptr(long_row),
-                                      long_seg_ptr.data_ptr(), scratch.data_ptr(), stream),
-               "gnn_spmm_plan_fill")
-    return RowSplitPlan(seg_len, seg_row, seg_begin, long_row, long_seg_ptr)
+    long_row = torch.empty(n_long, **i32)
+    long_seg_ptr = torch.empty(n_long + 1, **i32)
+    small_row = torch.empty(n_small, **i32)
+    small_col = torch.empty(n_small, **i32)
+    small_val = torch.empty(n_small, dtype=torch.float32, device=dev)
+    mid_row = torch.empty(n_mid, **i32)
+    col = g.col if g.nnz else torch.zeros(1, **i32)
+    val = g.val if g.nnz else torch.zeros(1, dtype=torch.float32, device=dev)
+    _lib.check(lib.gnn_spmm_plan_fill(g.rowptr.data_ptr(), col.data_ptr(), val.data_ptr(),
+                                      g.n_rows, seg_len, _lib.ptr(seg_row), _lib.ptr(seg_begin),
+                                      _lib.ptr(long_row), long_seg_ptr.data_ptr(),
+                                      _lib.ptr(small_row), _lib.ptr(small_col),
+                                      _lib.ptr(small_val), _lib.ptr(mid_row), scratch.data_ptr(),
+                                      stream), "gnn_spmm_plan_fill")
+    return RowSplitPlan(seg_len, seg_row, seg_begin, long_row, long_seg_ptr, small_row,
+                        small_col, small_val, mid_row)
 
 
 # ---------------------------------------------------------------- builders

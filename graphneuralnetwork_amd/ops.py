@@ -69,8 +69,7 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
     rc = lib.gnn_spmm_csr_f32(
         g.rowptr.data_ptr(), g.col.data_ptr(), g.val.data_ptr(), g.n_rows,
         x.data_ptr(), x.stride(0), feat, _lib.ptr(bias), out.data_ptr(), out.stride(0),
-        plan.seg_len, _lib.ptr(plan.seg_row), _lib.ptr(plan.seg_begin), plan.n_seg,
-        _lib.ptr(plan.long_row), plan.long_seg_ptr.data_ptr(), plan.n_long, _lib.ptr(partial),
+        plan.seg_len, *plan.args(), _lib.ptr(partial),
         _ACT_FLAGS[activation] | (_lib.EPI_ACCUMULATE if accumulate else 0),
         _lib.stream_handle(x.device))
     _lib.check(rc, "gnn_spmm_csr_f32")
@@ -169,12 +168,13 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
         partial = torch.empty((plan.n_seg, feat + 2 * heads), dtype=torch.float32,
                               device=wh.device)
     lib = _lib.load()
+    pa = plan.args()  # (seg_row, seg_begin, n_seg, long_row, long_seg_ptr, n_long,
+    #                    small_row, small_col, small_val, n_small, mid_row, n_mid)
     rc = lib.gnn_gat_csr_f32(
         g.rowptr.data_ptr(), g.col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
         el.data_ptr(), er.data_ptr(), heads, float(negative_slope), int(mode), _lib.ptr(fill),
         float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), out.stride(0),
-        plan.seg_len, _lib.ptr(plan.seg_row), _lib.ptr(plan.seg_begin), plan.n_seg,
-        _lib.ptr(plan.long_row), plan.long_seg_ptr.data_ptr(), plan.n_long, _lib.ptr(partial),
+        plan.seg_len, *pa[:6], pa[6], pa[7], pa[9], pa[10], pa[11], _lib.ptr(partial),
         _ACT_FLAGS[activation], _lib.stream_handle(wh.device))
     _lib.check(rc, "gnn_gat_csr_f32")
     return out

@@ -53,40 +53,46 @@ const char* gnn_error_string(int code);
  * Replaces `torch.spmm(adj, support)` + `output + self.bias` at
  * GCN/GCN.py:43-45 (Graph_conv_layer.forward).
  *
- * Rows whose degree exceeds `seg_len` are "long rows": they are not reduced by
- * one wavefront but split into segments of at most `seg_len` edges described by
- * a row-split plan (gnn_spmm_plan_* below). Pass n_seg = 0 / n_long = 0 and
- * seg_len = INT64_MAX-like value when the graph has no long rows.
- *
- *   seg_row[n_seg], seg_begin[n_seg] : owning row and first edge of every segment
- *                                      (segment s ends at min(seg_begin+seg_len, rowptr[row+1]))
- *   long_row[n_long]                 : the long rows
- *   long_seg_ptr[n_long+1]           : segments of long_row[i] are [long_seg_ptr[i], long_seg_ptr[i+1])
- *   partial[n_seg * feat]            : fp32 workspace for per-segment partial rows
+ * Rows are scheduled by a row-class plan (gnn_spmm_plan_* below):
+ *   small rows (degree <= 1)       small_row/small_col/small_val[n_small]: the
+ *                                  single edge resolved (col -1 = no edge);
+ *                                  packed many rows per wavefront;
+ *   mid rows (1 < degree <= seg_len) mid_row[n_mid]: one wavefront per row;
+ *   long rows (degree > seg_len)   long_row[n_long], long_seg_ptr[n_long+1],
+ *                                  segments seg_row/seg_begin[n_seg] (segment s
+ *                                  ends at min(seg_begin+seg_len, rowptr[row+1])),
+ *                                  reduced into partial[n_seg * feat] and merged
+ *                                  in a fixed order.
+ * mid_row == NULL means "no plan": every row is reduced by one wavefront
+ * (n_seg / n_long / n_small are then ignored).
  * flags: GNN_EPI_* ; bias may be NULL.
  */
 int gnn_spmm_csr_f32(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
                      const float* x, int64_t ldx, int64_t feat, const float* bias, float* y,
                      int64_t ldy, int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin,
                      int64_t n_seg, const int32_t* long_row, const int32_t* long_seg_ptr,
-                     int64_t n_long, float* partial, uint32_t flags, void* stream);
+                     int64_t n_long, const int32_t* small_row, const int32_t* small_col,
+                     const float* small_val, int64_t n_small, const int32_t* mid_row,
+                     int64_t n_mid, float* partial, uint32_t flags, void* stream);
 
 /*
- * Row-split plan for gnn_spmm_csr_f32 / gnn_gat_csr_f32 (built once per graph).
+ * Row-class plan for gnn_spmm_csr_f32 / gnn_gat_csr_f32 (built once per graph).
  *
- * gnn_spmm_plan_count: counts long rows (degree > seg_len) and their segments.
- *   Writes two int64 counters into `counts_dev` (device memory, [2]:
- *   n_long, n_seg). The caller reads them back once (this is the only
- *   host round-trip of a plan and happens once per graph, never per forward).
- * gnn_spmm_plan_fill: fills seg_row / seg_begin / long_row / long_seg_ptr for the
- *   counts above. `scratch` needs gnn_spmm_plan_scratch_bytes(n_rows) bytes.
+ * gnn_spmm_plan_count: classifies the rows and writes four int64 counters into
+ *   `counts_dev` (device memory, [4]: n_long, n_seg, n_small, n_mid). The caller
+ *   reads them back once (the only host round-trip of a plan: once per graph,
+ *   never per forward).
+ * gnn_spmm_plan_fill: fills the lists (ascending row order) for those counts.
+ *   `scratch` needs gnn_spmm_plan_scratch_bytes(n_rows) bytes and must be the
+ *   buffer passed to gnn_spmm_plan_count.
  */
 int64_t gnn_spmm_plan_scratch_bytes(int64_t n_rows);
 int gnn_spmm_plan_count(const int64_t* rowptr, int64_t n_rows, int64_t seg_len,
                         int64_t* counts_dev, void* scratch, void* stream);
-int gnn_spmm_plan_fill(const int64_t* rowptr, int64_t n_rows, int64_t seg_len, int32_t* seg_row,
-                       int64_t* seg_begin, int32_t* long_row, int32_t* long_seg_ptr,
-                       void* scratch, void* stream);
+int gnn_spmm_plan_fill(const int64_t* rowptr, const int32_t* col, const float* val, int64_t n_rows,
+                       int64_t seg_len, int32_t* seg_row, int64_t* seg_begin, int32_t* long_row,
+                       int32_t* long_seg_ptr, int32_t* small_row, int32_t* small_col,
+                       float* small_val, int32_t* mid_row, void* scratch, void* stream);
 
 /*
  * GAT attention logits for all heads: el[n,h] = a_src[h,:] . Wh[n, h*fh:(h+1)*fh],
@@ -111,8 +117,10 @@ int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t hea
  *     rows with no edge -> 0/0 = NaN (the reference then fails its isnan assert)
  * dropout_p > 0 (training) drops numerator weights with a hash RNG keyed by
  * (dropout_seed, edge, head) and rescales by 1/(1-p), as F.dropout does.
- * Long rows use the row-split plan of gnn_spmm_plan_* with
- * partial[n_seg * (heads*fh + 2*heads)].  flags: GNN_EPI_ELU for concat=True.
+ * Rows are scheduled by the row-class plan of gnn_spmm_plan_* (small rows packed,
+ * mid rows one wave each, long rows in segments with
+ * partial[n_seg * (heads*fh + 2*heads)] merged by the log-sum-exp rule);
+ * mid_row == NULL: no plan, one wave per row. flags: GNN_EPI_ELU for concat=True.
  */
 int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows, const float* wh,
                     int64_t ldw, int64_t heads, int64_t fh, const float* el, const float* er,
@@ -120,7 +128,9 @@ int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows, c
                     float dropout_p, uint64_t dropout_seed, float* out, int64_t ldo,
                     int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin,
                     int64_t n_seg, const int32_t* long_row, const int32_t* long_seg_ptr,
-                    int64_t n_long, float* partial, uint32_t flags, void* stream);
+                    int64_t n_long, const int32_t* small_row, const int32_t* small_col,
+                    int64_t n_small, const int32_t* mid_row, int64_t n_mid, float* partial,
+                    uint32_t flags, void* stream);
 
 /*
  * Column mean of x[n_rows, feat] (double accumulation, deterministic): the dense
@@ -181,17 +191,16 @@ int gnn_sample_neighbors(const int64_t* rowptr, const int32_t* col, int64_t n_gr
 
 /* ---- developer entry (not part of the drop-in surface) ----
  * gnn_dev_spmm_variant_f32: gnn_spmm_csr_f32 at feat == 128 with a compile-time
- * kernel variant (0 shipped: U=4, non-temporal Y stores; 1 U=8; 2 U=2; 3 = 0;
- * 4 one edge per instruction (64 lanes x 8 B); 5 = 4 + U=8 + nt stores;
- * 6 U=8 + nt stores; 7 U=4 plain stores; 8 all X gathers non-temporal;
- * 9 col sign bit marks cold columns -> non-temporal gathers), for interleaved A/B
- * timing (tools/spmm_ab.py). */
+ * kernel variant (0 shipped: U=4, non-temporal Y stores; 1 U=8; 2 U=2; 7 U=4 with
+ * plain Y stores) and no epilogue, for interleaved A/B timing (tools/spmm_ab.py). */
 int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* col, const float* val,
                              int64_t n_rows, const float* x, int64_t ldx, int64_t feat,
                              const float* bias, float* y, int64_t ldy, int64_t seg_len,
                              const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
                              const int32_t* long_row, const int32_t* long_seg_ptr, int64_t n_long,
-                             float* partial, int32_t variant, void* stream);
+                             const int32_t* small_row, const int32_t* small_col,
+                             const float* small_val, int64_t n_small, const int32_t* mid_row,
+                             int64_t n_mid, float* partial, int32_t variant, void* stream);
 
 #ifdef __cplusplus
 }

@@ -47,11 +47,10 @@ def test_error_strings_and_version(lib):
 
 def test_argument_rejection_without_launch(lib):
     # null pointers / negative sizes -> GNN_E_ARG before anything reaches the device
-    rc = lib.gnn_spmm_csr_f32(None, None, None, 10, None, 4, 4, None, None, 4, 8, None, None, 0,
-                              None, None, 0, None, 0, None)
+    tail = (8, None, None, 0, None, None, 0, None, None, None, 0, None, 0, None, 0, None)
+    rc = lib.gnn_spmm_csr_f32(None, None, None, 10, None, 4, 4, None, None, 4, *tail)
     assert rc == -1
-    rc = lib.gnn_spmm_csr_f32(None, None, None, -1, None, 4, 4, None, None, 4, 8, None, None, 0,
-                              None, None, 0, None, 0, None)
+    rc = lib.gnn_spmm_csr_f32(None, None, None, -1, None, 4, 4, None, None, 4, *tail)
     assert rc == -1
     assert lib.gnn_spmm_plan_count(None, 10, 4, None, None, None) == -1
     assert lib.gnn_spmm_plan_scratch_bytes(-5) < 0

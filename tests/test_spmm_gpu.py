@@ -135,6 +135,31 @@ def test_plan_fill_matches_host(dev):
     ptr = p.long_seg_ptr.cpu().numpy()
     assert ptr[0] == 0 and ptr[-1] == len(seg_row)
     np.testing.assert_array_equal(np.diff(ptr), np.ceil(deg[deg > T] / T).astype(int))
+    small = np.nonzero(deg <= 1)[0]
+    np.testing.assert_array_equal(p.small_row.cpu().numpy(), small)
+    np.testing.assert_array_equal(p.mid_row.cpu().numpy(), np.nonzero((deg > 1) & (deg <= T))[0])
+    assert (p.small_col.cpu().numpy()[deg[small] == 0] == -1).all()
+    assert p.n_small + p.n_mid + p.n_long == deg.size
+
+
+def test_no_plan_path_matches(dev):
+    """mid_row = NULL (the INTEGRATION.md stub): every row by one wave, same result."""
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd.ops import spmm_forward
+    n, F = 2000, 64
+    rowptr, col, val = _rand_graph(n, 30 * n, 21, hub_deg=5000)
+    g = _graph(rowptr, col, val, n, dev)
+    X = torch.randn(n, F, device=dev)
+    b = torch.randn(F, device=dev)
+    y = torch.empty(n, F, device=dev)
+    lib = _lib.load()
+    rc = lib.gnn_spmm_csr_f32(g.rowptr.data_ptr(), g.col.data_ptr(), g.val.data_ptr(), n,
+                              X.data_ptr(), F, F, b.data_ptr(), y.data_ptr(), F,
+                              1, None, None, 0, None, None, 0, None, None, None, 0, None, 0,
+                              None, 0, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    close(y.cpu().numpy(), spmm_forward(g, X, b).cpu().numpy())
+    close(y.cpu().numpy(), O.spmm_csr(rowptr, col, val, X.cpu().numpy(), b.cpu().numpy()))
 
 
 def test_empty_rows_edges_and_strides(dev):

@@ -17,10 +17,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--rounds", type=int, default=8)
-    ap.add_argument("--variants", default="0,8,9")
-    ap.add_argument("--hot-mib", type=int, default=128)
+    ap.add_argument("--variants", default="0,1,7")
     ap.add_argument("--seg-lens", default="")
-    ap.add_argument("--seg-len", type=int, default=128)
+    ap.add_argument("--seg-len", type=int, default=192)
     args = ap.parse_args()
     from graphneuralnetwork_amd import _lib
     from graphneuralnetwork_amd.preprocess import gcn_normalized_csr
@@ -38,23 +37,13 @@ def main():
     stream = torch.cuda.current_stream(dev)
     nbytes = g.nnz * (8 + 4 * F) + n * (8 + 4 * F)
 
-    # hot/cold tags for variant 9: the hottest columns (by in-degree) whose rows fit HOT_MIB
-    indeg = torch.bincount(g.col.long(), minlength=n)
-    k_hot = min(n, args.hot_mib * 2**20 // (4 * F))
-    hot = torch.zeros(n, dtype=torch.bool, device=dev)
-    hot[torch.topk(indeg, k_hot).indices] = True
-    col_tag = torch.where(hot[g.col.long()], g.col, g.col | torch.tensor(-2**31, dtype=torch.int32, device=dev))
-    print(json.dumps({"hot_rows": k_hot, "hot_edge_frac": float(hot[g.col.long()].float().mean())}))
-
     def run(variant, seg_len):
         p = g.plan(seg_len)
         partial = torch.empty((max(p.n_seg, 1), F), device=dev)
-        colp = col_tag if variant == 9 else g.col
         rc = lib.gnn_dev_spmm_variant_f32(
-            g.rowptr.data_ptr(), colp.data_ptr(), g.val.data_ptr(), n, X.data_ptr(), F, F, None,
-            Y.data_ptr(), F, p.seg_len, _lib.ptr(p.seg_row), _lib.ptr(p.seg_begin), p.n_seg,
-            _lib.ptr(p.long_row), p.long_seg_ptr.data_ptr(), p.n_long, partial.data_ptr(),
-            variant, stream.cuda_stream)
+            g.rowptr.data_ptr(), g.col.data_ptr(), g.val.data_ptr(), n, X.data_ptr(), F, F, None,
+            Y.data_ptr(), F, p.seg_len, *p.args(), partial.data_ptr(), variant,
+            stream.cuda_stream)
         _lib.check(rc, "variant")
 
     configs = [(v, args.seg_len) for v in map(int, args.variants.split(","))] + \
