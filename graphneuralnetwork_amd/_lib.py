@@ -53,8 +53,23 @@ SIGNATURES: dict[str, tuple] = {
         _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
         _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
         _vp, _vp, _i64,                 # small_row, small_col, n_small
-        _vp, _i64, _vp,                 # mid_row, n_mid, partial
+        _vp, _i64, _vp, _vp,            # mid_row, n_mid, partial, stats
         _u32, _vp]),                    # flags, stream
+    "gnn_gat_backward_prep_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp,
+                                                 _vp]),
+    "gnn_gat_backward_edges_f32": (ctypes.c_int, [
+        _vp, _vp, _i64, _vp, _i64, _i64, _i64,      # rowptr, col, n_rows, wh, ldw, heads, fh
+        _vp, _vp, _vp, _vp, _vp,                    # el, er, lse, dout, D
+        ctypes.c_float, _i32, ctypes.c_float, ctypes.c_uint64,  # slope, mode, drop_p, seed
+        _vp, _vp, _vp,                              # w_edge, ds_edge, del
+        _i64, _vp, _vp, _i64, _vp, _vp, _i64,       # seg_len, seg_row, seg_begin, n_seg, long...
+        _vp, _i64, _vp, _vp]),                      # rows, n_rows_list, del_part, stream
+    "gnn_gat_backward_nodes_f32": (ctypes.c_int, [
+        _vp, _vp, _vp, _i64, _i64, _i64,            # rowptr_t, src_t, eid_t, n, heads, fh
+        _vp, _vp, _vp, _vp, _vp, _vp,               # dout, w_edge, ds_edge, del, a_src, a_dst
+        _vp, _vp,                                   # dwh, der
+        _i64, _vp, _vp, _i64, _vp, _vp, _i64,       # plan of the transposed graph
+        _vp, _i64, _vp, _vp]),                      # rows, n_rows_list, part, stream
     "gnn_col_mean_scratch_bytes": (_i64, [_i64, _i64]),
     "gnn_col_mean_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
     "gnn_sage_aggregate_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _i64,

@@ -95,6 +95,8 @@ struct GatParams {
   float* partial;  // per segment: [feat acc][heads l][heads m]
   int64_t ldp;
   uint32_t flags;
+  float* stats;    // optional [n_rows, lds]: per-head log-sum-exp of the row (backward)
+  int64_t lds;
 };
 
 constexpr int kGatSmallUnroll = 4;
@@ -136,6 +138,16 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
       const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
       if (f >= P.feat) continue;
       typename Vec<VW>::T r;
+      if (P.stats && f % P.fh == 0) {  // one lane per head records the row's log-sum-exp
+        const int h = static_cast<int>(f / P.fh);
+        float lse = -INFINITY;
+        if (cols[u] >= 0) {
+          const float sv = P.el[rows[u] * P.lde + h] + P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
+          const float x = sv > 0.f ? sv : P.slope * sv;
+          lse = SPARSE ? -x : x;
+        }
+        P.stats[rows[u] * P.lds + h] = lse;
+      }
       if (cols[u] < 0) {
         r = (!SPARSE && P.empty_fill) ? vload<VW>(P.empty_fill + f) : typename Vec<VW>::T(NAN);
       } else if (SPARSE) {
@@ -290,6 +302,8 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
     }
     return;
   }
+  if (P.stats && lane < HP && head_ok)
+    P.stats[row * P.lds + lane] = end == beg ? -INFINITY : (SPARSE ? 0.f : m) + __logf(lsum);
   const bool empty = end == beg;
   float lh[NCH];
 #pragma unroll
@@ -312,32 +326,107 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
   }
 }
 
-// Merge the (acc, l, m) partial states of each long row (log-sum-exp rule; m = 0 for sparse).
+// Merge the (acc, l, m) partial states of each long row with the log-sum-exp rule
+// (m = 0 for sparse). One workgroup per long row: pass 1 takes the max of the
+// segment maxima, pass 2 sums the rescaled partials; segments are spread over
+// the 4 waves x EPI slots and combined in a fixed order (xor tree, then LDS):
+// no serial tail for the hub rows, bitwise reproducible.
 template <int VW, int LPR, int NCH, bool SPARSE>
 __global__ __launch_bounds__(kGatBlock) void gat_fixup_kernel(GatParams P) {
+  constexpr int EPI = kWave / LPR;
+  constexpr int STRIDE = kGatWaves * EPI;
+  __shared__ typename Vec<VW>::T red_a[kGatWaves][NCH][LPR];
+  __shared__ float red_s[kGatWaves][NCH][LPR];
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kGatWaves + (threadIdx.x >> 6);
-  if (i >= P.n_long || lane >= LPR) return;
-  const int sub = lane;
+  const int wid = threadIdx.x >> 6;
+  const int64_t i = blockIdx.x;
+  if (i >= P.n_long) return;
+  const int sub = lane & (LPR - 1);
+  const int grp = lane / LPR;
   const int32_t s0 = P.long_seg_ptr[i], s1 = P.long_seg_ptr[i + 1];
   const int64_t row = P.long_row[i];
+  int hid[NCH];
+  float M[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+    hid[ch] = f < P.feat ? static_cast<int>(f / P.fh) : 0;
+    M[ch] = SPARSE ? 0.f : -INFINITY;
+  }
+  if (!SPARSE) {  // pass 1: max of the segment maxima per head
+    for (int32_t s = s0 + wid * EPI + grp; s < s1; s += STRIDE) {
+      const float* pm = P.partial + static_cast<int64_t>(s) * P.ldp + P.feat + P.heads;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) M[ch] = fmaxf(M[ch], pm[hid[ch]]);
+    }
+#pragma unroll
+    for (int o = LPR; o < kWave; o <<= 1) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) M[ch] = fmaxf(M[ch], __shfl_xor(M[ch], o, kWave));
+    }
+    if (lane < LPR) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) red_s[wid][ch][lane] = M[ch];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      float v = red_s[0][ch][sub];
+#pragma unroll
+      for (int w = 1; w < kGatWaves; ++w) v = fmaxf(v, red_s[w][ch][sub]);
+      M[ch] = v;
+    }
+    __syncthreads();
+  }
+  // pass 2: rescaled sums of acc and l
+  typename Vec<VW>::T a[NCH];
+  float l[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    a[ch] = vzero<VW>();
+    l[ch] = 0.f;
+  }
+  for (int32_t s = s0 + wid * EPI + grp; s < s1; s += STRIDE) {
+    const float* pr = P.partial + static_cast<int64_t>(s) * P.ldp;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+      if (f >= P.feat) continue;
+      const float sc = SPARSE ? 1.f : __expf(pr[P.feat + P.heads + hid[ch]] - M[ch]);
+      a[ch] += sc * vload<VW>(pr + f);
+      l[ch] += sc * pr[P.feat + hid[ch]];
+    }
+  }
+#pragma unroll
+  for (int o = LPR; o < kWave; o <<= 1) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      a[ch] += shfl_xor_f(a[ch], o);
+      l[ch] += __shfl_xor(l[ch], o, kWave);
+    }
+  }
+  if (lane < LPR) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      red_a[wid][ch][lane] = a[ch];
+      red_s[wid][ch][lane] = l[ch];
+    }
+  }
+  __syncthreads();
+  if (wid != 0 || lane >= LPR) return;
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
     if (f >= P.feat) continue;
-    const int h = static_cast<int>(f / P.fh);
-    float M = SPARSE ? 0.f : -INFINITY;
-    if (!SPARSE)
-      for (int32_t s = s0; s < s1; ++s) M = fmaxf(M, P.partial[s * P.ldp + P.feat + P.heads + h]);
-    typename Vec<VW>::T a = vzero<VW>();
-    float l = 0.f;
-    for (int32_t s = s0; s < s1; ++s) {
-      const float* pr = P.partial + static_cast<int64_t>(s) * P.ldp;
-      const float sc = SPARSE ? 1.f : __expf(pr[P.feat + P.heads + h] - M);
-      a += sc * vload<VW>(pr + f);
-      l += sc * pr[P.feat + h];
+    typename Vec<VW>::T av = red_a[0][ch][lane];
+    float lv = red_s[0][ch][lane];
+#pragma unroll
+    for (int w = 1; w < kGatWaves; ++w) {
+      av += red_a[w][ch][lane];
+      lv += red_s[w][ch][lane];
     }
-    typename Vec<VW>::T r = a / l;
+    if (P.stats && f % P.fh == 0) P.stats[row * P.lds + hid[ch]] = M[ch] + __logf(lv);
+    typename Vec<VW>::T r = av / lv;
 #pragma unroll
     for (int k = 0; k < VW; ++k) vset(r, k, act_apply(vget(r, k), P.flags));
     vstore<VW>(P.out + row * P.ldo + f, r);
@@ -363,8 +452,7 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
                        dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), 0, s, Q);
   if (P.n_long > 0)
     hipLaunchKernelGGL((gat_fixup_kernel<VW, LPR, NCH, SPARSE>),
-                       dim3(static_cast<unsigned>((P.n_long + kGatWaves - 1) / kGatWaves)),
-                       dim3(kGatBlock), 0, s, Q);
+                       dim3(static_cast<unsigned>(P.n_long)), dim3(kGatBlock), 0, s, Q);
 }
 
 template <int VW, int HP, bool SPARSE>
@@ -491,7 +579,7 @@ extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_
                                const int32_t* long_row, const int32_t* long_seg_ptr,
                                int64_t n_long, const int32_t* small_row, const int32_t* small_col,
                                int64_t n_small, const int32_t* mid_row, int64_t n_mid,
-                               float* partial, uint32_t flags, void* stream) {
+                               float* partial, float* stats, uint32_t flags, void* stream) {
   if (n_rows < 0 || heads < 1 || fh < 1 || seg_len < 1 || n_seg < 0 || n_long < 0 || n_small < 0)
     return GNN_E_ARG;
   const bool plan = mid_row != nullptr;
@@ -552,6 +640,8 @@ extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_
     P.partial = partial ? partial + g * (kMaxHeads * fh + 2 * kMaxHeads) : nullptr;
     P.ldp = ldp;  // same row stride for every group
     P.flags = flags;
+    P.stats = stats ? stats + h0 : nullptr;
+    P.lds = heads;
     const bool vec4 = (fh % 4 == 0) && (ldw % 4 == 0) && (ldo % 4 == 0) && aligned_to(P.wh, 16) &&
                       aligned_to(P.out, 16) &&
                       (P.empty_fill == nullptr || aligned_to(P.empty_fill, 16)) &&

@@ -20,9 +20,10 @@ MFMA), one HIP launch for the attention logits, one HIP launch for the fused
 edge-softmax + aggregation (+ ELU) over the CSR adjacency.  ``adj`` may be the
 reference's dense tensor, a torch sparse tensor or a ``CsrGraph``.
 
-Forward only: autograd through these layers is not implemented yet
-(backward kernels are the next row of the plan); a forward with gradients
-enabled on trainable parameters raises.
+Training: the aggregation is an autograd Function whose backward is three
+more HIP passes (gat_bwd.hip: ELU/softmax backward, SDDMM edge gradients,
+transposed aggregation), with the forward's per-row log-sum-exp and dropout
+seed saved instead of the attention matrix; dropout masks are recomputed.
 """
 from __future__ import annotations
 
@@ -31,7 +32,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
-from .ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_logits
+from .ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_backward, gat_logits
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
@@ -39,11 +40,34 @@ from .ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_logits
 SPARSE_NAN_CHECK = True
 
 
-def _no_autograd(module: nn.Module) -> None:
-    if torch.is_grad_enabled() and any(p.requires_grad for p in module.parameters()):
-        raise NotImplementedError(
-            f"{type(module).__name__}: the MI355X GAT path is forward-only for now; run it under "
-            "torch.no_grad() / torch.inference_mode() or freeze its parameters")
+class _GatLayerFn(torch.autograd.Function):
+    """Fused attention layer: Wh, a_src, a_dst -> act(edge-softmax aggregation)."""
+
+    @staticmethod
+    def forward(ctx, Wh, a_src, a_dst, g, heads, fh, slope, mode, activation, drop_p, seed):
+        el, er = gat_logits(Wh, heads, fh, a_src, a_dst)
+        stats = torch.empty((g.n_rows, heads), dtype=torch.float32, device=Wh.device)
+        out = gat_aggregate(g, Wh, el, er, heads, fh, slope, mode, activation,
+                            dropout_p=drop_p, seed=seed, stats=stats)
+        ctx.save_for_backward(Wh, a_src, a_dst, el, er, stats, out)
+        ctx.cfg = (g, heads, fh, slope, mode, activation, drop_p, seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        Wh, a_src, a_dst, el, er, stats, out = ctx.saved_tensors
+        g, heads, fh, slope, mode, activation, drop_p, seed = ctx.cfg
+        dwh, dout, dl, der = gat_backward(g, Wh, el, er, stats, out, dy, a_src, a_dst, heads, fh,
+                                          slope, mode, activation == "elu", drop_p, seed)
+        n = Wh.shape[0]
+        W3 = Wh.detach().view(n, heads, fh)
+        da_src = (dl.unsqueeze(-1) * W3).sum(0).reshape(-1)   # el = a_src . Wh
+        da_dst = (der.unsqueeze(-1) * W3).sum(0).reshape(-1)  # er = a_dst . Wh
+        if mode == GAT_DENSE and g.has_empty_rows():
+            # an edgeless row is the uniform average of every row (layers.py:29-32)
+            empty = (g.rowptr[1:] - g.rowptr[:-1]) == 0
+            dwh = dwh + dout[empty].sum(0) / n
+        return dwh, da_src, da_dst, None, None, None, None, None, None, None, None
 
 
 def _dropout_seed() -> int:
@@ -61,16 +85,21 @@ class _AttentionBase(nn.Module):
 
     def _aggregate(self, Wh, adj, heads, fh, a_src, a_dst, activation, dropout_p):
         g = as_csr(adj, self.PREDICATE)
-        el, er = gat_logits(Wh, heads, fh, a_src, a_dst)
         p = dropout_p if self.training else 0.0
-        out = gat_aggregate(g, Wh, el, er, heads, fh, self.alpha, self.MODE, activation,
-                            dropout_p=p, seed=_dropout_seed() if p > 0 else 0)
+        seed = _dropout_seed() if p > 0 else 0
+        if torch.is_grad_enabled() and (Wh.requires_grad or a_src.requires_grad
+                                        or a_dst.requires_grad):
+            out = _GatLayerFn.apply(Wh, a_src, a_dst, g, heads, fh, self.alpha, self.MODE,
+                                    activation, p, seed)
+        else:
+            el, er = gat_logits(Wh, heads, fh, a_src, a_dst)
+            out = gat_aggregate(g, Wh, el, er, heads, fh, self.alpha, self.MODE, activation,
+                                dropout_p=p, seed=seed)
         if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
             assert not torch.isnan(out).any()
         return out
 
     def forward(self, h, adj, activation: str | None = "__concat__"):
-        _no_autograd(self)
         if activation == "__concat__":
             activation = "elu" if self.concat else None
         Wh = torch.mm(h, self.W)
@@ -147,8 +176,6 @@ class GATBase(nn.Module):
                       and m._drop_p() == first._drop_p() for m in heads)
         if not uniform:
             return torch.cat([att(x, adj) for att in heads], dim=1)
-        for m in heads:
-            _no_autograd(m)
         fh = first.out_features
         W = torch.cat([m.W for m in heads], dim=1)          # [in, H*fh]
         Wh = torch.mm(x, W)                                  # one MFMA GEMM for all heads

@@ -68,6 +68,12 @@ class RowSplitPlan:
     def n_mid(self) -> int:
         return int(self.mid_row.numel())
 
+    def row_list(self) -> torch.Tensor:
+        """mid + small rows (every row that is not split into segments)."""
+        if not hasattr(self, "_row_list"):
+            self._row_list = torch.cat([self.mid_row, self.small_row]).contiguous()
+        return self._row_list
+
     def args(self):
         """The plan arguments of gnn_spmm_csr_f32 / gnn_gat_csr_f32 (after seg_len)."""
         from ._lib import ptr
@@ -131,6 +137,25 @@ class CsrGraph:
             self._transpose = from_coo(self.col.to(torch.int64), rows, self.val,
                                        self.n_cols, self.n_rows)
         return self._transpose
+
+    def transpose_eid(self):
+        """(rowptr_t, src_t int32, eid_t int64, plan-able CsrGraph of A^T) -- the GAT
+        backward's column view: for node j, the CSR edges (i, j) and their ids."""
+        t = self._plans.get("_transpose_eid")
+        if t is None:
+            rows = torch.repeat_interleave(
+                torch.arange(self.n_rows, device=self.device, dtype=torch.int64),
+                self.rowptr[1:] - self.rowptr[:-1])
+            eid = torch.argsort(self.col.to(torch.int64), stable=True)
+            rowptr_t = torch.zeros(self.n_cols + 1, dtype=torch.int64, device=self.device)
+            torch.cumsum(torch.bincount(self.col.to(torch.int64), minlength=self.n_cols), 0,
+                         out=rowptr_t[1:])
+            src_t = rows[eid].to(torch.int32).contiguous()
+            gt = CsrGraph(rowptr_t, src_t, torch.ones(src_t.numel(), device=self.device),
+                          self.n_cols, self.n_rows)
+            t = (rowptr_t, src_t, eid.contiguous(), gt)
+            self._plans["_transpose_eid"] = t
+        return t
 
     def to(self, device) -> "CsrGraph":
         return CsrGraph(self.rowptr.to(device), self.col.to(device), self.val.to(device),

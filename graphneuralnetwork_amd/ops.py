@@ -141,7 +141,8 @@ def col_mean(x: torch.Tensor) -> torch.Tensor:
 def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tensor, heads: int,
                   fh: int, negative_slope: float, mode: int, activation: str | None = None,
                   dropout_p: float = 0.0, seed: int = 0, seg_len: int | None = None,
-                  out: torch.Tensor | None = None) -> torch.Tensor:
+                  out: torch.Tensor | None = None,
+                  stats: torch.Tensor | None = None) -> torch.Tensor:
     """Fused edge-softmax + neighbour aggregation for all heads (one HIP launch + fix-up)."""
     _require_device(g.rowptr, wh, el, er, out)
     wh = _rows_f32(wh, "Wh")
@@ -175,7 +176,7 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
         el.data_ptr(), er.data_ptr(), heads, float(negative_slope), int(mode), _lib.ptr(fill),
         float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), out.stride(0),
         plan.seg_len, *pa[:6], pa[6], pa[7], pa[9], pa[10], pa[11], _lib.ptr(partial),
-        _ACT_FLAGS[activation], _lib.stream_handle(wh.device))
+        _lib.ptr(stats), _ACT_FLAGS[activation], _lib.stream_handle(wh.device))
     _lib.check(rc, "gnn_gat_csr_f32")
     return out
 
@@ -267,3 +268,63 @@ def gather_rows(x: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = N
     if check:
         _check_err(err, "gather_rows")
     return out
+
+
+# ---------------------------------------------------------------- GAT backward
+def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tensor,
+                 stats: torch.Tensor, y: torch.Tensor, dy: torch.Tensor, a_src: torch.Tensor,
+                 a_dst: torch.Tensor, heads: int, fh: int, negative_slope: float, mode: int,
+                 elu: bool, dropout_p: float = 0.0, seed: int = 0,
+                 seg_len: int | None = None):
+    """dWh (incl. the el/er terms), del, der for one GAT layer (three HIP passes).
+
+    Returns (dwh [N, H*fh], dout [N, H*fh], del [N, H], der [N, H])."""
+    _require_device(wh, dy)
+    n = g.n_rows
+    feat = heads * fh
+    dev = wh.device
+    lib = _lib.load()
+    stream = _lib.stream_handle(dev)
+    dy = dy.contiguous()
+    y = y.contiguous()
+    dout = torch.empty((n, feat), dtype=torch.float32, device=dev)
+    D = torch.empty((n, heads), dtype=torch.float32, device=dev)
+    _lib.check(lib.gnn_gat_backward_prep_f32(dy.data_ptr(), y.data_ptr(), feat, n, heads, fh,
+                                             int(elu), dout.data_ptr(), D.data_ptr(), stream),
+               "gnn_gat_backward_prep_f32")
+    sl = seg_len if seg_len is not None else seg_len_for(feat)
+    plan = g.plan(sl)
+    E = g.nnz
+    w_edge = torch.empty((max(E, 1), heads), dtype=torch.float32, device=dev)
+    ds_edge = torch.empty((max(E, 1), heads), dtype=torch.float32, device=dev)
+    dl = torch.zeros((n, heads), dtype=torch.float32, device=dev)
+    del_part = torch.empty((max(plan.n_seg, 1), heads), dtype=torch.float32, device=dev)
+    rows = plan.row_list()
+    _lib.check(lib.gnn_gat_backward_edges_f32(
+        g.rowptr.data_ptr(), g.col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
+        el.data_ptr(), er.data_ptr(), stats.data_ptr(), dout.data_ptr(), D.data_ptr(),
+        float(negative_slope), int(mode), float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF,
+        w_edge.data_ptr(), ds_edge.data_ptr(), dl.data_ptr(), plan.seg_len,
+        _lib.ptr(plan.seg_row), _lib.ptr(plan.seg_begin), plan.n_seg, _lib.ptr(plan.long_row),
+        plan.long_seg_ptr.data_ptr(), plan.n_long, _lib.ptr(rows), rows.numel(),
+        del_part.data_ptr(), stream), "gnn_gat_backward_edges_f32")
+    rowptr_t, src_t, eid_t, gt = g.transpose_eid()
+    pt = gt.plan(sl)
+    rows_t = pt.row_list()
+    dwh = torch.empty((n, feat), dtype=torch.float32, device=dev)
+    der = torch.zeros((n, heads), dtype=torch.float32, device=dev)
+    part = torch.empty((max(pt.n_seg, 1), feat + heads), dtype=torch.float32, device=dev)
+    a_src = a_src.contiguous().float()
+    a_dst = a_dst.contiguous().float()
+    for h0 in range(0, heads, 8):  # the node pass takes <= 8 heads per call
+        hg = min(8, heads - h0)
+        if hg != heads:
+            raise NotImplementedError("GAT backward with more than 8 heads")
+        _lib.check(lib.gnn_gat_backward_nodes_f32(
+            rowptr_t.data_ptr(), src_t.data_ptr(), eid_t.data_ptr(), n, heads, fh,
+            dout.data_ptr(), w_edge.data_ptr(), ds_edge.data_ptr(), dl.data_ptr(),
+            a_src.data_ptr(), a_dst.data_ptr(), dwh.data_ptr(), der.data_ptr(), pt.seg_len,
+            _lib.ptr(pt.seg_row), _lib.ptr(pt.seg_begin), pt.n_seg, _lib.ptr(pt.long_row),
+            pt.long_seg_ptr.data_ptr(), pt.n_long, _lib.ptr(rows_t), rows_t.numel(),
+            part.data_ptr(), stream), "gnn_gat_backward_nodes_f32")
+    return dwh, dout, dl, der

@@ -121,6 +121,9 @@ int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t hea
  * mid rows one wave each, long rows in segments with
  * partial[n_seg * (heads*fh + 2*heads)] merged by the log-sum-exp rule);
  * mid_row == NULL: no plan, one wave per row. flags: GNN_EPI_ELU for concat=True.
+ * stats (nullable, [n_rows, heads]): per-(row, head) log-sum-exp of the attention
+ * logits (dense: max + log sum exp; sparse: log sum exp(-LeakyReLU)), -inf for an
+ * edgeless row -- saved by training forwards for gnn_gat_backward_*.
  */
 int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows, const float* wh,
                     int64_t ldw, int64_t heads, int64_t fh, const float* el, const float* er,
@@ -130,7 +133,7 @@ int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows, c
                     int64_t n_seg, const int32_t* long_row, const int32_t* long_seg_ptr,
                     int64_t n_long, const int32_t* small_row, const int32_t* small_col,
                     int64_t n_small, const int32_t* mid_row, int64_t n_mid, float* partial,
-                    uint32_t flags, void* stream);
+                    float* stats, uint32_t flags, void* stream);
 
 /*
  * Column mean of x[n_rows, feat] (double accumulation, deterministic): the dense
@@ -140,6 +143,44 @@ int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows, c
 int64_t gnn_col_mean_scratch_bytes(int64_t n_rows, int64_t feat);
 int gnn_col_mean_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t feat, float* out,
                      void* scratch, void* stream);
+
+/*
+ * GAT backward (training through GraphAttentionLayer / SpGraphAttentionLayer;
+ * replaces ATen autograd of GAT/models/layers.py:22-37 and
+ * SpecialSpmmFunction.backward, layers.py:54-64). With per head
+ *   out_i = sum_j m_ij a_ij Wh_j, a_ij = exp(z_ij - lse_i), z = +-LeakyReLU(el_i + er_j):
+ * prep : dout = dy * ELU'(out) (elu != 0; out recovered from y), D_i = dout_i . out_i
+ *        (dout [n, heads*fh], D [n, heads]);
+ * edges: over CSR rows (plan segments + `rows` = every other row), per edge e and head:
+ *        w_edge[e,h] = m a, ds_edge[e,h] = a (m dout_i.Wh_j - D_i) dz/ds, del[i,h] = sum_e ds
+ *        (del_part [n_seg, heads] workspace for long rows);
+ * nodes: over the transposed CSR (rowptr_t, src_t = source row, eid_t = CSR edge id)
+ *        with its own plan: dwh[j] = sum_e w_edge[e,h] dout_i + der_j a_dst + del_j a_src,
+ *        der[j,h] = sum_e ds_edge[e,h] (part [n_seg_t, heads*fh + heads] workspace);
+ *        heads <= 8 per call.
+ * The dropout mask is recomputed from (dropout_seed, edge, head) exactly as the forward drew it.
+ */
+int gnn_gat_backward_prep_f32(const float* dy, const float* y, int64_t ldo, int64_t n_rows,
+                              int64_t heads, int64_t fh, int32_t elu, float* dout, float* D,
+                              void* stream);
+int gnn_gat_backward_edges_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                               const float* wh, int64_t ldw, int64_t heads, int64_t fh,
+                               const float* el, const float* er, const float* lse,
+                               const float* dout, const float* D, float negative_slope,
+                               int32_t mode, float dropout_p, uint64_t dropout_seed,
+                               float* w_edge, float* ds_edge, float* del, int64_t seg_len,
+                               const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
+                               const int32_t* long_row, const int32_t* long_seg_ptr,
+                               int64_t n_long, const int32_t* rows, int64_t n_rows_list,
+                               float* del_part, void* stream);
+int gnn_gat_backward_nodes_f32(const int64_t* rowptr_t, const int32_t* src_t,
+                               const int64_t* eid_t, int64_t n_nodes, int64_t heads, int64_t fh,
+                               const float* dout, const float* w_edge, const float* ds_edge,
+                               const float* del, const float* a_src, const float* a_dst,
+                               float* dwh, float* der, int64_t seg_len, const int32_t* seg_row,
+                               const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
+                               const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows,
+                               int64_t n_rows_list, float* part, void* stream);
 
 /* ---- GraphSAGE aggregation modes ---- */
 #define GNN_SAGE_MEAN 0   /* torch.mean(neigh_feat, dim=1)               -> fp32 out  */
