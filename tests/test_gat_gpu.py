@@ -196,18 +196,19 @@ def test_gat_backward_vs_torch(dev, heads, fh, sparse, seg_len):
     close(a_d.grad.cpu().numpy(), adt.grad.numpy(), rtol=2e-4)
 
 
-def test_gat_model_trains(golden, dev):
-    """GAT drop-in under autograd: reference state_dict, loss decreases with SGD."""
-    from graphneuralnetwork_amd.gat import SpGAT
+@pytest.mark.parametrize("kind", ["dense", "sparse"])
+def test_gat_model_trains(golden, dev, kind):
+    """GAT drop-in under autograd (train mode, dropout 0.6): loss decreases with SGD."""
+    from graphneuralnetwork_amd.gat import GAT, SpGAT
     g = golden("gat")
     n = int(g["n"])
     A = torch.from_numpy(_dense(g, "adj", n)).to(dev)
     h = torch.from_numpy(g["h"]).to(dev)
-    model = SpGAT(64, 8, 7, 0.6, float(g["alpha"]), 8).to(dev)
-    _load_heads(model, g, "sparse")
+    model = (GAT if kind == "dense" else SpGAT)(64, 8, 7, 0.6, float(g["alpha"]), 8).to(dev)
+    _load_heads(model, g, kind)
     model.to(dev).train()
     labels = torch.from_numpy(np.random.default_rng(0).integers(0, 7, n)).to(dev)
-    opt = torch.optim.SGD(model.parameters(), lr=0.5)
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
     losses = []
     torch.manual_seed(0)
     for _ in range(30):
@@ -215,5 +216,51 @@ def test_gat_model_trains(golden, dev):
         loss = torch.nn.functional.cross_entropy(model(h, A), labels)
         loss.backward()
         opt.step()
-        losses.append(float(loss))
-    assert all(np.isfinite(losses)) and losses[-1] < losses[0]
+        losses.append(float(loss.detach()))
+    assert all(np.isfinite(losses)) and np.mean(losses[-5:]) < np.mean(losses[:5])
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gat_dropout_backward_exact(dev, sparse):
+    """With dropout the backward must use the forward's mask: recover the mask by running
+    the forward on an identity Wh (out = m * alpha), then check gradients against torch."""
+    from graphneuralnetwork_amd.gat import _GatLayerFn
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_logits
+    n, p, seed = 64, 0.4, 1234
+    rng = np.random.default_rng(3)
+    s = np.concatenate([rng.integers(0, n, 600), np.arange(n)])
+    d = np.concatenate([rng.integers(0, n, 600), np.arange(n)])
+    key = np.unique(s * n + d)
+    rowptr, col, _ = O.coo_to_csr(key // n, key % n, np.ones(key.size, np.float32), n)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.ones(col.size, device=dev), n, n)
+    mode = GAT_SPARSE if sparse else GAT_DENSE
+    # mask: the logits do not depend on Wh when a_src = a_dst = 0 -> alpha = uniform
+    eye = torch.eye(n, device=dev)
+    z = torch.zeros(n, 1, device=dev)
+    masked = gat_aggregate(g, eye, z, z, 1, n, 0.2, mode, dropout_p=p, seed=seed)
+    plain = gat_aggregate(g, eye, z, z, 1, n, 0.2, mode)
+    M = torch.where(plain > 0, masked / plain, torch.zeros_like(plain)).double().cpu()
+    mask = torch.zeros(n, n, dtype=torch.bool)
+    mask[key // n, key % n] = True
+    Wh0 = torch.randn(n, n, dtype=torch.float64) * 0.5
+    as0 = torch.randn(n, dtype=torch.float64) * 0.2
+    ad0 = torch.randn(n, dtype=torch.float64) * 0.2
+    R = torch.randn(n, n, dtype=torch.float64)
+    Wh = Wh0.float().to(dev).requires_grad_()
+    a_s = as0.float().to(dev).requires_grad_()
+    a_d = ad0.float().to(dev).requires_grad_()
+    out = _GatLayerFn.apply(Wh, a_s, a_d, g, 1, n, 0.2, mode, None, p, seed)
+    (out * R.float().to(dev)).sum().backward()
+    Wt, ast, adt = (t.clone().requires_grad_() for t in (Wh0, as0, ad0))
+    el = Wt @ ast
+    er = Wt @ adt
+    x = torch.nn.functional.leaky_relu(el[:, None] + er[None, :], 0.2)
+    zz = (-x if sparse else x).masked_fill(~mask, float("-inf"))
+    ref = (M * torch.softmax(zz, dim=1)) @ Wt
+    (ref * R).sum().backward()
+    close(out.detach().cpu().numpy(), ref.detach().numpy())
+    close(Wh.grad.cpu().numpy(), Wt.grad.numpy(), rtol=2e-4)
+    close(a_s.grad.cpu().numpy(), ast.grad.numpy(), rtol=2e-4)
+    close(a_d.grad.cpu().numpy(), adt.grad.numpy(), rtol=2e-4)
