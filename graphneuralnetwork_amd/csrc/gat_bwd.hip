@@ -56,9 +56,12 @@ __global__ __launch_bounds__(256) void gat_bwd_prep_kernel(const float* __restri
   for (int64_t f = 0; f < fh; ++f) {
     const float yv = yr[f], g = dyr[f];
     float d = g, o = yv;
-    if (elu) {
-      d = yv > 0.f ? g : g * (yv + 1.f);  // ELU'(x) = exp(x) = y + 1 for x <= 0
-      o = yv > 0.f ? yv : log1pf(yv);
+    if (elu && yv <= 0.f) {
+      // ELU'(x) = exp(x) = y + 1 for x <= 0, and x = log1p(y); a saturated y = -1
+      // (x < -17 in fp32) has ELU' = 0: its D term is 0 * log(0) := 0, not NaN.
+      const float t = yv + 1.f;
+      d = g * t;
+      o = t > 0.f ? log1pf(yv) : 0.f;
     }
     dr[f] = d;
     acc = fmaf(d, o, acc);
