@@ -179,3 +179,62 @@ class EdgeCutSpmm:
         self._spmm(p.halo, self.recv_buf, None, activation=activation, out=self.out,
                    accumulate=True)
         return self.out
+
+
+def extended_graph(part: EdgeCutPartition) -> CsrGraph:
+    """Rank-local CSR over [own rows | halo slots]: rows = owned rows, columns
+    0..n_own-1 = owned nodes, n_own + k = halo slot k (interior edges first in each row)."""
+    g = getattr(part, "_ext", None)
+    if g is None:
+        dev = part.interior.device
+        parts = []
+        for csr, off in ((part.interior, 0), (part.halo, part.n_own)):
+            rows = torch.repeat_interleave(torch.arange(part.n_own, device=dev, dtype=torch.int64),
+                                           csr.rowptr[1:] - csr.rowptr[:-1])
+            parts.append((rows, csr.col.to(torch.int64) + off, csr.val))
+        g = from_coo(torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts]),
+                     torch.cat([p[2] for p in parts]), part.n_own, part.n_own + part.n_halo)
+        part._ext = g
+    return g
+
+
+class EdgeCutGat:
+    """One GAT attention layer (all heads) on one rank of the edge-cut.
+
+    The halo rows of Wh AND of the column logits er are packed into one buffer
+    and exchanged with a single all-to-all-v; the fused edge-softmax aggregation
+    then runs over the rank's extended graph [own | halo] (the softmax of a row
+    needs all its edges, so the interior and halo edges are reduced together).
+    """
+
+    def __init__(self, part: EdgeCutPartition, heads: int, fh: int, device, group=None,
+                 logits=None, aggregate=None, gather=None):
+        self.part = part
+        self.heads, self.fh = heads, fh
+        self.group = group
+        self.device = torch.device(device)
+        if logits is None or aggregate is None or gather is None:
+            from .ops import gat_aggregate, gat_logits, gather_rows
+            logits = logits or gat_logits
+            aggregate = aggregate or gat_aggregate
+            gather = gather or (lambda x, idx, out: gather_rows(x, idx, out=out, check=False))
+        self._logits, self._aggregate, self._gather = logits, aggregate, gather
+        w = heads * fh + heads
+        self.send_buf = torch.empty((part.send_idx.numel(), w), dtype=torch.float32,
+                                    device=self.device)
+        self.recv_buf = torch.empty((part.n_halo, w), dtype=torch.float32, device=self.device)
+        self.ext = extended_graph(part)
+
+    def __call__(self, wh_own: torch.Tensor, a_src: torch.Tensor, a_dst: torch.Tensor,
+                 negative_slope: float, mode: int, activation: str | None = None):
+        p = self.part
+        F = self.heads * self.fh
+        el, er = self._logits(wh_own, self.heads, self.fh, a_src, a_dst)
+        packed = torch.cat([wh_own, er], dim=1)
+        if p.send_idx.numel():
+            self._gather(packed, p.send_idx, self.send_buf)
+        _all_to_all_v(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts, self.group)
+        wh_ext = torch.cat([wh_own, self.recv_buf[:, :F]], dim=0)
+        er_ext = torch.cat([er, self.recv_buf[:, F:]], dim=0)
+        return self._aggregate(self.ext, wh_ext, el, er_ext, self.heads, self.fh,
+                               negative_slope, mode, activation)

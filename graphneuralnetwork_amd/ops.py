@@ -149,12 +149,10 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
     n = g.n_rows
     if wh.shape[0] != g.n_cols or wh.shape[1] != heads * fh:
         raise ValueError("Wh must be [n_cols, heads * fh]")
-    if g.n_rows != g.n_cols:
-        raise ValueError("GAT attention needs a square adjacency")
     el = el.contiguous()
     er = er.contiguous()
-    if el.shape != (n, heads) or er.shape != (n, heads):
-        raise ValueError("el / er must be [N, heads]")
+    if el.shape != (n, heads) or er.shape != (g.n_cols, heads):
+        raise ValueError("el must be [n_rows, heads] and er [n_cols, heads]")
     feat = heads * fh
     if out is None:
         out = torch.empty((n, feat), dtype=torch.float32, device=wh.device)

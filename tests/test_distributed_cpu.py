@@ -120,3 +120,61 @@ def test_nnz_balanced_bounds():
     rowptr = torch.from_numpy(np.concatenate([[0], np.cumsum(deg)]))
     b = nnz_balanced_bounds(rowptr, 4).tolist()
     assert b[0] == 0 and b[-1] == 10 and b == sorted(b)
+
+
+def _cpu_gat_logits(wh, heads, fh, a_src, a_dst):
+    el, er = O.gat_logits(wh.numpy(), heads, fh, a_src.numpy(), a_dst.numpy())
+    return torch.from_numpy(el.astype(np.float32)), torch.from_numpy(er.astype(np.float32))
+
+
+def _cpu_gat_aggregate(g, wh, el, er, heads, fh, slope, mode, activation=None):
+    out = O.gat_csr(g.rowptr.numpy(), g.col.numpy(), wh.numpy(), el.numpy(), er.numpy(), heads,
+                    fh, slope, mode == 1)
+    if activation == "elu":
+        out = np.where(out > 0, out, np.expm1(np.minimum(out, 0)))
+    return torch.from_numpy(out.astype(np.float32))
+
+
+def _gat_worker(rank, world, port, n, heads, fh, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from graphneuralnetwork_amd.distributed import EdgeCutGat, build_partition
+        g = _graph(n, 4)
+        part = build_partition(g, rank, world)
+        rng = np.random.default_rng(0)
+        Wh = torch.from_numpy((rng.standard_normal((n, heads * fh)) * 0.5).astype(np.float32))
+        a_s = torch.from_numpy((rng.standard_normal(heads * fh) * 0.3).astype(np.float32))
+        a_d = torch.from_numpy((rng.standard_normal(heads * fh) * 0.3).astype(np.float32))
+        r0, r1 = part.bounds[rank], part.bounds[rank + 1]
+        layer = EdgeCutGat(part, heads, fh, "cpu", logits=_cpu_gat_logits,
+                           aggregate=_cpu_gat_aggregate, gather=_cpu_gather)
+        y = layer(Wh[r0:r1].contiguous(), a_s, a_d, 0.2, 0, "elu")
+        q.put((rank, r0, r1, y.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gat_edge_cut_matches_single_device():
+    n, heads, fh, world = 2000, 4, 8, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gat_worker, args=(r, world, port, n, heads, fh, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(_collect(procs, q, world, 300), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = _graph(n, 4)
+    rng = np.random.default_rng(0)
+    Wh = (rng.standard_normal((n, heads * fh)) * 0.5).astype(np.float32)
+    a_s = (rng.standard_normal(heads * fh) * 0.3).astype(np.float32)
+    a_d = (rng.standard_normal(heads * fh) * 0.3).astype(np.float32)
+    el, er = O.gat_logits(Wh, heads, fh, a_s, a_d)
+    ref = O.gat_csr(g.rowptr.numpy(), g.col.numpy(), Wh, el, er, heads, fh, 0.2, False)
+    ref = np.where(ref > 0, ref, np.expm1(np.minimum(ref, 0)))
+    for rank, r0, r1, y in res:
+        np.testing.assert_allclose(y, ref[r0:r1], rtol=1e-5, atol=1e-5)

@@ -74,12 +74,57 @@ def test_edge_cut_hip_path_matches_single_gpu(dev):
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, F, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(_collect(procs, q, world))
+    res = sorted(_collect(procs, q, world), key=lambda r: r[0])
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     g = _graph(n, dev)
     X = torch.from_numpy(np.random.default_rng(1).standard_normal((n, F)).astype(np.float32)).to(dev)
     ref = spmm_forward(g, X, torch.linspace(-1, 1, F, device=dev), activation="relu").cpu().numpy()
+    for rank, r0, r1, y in res:
+        np.testing.assert_allclose(y, ref[r0:r1], rtol=1e-5, atol=1e-5)
+
+
+def _gat_worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from graphneuralnetwork_amd.distributed import EdgeCutGat, build_partition
+        dev = torch.device("cuda:0")
+        g = _graph(n, dev)
+        part = build_partition(g, rank, world)
+        gen = torch.Generator().manual_seed(0)
+        Wh = (torch.randn(n, 64, generator=gen) * 0.5).to(dev)
+        a_s = (torch.randn(64, generator=gen) * 0.3).to(dev)
+        a_d = (torch.randn(64, generator=gen) * 0.3).to(dev)
+        r0, r1 = part.bounds[rank], part.bounds[rank + 1]
+        layer = EdgeCutGat(part, 8, 8, dev)
+        y = layer(Wh[r0:r1].contiguous(), a_s, a_d, 0.2, 0, "elu")
+        torch.cuda.synchronize()
+        q.put((rank, r0, r1, y.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gat_edge_cut_hip_path_matches_single_gpu(dev):
+    from graphneuralnetwork_amd.ops import GAT_DENSE, gat_aggregate, gat_logits
+    n, world = 20000, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gat_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(_collect(procs, q, world), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    g = _graph(n, dev)
+    gen = torch.Generator().manual_seed(0)
+    Wh = (torch.randn(n, 64, generator=gen) * 0.5).to(dev)
+    a_s = (torch.randn(64, generator=gen) * 0.3).to(dev)
+    a_d = (torch.randn(64, generator=gen) * 0.3).to(dev)
+    el, er = gat_logits(Wh, 8, 8, a_s, a_d)
+    ref = gat_aggregate(g, Wh, el, er, 8, 8, 0.2, GAT_DENSE, "elu").cpu().numpy()
     for rank, r0, r1, y in res:
         np.testing.assert_allclose(y, ref[r0:r1], rtol=1e-5, atol=1e-5)
