@@ -80,6 +80,10 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_dev_spmm_variant_f32": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64,
                                                 _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp,
                                                 _vp, _i64, _vp, _i64, _vp, _i32, _vp]),
+    "gnn_gcn_adjacency_workspace_bytes": (_i64, [_i64, _i64]),
+    "gnn_gcn_adjacency_build": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _i64,
+                                               ctypes.POINTER(ctypes.c_int64), _vp]),
+    "gnn_gcn_adjacency_fill": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gnn_sample_neighbors": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, ctypes.c_uint64, _vp,
                                             _vp, _vp]),
 }

@@ -18,13 +18,53 @@ reference-generated fixtures in tests/test_preprocess.py).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
+from . import _lib
 from .graph import CsrGraph
 
 
+def gcn_adjacency(src, dst, n: int, device=None) -> CsrGraph:
+    """The reference GCN adjacency built by the HIP graph builder (graph_build.hip).
+
+    Same result as :func:`gcn_normalized_csr` (bit-identical), as native
+    sort / reduce passes on the device. Device tensors only."""
+    src = torch.as_tensor(src, dtype=torch.int64, device=device).contiguous()
+    dst = torch.as_tensor(dst, dtype=torch.int64, device=device).contiguous()
+    if not src.is_cuda:
+        raise RuntimeError("gcn_adjacency runs on the ROCm device (no CPU fallback)")
+    if src.shape != dst.shape:
+        raise ValueError("src and dst must have the same length")
+    lib = _lib.load()
+    e = src.numel()
+    nbytes = int(lib.gnn_gcn_adjacency_workspace_bytes(e, n))
+    if nbytes < 0:
+        _lib.check(nbytes, "gnn_gcn_adjacency_workspace_bytes")
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=src.device)
+    nnz = ctypes.c_int64(0)
+    stream = _lib.stream_handle(src.device)
+    rc = lib.gnn_gcn_adjacency_build(src.data_ptr() if e else None, dst.data_ptr() if e else None,
+                                     e, n, ws.data_ptr(), nbytes, ctypes.byref(nnz), stream)
+    if rc == -1 and e:
+        raise IndexError("edge endpoint out of range")
+    _lib.check(rc, "gnn_gcn_adjacency_build")
+    m = int(nnz.value)
+    rowptr = torch.empty(n + 1, dtype=torch.int64, device=src.device)
+    col = torch.empty(m, dtype=torch.int32, device=src.device)
+    val = torch.empty(m, dtype=torch.float32, device=src.device)
+    _lib.check(lib.gnn_gcn_adjacency_fill(ws.data_ptr(), e, n, m, rowptr.data_ptr(),
+                                          col.data_ptr(), val.data_ptr(), stream),
+               "gnn_gcn_adjacency_fill")
+    return CsrGraph(rowptr, col, val, n, n)
+
+
 def gcn_normalized_csr(src, dst, n: int, device=None) -> CsrGraph:
-    """CSR of D^-1/2 (A_sym + I)^T D^-1/2 for a directed edge list (src -> dst)."""
+    """CSR of D^-1/2 (A_sym + I)^T D^-1/2 for a directed edge list (src -> dst).
+
+    torch sort/unique formulation (runs on CPU tensors too: the CPU tests and
+    the oracle cross-check use it); the device path of record is gcn_adjacency."""
     src = torch.as_tensor(src, dtype=torch.int64, device=device)
     dst = torch.as_tensor(dst, dtype=torch.int64, device=device)
     dev = src.device

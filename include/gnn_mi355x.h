@@ -230,6 +230,26 @@ int gnn_sample_neighbors(const int64_t* rowptr, const int32_t* col, int64_t n_gr
                          const int64_t* nodes, int64_t n, int64_t k, uint64_t seed, int64_t* out,
                          int32_t* err_flag, void* stream);
 
+/*
+ * Reference GCN adjacency on the device: D^-1/2 (max(A, A^T) + I)^T D^-1/2 as fp32 CSR
+ * (GCN/data_utils.py:32-35 symmetrise, :78 + sp.eye, :54-60 normalize_adj, :63-70 fp32),
+ * from a directed edge list (src -> dst, int64, duplicates allowed). Bit-identical to
+ * the scipy pipeline (float64 normalisation). Two calls:
+ *   gnn_gcn_adjacency_build: sorts / reduces in `workspace`
+ *     (gnn_gcn_adjacency_workspace_bytes(n_edges, n_nodes) bytes) and returns nnz in
+ *     *nnz_out (host). An endpoint outside [0, n_nodes) -> GNN_E_ARG.
+ *   gnn_gcn_adjacency_fill: writes rowptr [n_nodes+1], col [nnz], val [nnz] from the
+ *     same workspace.
+ * Unlike the aggregation entry points these SYNCHRONISE `stream` between stages
+ * (graph construction runs once per graph).
+ */
+int64_t gnn_gcn_adjacency_workspace_bytes(int64_t n_edges, int64_t n_nodes);
+int gnn_gcn_adjacency_build(const int64_t* src, const int64_t* dst, int64_t n_edges,
+                            int64_t n_nodes, void* workspace, int64_t workspace_bytes,
+                            int64_t* nnz_out, void* stream);
+int gnn_gcn_adjacency_fill(const void* workspace, int64_t n_edges, int64_t n_nodes, int64_t nnz,
+                           int64_t* rowptr, int32_t* col, float* val, void* stream);
+
 /* ---- developer entry (not part of the drop-in surface) ----
  * gnn_dev_spmm_variant_f32: gnn_spmm_csr_f32 at feat == 128 with a compile-time
  * kernel variant (0 shipped: U=4, non-temporal Y stores; 1 U=8; 2 U=2; 7 U=4 with
