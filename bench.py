@@ -261,6 +261,9 @@ def main():
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", default="cover", choices=["cover", "gather"],
+                    help="N>1 halo exchange: feature rows + remote partial sums (cover) or "
+                         "feature rows only (gather)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = multi-rank rehearsal (host-staged exchange), never for numbers")
     ap.add_argument("--traffic-json", default=None,
@@ -309,15 +312,26 @@ def main():
         bytes_local = algorithmic_bytes(nnz_local, rows_local, F)
         halo_rows = 0
     else:
-        from graphneuralnetwork_amd.distributed import EdgeCutSpmm, build_partition
-        part = build_partition(g, rank, world)
+        from graphneuralnetwork_amd.distributed import (EdgeCutSpmm, build_cover_exchange,
+                                                        build_partition, nnz_balanced_bounds)
+        t0 = time.time()
+        bounds = nnz_balanced_bounds(g.rowptr, world)
+        if args.exchange == "cover":
+            part = build_cover_exchange(g, rank, world, bounds=bounds)
+            work = (f"interior {part.interior.nnz}, send {part.send.nnz}, halo {part.halo.nnz}; "
+                    f"recv {part.n_partial_recv} partial + {part.n_feature_recv} feature rows")
+        else:
+            part = build_partition(g, rank, world, bounds=bounds)
+            work = f"interior {part.interior.nnz}, halo {part.halo.nnz}"
+        BUILD_INFO["partition_build_s"] = time.time() - t0
         X = torch.randn(part.n_own, F, device=dev, generator=gen)
         runner = EdgeCutSpmm(part, F, dev)
         step = lambda: runner(X, bias)  # noqa: E731
-        log(f"[bench] rank0 partition: rows {part.n_own} nnz {part.nnz} (interior "
-            f"{part.interior.nnz}, halo {part.halo.nnz}) halo rows {part.n_halo} send rows "
-            f"{part.send_idx.numel()}")
-        rows_local, nnz_local = part.n_own, part.nnz
+        r0, r1 = part.bounds[rank], part.bounds[rank + 1]
+        rows_local = part.n_own
+        nnz_local = int(g.rowptr[r1] - g.rowptr[r0])        # graph edges of the owned rows
+        log(f"[bench] rank{rank} {args.exchange} exchange: rows {rows_local} edges {nnz_local} "
+            f"({work}) recv rows {part.n_halo} send rows {sum(part.send_counts)}")
         bytes_local = algorithmic_bytes(nnz_local, rows_local, F)
         halo_rows = part.n_halo
         del g
@@ -376,9 +390,11 @@ def main():
             "config": {"workload": wl["name"], "nodes": nodes, "directed_edges": edges,
                        "nnz": int(tot_nnz.item()), "feat_dim": F, "global_batch": nodes,
                        "parallelism": f"edge-cut{world}" if world > 1 else "single-gpu",
-                       "nnz_rank0": nnz_local, "halo_rows_rank0": halo_rows},
+                       "nnz_rank0": nnz_local, "halo_rows_rank0": halo_rows,
+                       **({"exchange": args.exchange} if world > 1 else {})},
             "achieved_GBps": achieved,
             "graph_build_s": BUILD_INFO.get("gcn_adjacency_build_s"),
+            **({"partition_build_s": BUILD_INFO.get("partition_build_s")} if world > 1 else {}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic["traffic_bytes"] if traffic else None,

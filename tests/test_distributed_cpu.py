@@ -64,30 +64,39 @@ def _graph(n, seed):
     return gcn_normalized_csr(s, d, n)
 
 
-def _worker(rank, world, port, n, F, q):
+def _worker(rank, world, port, n, F, q, kind="gather"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from graphneuralnetwork_amd.distributed import EdgeCutSpmm, build_partition
+        from graphneuralnetwork_amd.distributed import (EdgeCutSpmm, build_cover_exchange,
+                                                        build_partition)
         g = _graph(n, 3)
-        part = build_partition(g, rank, world)
+        if kind == "cover":
+            part = build_cover_exchange(g, rank, world)
+            # cut edges reduced here: halo column entries + partial edges computed for peers
+            edges = (part.interior.nnz + part.halo.nnz - part.n_partial_recv
+                     + part.send.nnz - part.n_feature_recv)
+        else:
+            part = build_partition(g, rank, world)
+            edges = part.nnz
         X = torch.from_numpy(np.random.default_rng(0).standard_normal((n, F)).astype(np.float32))
         b = torch.arange(F, dtype=torch.float32) / F
         r0, r1 = part.bounds[rank], part.bounds[rank + 1]
         run = EdgeCutSpmm(part, F, "cpu", spmm=_cpu_spmm, gather=_cpu_gather)
         y = run(X[r0:r1].contiguous(), b, activation="relu").clone()
-        q.put((rank, r0, r1, y.numpy(), part.nnz, part.n_halo, part.send_counts, part.recv_counts))
+        q.put((rank, r0, r1, y.numpy(), edges, part.n_halo, part.send_counts, part.recv_counts))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_edge_cut_matches_single_device(world):
+@pytest.mark.parametrize("world,kind", [(2, "gather"), (3, "gather"), (2, "cover"), (3, "cover")])
+def test_edge_cut_matches_single_device(world, kind):
     n, F = 3000, 16
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, F, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, F, q, kind))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = _collect(procs, q, world, 300)

@@ -45,14 +45,16 @@ def _graph(n, dev):
     return gcn_normalized_csr(s, d, n, device=dev)
 
 
-def _worker(rank, world, port, n, F, q):
+def _worker(rank, world, port, n, F, q, kind="gather"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from graphneuralnetwork_amd.distributed import EdgeCutSpmm, build_partition
+        from graphneuralnetwork_amd.distributed import (EdgeCutSpmm, build_cover_exchange,
+                                                        build_partition)
         dev = torch.device("cuda:0")
         g = _graph(n, dev)
-        part = build_partition(g, rank, world)
+        build = build_cover_exchange if kind == "cover" else build_partition
+        part = build(g, rank, world)
         X = torch.from_numpy(np.random.default_rng(1).standard_normal((n, F)).astype(np.float32)).to(dev)
         b = torch.linspace(-1, 1, F, device=dev)
         r0, r1 = part.bounds[rank], part.bounds[rank + 1]
@@ -65,13 +67,15 @@ def _worker(rank, world, port, n, F, q):
         dist.destroy_process_group()
 
 
-def test_edge_cut_hip_path_matches_single_gpu(dev):
+@pytest.mark.parametrize("world,kind", [(2, "gather"), (2, "cover"), (3, "cover")])
+def test_edge_cut_hip_path_matches_single_gpu(dev, world, kind):
     from graphneuralnetwork_amd.ops import spmm_forward
-    n, F, world = 20000, 64, 2
+    n, F = 20000, 64
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, F, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, F, q, kind))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(_collect(procs, q, world), key=lambda r: r[0])

@@ -19,6 +19,7 @@ step() {  # step <name> <timeout> <cmd...>
 for MODE in "$@"; do
   case $MODE in
     tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     testsk) step pytest_gpu_k 900 python -m pytest tests -m gpu -v -p no:cacheprovider -k "${K:-spmm}" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
     ab) step spmm_ab 900 python tools/spmm_ab.py --workload ${AB_WL:-cfg2} ${AB_ARGS:-} ;;
