@@ -117,6 +117,17 @@ def cpu_baseline(g, X, feat: int):
             "seconds_per_step": t}
 
 
+def load_traffic(name: str):
+    """PMC traffic summary profiles/traffic_<name>.json (tools/pmc_traffic.py) or None."""
+    path = ROOT / "profiles" / f"traffic_{name}.json"
+    try:
+        t = json.loads(path.read_text())
+    except (OSError, ValueError):
+        return None, None
+    return t["traffic_bytes"], (str(path.relative_to(ROOT)) + ": rocprofv3 --pmc FETCH_SIZE x2 + "
+                                "WRITE_SIZE of this command")
+
+
 def time_steps(step, steps: int, warmup: int, dev):
     """Per-step HIP-event times (ms) on the current stream + wall seconds for `steps` steps."""
     stream = torch.cuda.current_stream(dev)
@@ -162,6 +173,7 @@ def run_gat(args, dev):
     bytes_agg = nnz * (4 + 4 * H + 4 * H * Fh) + n * (8 + 4 * H + 4 * H * Fh)
     k_ms = statistics.mean(agg_ms[GAT_DENSE])
     achieved = bytes_agg / (k_ms / 1e3) / 1e9
+    traffic, tsrc = load_traffic("cfg3_F64")
     res = {"metric": "GAT 8-head aggregated edges/sec (all heads) + achieved HBM GB/s",
            "value": nnz * args.steps / wall, "unit": "edges/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
@@ -171,7 +183,8 @@ def run_gat(args, dev):
            "layer_ms": statistics.mean(layer_ms),
            "aggregate_ms": {"dense": k_ms, "sparse": statistics.mean(agg_ms[GAT_SPARSE])},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                        "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                        "traffic_source": tsrc,
                         "kernel": "gat_csr_kernel<dense> (+ fixup)",
                         "algorithmic_bytes_per_launch": bytes_agg, "avg_launch_ms": k_ms}}
     if not args.no_cpu_baseline:
@@ -227,6 +240,7 @@ def run_sage(args, dev):
     bytes_l0 = M * k1 * (4 * F + 8) + M * 4 * F
     k_ms = statistics.mean(agg_ms)
     achieved = bytes_l0 / (k_ms / 1e3) / 1e9
+    traffic, tsrc = load_traffic(f"cfg4_F{F}")
     res = {"metric": "GraphSAGE sampled-neighbour aggregated edges/sec (2-layer forward)",
            "value": edges * args.steps / wall, "unit": "edges/s", "n_gpus": 1, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
@@ -238,7 +252,8 @@ def run_sage(args, dev):
            "forward_ms": statistics.mean(fwd_ms), "sample_ms": statistics.mean(smp_ms),
            "first_sample_s": t_sample,
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                        "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                        "traffic_source": tsrc,
                         "kernel": "sage_aggregate_kernel<gather, mean> (layer 0: |S1| x 10 from the 10M table)",
                         "algorithmic_bytes_per_launch": bytes_l0, "avg_launch_ms": k_ms}}
     if not args.no_cpu_baseline:

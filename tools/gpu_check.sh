@@ -26,9 +26,9 @@ for MODE in "$@"; do
     bench_gat) step bench_gat 600 python bench.py --steps 20 --warmup 5 --workload cfg3 ;;
     bench_sage) step bench_sage 900 python bench.py --steps 20 --warmup 5 --workload cfg4 ;;
     bench_ns) step bench_ns 900 python bench.py --steps 20 --warmup 5 --workload ns ;;
-    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} ;;
-    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
-         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    prof) step rocprof${PTAG:-} 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof${PTAG:-}" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    pmc) step pmc_fetch${PTAG:-} 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch${PTAG:-}" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
+         step pmc_write${PTAG:-} 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write${PTAG:-}" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
     rehearse2) GNN_BENCH_DEVICE=0 step rehearse2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 ;;
     *) echo "unknown mode $MODE"; exit 2 ;;
   esac

@@ -4,7 +4,11 @@ Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half
 bytes of wide (16 B/lane) coalesced reads -> doubled; WRITE_SIZE is exact for
 16-B stores. Both counters are in KiB.
 
-    python tools/pmc_traffic.py <fetch_csv> <write_csv> <kernel-substring> [out.json]
+    python tools/pmc_traffic.py <fetch_csv> <write_csv> <kernel-substring> [out.json] [--largest]
+
+--largest keeps, per counter, the largest launch instead of the median (for a
+command that launches the same kernel at several sizes, e.g. the two
+GraphSAGE layers, where the bench's roofline names the largest).
 """
 import csv
 import json
@@ -12,25 +16,30 @@ import statistics
 import sys
 
 
-def per_launch(path, counter, kernel):
+def per_launch(path, counter, kernel, largest=False):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
             if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
     if not vals:
         raise SystemExit(f"no {counter} rows for {kernel!r} in {path}")
-    return statistics.median(vals), len(vals)
+    return (max(vals) if largest else statistics.median(vals)), len(vals)
 
 
 def main():
-    fetch_csv, write_csv, kernel = sys.argv[1:4]
-    f, nf = per_launch(fetch_csv, "FETCH_SIZE", kernel)
-    w, nw = per_launch(write_csv, "WRITE_SIZE", kernel)
+    largest = "--largest" in sys.argv
+    argv = [a for a in sys.argv if a != "--largest"]
+    fetch_csv, write_csv, kernel = argv[1:4]
+    f, nf = per_launch(fetch_csv, "FETCH_SIZE", kernel, largest)
+    w, nw = per_launch(write_csv, "WRITE_SIZE", kernel, largest)
     res = {"kernel": kernel, "fetch_kib_raw": f, "write_kib": w, "launches": [nf, nw],
            "fetch_bytes_corrected": 2 * f * 1024, "write_bytes": w * 1024,
            "traffic_bytes": (2 * f + w) * 1024,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), WRITE_SIZE exact; KiB->B"}
     out = json.dumps(res, indent=1)
-    if len(sys.argv) > 4:
-        open(sys.argv[4], "w").write(out + "\n")
+    if largest:
+        res["selection"] = "largest launch"
+        out = json.dumps(res, indent=1)
+    if len(argv) > 4:
+        open(argv[4], "w").write(out + "\n")
     print(out)
 
 
