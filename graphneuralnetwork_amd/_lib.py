@@ -121,6 +121,22 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
         return lib
 
 
+def use_variant(path) -> ctypes.CDLL:
+    """Kernel-tuning hook (tools/*_ab.py): route every op through another build
+    of the same C-ABI (``build.build_variant``); ``use_variant(None)`` restores."""
+    global _lib
+    if path is None:
+        _lib = None
+        return load()
+    lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_LOCAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
 def error_string(code: int) -> str:
     return load().gnn_error_string(int(code)).decode()
 

@@ -90,5 +90,28 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     return LIB_PATH
 
 
+def build_variant(tag: str, defines: list[str]) -> Path:
+    """Kernel-tuning build: every source with extra ``-D`` flags, linked into
+    ``lib/variants/libgnn_<tag>.so`` (same C-ABI; used by tools/*_ab.py only)."""
+    odir = OBJ_DIR / "variants" / tag
+    odir.mkdir(parents=True, exist_ok=True)
+    out = LIB_DIR / "variants" / f"libgnn_{tag}.so"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    hipcc = _hipcc()
+    flags = [*HIPCC_FLAGS, *(f"-D{d}" for d in defines)]
+    procs = [(src, subprocess.Popen([hipcc, *flags, "-c", str(src), "-o", str(odir / (src.stem + ".o"))],
+                                    stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+             for src in sources()]
+    failed = [f"--- {src.name} ---\n{p.communicate()[0]}" for src, p in procs if p.wait() != 0]
+    if failed:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(failed))
+    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out),
+                        *(str(odir / (src.stem + ".o")) for src in sources())],
+                       capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
+    return out
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))

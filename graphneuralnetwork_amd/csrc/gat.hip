@@ -100,6 +100,12 @@ struct GatParams {
 };
 
 constexpr int kGatSmallUnroll = 4;
+#ifndef GNN_GAT_U
+#define GNN_GAT_U 2  // feature-row gathers in flight per lane in phase B (A/B: tools/gat_ab.py)
+#endif
+#ifndef GNN_GAT_CHUNK
+#define GNN_GAT_CHUNK 16  // edges per phase-A chunk (A/B: 16 >= 8 > 32 > 64 at cfg3)
+#endif
 
 // Rows with at most one edge (44 % of the R-MAT rows: the self-loop only), packed
 // EPI x kGatSmallUnroll per wave. One edge j: dense softmax weight exp(z - z) = 1,
@@ -177,10 +183,12 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
   }
 }
 
-template <int VW, int LPR, int NCH, int HP, bool SPARSE, int U>
+template <int VW, int LPR, int NCH, int HP, bool SPARSE, int U, int J>
 __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
   constexpr int EPI = kWave / LPR;  // phase B: edges per gather instruction
   constexpr int EPP = kWave / HP;   // phase A: edges per pass (lane = edge x head)
+  constexpr int C = EPP * J;        // edges per chunk
+  static_assert(J == 1 || (EPI <= EPP && EPP % EPI == 0), "multi-pass chunks need EPI | EPP");
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = static_cast<int64_t>(blockIdx.x) * kGatWaves + (threadIdx.x >> 6);
   const int sub = lane & (LPR - 1);
@@ -219,48 +227,78 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
     acc[ch] = vzero<VW>();
   }
 
-  for (int64_t b = beg; b < end; b += EPP) {
-    const int np = static_cast<int>(min(static_cast<int64_t>(EPP), end - b));
-    // ---- phase A: lane (edge ae, head ah)
-    const bool live = ae < np && head_ok;
-    const int c = ae < np ? P.col[b + ae] : 0;
-    float z = -INFINITY;
-    if (live) {
-      const float sv = eli + P.er[static_cast<int64_t>(c) * P.lde + ah];
-      const float x = sv > 0.f ? sv : P.slope * sv;
-      z = SPARSE ? -x : x;
+  // A chunk is J phase-A passes (C = J * EPP edges): every lane issues its J column
+  // and J er loads at once, then the whole chunk's feature rows are gathered in
+  // C / EPI slots -- one dependent round trip per chunk instead of per pass.
+  for (int64_t b = beg; b < end; b += C) {
+    const int np = static_cast<int>(min(static_cast<int64_t>(C), end - b));
+    // ---- phase A: lane (edge j * EPP + ae, head ah)
+    int cj[J];
+    float zj[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int e = j * EPP + ae;
+      cj[j] = e < np ? P.col[b + e] : 0;
     }
-    float p, scale = 1.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const bool live = j * EPP + ae < np && head_ok;
+      zj[j] = -INFINITY;
+      if (live) {
+        const float sv = eli + P.er[static_cast<int64_t>(cj[j]) * P.lde + ah];
+        const float x = sv > 0.f ? sv : P.slope * sv;
+        zj[j] = SPARSE ? -x : x;
+      }
+    }
+    float pj[J];
     if (!SPARSE) {
-      float pm = z;
+      float pm = zj[0];
+#pragma unroll
+      for (int j = 1; j < J; ++j) pm = fmaxf(pm, zj[j]);
 #pragma unroll
       for (int o = HP; o < kWave; o <<= 1) pm = fmaxf(pm, __shfl_xor(pm, o, kWave));
       const float mn = fmaxf(m, pm);
-      scale = __expf(m - mn);  // 0 on the first pass (m = -inf)
+      const float scale = __expf(m - mn);  // 0 on the first chunk (m = -inf)
       m = mn;
-      p = live ? __expf(z - mn) : 0.f;
-      lsum = lsum * scale + p;
+      float ps = 0.f;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        pj[j] = zj[j] == -INFINITY ? 0.f : __expf(zj[j] - mn);
+        ps += pj[j];
+      }
+      lsum = lsum * scale + ps;
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) acc[ch] *= __shfl(scale, hid[ch], kWave);
     } else {
-      p = live ? expf(z) : 0.f;  // the reference's exp(-LeakyReLU), no max subtraction
-      lsum += p;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        pj[j] = zj[j] == -INFINITY ? 0.f : expf(zj[j]);  // exp(-LeakyReLU), no max subtraction
+        lsum += pj[j];
+      }
     }
-    // ---- phase B: lanes = features, EPI edges per gather instruction
-    for (int k = 0; k < np; k += EPI * U) {
+    // ---- phase B: lanes = features, EPI edges per gather instruction, U in flight
+#pragma unroll 1
+    for (int k0 = 0; k0 < C / EPI; k0 += U) {
+      if (k0 * EPI >= np) break;
       typename Vec<VW>::T xv[U][NCH];
       float w[U][NCH];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = k + u * EPI + grp;
-        const int es = (e < EPP ? e : 0) * HP;
-        const int ce = __shfl(c, es, kWave);
+        const int e = (k0 + u) * EPI + grp;                 // edge within the chunk
+        const int j = J == 1 ? 0 : ((k0 + u) * EPI) / EPP;  // uniform: EPI <= EPP when J > 1
+        const int es = (J == 1 ? (e < EPP ? e : 0) : (e - j * EPP)) * HP;
+        int cv = cj[0];
+        float pv = pj[0];
+#pragma unroll
+        for (int jj = 1; jj < J; ++jj)
+          if (jj == j) { cv = cj[jj]; pv = pj[jj]; }
+        const int ce = __shfl(cv, es, kWave);
         const float* xr = P.wh + static_cast<int64_t>(ce) * P.ldw;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
           const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
           const bool ok = e < np && f < P.feat;
-          float wv = __shfl(p, es + hid[ch], kWave);
+          float wv = __shfl(pv, es + hid[ch], kWave);
           xv[u][ch] = ok ? vload<VW>(xr + f) : vzero<VW>();
           if (P.drop_p > 0.f && ok) {
             const uint32_t r = hash3(P.drop_seed, b + e, P.head0 + hid[ch]);
@@ -437,8 +475,11 @@ template <int VW, int LPR, int NCH, int HP, bool SPARSE>
 static void launch_gat(const GatParams& P, hipStream_t s) {
   // phase B covers a pass of 64/HP edges in ceil(EPP/EPI) gather instructions
   constexpr int EPI = kWave / LPR, EPP = kWave / HP;
-  constexpr int U0 = (EPP + EPI - 1) / EPI;
-  constexpr int U = NCH >= 2 ? 1 : (U0 < 4 ? U0 : 4);
+  // chunk = J passes (~32 edges) when an EPI group never straddles two passes
+  constexpr int J = (EPI <= EPP && EPP % EPI == 0 && EPP < GNN_GAT_CHUNK && NCH == 1)
+                        ? GNN_GAT_CHUNK / EPP : 1;
+  constexpr int CE = (EPP * J + EPI - 1) / EPI;  // gather slots per chunk
+  constexpr int U = NCH >= 2 ? 1 : (CE < GNN_GAT_U ? CE : GNN_GAT_U);
   const int64_t seg_blocks = (P.n_seg + kGatWaves - 1) / kGatWaves;
   const int64_t mid_blocks = (P.n_mid + kGatWaves - 1) / kGatWaves;
   const int64_t small_waves = (P.n_small + EPI * kGatSmallUnroll - 1) / (EPI * kGatSmallUnroll);
@@ -448,7 +489,7 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
   Q.mid_waves = mid_blocks * kGatWaves;
   const int64_t blocks = seg_blocks + mid_blocks + small_blocks;
   if (blocks > 0)
-    hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U>),
+    hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U, J>),
                        dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), 0, s, Q);
   if (P.n_long > 0)
     hipLaunchKernelGGL((gat_fixup_kernel<VW, LPR, NCH, SPARSE>),
@@ -509,6 +550,35 @@ __global__ __launch_bounds__(256) void gat_logits_kernel(const float* __restrict
   er[n * lde + h] = sr;
 }
 
+// Vector form of gat_logits_kernel for fh % 4 == 0 and 16-B aligned rows: a lane per
+// (node, head) loads its head's fh floats as float4 (a wave reads 64 contiguous head
+// slices), 32-bit index math. Same fmaf order over f as the scalar kernel.
+__global__ __launch_bounds__(256) void gat_logits_vec_kernel(const float* __restrict__ wh,
+                                                             uint32_t ldw4, uint32_t total,
+                                                             uint32_t heads, uint32_t fh4,
+                                                             const float* __restrict__ a_src,
+                                                             const float* __restrict__ a_dst,
+                                                             float* __restrict__ el,
+                                                             float* __restrict__ er, uint32_t lde) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const uint32_t n = t / heads, h = t - n * heads;
+  const float4* x = reinterpret_cast<const float4*>(wh) + static_cast<uint64_t>(n) * ldw4 + h * fh4;
+  const float4* as = reinterpret_cast<const float4*>(a_src) + h * fh4;
+  const float4* ad = reinterpret_cast<const float4*>(a_dst) + h * fh4;
+  float sl = 0.f, sr = 0.f;
+  for (uint32_t k = 0; k < fh4; ++k) {
+    const float4 v = x[k];
+    const float4 a = as[k], d = ad[k];
+    sl = fmaf(v.x, a.x, sl); sr = fmaf(v.x, d.x, sr);
+    sl = fmaf(v.y, a.y, sl); sr = fmaf(v.y, d.y, sr);
+    sl = fmaf(v.z, a.z, sl); sr = fmaf(v.z, d.z, sr);
+    sl = fmaf(v.w, a.w, sl); sr = fmaf(v.w, d.w, sr);
+  }
+  el[static_cast<uint64_t>(n) * lde + h] = sl;
+  er[static_cast<uint64_t>(n) * lde + h] = sr;
+}
+
 // out[f] = mean over rows of x[:, f] (double accumulation; two passes, deterministic).
 constexpr int kMeanRows = 4096;
 __global__ __launch_bounds__(256) void col_sum_partial_kernel(const float* __restrict__ x,
@@ -544,6 +614,17 @@ extern "C" int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, 
   if (n_rows == 0) return GNN_OK;
   if (!wh || !a_src || !a_dst || !el || !er) return GNN_E_ARG;
   const int64_t total = n_rows * heads;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(wh) | reinterpret_cast<uintptr_t>(a_src) |
+                         reinterpret_cast<uintptr_t>(a_dst)) & 15) == 0;
+  if (aligned && fh % 4 == 0 && ldw % 4 == 0 && total < (int64_t{1} << 31) &&
+      ldw < (int64_t{1} << 31) && lde < (int64_t{1} << 31)) {
+    hipLaunchKernelGGL(gat_logits_vec_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
+                       dim3(256), 0, static_cast<hipStream_t>(stream), wh,
+                       static_cast<uint32_t>(ldw / 4), static_cast<uint32_t>(total),
+                       static_cast<uint32_t>(heads), static_cast<uint32_t>(fh / 4), a_src, a_dst,
+                       el, er, static_cast<uint32_t>(lde));
+    return launch_status();
+  }
   hipLaunchKernelGGL(gat_logits_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256),
                      0, static_cast<hipStream_t>(stream), wh, ldw, n_rows, heads, fh, a_src, a_dst,
                      el, er, lde);

@@ -115,6 +115,26 @@ def test_gat_aggregate_vs_oracle(dev, heads, fh, sparse, seg_len):
     close(out, ref)
 
 
+@pytest.mark.parametrize("heads,fh,ld,off", [(8, 8, 80, 0), (8, 8, 67, 0), (4, 16, 64, 1),
+                                              (3, 12, 40, 4)])
+def test_gat_logits_strided_and_unaligned(dev, heads, fh, ld, off):
+    """Vector (16-B aligned, fh % 4 == 0) and scalar fallbacks agree with the oracle."""
+    from graphneuralnetwork_amd.ops import gat_logits
+    n = 3000
+    rng = np.random.default_rng(ld)
+    big = rng.standard_normal((n, ld + off)).astype(np.float32)
+    a = (rng.standard_normal(2 * heads * fh + 1) * 0.3).astype(np.float32)
+    wh = big[:, off:off + heads * fh]
+    whd = torch.from_numpy(big).to(dev)[:, off:off + heads * fh]
+    ad = torch.from_numpy(a).to(dev)
+    el, er = gat_logits(whd, heads, fh, ad[off % 2:off % 2 + heads * fh],
+                        ad[heads * fh:2 * heads * fh])
+    el_o, er_o = O.gat_logits(wh, heads, fh, a[off % 2:off % 2 + heads * fh],
+                              a[heads * fh:2 * heads * fh])
+    close(el.cpu().numpy(), el_o)
+    close(er.cpu().numpy(), er_o)
+
+
 def test_gat_dropout_is_seeded_and_unbiased(dev):
     from graphneuralnetwork_amd.graph import CsrGraph
     from graphneuralnetwork_amd.ops import GAT_DENSE, gat_aggregate

@@ -1,0 +1,79 @@
+"""Interleaved A/B of GAT aggregation builds (lib/variants/*.so) at cfg3 (one process).
+
+    python tools/gat_ab.py --variants base,j1,... [--rounds 6]
+Variants are built on the CPU side by ``python tools/gat_ab.py --build`` (see VARIANTS).
+"""
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+VARIANTS = {
+    "j1u2": ["GNN_GAT_CHUNK=1", "GNN_GAT_U=2"],     # one pass per chunk (previous kernel)
+    "c16u2": ["GNN_GAT_CHUNK=16", "GNN_GAT_U=2"],
+    "c32u2": ["GNN_GAT_CHUNK=32", "GNN_GAT_U=2"],
+    "c32u4": ["GNN_GAT_CHUNK=32", "GNN_GAT_U=4"],
+    "c64u4": ["GNN_GAT_CHUNK=64", "GNN_GAT_U=4"],
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--rounds", type=int, default=6)
+    args = ap.parse_args()
+    names = args.variants.split(",")
+    if args.build:
+        from graphneuralnetwork_amd.build import build_variant
+        for n in names:
+            print(build_variant(n, VARIANTS[n]))
+        return
+    import torch
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd.ops import GAT_DENSE, gat_aggregate, gat_logits
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    dev = torch.device("cuda:0")
+    n = 1_000_000
+    s, d = rmat_edges(n, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n, device=dev)
+    H, Fh = 8, 8
+    gen = torch.Generator(device=dev).manual_seed(0)
+    Wh = torch.randn(n, H * Fh, device=dev, generator=gen)
+    a_s = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
+    a_d = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
+    el, er = gat_logits(Wh, H, Fh, a_s, a_d)
+    out = torch.empty_like(Wh)
+    ref = gat_aggregate(g, Wh, el, er, H, Fh, 0.2, GAT_DENSE, "elu").clone()
+    libs = {v: ROOT / "graphneuralnetwork_amd" / "lib" / "variants" / f"libgnn_{v}.so" for v in names}
+    times = {v: [] for v in names}
+    for r in range(args.rounds):
+        for v in names:
+            _lib.use_variant(libs[v])
+            f = lambda: gat_aggregate(g, Wh, el, er, H, Fh, 0.2, GAT_DENSE, "elu", out=out)  # noqa
+            for _ in range(3):
+                f()
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(10):
+                f()
+            b.record()
+            torch.cuda.synchronize()
+            times[v].append(a.elapsed_time(b) / 10)
+            if r == 0:
+                err = (out - ref).abs().max().item()
+                print(f"{v}: max |diff| vs default build {err:.3g}", flush=True)
+    bytes_agg = g.nnz * (4 + 4 * H + 4 * H * Fh) + n * (8 + 4 * H + 4 * H * Fh)
+    res = {v: {"ms": statistics.median(t), "GBps": bytes_agg / statistics.median(t) / 1e6}
+           for v, t in times.items()}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

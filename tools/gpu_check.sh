@@ -22,6 +22,7 @@ for MODE in "$@"; do
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     testsk) step pytest_gpu_k 900 python -m pytest tests -m gpu -v -p no:cacheprovider -k "${K:-spmm}" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
+    gat_ab) step gat_ab 900 python tools/gat_ab.py ${GAT_AB_ARGS:-} ;;
     ab) step spmm_ab 900 python tools/spmm_ab.py --workload ${AB_WL:-cfg2} ${AB_ARGS:-} ;;
     bench_gat) step bench_gat 600 python bench.py --steps 20 --warmup 5 --workload cfg3 ;;
     bench_sage) step bench_sage 900 python bench.py --steps 20 --warmup 5 --workload cfg4 ;;
