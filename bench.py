@@ -333,7 +333,8 @@ def main():
         bounds = nnz_balanced_bounds(g.rowptr, world)
         if args.exchange == "cover":
             part = build_cover_exchange(g, rank, world, bounds=bounds)
-            work = (f"interior {part.interior.nnz}, send {part.send.nnz}, halo {part.halo.nnz}; "
+            work = (f"interior {part.interior.nnz}, partial {part.send_p.nnz}, halo "
+                    f"{part.halo_x.nnz} + {part.halo_p.nnz}; "
                     f"recv {part.n_partial_recv} partial + {part.n_feature_recv} feature rows")
         else:
             part = build_partition(g, rank, world, bounds=bounds)

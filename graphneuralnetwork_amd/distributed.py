@@ -27,8 +27,9 @@ single-GPU reduction up to fp32 summation order.
 ``build_cover_exchange`` is the SpMM default: instead of shipping the feature
 row of every remote column, each cut block is covered by feature rows AND
 remotely computed partial row sums (a greedy vertex cover of the block's
-bipartite edge set), which ships ~1.8x fewer rows on an 8-way RMAT cut; step 1
-becomes one SpMM over a "send" CSR and the exchange is still one all-to-all-v.
+bipartite edge set), which ships 2-3x fewer rows on an RMAT cut; the two kinds
+travel in two all-to-all-v's that pipeline with the partial-sum, interior and
+halo SpMMs.
 """
 from __future__ import annotations
 
@@ -146,44 +147,71 @@ class CoverExchange:
     (i, j) is covered either by shipping X_j from q to p (column cover) or by q
     computing the partial row sum  s_qi = sum_{j in q} A_ij X_j  over its own
     rows of X and shipping s_qi to p (row cover).  Picking, per block, a small
-    vertex cover of the bipartite edge set cuts the exchanged rows of an 8-way
-    RMAT edge-cut ~1.8x (hub rows are covered once instead of once per
+    vertex cover of the bipartite edge set cuts the rows exchanged by an 8-way
+    RMAT edge-cut ~2-3x (a hub row is covered once instead of once per
     neighbour), see DESIGN.md section 6.
 
-    Per aggregation it is still ONE all-to-all-v: the send buffer is produced
-    by one SpMM over ``send`` (rows = send slots grouped by peer,
-    [partial rows | feature rows]; a feature row is a 1-entry row with value
-    1.0, an exact copy), and the receive buffer is reduced by ``halo`` (rows =
-    owned rows; a column entry carries A_ij, a partial entry 1.0).
+    Per aggregation the two kinds travel in two all-to-all-v's so that the
+    exchange pipelines with the compute:
+      gather feature rows -> [exchange 1]  while the partial-sum SpMM (``send_p``)
+      -> [exchange 2] while the interior SpMM, then the ``halo_x`` SpMM (A_ij over
+      the received feature rows) -> ``halo_p`` (1.0 x each received partial row).
     """
 
     rank: int
     world: int
     bounds: list
     interior: CsrGraph      # rows: owned rows; cols: owned rows (local ids)
-    send: CsrGraph          # rows: send slots; cols: owned rows (local ids)
-    halo: CsrGraph          # rows: owned rows; cols: receive slots
-    send_counts: list       # rows sent to each peer
-    recv_counts: list       # rows received from each peer
-    n_partial_recv: int     # partial-sum rows among the received rows
-    n_feature_recv: int     # feature rows among the received rows
+    send_x_idx: torch.Tensor  # int64: local rows whose features peers need, grouped by peer
+    send_p: CsrGraph        # rows: partial-sum slots grouped by peer; cols: owned rows
+    halo_x: CsrGraph        # rows: owned rows; cols: received feature-row slots
+    halo_p: CsrGraph        # rows: owned rows; cols: received partial-row slots (values 1.0)
+    send_x_counts: list
+    send_p_counts: list
+    recv_x_counts: list
+    recv_p_counts: list
+    any_x: bool             # some rank exchanges feature rows (collective is needed)
+    any_p: bool             # some rank exchanges partial rows
 
     @property
     def n_own(self) -> int:
         return self.bounds[self.rank + 1] - self.bounds[self.rank]
 
     @property
+    def send_counts(self) -> list:
+        return [a + b for a, b in zip(self.send_x_counts, self.send_p_counts)]
+
+    @property
+    def recv_counts(self) -> list:
+        return [a + b for a, b in zip(self.recv_x_counts, self.recv_p_counts)]
+
+    @property
     def n_halo(self) -> int:
         return int(sum(self.recv_counts))
 
     @property
+    def n_partial_recv(self) -> int:
+        return int(sum(self.recv_p_counts))
+
+    @property
+    def n_feature_recv(self) -> int:
+        return int(sum(self.recv_x_counts))
+
+    @property
     def nnz(self) -> int:
-        """Stored edges this rank reduces per aggregation (interior + send + halo)."""
-        return self.interior.nnz + self.send.nnz + self.halo.nnz
+        """Stored entries this rank reduces per aggregation."""
+        return self.interior.nnz + self.send_p.nnz + self.halo_x.nnz + self.halo_p.nnz
 
 
 def _exclusive_cumsum(t: torch.Tensor) -> torch.Tensor:
     return torch.cumsum(t, 0) - t
+
+
+def _global_sum(v: int, device, group=None) -> int:
+    on_dev = torch.device(device).type == "cuda" and dist.get_backend(group) != "gloo"
+    t = torch.tensor([v], dtype=torch.int64, device=device if on_dev else "cpu")
+    dist.all_reduce(t, group=group)
+    return int(t.item())
 
 
 def build_cover_exchange(g: CsrGraph, rank: int, world: int, group=None,
@@ -234,11 +262,12 @@ def build_cover_exchange(g: CsrGraph, rank: int, world: int, group=None,
     nx = torch.bincount(torch.searchsorted(bt, xcols, right=True) - 1, minlength=world).to(i64)
     # row cover: partial rows (q, i) and the edges the owner q reduces for them
     pr, pc, pv, pq = rc[part], cc[part], vc[part], qc[part]
-    pkey = pq * max(n_own, 1) + pr
+    stride = max(n_own, 1)
+    pkey = pq * stride + pr
     order = torch.sort(pkey, stable=True).indices              # by (peer, row), edge order kept
     pr, pc, pv, pq, pkey = pr[order], pc[order], pv[order], pq[order], pkey[order]
     pkeys = torch.unique_consecutive(pkey)
-    np_ = torch.bincount(pkeys // max(n_own, 1), minlength=world).to(i64)
+    np_ = torch.bincount(pkeys // stride, minlength=world).to(i64)
     npe = torch.bincount(pq, minlength=world).to(i64)
 
     # ---- one-time handshake -----------------------------------------------------------------
@@ -248,48 +277,34 @@ def build_cover_exchange(g: CsrGraph, rank: int, world: int, group=None,
     mine_l, theirs_l = mine.cpu().tolist(), theirs.cpu().tolist()
     req_x = torch.empty(sum(t[0] for t in theirs_l), dtype=i64, device=dev)
     _all_to_all_v(req_x, xcols.contiguous(), [t[0] for t in theirs_l], [m[0] for m in mine_l], group)
-    pe_send = torch.stack([pr + r0, pc], 0).contiguous()       # global (row, col) per edge
-    n_pe_in = sum(t[2] for t in theirs_l)
-    pe_ij = torch.empty((2, n_pe_in), dtype=i64, device=dev)
     spl_out, spl_in = [t[2] for t in theirs_l], [m[2] for m in mine_l]
-    for k in range(2):
-        buf = torch.empty(n_pe_in, dtype=i64, device=dev)
-        _all_to_all_v(buf, pe_send[k].contiguous(), spl_out, spl_in, group)
-        pe_ij[k] = buf
+    n_pe_in = sum(spl_out)
+    pe_i = torch.empty(n_pe_in, dtype=i64, device=dev)
+    pe_j = torch.empty(n_pe_in, dtype=i64, device=dev)
     pe_v = torch.empty(n_pe_in, dtype=val.dtype, device=dev)
+    _all_to_all_v(pe_i, (pr + r0).contiguous(), spl_out, spl_in, group)
+    _all_to_all_v(pe_j, pc.contiguous(), spl_out, spl_in, group)
     _all_to_all_v(pe_v, pv.contiguous(), spl_out, spl_in, group)
 
-    # ---- send CSR (what this rank computes for its peers) ---------------------------------
-    tx = torch.tensor([t[0] for t in theirs_l], dtype=i64, device=dev)
-    tp = torch.tensor([t[1] for t in theirs_l], dtype=i64, device=dev)
-    send_sizes = tx + tp
-    send_off = _exclusive_cumsum(send_sizes)
+    # ---- what this rank computes / copies for its peers ------------------------------------
     peer_e = torch.repeat_interleave(torch.arange(world, device=dev, dtype=i64),
                                      torch.tensor(spl_out, dtype=i64, device=dev))
-    n_tot = b[-1]
-    _, prow = torch.unique_consecutive(peer_e * n_tot + pe_ij[0], return_inverse=True)
-    p_slot = send_off[peer_e] + (prow - _exclusive_cumsum(tp)[peer_e])
-    peer_x = torch.repeat_interleave(torch.arange(world, device=dev, dtype=i64), tx)
-    x_slot = send_off[peer_x] + tp[peer_x] + (torch.arange(req_x.numel(), device=dev, dtype=i64)
-                                              - _exclusive_cumsum(tx)[peer_x])
-    send = from_coo(torch.cat([p_slot, x_slot]), torch.cat([pe_ij[1] - r0, req_x - r0]),
-                    torch.cat([pe_v, torch.ones(req_x.numel(), dtype=val.dtype, device=dev)]),
-                    int(send_sizes.sum()), n_own)
+    _, p_slot = torch.unique_consecutive(peer_e * b[-1] + pe_i, return_inverse=True)
+    n_p_send = sum(t[1] for t in theirs_l)
+    send_p = from_coo(p_slot.view(-1), pe_j - r0, pe_v, n_p_send, n_own)
 
-    # ---- halo CSR (how this rank folds in what it receives) -------------------------------
-    recv_off = _exclusive_cumsum(nx + np_)
-    xq = torch.searchsorted(bt, xc, right=True) - 1
-    xs = recv_off[xq] + np_[xq] + (torch.searchsorted(xcols, xc) - _exclusive_cumsum(nx)[xq])
-    kq = pkeys // max(n_own, 1)
-    ki = pkeys - kq * max(n_own, 1)
-    ks = recv_off[kq] + (torch.arange(pkeys.numel(), device=dev, dtype=i64) - _exclusive_cumsum(np_)[kq])
-    halo = from_coo(torch.cat([xr, ki]), torch.cat([xs, ks]),
-                    torch.cat([xv, torch.ones(pkeys.numel(), dtype=val.dtype, device=dev)]),
-                    n_own, int((nx + np_).sum()))
-    return CoverExchange(rank, world, b, interior, send, halo,
-                         [int(v) for v in send_sizes.cpu().tolist()],
-                         [int(v) for v in (nx + np_).cpu().tolist()],
-                         int(np_.sum()), int(nx.sum()))
+    # ---- how this rank folds in what it receives ------------------------------------------
+    halo_x = from_coo(xr, torch.searchsorted(xcols, xc), xv, n_own, int(xcols.numel()))
+    ki = pkeys - (pkeys // stride) * stride
+    halo_p = from_coo(ki, torch.arange(pkeys.numel(), device=dev, dtype=i64),
+                      torch.ones(pkeys.numel(), dtype=val.dtype, device=dev), n_own,
+                      int(pkeys.numel()))
+    any_x = _global_sum(int(xcols.numel()), dev, group) > 0
+    any_p = _global_sum(int(pkeys.numel()), dev, group) > 0
+    return CoverExchange(rank, world, b, interior, (req_x - r0).contiguous(), send_p, halo_x,
+                         halo_p, [t[0] for t in theirs_l], [t[1] for t in theirs_l],
+                         [int(v) for v in nx.cpu().tolist()], [int(v) for v in np_.cpu().tolist()],
+                         any_x, any_p)
 
 
 class EdgeCutSpmm:
@@ -312,35 +327,73 @@ class EdgeCutSpmm:
         self._spmm = spmm
         self._gather = gather
         self.cover = isinstance(part, CoverExchange)
-        self.send_buf = torch.empty((sum(part.send_counts), feat), dtype=torch.float32,
-                                    device=self.device)
-        self.recv_buf = torch.empty((part.n_halo, feat), dtype=torch.float32, device=self.device)
-        self.out = torch.empty((part.n_own, feat), dtype=torch.float32, device=self.device)
+        f32 = dict(dtype=torch.float32, device=self.device)
+        if self.cover:
+            self.send_x = torch.empty((sum(part.send_x_counts), feat), **f32)
+            self.send_p = torch.empty((sum(part.send_p_counts), feat), **f32)
+            self.recv_x = torch.empty((sum(part.recv_x_counts), feat), **f32)
+            self.recv_p = torch.empty((sum(part.recv_p_counts), feat), **f32)
+        else:
+            self.send_buf = torch.empty((sum(part.send_counts), feat), **f32)
+            self.recv_buf = torch.empty((part.n_halo, feat), **f32)
+        self.out = torch.empty((part.n_own, feat), **f32)
         self.cuda = self.device.type == "cuda"
         self.comm_stream = torch.cuda.Stream(self.device) if self.cuda else None
+
+    def _exchange(self, recv, send, recv_counts, send_counts, cur):
+        """All-to-all-v on the communication stream after the work queued on ``cur``;
+        returns an event marking its completion (None off-GPU: done on return)."""
+        if not self.cuda:
+            _all_to_all_v(recv, send, recv_counts, send_counts, self.group)
+            return None
+        self.comm_stream.wait_stream(cur)
+        with torch.cuda.stream(self.comm_stream):
+            _all_to_all_v(recv, send, recv_counts, send_counts, self.group)
+            ev = torch.cuda.Event()
+            ev.record(self.comm_stream)
+        return ev
+
+    def _wait(self, ev, cur):
+        if ev is not None:
+            cur.wait_event(ev)
 
     def __call__(self, x: torch.Tensor, bias: torch.Tensor | None = None,
                  activation: str | None = None) -> torch.Tensor:
         p = self.part
         if x.shape != (p.n_own, self.feat):
             raise ValueError("x must be this rank's [n_own, feat] feature rows")
+        cur = torch.cuda.current_stream(self.device) if self.cuda else None
         if self.cover:
-            if self.send_buf.shape[0]:
-                self._spmm(p.send, x, None, out=self.send_buf)   # partial sums + feature rows
-        elif p.send_idx.numel():
+            ev_x = ev_p = None
+            if p.any_x:
+                if self.send_x.shape[0]:
+                    self._gather(x, p.send_x_idx, self.send_x)
+                ev_x = self._exchange(self.recv_x, self.send_x, p.recv_x_counts,
+                                      p.send_x_counts, cur)
+            if p.any_p:
+                if self.send_p.shape[0]:
+                    self._spmm(p.send_p, x, None, out=self.send_p)  # partial sums for peers
+                ev_p = self._exchange(self.recv_p, self.send_p, p.recv_p_counts,
+                                      p.send_p_counts, cur)
+            self._spmm(p.interior, x, bias, out=self.out)           # overlaps both exchanges
+            last = "p" if p.any_p else ("x" if p.any_x else None)
+            if p.any_x:
+                self._wait(ev_x, cur)
+                self._spmm(p.halo_x, self.recv_x, None, out=self.out, accumulate=True,
+                           activation=activation if last == "x" else None)
+            if p.any_p:
+                self._wait(ev_p, cur)
+                self._spmm(p.halo_p, self.recv_p, None, out=self.out, accumulate=True,
+                           activation=activation)
+            if last is None and activation is not None:
+                self._spmm(p.halo_x, self.recv_x, None, out=self.out, accumulate=True,
+                           activation=activation)
+            return self.out
+        if p.send_idx.numel():
             self._gather(x, p.send_idx, self.send_buf)
-        if self.cuda:
-            cur = torch.cuda.current_stream(self.device)
-            self.comm_stream.wait_stream(cur)
-            with torch.cuda.stream(self.comm_stream):
-                _all_to_all_v(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts,
-                              self.group)
-            # interior rows overlap the exchange on the compute stream
-            self._spmm(p.interior, x, bias, out=self.out)
-            cur.wait_stream(self.comm_stream)
-        else:
-            _all_to_all_v(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts, self.group)
-            self._spmm(p.interior, x, bias, out=self.out)
+        ev = self._exchange(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts, cur)
+        self._spmm(p.interior, x, bias, out=self.out)               # overlaps the exchange
+        self._wait(ev, cur)
         self._spmm(p.halo, self.recv_buf, None, activation=activation, out=self.out,
                    accumulate=True)
         return self.out

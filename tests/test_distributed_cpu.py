@@ -74,8 +74,7 @@ def _worker(rank, world, port, n, F, q, kind="gather"):
         if kind == "cover":
             part = build_cover_exchange(g, rank, world)
             # cut edges reduced here: halo column entries + partial edges computed for peers
-            edges = (part.interior.nnz + part.halo.nnz - part.n_partial_recv
-                     + part.send.nnz - part.n_feature_recv)
+            edges = part.interior.nnz + part.halo_x.nnz + part.send_p.nnz
         else:
             part = build_partition(g, rank, world)
             edges = part.nnz
@@ -121,6 +120,47 @@ def test_edge_cut_matches_single_device(world, kind):
     for p in range(world):  # what p sends to q is what q receives from p
         for qq in range(world):
             assert sends[p][0][qq] == sends[qq][1][p]
+
+
+def _blockdiag_worker(rank, world, port, q):
+    """Rows of each rank only touch its own columns: no exchange at all (any_x = any_p = False)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from graphneuralnetwork_amd.distributed import EdgeCutSpmm, build_cover_exchange
+        from graphneuralnetwork_amd.graph import from_coo
+        n, F = 40, 4
+        r = torch.arange(n)
+        rows = torch.cat([r, r])
+        cols = torch.cat([r, (r + 1) % 20 + (r // 20) * 20])   # two 20-cycles + self loops
+        g = from_coo(rows, cols, torch.full((2 * n,), -0.5), n, n)
+        part = build_cover_exchange(g, rank, world, bounds=torch.tensor([0, 20, 40]))
+        X = torch.from_numpy(np.random.default_rng(2).standard_normal((n, F)).astype(np.float32))
+        run = EdgeCutSpmm(part, F, "cpu", spmm=_cpu_spmm, gather=_cpu_gather)
+        y = run(X[rank * 20:(rank + 1) * 20].contiguous(), None, activation="relu").clone()
+        q.put((rank, part.any_x, part.any_p, y.numpy(), X.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cover_exchange_without_cut_edges():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_blockdiag_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(_collect(procs, q, 2, 120), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X = res[0][4]
+    for rank, ax, ap, y, _ in res:
+        assert not ax and not ap
+        rr = np.arange(rank * 20, rank * 20 + 20)
+        nxt = (rr + 1) % 20 + (rr // 20) * 20
+        ref = np.maximum(-0.5 * (X[rr] + X[nxt]), 0)
+        np.testing.assert_allclose(y, ref, rtol=1e-6, atol=1e-6)
 
 
 def test_nnz_balanced_bounds():

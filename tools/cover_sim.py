@@ -32,7 +32,7 @@ for W in [int(a) for a in sys.argv[1:]]:
         for kind in ("gather", "cover"):
             t = time.time()
             p = D.build_partition(g, r, W, bounds=bounds) if kind == "gather" else D.build_cover_exchange(g, r, W, bounds=bounds)
-            res[(kind, r)] = (p.n_halo, sum(p.send_counts), p.nnz if kind == "gather" else (p.interior.nnz, p.send.nnz, p.halo.nnz), time.time() - t)
+            res[(kind, r)] = (p.n_halo, sum(p.send_counts), p.nnz if kind == "gather" else (p.interior.nnz, p.send_p.nnz, p.halo_x.nnz + p.halo_p.nnz), time.time() - t)
     th = [threading.Thread(target=run, args=(r,)) for r in range(W)]
     [t.start() for t in th]; [t.join() for t in th]
     for kind in ("gather", "cover"):
