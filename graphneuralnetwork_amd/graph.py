@@ -196,10 +196,13 @@ def _build_plan(g: CsrGraph, seg_len: int) -> RowSplitPlan:
 
 # ---------------------------------------------------------------- builders
 def from_coo(row: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n_rows: int,
-             n_cols: int) -> CsrGraph:
-    """CSR from COO triplets (any order, duplicates kept), rows stably sorted."""
+             n_cols: int, check: bool = True) -> CsrGraph:
+    """CSR from COO triplets (any order, duplicates kept), rows stably sorted.
+
+    ``check=False`` skips the (host-syncing) index range check for indices the
+    caller has already validated."""
     row = row.to(torch.int64)
-    if row.numel() and (int(row.min()) < 0 or int(row.max()) >= n_rows
+    if check and row.numel() and (int(row.min()) < 0 or int(row.max()) >= n_rows
                         or int(col.min()) < 0 or int(col.max()) >= n_cols):
         raise IndexError("COO index out of range for the adjacency shape")
     order = torch.argsort(row, stable=True)

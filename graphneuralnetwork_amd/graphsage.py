@@ -23,7 +23,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .ops import gather_rows, sage_aggregate, sage_gather_aggregate
+from .graph import from_coo
+from .ops import gather_rows, sage_aggregate, sage_gather_aggregate, spmm_forward
 
 
 class Gathered(NamedTuple):
@@ -36,6 +37,19 @@ class Gathered(NamedTuple):
     """
     table: torch.Tensor
     index: torch.Tensor
+
+
+def _scatter_rows(g: torch.Tensor, idx: torch.Tensor, n: int, scale: float) -> torch.Tensor:
+    """out[t] = scale * sum of g[m] over the (m, j) with idx[m, j] == t  (the adjoint of a
+    row gather), as the HIP SpMM over the transposed index map: deterministic, no atomics.
+    ``idx`` was bounds-checked by the forward gather."""
+    M = idx.shape[0]
+    k = idx.numel() // max(M, 1)
+    rows = idx.reshape(-1)
+    cols = torch.arange(M, device=idx.device, dtype=torch.int64).repeat_interleave(k)
+    at = from_coo(rows, cols, torch.full((rows.numel(),), scale, dtype=torch.float32,
+                                         device=idx.device), n, M, check=False)
+    return spmm_forward(at, g.contiguous())
 
 
 class _MeanAgg(torch.autograd.Function):
@@ -63,10 +77,7 @@ class _GatherMeanAgg(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        k = idx.shape[1]
-        gt = torch.zeros((ctx.n, g.shape[1]), dtype=g.dtype, device=g.device)
-        gt.index_add_(0, idx.reshape(-1), (g / k).repeat_interleave(k, dim=0))
-        return gt, None
+        return _scatter_rows(g, idx, ctx.n, 1.0 / idx.shape[1]), None
 
 
 class _GatherRows(torch.autograd.Function):
@@ -79,9 +90,7 @@ class _GatherRows(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        gx = torch.zeros((ctx.n, g.shape[1]), dtype=g.dtype, device=g.device)
-        gx.index_add_(0, idx, g)
-        return gx, None
+        return _scatter_rows(g, idx.reshape(-1, 1), ctx.n, 1.0), None
 
 
 def Aggregator(neigh_feat, agg_func='MEAN'):

@@ -107,3 +107,25 @@ def test_mean_backward(dev):
     y = Aggregator(x, "MEAN")
     y.backward(torch.ones_like(y))
     assert torch.allclose(x.grad, torch.full_like(x, 0.25))
+
+
+@pytest.mark.parametrize("M,k,n,F", [(300, 10, 500, 64), (1000, 25, 120, 128), (7, 3, 5, 12)])
+def test_gather_backward_is_the_transposed_aggregation(dev, M, k, n, F):
+    """d table of the fused gather-mean / row gather (HIP SpMM over the transposed
+    index map) vs torch autograd of table[idx].mean(1) / table[idx] in float64."""
+    from graphneuralnetwork_amd.graphsage import Aggregator, Gathered, _gather
+    gen = torch.Generator().manual_seed(M + k)
+    table = torch.randn(n, F, generator=gen)
+    idx = torch.randint(0, n, (M, k), generator=gen)
+    ctr = torch.randint(0, n, (M,), generator=gen)
+    gy = torch.randn(M, F, generator=gen)
+    gz = torch.randn(M, F, generator=gen)
+    t = table.to(dev).requires_grad_(True)
+    y = Aggregator(Gathered(t, idx.to(dev)), "MEAN")
+    z = _gather(t, ctr.to(dev))
+    (y * gy.to(dev)).sum().add((z * gz.to(dev)).sum()).backward()
+    t64 = table.double().requires_grad_(True)
+    (t64[idx].mean(1) * gy.double()).sum().add((t64[ctr] * gz.double()).sum()).backward()
+    ref = t64.grad.numpy()
+    got = t.grad.cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=2e-5 * np.abs(ref).max())
