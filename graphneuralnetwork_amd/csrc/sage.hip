@@ -25,7 +25,7 @@ namespace gnn {
 constexpr int kSageBlock = 256;
 constexpr int kSageWaves = kSageBlock / kWave;
 
-enum SageMode : int32_t { kMean = 0, kArgmax = 1 };
+enum SageMode : int32_t { kMean = 0, kArgmax = 1, kSum = 2 };
 
 // (val, idx) "a beats b" under torch.argmax's rule.
 __device__ __forceinline__ bool beats(float va, int32_t ia, float vb, int32_t ib) {
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
   int32_t arg[NCH][VW];
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
-    acc[ch] = MODE == kMean ? vzero<VW>() : typename Vec<VW>::T(-INFINITY);
+    acc[ch] = MODE != kArgmax ? vzero<VW>() : typename Vec<VW>::T(-INFINITY);
 #pragma unroll
     for (int i = 0; i < VW; ++i) arg[ch][i] = 0x7fffffff;
   }
@@ -82,14 +82,14 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
       for (int ch = 0; ch < NCH; ++ch) {
         const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
         xv[u][ch] = (ok && f < feat) ? vload<VW>(row + f)
-                                     : (MODE == kMean ? vzero<VW>() : typename Vec<VW>::T(-INFINITY));
+                                     : (MODE != kArgmax ? vzero<VW>() : typename Vec<VW>::T(-INFINITY));
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
-        if (MODE == kMean) {
+        if (MODE != kArgmax) {
           acc[ch] += xv[u][ch];
         } else if (kk[u] != 0x7fffffff) {
 #pragma unroll
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
   for (int mm = LPR; mm < kWave; mm <<= 1) {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
-      if (MODE == kMean) {
+      if (MODE != kArgmax) {
         acc[ch] += shfl_xor_f(acc[ch], mm);
       } else {
 #pragma unroll
@@ -129,8 +129,9 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
   for (int ch = 0; ch < NCH; ++ch) {
     const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
     if (f >= feat) continue;
-    if (MODE == kMean) {
-      typename Vec<VW>::T r = acc[ch] / static_cast<float>(k);  // torch.mean: sum / k
+    if (MODE != kArgmax) {
+      // torch.mean: sum / k;  torch.sum: the sum
+      typename Vec<VW>::T r = MODE == kMean ? acc[ch] / static_cast<float>(k) : acc[ch];
       vstore<VW>(static_cast<float*>(out) + m * ldo + f, r);
     } else {
       int64_t* o = static_cast<int64_t*>(out) + m * ldo + f;
@@ -213,11 +214,13 @@ static int run_sage(SageArgs a, int32_t mode, bool vec4) {
   for (int64_t c0 = 0; c0 < feat; c0 += blk) {
     a.feat = feat - c0 < blk ? feat - c0 : blk;
     a.src = src0 + c0;
-    a.out = mode == kMean ? static_cast<void*>(static_cast<float*>(out0) + c0)
-                          : static_cast<void*>(static_cast<int64_t*>(out0) + c0);
+    a.out = mode != kArgmax ? static_cast<void*>(static_cast<float*>(out0) + c0)
+                            : static_cast<void*>(static_cast<int64_t*>(out0) + c0);
     int rc;
     if (mode == kMean)
       rc = vec4 ? dispatch_sage<4, kMean, GATHER>(a) : dispatch_sage<1, kMean, GATHER>(a);
+    else if (mode == kSum)
+      rc = vec4 ? dispatch_sage<4, kSum, GATHER>(a) : dispatch_sage<1, kSum, GATHER>(a);
     else
       rc = vec4 ? dispatch_sage<4, kArgmax, GATHER>(a) : dispatch_sage<1, kArgmax, GATHER>(a);
     if (rc != GNN_OK) return rc;
@@ -232,12 +235,12 @@ using namespace gnn;
 extern "C" int gnn_sage_aggregate_f32(const float* neigh, int64_t ld_k, int64_t ld_m, int64_t M,
                                       int64_t k, int64_t feat, int32_t mode, void* out,
                                       int64_t ldo, void* stream) {
-  if (M < 0 || k < 0 || feat < 0 || (mode != kMean && mode != kArgmax)) return GNN_E_ARG;
+  if (M < 0 || k < 0 || feat < 0 || (mode != kMean && mode != kArgmax && mode != kSum)) return GNN_E_ARG;
   if (M == 0 || feat == 0) return GNN_OK;
   if (!neigh || !out || ld_k < feat || ldo < feat) return GNN_E_ARG;
   if (k == 0) return GNN_E_UNSUPPORTED;  // torch: mean of nothing is NaN, argmax raises
   const bool vec4 = feat % 4 == 0 && ld_k % 4 == 0 && ld_m % 4 == 0 && ldo % 4 == 0 &&
-                    aligned_to(neigh, 16) && aligned_to(out, mode == kMean ? 16 : 32);
+                    aligned_to(neigh, 16) && aligned_to(out, mode != kArgmax ? 16 : 32);
   SageArgs a{neigh, ld_k, ld_m, 0, nullptr, 0, M, k, feat, out, ldo, nullptr,
              static_cast<hipStream_t>(stream)};
   return run_sage<false>(a, mode, vec4);
@@ -247,13 +250,13 @@ extern "C" int gnn_sage_gather_aggregate_f32(const float* table, int64_t ldt, in
                                              const int64_t* idx, int64_t ldi, int64_t M, int64_t k,
                                              int64_t feat, int32_t mode, void* out, int64_t ldo,
                                              int32_t* err_flag, void* stream) {
-  if (M < 0 || k < 0 || feat < 0 || n_table < 0 || (mode != kMean && mode != kArgmax))
+  if (M < 0 || k < 0 || feat < 0 || n_table < 0 || (mode != kMean && mode != kArgmax && mode != kSum))
     return GNN_E_ARG;
   if (M == 0 || feat == 0) return GNN_OK;
   if (!table || !idx || !out || !err_flag || ldt < feat || ldo < feat || ldi < k) return GNN_E_ARG;
   if (k == 0) return GNN_E_UNSUPPORTED;
   const bool vec4 = feat % 4 == 0 && ldt % 4 == 0 && ldo % 4 == 0 && aligned_to(table, 16) &&
-                    aligned_to(out, mode == kMean ? 16 : 32);
+                    aligned_to(out, mode != kArgmax ? 16 : 32);
   SageArgs a{table, ldt, 0, n_table, idx, ldi, M, k, feat, out, ldo, err_flag,
              static_cast<hipStream_t>(stream)};
   return run_sage<true>(a, mode, vec4);

@@ -53,31 +53,35 @@ def _scatter_rows(g: torch.Tensor, idx: torch.Tensor, n: int, scale: float) -> t
 
 
 class _MeanAgg(torch.autograd.Function):
-    """Pre-gathered MEAN with autograd (d neigh = d out / k broadcast over k)."""
+    """Pre-gathered MEAN / SUM with autograd (d neigh = d out (/ k) broadcast over k)."""
 
     @staticmethod
-    def forward(ctx, neigh):
+    def forward(ctx, neigh, kind="MEAN"):
         ctx.k = neigh.shape[1]
-        return sage_aggregate(neigh, "MEAN")
+        ctx.kind = kind
+        return sage_aggregate(neigh, kind)
 
     @staticmethod
     def backward(ctx, g):
-        return (g / ctx.k).unsqueeze(1).expand(-1, ctx.k, -1)
+        g = g / ctx.k if ctx.kind == "MEAN" else g
+        return g.unsqueeze(1).expand(-1, ctx.k, -1), None
 
 
 class _GatherMeanAgg(torch.autograd.Function):
-    """Fused gather + MEAN with autograd w.r.t. the table (scatter of d out / k)."""
+    """Fused gather + MEAN / SUM with autograd w.r.t. the table (scatter of d out (/ k))."""
 
     @staticmethod
-    def forward(ctx, table, idx):
+    def forward(ctx, table, idx, kind="MEAN"):
         ctx.save_for_backward(idx)
         ctx.n = table.shape[0]
-        return sage_gather_aggregate(table, idx, "MEAN")
+        ctx.kind = kind
+        return sage_gather_aggregate(table, idx, kind)
 
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        return _scatter_rows(g, idx, ctx.n, 1.0 / idx.shape[1]), None
+        scale = 1.0 / idx.shape[1] if ctx.kind == "MEAN" else 1.0
+        return _scatter_rows(g, idx, ctx.n, scale), None, None
 
 
 class _GatherRows(torch.autograd.Function):
@@ -95,17 +99,26 @@ class _GatherRows(torch.autograd.Function):
 
 def Aggregator(neigh_feat, agg_func='MEAN'):
     """GraphSAGE/graph_utils.py:4-11 on the device ('MEAN' -> fp32, 'MAX' -> int64 argmax)."""
-    if isinstance(neigh_feat, Gathered):
-        return _gather_aggregate(neigh_feat.table, neigh_feat.index, agg_func)
-    if agg_func == 'MEAN' and torch.is_grad_enabled() and neigh_feat.requires_grad:
-        return _MeanAgg.apply(neigh_feat)
-    return sage_aggregate(neigh_feat, agg_func)
+    if agg_func not in ('MEAN', 'MAX'):
+        print('请选择合适的聚合函数')  # the reference prints this, then a bare raise
+        raise RuntimeError("No active exception to reraise")
+    return reduce_neighbors(neigh_feat, agg_func)
 
 
 def _gather_aggregate(table, idx, agg_func):
-    if agg_func == 'MEAN' and torch.is_grad_enabled() and table.requires_grad:
-        return _GatherMeanAgg.apply(table, idx)
+    if agg_func in ('MEAN', 'SUM') and torch.is_grad_enabled() and table.requires_grad:
+        return _GatherMeanAgg.apply(table, idx, agg_func)
     return sage_gather_aggregate(table, idx, agg_func)
+
+
+def reduce_neighbors(neigh_feat, kind='MEAN'):
+    """MEAN / SUM / MAX(argmax) over dim 1 of a pre-gathered [M, k, F] tensor or a
+    ``Gathered`` (table, [M, k] index), with autograd for MEAN / SUM."""
+    if isinstance(neigh_feat, Gathered):
+        return _gather_aggregate(neigh_feat.table, neigh_feat.index, kind)
+    if kind in ('MEAN', 'SUM') and torch.is_grad_enabled() and neigh_feat.requires_grad:
+        return _MeanAgg.apply(neigh_feat, kind)
+    return sage_aggregate(neigh_feat, kind)
 
 
 def _gather(x, idx):

@@ -180,18 +180,19 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
 
 
 # ---------------------------------------------------------------- GraphSAGE
-SAGE_MODES = {"MEAN": 0, "MAX": 1}
+SAGE_MODES = {"MEAN": 0, "MAX": 1}   # GraphSAGE/graph_utils.py Aggregator
+SAGE_KINDS = {"MEAN": 0, "MAX": 1, "SUM": 2}   # + NeighborAggregator 'sum' (GraphSAGE_Pytorch)
 
 
 def _sage_out(M, F, mode, dev):
-    dt = torch.float32 if mode == 0 else torch.int64
+    dt = torch.int64 if mode == 1 else torch.float32
     return torch.empty((M, F), dtype=dt, device=dev)
 
 
 def sage_aggregate(neigh: torch.Tensor, agg_func: str = "MEAN") -> torch.Tensor:
-    """Aggregator over a pre-gathered [M, k, F] tensor (GraphSAGE/graph_utils.py:4-11)."""
-    if agg_func not in SAGE_MODES:
-        print('请选择合适的聚合函数')  # the reference's message before its bare raise
+    """Aggregator over a pre-gathered [M, k, F] tensor (GraphSAGE/graph_utils.py:4-11);
+    'SUM' is NeighborAggregator's sum (GraphSAGE_Pytorch/models/Aggregator.py:21-22)."""
+    if agg_func not in SAGE_KINDS:
         raise RuntimeError(f"unknown agg_func {agg_func!r}")
     _require_device(neigh)
     if neigh.dtype != torch.float32 or neigh.dim() != 3:
@@ -199,11 +200,11 @@ def sage_aggregate(neigh: torch.Tensor, agg_func: str = "MEAN") -> torch.Tensor:
     if neigh.stride(2) != 1:
         neigh = neigh.contiguous()
     M, k, F = neigh.shape
-    mode = SAGE_MODES[agg_func]
+    mode = SAGE_KINDS[agg_func]
     if k == 0:
         if mode == 1:
             raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
-        return torch.full((M, F), float("nan"), device=neigh.device)
+        return torch.full((M, F), 0.0 if mode == 2 else float("nan"), device=neigh.device)
     out = _sage_out(M, F, mode, neigh.device)
     lib = _lib.load()
     _lib.check(lib.gnn_sage_aggregate_f32(neigh.data_ptr(), neigh.stride(1), neigh.stride(0), M, k,
@@ -221,7 +222,7 @@ def _check_err(err: torch.Tensor, what: str) -> None:
 def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str = "MEAN",
                           check: bool = True) -> torch.Tensor:
     """Aggregator(torch.embedding(table, idx)) fused: [M, k] int64 indices into table [n, F]."""
-    if agg_func not in SAGE_MODES:
+    if agg_func not in SAGE_KINDS:
         raise RuntimeError(f"unknown agg_func {agg_func!r}")
     _require_device(table, idx)
     table = _rows_f32(table, "table")
@@ -232,11 +233,11 @@ def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str 
         idx = idx.contiguous()
     M, k = idx.shape
     F = table.shape[1]
-    mode = SAGE_MODES[agg_func]
+    mode = SAGE_KINDS[agg_func]
     if k == 0:
         if mode == 1:
             raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
-        return torch.full((M, F), float("nan"), device=table.device)
+        return torch.full((M, F), 0.0 if mode == 2 else float("nan"), device=table.device)
     out = _sage_out(M, F, mode, table.device)
     err = torch.zeros(1, dtype=torch.int32, device=table.device)
     lib = _lib.load()

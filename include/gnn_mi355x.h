@@ -186,12 +186,15 @@ int gnn_gat_backward_nodes_f32(const int64_t* rowptr_t, const int32_t* src_t,
 #define GNN_SAGE_MEAN 0   /* torch.mean(neigh_feat, dim=1)               -> fp32 out  */
 #define GNN_SAGE_ARGMAX 1 /* torch.argmax(neigh_feat, dim=1): first max,
                              NaN counts as the maximum                   -> int64 out */
+#define GNN_SAGE_SUM 2    /* neighbor_feature.sum(dim=1)                  -> fp32 out
+                             (GraphSAGE_Pytorch/models/Aggregator.py:21-22)          */
 
 /*
  * GraphSAGE Aggregator over a pre-gathered neighbour tensor
  *   neigh[m, j, f] at neigh + m*ld_m + j*ld_k + f   (m < M, j < k, f < feat)
  * Replaces Aggregator(neigh_feat, agg_func) at GraphSAGE/graph_utils.py:4-11.
- * out: fp32 [M, ldo] (MEAN) or int64 [M, ldo] (ARGMAX). k == 0 -> GNN_E_UNSUPPORTED.
+ * Also NeighborAggregator.forward 'mean' / 'sum' (GraphSAGE_Pytorch/models/Aggregator.py:18-22).
+ * out: fp32 [M, ldo] (MEAN, SUM) or int64 [M, ldo] (ARGMAX). k == 0 -> GNN_E_UNSUPPORTED.
  */
 int gnn_sage_aggregate_f32(const float* neigh, int64_t ld_k, int64_t ld_m, int64_t M, int64_t k,
                            int64_t feat, int32_t mode, void* out, int64_t ldo, void* stream);

@@ -295,3 +295,61 @@ def gat_logits(wh, heads, fh, a_src, a_dst):
     w = np.asarray(wh, np.float64).reshape(-1, heads, fh)
     return (w * np.asarray(a_src, np.float64).reshape(heads, fh)).sum(-1), \
            (w * np.asarray(a_dst, np.float64).reshape(heads, fh)).sum(-1)
+
+
+# ------------------------------------------------------------------ HAN
+def han_gatconv(h, adj_dense, heads, alpha=0.2, out_head=None):
+    """GATConv.forward, eval mode (HAN/models/NodeAttention.py:59-62): concat of the
+    ELU'd dense heads, then ELU(out_att) -- or, without out_att, ELU once more."""
+    x = np.concatenate([gat_dense_head(h, adj_dense, W, a, alpha, True) for W, a in heads], 1)
+    if out_head is not None:
+        return _elu(gat_dense_head(x, adj_dense, out_head[0], out_head[1], alpha, False))
+    return _elu(x)
+
+
+def han_semantic_attention(z, w1, b1, w2):
+    """SemanticAttention.forward (HAN/models/SemanticAttention.py:15-20):
+    beta = softmax_M(mean_N(tanh(z W1^T + b1) W2^T)); out = sum_M beta_M z[:, M]."""
+    z = np.asarray(z, np.float64)
+    w = (np.tanh(z @ np.asarray(w1, np.float64).T + np.asarray(b1, np.float64))
+         @ np.asarray(w2, np.float64).T).mean(0)                       # (M, 1)
+    beta = np.exp(w - w.max(0)) / np.exp(w - w.max(0)).sum(0)
+    return (beta[None] * z).sum(1)
+
+
+def han_layer(gs, h, gat_heads, sem):
+    """HANLayer.forward (HAN/models/HAN.py:17-23): one GATConv per metapath graph,
+    stacked (N, M, D*K), semantic attention over M."""
+    z = np.stack([han_gatconv(h, g, heads) for g, heads in zip(gs, gat_heads)], 1)
+    return han_semantic_attention(z, *sem)
+
+
+# -------------------------------------------------- GraphSAGE_Pytorch (SURVEY 8f row 4)
+def neighbor_aggregator(nb, weight, bias=None, method="mean"):
+    """NeighborAggregator.forward (GraphSAGE_Pytorch/models/Aggregator.py:18-33):
+    mean / sum over dim 1, then @ weight (+ bias)."""
+    nb = np.asarray(nb, np.float64)
+    a = nb.mean(1) if method == "mean" else nb.sum(1)
+    out = a @ np.asarray(weight, np.float64)
+    return out if bias is None else out + np.asarray(bias, np.float64)
+
+
+def sage_gcn(src, nb, weight, agg_weight, agg_bias=None, neigh="mean", hidden="sum", relu=True):
+    """SageGCN.forward (GraphSAGE_Pytorch/models/SageGCN.py:24-37)."""
+    nh = neighbor_aggregator(nb, agg_weight, agg_bias, neigh)
+    sh = np.asarray(src, np.float64) @ np.asarray(weight, np.float64)
+    out = sh + nh if hidden == "sum" else np.concatenate([sh, nh], 1)
+    return np.maximum(out, 0) if relu else out
+
+
+def graphsage_tree(feats, layers, nbrs):
+    """GraphSage.forward (GraphSAGE_Pytorch/models/GraphSage.py:20-31): layer l folds hop
+    features pairwise (hop, hop+1 viewed as [n_hop, k_hop, F]); last layer has no ReLU.
+    layers: [(weight, agg_weight)] per layer."""
+    hidden = [np.asarray(f, np.float64) for f in feats]
+    L = len(nbrs)
+    for l in range(L):
+        w, aw = layers[l]
+        hidden = [sage_gcn(hidden[hop], hidden[hop + 1].reshape(len(hidden[hop]), nbrs[hop], -1),
+                           w, aw, relu=l < L - 1) for hop in range(L - l)]
+    return hidden[0]

@@ -307,7 +307,88 @@ def part_sage():
     print("sage unsup", emb.shape, scores.shape)
 
 
-PARTS = {"gcn": part_gcn, "gat": part_gat, "sage": part_sage}
+# ----------------------------------------------------------------------- HAN
+def part_han():
+    """HAN node-level attention (GATConv per metapath) + semantic attention, 2 layers."""
+    sys.path.insert(0, str(REF / "HAN"))
+    import torch
+    from models import HANModel                       # HAN/models/__init__.py
+    rng = np.random.default_rng(11)
+    torch.manual_seed(0)
+    N, M, Fin, hid, C = 300, 3, 32, 8, 3
+    heads = [4, 2]
+    gs = []
+    for _ in range(M):
+        A = np.zeros((N, N), np.float32)
+        s, t = rng.integers(0, N, 1500), rng.integers(0, N, 1500)
+        A[s, t] = 1
+        A[t, s] = 1
+        A[np.arange(N), np.arange(N)] = 1             # metapath graphs keep self loops
+        gs.append(A)
+    h = _q(rng, (N, Fin), 32, 32)
+    net = HANModel(M, Fin, hid, C, heads, dropout=0.6)
+    _set_params(net, rng, 64, 40)
+    net.eval()
+    with torch.no_grad():
+        gt = [torch.from_numpy(a) for a in gs]
+        layer0 = net.layers[0](gt, torch.from_numpy(h))
+        logits = net(gt, torch.from_numpy(h))
+    out = {"h": h, "heads": np.array(heads), "layer0": layer0.numpy(), "logits": logits.numpy()}
+    for i, a in enumerate(gs):
+        nz = np.nonzero(a)
+        out[f"g{i}_row"], out[f"g{i}_col"] = nz[0].astype(np.int32), nz[1].astype(np.int32)
+    for k, v in net.state_dict().items():
+        out[f"sd_{k}"] = v.numpy()
+    out["dims"] = np.array([N, M, Fin, hid, C])
+    np.savez_compressed(HERE / "han.npz", **out)
+    print("han", logits.shape, len(net.state_dict()))
+
+
+# ------------------------------------------------------- GraphSAGE_Pytorch
+def part_sagepy():
+    """GraphSAGE_Pytorch GraphSage over pre-sampled hop features + SageGCN variants."""
+    sys.path.insert(0, str(REF / "GraphSAGE_Pytorch"))
+    import torch
+    from models import GraphSage, SageGCN             # GraphSAGE_Pytorch/models/__init__.py
+    from models.Aggregator import NeighborAggregator
+    rng = np.random.default_rng(12)
+    torch.manual_seed(0)
+    Fin, hidden, nbrs, B = 32, [16, 5], [10, 5], 20
+    feats = [_q(rng, (B, Fin), 32, 32), _q(rng, (B * nbrs[0], Fin), 32, 32),
+             _q(rng, (B * nbrs[0] * nbrs[1], Fin), 32, 32)]
+    net = GraphSage(Fin, hidden, nbrs)
+    _set_params(net, rng, 64, 40)
+    with torch.no_grad():
+        y = net([torch.from_numpy(f) for f in feats])
+    out = {f"X{i}": f for i, f in enumerate(feats)}
+    out["y"] = y.numpy()
+    for k, v in net.state_dict().items():
+        out[f"sd_{k}"] = v.numpy()
+    # SageGCN with 'sum' neighbours + 'concat' hidden, and a biased 'mean' aggregator
+    src, nb = torch.from_numpy(feats[0]), torch.from_numpy(feats[1]).view(B, nbrs[0], Fin)
+    layer = SageGCN(Fin, 12, aggr_neighbor_method="sum", aggr_hidden_method="concat")
+    agg = NeighborAggregator(Fin, 7, use_bias=True, aggr_method="mean")
+    for m in (layer, agg):
+        _set_params(m, rng, 64, 40)
+    with torch.no_grad():
+        out["sumcat_y"] = layer(src, nb).numpy()
+        out["biasmean_y"] = agg(nb).numpy()
+    for k, v in layer.state_dict().items():
+        out[f"sumcat_sd_{k}"] = v.numpy()
+    for k, v in agg.state_dict().items():
+        out[f"biasmean_sd_{k}"] = v.numpy()
+    try:                                              # 'max' gets a namedtuple -> matmul fails
+        NeighborAggregator(Fin, 7, aggr_method="max")(nb)
+        out["max_raises"] = np.int64(0)
+    except TypeError:
+        out["max_raises"] = np.int64(1)
+    out["dims"] = np.array([Fin, B] + hidden + nbrs)
+    np.savez_compressed(HERE / "sagepy.npz", **out)
+    print("sagepy", y.shape)
+
+
+PARTS = {"gcn": part_gcn, "gat": part_gat, "sage": part_sage, "han": part_han,
+         "sagepy": part_sagepy}
 
 if __name__ == "__main__":
     sys.dont_write_bytecode = True

@@ -165,3 +165,54 @@ def test_gat_csr_form_matches_reference_heads(golden, kind):
     out = O.gat_csr(rowptr, col, wh, el, er, H, fh, alpha, kind == "sparse")
     out = np.where(out > 0, out, np.expm1(np.minimum(out, 0)))
     close(out, g[f"{kind}_concat"])
+
+
+def _han_params(d, layer, M, heads):
+    p = f"sd_layers.{layer}."
+    gat = [[(d[f"{p}gat_layers.meta_path_model{m}.attentions.AttentionHead{i}.W"],
+             d[f"{p}gat_layers.meta_path_model{m}.attentions.AttentionHead{i}.a"])
+            for i in range(heads)] for m in range(M)]
+    sem = (d[f"{p}semantic_attention.project.0.weight"], d[f"{p}semantic_attention.project.0.bias"],
+           d[f"{p}semantic_attention.project.2.weight"])
+    return gat, sem
+
+
+def _han_graphs(d, N, M):
+    gs = []
+    for m in range(M):
+        A = np.zeros((N, N), np.float32)
+        A[d[f"g{m}_row"], d[f"g{m}_col"]] = 1
+        gs.append(A)
+    return gs
+
+
+def test_han_oracle_matches_reference(golden):
+    """HANModel (HAN/models/HAN.py:26-41) restated layer by layer == the reference's logits."""
+    d = golden("han")
+    N, M, Fin, hid, C = d["dims"]
+    heads = d["heads"]
+    gs = _han_graphs(d, N, M)
+    h = d["h"]
+    for layer in range(len(heads)):
+        gat, sem = _han_params(d, layer, M, heads[layer])
+        h = O.han_layer(gs, h, gat, sem)
+        if layer == 0:
+            np.testing.assert_allclose(h, d["layer0"], rtol=1e-4, atol=1e-5)
+    logits = h @ d["sd_predict.weight"].T.astype(np.float64) + d["sd_predict.bias"]
+    np.testing.assert_allclose(logits, d["logits"], rtol=1e-4, atol=1e-5)
+
+
+def test_graphsage_tree_oracle_matches_reference(golden):
+    """GraphSAGE_Pytorch GraphSage / SageGCN / NeighborAggregator restated == reference outputs."""
+    d = golden("sagepy")
+    Fin, B, h0, h1, k0, k1 = d["dims"]
+    layers = [(d[f"sd_gcn.{i}.weight"], d[f"sd_gcn.{i}.aggregator.weight"]) for i in range(2)]
+    y = O.graphsage_tree([d["X0"], d["X1"], d["X2"]], layers, [k0, k1])
+    np.testing.assert_allclose(y, d["y"], rtol=1e-4, atol=1e-5)
+    nb = d["X1"].reshape(B, k0, Fin)
+    y2 = O.sage_gcn(d["X0"], nb, d["sumcat_sd_weight"], d["sumcat_sd_aggregator.weight"],
+                    neigh="sum", hidden="concat")
+    np.testing.assert_allclose(y2, d["sumcat_y"], rtol=1e-4, atol=1e-5)
+    y3 = O.neighbor_aggregator(nb, d["biasmean_sd_weight"], d["biasmean_sd_bias"], "mean")
+    np.testing.assert_allclose(y3, d["biasmean_y"], rtol=1e-4, atol=1e-5)
+    assert int(d["max_raises"]) == 1
