@@ -34,9 +34,24 @@ class Gathered(NamedTuple):
     ``center_feats_data`` ([M] index) / ``center_neigh_feats_data`` ([M, k] index)
     the reference's collate_fn builds with torch.embedding
     (GraphSAGE/data_utils.py:161-162); see ``sampler.sample_batch``.
+    ``trusted``: the indices are known to be in range (built by the device
+    sampler), so the gather skips its index check and the host sync it costs.
     """
     table: torch.Tensor
     index: torch.Tensor
+    trusted: bool = False
+
+
+def trust_map(t: torch.Tensor) -> torch.Tensor:
+    """Mark an index map as -1-free and in range (the device sampler's maps): the
+    forward then skips the reference's ``map != -1`` filtering and the index check,
+    i.e. every host synchronisation."""
+    t._gnn_trusted = True
+    return t
+
+
+def _trusted(t) -> bool:
+    return bool(getattr(t, "_gnn_trusted", False))
 
 
 def _scatter_rows(g: torch.Tensor, idx: torch.Tensor, n: int, scale: float) -> torch.Tensor:
@@ -71,30 +86,30 @@ class _GatherMeanAgg(torch.autograd.Function):
     """Fused gather + MEAN / SUM with autograd w.r.t. the table (scatter of d out (/ k))."""
 
     @staticmethod
-    def forward(ctx, table, idx, kind="MEAN"):
+    def forward(ctx, table, idx, kind="MEAN", check=True):
         ctx.save_for_backward(idx)
         ctx.n = table.shape[0]
         ctx.kind = kind
-        return sage_gather_aggregate(table, idx, kind)
+        return sage_gather_aggregate(table, idx, kind, check=check)
 
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
         scale = 1.0 / idx.shape[1] if ctx.kind == "MEAN" else 1.0
-        return _scatter_rows(g, idx, ctx.n, scale), None, None
+        return _scatter_rows(g, idx, ctx.n, scale), None, None, None
 
 
 class _GatherRows(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, idx):
+    def forward(ctx, x, idx, check=True):
         ctx.save_for_backward(idx)
         ctx.n = x.shape[0]
-        return gather_rows(x, idx)
+        return gather_rows(x, idx, check=check)
 
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        return _scatter_rows(g, idx.reshape(-1, 1), ctx.n, 1.0), None
+        return _scatter_rows(g, idx.reshape(-1, 1), ctx.n, 1.0), None, None
 
 
 def Aggregator(neigh_feat, agg_func='MEAN'):
@@ -105,26 +120,26 @@ def Aggregator(neigh_feat, agg_func='MEAN'):
     return reduce_neighbors(neigh_feat, agg_func)
 
 
-def _gather_aggregate(table, idx, agg_func):
+def _gather_aggregate(table, idx, agg_func, trusted=False):
     if agg_func in ('MEAN', 'SUM') and torch.is_grad_enabled() and table.requires_grad:
-        return _GatherMeanAgg.apply(table, idx, agg_func)
-    return sage_gather_aggregate(table, idx, agg_func)
+        return _GatherMeanAgg.apply(table, idx, agg_func, not trusted)
+    return sage_gather_aggregate(table, idx, agg_func, check=not trusted)
 
 
 def reduce_neighbors(neigh_feat, kind='MEAN'):
     """MEAN / SUM / MAX(argmax) over dim 1 of a pre-gathered [M, k, F] tensor or a
     ``Gathered`` (table, [M, k] index), with autograd for MEAN / SUM."""
     if isinstance(neigh_feat, Gathered):
-        return _gather_aggregate(neigh_feat.table, neigh_feat.index, kind)
+        return _gather_aggregate(neigh_feat.table, neigh_feat.index, kind, neigh_feat.trusted)
     if kind in ('MEAN', 'SUM') and torch.is_grad_enabled() and neigh_feat.requires_grad:
         return _MeanAgg.apply(neigh_feat, kind)
     return sage_aggregate(neigh_feat, kind)
 
 
-def _gather(x, idx):
+def _gather(x, idx, trusted=False):
     if torch.is_grad_enabled() and x.requires_grad:
-        return _GatherRows.apply(x, idx)
-    return gather_rows(x, idx)
+        return _GatherRows.apply(x, idx, not trusted)
+    return gather_rows(x, idx, check=not trusted)
 
 
 class SageLayer(nn.Module):
@@ -147,8 +162,12 @@ class SageLayer(nn.Module):
             self_feats = self_feats.to(torch.float32)
         n = self.input_size
         # cat([self, agg]) @ W^T == self @ W[:, :n]^T + agg @ W[:, n:]^T (no concat copy)
-        out = torch.addmm(F.linear(self_feats, W[:, :n]), aggregate_feats, W[:, n:].t())
-        return F.relu(out)
+        part = F.linear(self_feats, W[:, :n])
+        if torch.is_grad_enabled() and (W.requires_grad or self_feats.requires_grad
+                                        or aggregate_feats.requires_grad):
+            return F.relu(torch.addmm(part, aggregate_feats, W[:, n:].t()))
+        # inference: ReLU in the GEMM epilogue (hipBLASLt), one kernel fewer
+        return torch._addmm_activation(part, aggregate_feats, W[:, n:].t())
 
 
 class GraphSAGE(nn.Module):
@@ -175,18 +194,24 @@ class GraphSAGE(nn.Module):
             pending = None  # (table, index map) of a fused gather-aggregate
             feats_data = None
             if isinstance(center_feats_data, Gathered):
-                center_feats_data = _gather(center_feats_data.table, center_feats_data.index)
+                center_feats_data = _gather(center_feats_data.table, center_feats_data.index,
+                                            center_feats_data.trusted)
             for i, block in enumerate(self.sage_blocks):
                 if pending is None:
                     aggregator_feats_data = Aggregator(center_neigh_feats_data, self.agg_func)
                 else:
-                    aggregator_feats_data = _gather_aggregate(pending[0], pending[1], self.agg_func)
+                    aggregator_feats_data = _gather_aggregate(pending[0], pending[1], self.agg_func,
+                                                              pending[2])
                 feats_data = block(center_feats_data, aggregator_feats_data)
                 if i != self.num_layers - 1:
                     cm = center_nodes_map[i]
                     nm = center_neigh_nodes_map[i]
-                    center_feats_data = _gather(feats_data, cm[cm != -1])
-                    pending = (feats_data, nm[nm[:, 0] != -1, :])
+                    if _trusted(cm) and _trusted(nm):  # device-sampler maps: no -1, in range
+                        center_feats_data = _gather(feats_data, cm, True)
+                        pending = (feats_data, nm, True)
+                    else:                              # GraphSAGE.py:56-57 (-1 padding dropped)
+                        center_feats_data = _gather(feats_data, cm[cm != -1])
+                        pending = (feats_data, nm[nm[:, 0] != -1, :], False)
             classes = None
             if not self.Unsupervised:
                 classes = self.dense(feats_data)

@@ -31,13 +31,13 @@ _KINDS = {"mean": "MEAN", "sum": "SUM"}
 def _nbr_view(feat, n_src: int, k: int):
     """hidden[hop + 1].view(n_src, k, -1), for a tensor or a Gathered hop."""
     if isinstance(feat, Gathered):
-        return Gathered(feat.table, feat.index.reshape(n_src, k))
+        return Gathered(feat.table, feat.index.reshape(n_src, k), feat.trusted)
     return feat.view((n_src, k, -1))
 
 
 def _rows(feat):
     """A hop's feature rows as a tensor (row gather for a Gathered hop)."""
-    return _gather(feat.table, feat.index.reshape(-1)) if isinstance(feat, Gathered) else feat
+    return _gather(feat.table, feat.index.reshape(-1), feat.trusted) if isinstance(feat, Gathered) else feat
 
 
 def _len(feat) -> int:

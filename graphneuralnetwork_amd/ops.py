@@ -214,6 +214,20 @@ def sage_aggregate(neigh: torch.Tensor, agg_func: str = "MEAN") -> torch.Tensor:
     return out
 
 
+_ERR_SINK: dict = {}
+
+
+def _err_flag(dev, check: bool) -> torch.Tensor:
+    """A zeroed device flag for a checked gather; unchecked (trusted-index) calls share a
+    per-device sink that is never read, so they cost no memset and no host sync."""
+    if check:
+        return torch.zeros(1, dtype=torch.int32, device=dev)
+    t = _ERR_SINK.get(dev)
+    if t is None:
+        t = _ERR_SINK[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return t
+
+
 def _check_err(err: torch.Tensor, what: str) -> None:
     if int(err.item()) != 0:
         raise IndexError(f"{what}: index out of range in self")
@@ -239,7 +253,7 @@ def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str 
             raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
         return torch.full((M, F), 0.0 if mode == 2 else float("nan"), device=table.device)
     out = _sage_out(M, F, mode, table.device)
-    err = torch.zeros(1, dtype=torch.int32, device=table.device)
+    err = _err_flag(table.device, check)
     lib = _lib.load()
     _lib.check(lib.gnn_sage_gather_aggregate_f32(
         table.data_ptr(), table.stride(0), table.shape[0], idx.data_ptr(), idx.stride(0), M, k, F,
@@ -259,7 +273,7 @@ def gather_rows(x: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = N
     n, F = idx.numel(), x.shape[1]
     if out is None:
         out = torch.empty((n, F), dtype=torch.float32, device=x.device)
-    err = torch.zeros(1, dtype=torch.int32, device=x.device)
+    err = _err_flag(x.device, check)
     lib = _lib.load()
     _lib.check(lib.gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0], idx.data_ptr(), n, F,
                                        out.data_ptr(), out.stride(0), err.data_ptr(),

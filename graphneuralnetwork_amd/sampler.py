@@ -25,7 +25,7 @@ import torch
 
 from . import _lib
 from .graph import CsrGraph
-from .graphsage import Gathered
+from .graphsage import Gathered, trust_map
 
 
 def sample_neighbors(adj: CsrGraph, nodes: torch.Tensor, k: int, seed: int = 0) -> torch.Tensor:
@@ -63,8 +63,8 @@ class SampledBatch:
 
     def forward_args(self, table: torch.Tensor):
         """The 4 leading arguments of GraphSAGE.forward (supervised branch)."""
-        return (Gathered(table, self.frontier), [self.center_map],
-                Gathered(table, self.frontier_nbrs), [self.neigh_map])
+        return (Gathered(table, self.frontier, True), [trust_map(self.center_map)],
+                Gathered(table, self.frontier_nbrs, True), [trust_map(self.neigh_map)])
 
 
 def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int = 0,
