@@ -53,7 +53,8 @@ SIGNATURES: dict[str, tuple] = {
         _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
         _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
         _vp, _vp, _i64,                 # small_row, small_col, n_small
-        _vp, _i64, _vp, _vp,            # mid_row, n_mid, partial, stats
+        _vp, _i64, _vp, _i64,           # mid_row, n_mid, short_row, n_short
+        _vp, _vp,                       # partial, stats
         _u32, _vp]),                    # flags, stream
     "gnn_gat_backward_prep_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp,
                                                  _vp]),

@@ -85,6 +85,9 @@ struct GatParams {
   int64_t seg_waves;
   const int32_t* mid_row;  // NULL: every row is a mid row (no plan)
   int64_t n_mid;
+  const int32_t* short_row;  // short rows (a few edges): lane-private softmax, LPR lanes per row
+  int64_t n_short;
+  int64_t short_waves;
   int64_t mid_waves;
   const int32_t* small_row;
   const int32_t* small_col;
@@ -104,7 +107,7 @@ constexpr int kGatSmallUnroll = 4;
 #define GNN_GAT_U 2  // feature-row gathers in flight per lane in phase B (A/B: tools/gat_ab.py)
 #endif
 #ifndef GNN_GAT_CHUNK
-#define GNN_GAT_CHUNK 16  // edges per phase-A chunk (A/B: 16 >= 8 > 32 > 64 at cfg3)
+#define GNN_GAT_CHUNK 8  // edges per phase-A chunk (A/B at cfg3 with the short-row path: 8 > 16 > 32 > 64)
 #endif
 
 // Rows with at most one edge (44 % of the R-MAT rows: the self-loop only), packed
@@ -183,8 +186,89 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
   }
 }
 
+constexpr int kGatShortChunk = 8;  // edges whose loads one lane issues together
+
+// Short rows (deg 2..8 on R-MAT: 35 % of the rows, 6 % of the edges), 64/LPR rows per
+// wave: each LPR-lane group owns one row and every lane runs the edge softmax for the
+// head of its own VW features privately -- no cross-lane reduction, no LDS, no
+// shuffles; the row's column ids, er values and feature rows are all issued at once
+// (chunks of kGatShortChunk edges, online max across chunks). Same arithmetic per
+// edge as gat_csr_kernel (dense: exp(z - max), sparse: exp(z)); requires fh % VW == 0
+// and NCH == 1 (the launcher routes other shapes through the one-row-per-wave path).
+template <int VW, int LPR, bool SPARSE>
+__device__ __forceinline__ void gat_short_rows(const GatParams& P, int64_t wave, int lane) {
+  constexpr int RPW = kWave / LPR;
+  constexpr int K = kGatShortChunk;
+  const int64_t i = wave * RPW + lane / LPR;
+  const int64_t f = static_cast<int64_t>(lane & (LPR - 1)) * VW;
+  if (i >= P.n_short || f >= P.feat) return;
+  const int64_t row = P.short_row[i];
+  const int64_t beg = P.rowptr[row], end = P.rowptr[row + 1];
+  const int h = static_cast<int>(f / P.fh);
+  const float eli = P.el[row * P.lde + h];
+  float m = SPARSE ? 0.f : -INFINITY, l = 0.f;
+  typename Vec<VW>::T acc = vzero<VW>();
+  for (int64_t b = beg; b < end; b += K) {
+    const int n = static_cast<int>(min(static_cast<int64_t>(K), end - b));
+    int c[K];
+    float z[K];
+    typename Vec<VW>::T xv[K];
+#pragma unroll
+    for (int e = 0; e < K; ++e) c[e] = e < n ? P.col[b + e] : 0;
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      z[e] = -INFINITY;
+      if (e < n) {
+        const float sv = eli + P.er[static_cast<int64_t>(c[e]) * P.lde + h];
+        const float x = sv > 0.f ? sv : P.slope * sv;
+        z[e] = SPARSE ? -x : x;
+      }
+      xv[e] = e < n ? vload<VW>(P.wh + static_cast<int64_t>(c[e]) * P.ldw + f) : vzero<VW>();
+    }
+    if (!SPARSE) {
+      float cm = z[0];
+#pragma unroll
+      for (int e = 1; e < K; ++e) cm = fmaxf(cm, z[e]);
+      const float mn = fmaxf(m, cm);
+      const float scale = __expf(m - mn);  // 0 on the first chunk (m = -inf)
+      m = mn;
+      l *= scale;
+      acc *= scale;
+    }
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      if (e >= n) continue;
+      const float p = SPARSE ? expf(z[e]) : (z[e] == -INFINITY ? 0.f : __expf(z[e] - m));
+      l += p;
+      float w = p;
+      if (P.drop_p > 0.f) {
+        const uint32_t r = hash3(P.drop_seed, b + e, P.head0 + h);
+        w = (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f : w * P.drop_scale;
+      }
+      acc += w * xv[e];
+    }
+  }
+  if (P.stats && f % P.fh == 0) P.stats[row * P.lds + h] = (SPARSE ? 0.f : m) + __logf(l);
+  typename Vec<VW>::T r = acc / l;
+#pragma unroll
+  for (int k = 0; k < VW; ++k) vset(r, k, act_apply(vget(r, k), P.flags));
+  vstore<VW>(P.out + row * P.ldo + f, r);
+}
+
+template <int VW, int LPR, bool SPARSE>
+__global__ __launch_bounds__(kGatBlock) void gat_short_kernel(GatParams P) {
+  gat_short_rows<VW, LPR, SPARSE>(P, static_cast<int64_t>(blockIdx.x) * kGatWaves + (threadIdx.x >> 6),
+                                  threadIdx.x & (kWave - 1));
+}
+
+#ifdef GNN_GAT_WAVES_PER_EU
+#define GNN_GAT_OCC __attribute__((amdgpu_waves_per_eu(GNN_GAT_WAVES_PER_EU)))
+#else
+#define GNN_GAT_OCC
+#endif
+
 template <int VW, int LPR, int NCH, int HP, bool SPARSE, int U, int J>
-__global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
+__global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParams P) {
   constexpr int EPI = kWave / LPR;  // phase B: edges per gather instruction
   constexpr int EPP = kWave / HP;   // phase A: edges per pass (lane = edge x head)
   constexpr int C = EPP * J;        // edges per chunk
@@ -210,8 +294,17 @@ __global__ __launch_bounds__(kGatBlock) void gat_csr_kernel(GatParams P) {
     row = P.mid_row ? P.mid_row[i] : i;
     beg = P.rowptr[row];
     end = P.rowptr[row + 1];
+  } else if (NCH > 1 && wave < P.seg_waves + P.mid_waves + P.short_waves) {
+    // wide rows (NCH > 1) only: short rows take the one-row-per-wave path here;
+    // otherwise they have their own launch (gat_short_kernel, own register budget)
+    const int64_t i = wave - P.seg_waves - P.mid_waves;
+    if (i >= P.n_short) return;
+    row = P.short_row[i];
+    beg = P.rowptr[row];
+    end = P.rowptr[row + 1];
   } else {
-    gat_small_rows<VW, LPR, NCH, SPARSE>(P, wave - P.seg_waves - P.mid_waves, lane);
+    gat_small_rows<VW, LPR, NCH, SPARSE>(
+        P, wave - P.seg_waves - P.mid_waves - P.short_waves, lane);
     return;
   }
   const bool head_ok = ah < P.heads;
@@ -482,15 +575,27 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
   constexpr int U = NCH >= 2 ? 1 : (CE < GNN_GAT_U ? CE : GNN_GAT_U);
   const int64_t seg_blocks = (P.n_seg + kGatWaves - 1) / kGatWaves;
   const int64_t mid_blocks = (P.n_mid + kGatWaves - 1) / kGatWaves;
+  // NCH == 1: short rows in their own launch, EPI rows per wave; else one wave per row here
+  const int64_t short_waves = NCH == 1 ? 0 : P.n_short;
+  const int64_t short_blocks = (short_waves + kGatWaves - 1) / kGatWaves;
   const int64_t small_waves = (P.n_small + EPI * kGatSmallUnroll - 1) / (EPI * kGatSmallUnroll);
   const int64_t small_blocks = (small_waves + kGatWaves - 1) / kGatWaves;
   GatParams Q = P;
   Q.seg_waves = seg_blocks * kGatWaves;
   Q.mid_waves = mid_blocks * kGatWaves;
-  const int64_t blocks = seg_blocks + mid_blocks + small_blocks;
+  Q.short_waves = short_blocks * kGatWaves;
+  const int64_t blocks = seg_blocks + mid_blocks + short_blocks + small_blocks;
   if (blocks > 0)
     hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U, J>),
                        dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), 0, s, Q);
+  if constexpr (NCH == 1) {
+    if (P.n_short > 0) {
+      const int64_t sw = (P.n_short + EPI - 1) / EPI;
+      hipLaunchKernelGGL((gat_short_kernel<VW, LPR, SPARSE>),
+                         dim3(static_cast<unsigned>((sw + kGatWaves - 1) / kGatWaves)),
+                         dim3(kGatBlock), 0, s, Q);
+    }
+  }
   if (P.n_long > 0)
     hipLaunchKernelGGL((gat_fixup_kernel<VW, LPR, NCH, SPARSE>),
                        dim3(static_cast<unsigned>(P.n_long)), dim3(kGatBlock), 0, s, Q);
@@ -660,11 +765,14 @@ extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_
                                const int32_t* long_row, const int32_t* long_seg_ptr,
                                int64_t n_long, const int32_t* small_row, const int32_t* small_col,
                                int64_t n_small, const int32_t* mid_row, int64_t n_mid,
+                               const int32_t* short_row, int64_t n_short,
                                float* partial, float* stats, uint32_t flags, void* stream) {
   if (n_rows < 0 || heads < 1 || fh < 1 || seg_len < 1 || n_seg < 0 || n_long < 0 || n_small < 0)
     return GNN_E_ARG;
   const bool plan = mid_row != nullptr;
-  if (plan && (n_mid < 0 || n_mid + n_small + n_long > n_rows)) return GNN_E_ARG;
+  if (plan && (n_mid < 0 || n_short < 0 || n_mid + n_short + n_small + n_long > n_rows))
+    return GNN_E_ARG;
+  if (plan && n_short > 0 && !short_row) return GNN_E_ARG;
   if (plan && n_small > 0 && (!small_row || !small_col)) return GNN_E_ARG;
   if (mode != 0 && mode != 1) return GNN_E_ARG;
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return GNN_E_ARG;
@@ -714,6 +822,8 @@ extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_
     P.n_long = plan ? n_long : 0;
     P.mid_row = mid_row;
     P.n_mid = plan ? n_mid : n_rows;
+    P.short_row = short_row;
+    P.n_short = plan ? n_short : 0;
     P.small_row = small_row;
     P.small_col = small_col;
     P.n_small = plan ? n_small : 0;

@@ -74,6 +74,21 @@ class RowSplitPlan:
             self._row_list = torch.cat([self.mid_row, self.small_row]).contiguous()
         return self._row_list
 
+    def gat_split(self, rowptr: torch.Tensor, max_deg: int):
+        """(mid rows with deg > max_deg, short rows with deg <= max_deg), row order kept:
+        the GAT launch's short-row class (lane-private softmax, several rows per wave).
+        Cached per max_deg; no host round-trip beyond the two sizes."""
+        cache = self.__dict__.setdefault("_gat_split", {})
+        if max_deg not in cache:
+            if max_deg < 2 or self.n_mid == 0:
+                cache[max_deg] = (self.mid_row, self.mid_row[:0])
+            else:
+                r = self.mid_row.to(torch.int64)
+                short = (rowptr[r + 1] - rowptr[r]) <= max_deg
+                cache[max_deg] = (self.mid_row[~short].contiguous(),
+                                  self.mid_row[short].contiguous())
+        return cache[max_deg]
+
     def args(self):
         """The plan arguments of gnn_spmm_csr_f32 / gnn_gat_csr_f32 (after seg_len)."""
         from ._lib import ptr

@@ -138,6 +138,9 @@ def col_mean(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+GAT_SHORT_MAX_DEG = 16  # rows with 2..16 edges take the short-row path (A/B at cfg3: 16 best)
+
+
 def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tensor, heads: int,
                   fh: int, negative_slope: float, mode: int, activation: str | None = None,
                   dropout_p: float = 0.0, seed: int = 0, seg_len: int | None = None,
@@ -169,11 +172,14 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
     lib = _lib.load()
     pa = plan.args()  # (seg_row, seg_begin, n_seg, long_row, long_seg_ptr, n_long,
     #                    small_row, small_col, small_val, n_small, mid_row, n_mid)
+    mid, short = plan.gat_split(g.rowptr, GAT_SHORT_MAX_DEG)
     rc = lib.gnn_gat_csr_f32(
         g.rowptr.data_ptr(), g.col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
         el.data_ptr(), er.data_ptr(), heads, float(negative_slope), int(mode), _lib.ptr(fill),
         float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), out.stride(0),
-        plan.seg_len, *pa[:6], pa[6], pa[7], pa[9], pa[10], pa[11], _lib.ptr(partial),
+        plan.seg_len, *pa[:6], pa[6], pa[7], pa[9],
+        mid.data_ptr() if mid.numel() else pa[10], mid.numel(),
+        short.data_ptr() if short.numel() else None, short.numel(), _lib.ptr(partial),
         _lib.ptr(stats), _ACT_FLAGS[activation], _lib.stream_handle(wh.device))
     _lib.check(rc, "gnn_gat_csr_f32")
     return out

@@ -120,7 +120,10 @@ int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t hea
  * Rows are scheduled by the row-class plan of gnn_spmm_plan_* (small rows packed,
  * mid rows one wave each, long rows in segments with
  * partial[n_seg * (heads*fh + 2*heads)] merged by the log-sum-exp rule);
- * mid_row == NULL: no plan, one wave per row. flags: GNN_EPI_ELU for concat=True.
+ * mid_row == NULL: no plan, one wave per row. short_row[n_short] (nullable when
+ * n_short == 0): rows taken out of the mid list for the short-row path (64/LPR rows
+ * per wave, lane-private softmax; any degree >= 1 is correct, it pays for deg <= 8).
+ * flags: GNN_EPI_ELU for concat=True.
  * stats (nullable, [n_rows, heads]): per-(row, head) log-sum-exp of the attention
  * logits (dense: max + log sum exp; sparse: log sum exp(-LeakyReLU)), -inf for an
  * edgeless row -- saved by training forwards for gnn_gat_backward_*.
@@ -132,7 +135,8 @@ int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows, c
                     int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin,
                     int64_t n_seg, const int32_t* long_row, const int32_t* long_seg_ptr,
                     int64_t n_long, const int32_t* small_row, const int32_t* small_col,
-                    int64_t n_small, const int32_t* mid_row, int64_t n_mid, float* partial,
+                    int64_t n_small, const int32_t* mid_row, int64_t n_mid,
+                    const int32_t* short_row, int64_t n_short, float* partial,
                     float* stats, uint32_t flags, void* stream);
 
 /*

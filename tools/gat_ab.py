@@ -14,10 +14,12 @@ sys.path.insert(0, str(ROOT))
 
 VARIANTS = {
     "j1u2": ["GNN_GAT_CHUNK=1", "GNN_GAT_U=2"],     # one pass per chunk (previous kernel)
-    "c16u2": ["GNN_GAT_CHUNK=16", "GNN_GAT_U=2"],
     "c32u2": ["GNN_GAT_CHUNK=32", "GNN_GAT_U=2"],
     "c32u4": ["GNN_GAT_CHUNK=32", "GNN_GAT_U=4"],
     "c64u4": ["GNN_GAT_CHUNK=64", "GNN_GAT_U=4"],
+    "c16u2": ["GNN_GAT_CHUNK=16", "GNN_GAT_U=2"],
+    "c16u2w8": ["GNN_GAT_CHUNK=16", "GNN_GAT_U=2", "GNN_GAT_WAVES_PER_EU=8"],
+    "c8u2": ["GNN_GAT_CHUNK=8", "GNN_GAT_U=2"],
 }
 
 
@@ -26,6 +28,9 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--short-degs", default="",
+                    help="instead of library variants: time the default build with these "
+                         "GAT_SHORT_MAX_DEG values (0 = short-row path off)")
     args = ap.parse_args()
     names = args.variants.split(",")
     if args.build:
@@ -49,12 +54,24 @@ def main():
     a_d = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
     el, er = gat_logits(Wh, H, Fh, a_s, a_d)
     out = torch.empty_like(Wh)
-    ref = gat_aggregate(g, Wh, el, er, H, Fh, 0.2, GAT_DENSE, "elu").clone()
-    libs = {v: ROOT / "graphneuralnetwork_amd" / "lib" / "variants" / f"libgnn_{v}.so" for v in names}
+    from graphneuralnetwork_amd import ops as _ops
+    _deg, _ops.GAT_SHORT_MAX_DEG = _ops.GAT_SHORT_MAX_DEG, 0
+    ref = gat_aggregate(g, Wh, el, er, H, Fh, 0.2, GAT_DENSE, "elu").clone()  # short path off
+    _ops.GAT_SHORT_MAX_DEG = _deg
+    from graphneuralnetwork_amd import ops
+    if args.short_degs:
+        names = [f"short{d}" for d in args.short_degs.split(",")]
+        libs = {v: None for v in names}
+    else:
+        libs = {v: ROOT / "graphneuralnetwork_amd" / "lib" / "variants" / f"libgnn_{v}.so"
+                for v in names}
     times = {v: [] for v in names}
     for r in range(args.rounds):
         for v in names:
-            _lib.use_variant(libs[v])
+            if args.short_degs:
+                ops.GAT_SHORT_MAX_DEG = int(v[5:])
+            else:
+                _lib.use_variant(libs[v])
             f = lambda: gat_aggregate(g, Wh, el, er, H, Fh, 0.2, GAT_DENSE, "elu", out=out)  # noqa
             for _ in range(3):
                 f()
@@ -68,7 +85,7 @@ def main():
             times[v].append(a.elapsed_time(b) / 10)
             if r == 0:
                 err = (out - ref).abs().max().item()
-                print(f"{v}: max |diff| vs default build {err:.3g}", flush=True)
+                print(f"{v}: max |diff| vs the one-row-per-wave path {err:.3g}", flush=True)
     bytes_agg = g.nnz * (4 + 4 * H + 4 * H * Fh) + n * (8 + 4 * H + 4 * H * Fh)
     res = {v: {"ms": statistics.median(t), "GBps": bytes_agg / statistics.median(t) / 1e6}
            for v, t in times.items()}
