@@ -185,7 +185,7 @@ def run_gat(args, dev):
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                         "traffic_source": tsrc,
-                        "kernel": "gat_csr_kernel<dense> (+ fixup)",
+                        "kernel": "gat_csr_kernel<dense> + gat_short_kernel + gat_fixup_kernel",
                         "algorithmic_bytes_per_launch": bytes_agg, "avg_launch_ms": k_ms}}
     if not args.no_cpu_baseline:
         from oracle import gnn_oracle as O

@@ -4,7 +4,7 @@ Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half
 bytes of wide (16 B/lane) coalesced reads -> doubled; WRITE_SIZE is exact for
 16-B stores. Both counters are in KiB.
 
-    python tools/pmc_traffic.py <fetch_csv> <write_csv> <kernel-substring> [out.json] [--largest]
+    python tools/pmc_traffic.py <fetch_csv> <write_csv> <kernel-substring[+kernel2...]> [out.json] [--largest]
 
 --largest keeps, per counter, the largest launch instead of the median (for a
 command that launches the same kernel at several sizes, e.g. the two
@@ -28,8 +28,14 @@ def main():
     largest = "--largest" in sys.argv
     argv = [a for a in sys.argv if a != "--largest"]
     fetch_csv, write_csv, kernel = argv[1:4]
-    f, nf = per_launch(fetch_csv, "FETCH_SIZE", kernel, largest)
-    w, nw = per_launch(write_csv, "WRITE_SIZE", kernel, largest)
+    # "a+b+c": one logical launch made of several kernels -> sum of their per-launch values
+    parts = kernel.split("+")
+    fw = [(per_launch(fetch_csv, "FETCH_SIZE", k, largest), per_launch(write_csv, "WRITE_SIZE", k, largest))
+          for k in parts]
+    f = sum(a[0] for a, _ in fw)
+    w = sum(b[0] for _, b in fw)
+    nf = [a[1] for a, _ in fw]
+    nw = [b[1] for _, b in fw]
     res = {"kernel": kernel, "fetch_kib_raw": f, "write_kib": w, "launches": [nf, nw],
            "fetch_bytes_corrected": 2 * f * 1024, "write_bytes": w * 1024,
            "traffic_bytes": (2 * f + w) * 1024,
