@@ -234,6 +234,23 @@ def run_sage(args, dev):
                                                              check=False),
                                args.steps, args.warmup, dev)
         smp_ms, _ = time_steps(lambda: sample_batch(adj, seeds, (25, 10), seed=0), 3, 1, dev)
+        # the same forward replayed from a HIP graph (fixed-shape serving): GPU time without
+        # the Python launch overhead of the eager call
+        graph_ms = None
+        try:
+            s_cap = torch.cuda.Stream(dev)
+            s_cap.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s_cap):
+                for _ in range(2):
+                    net(*fargs, None, None, None, None, None)
+            torch.cuda.current_stream(dev).wait_stream(s_cap)
+            hg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(hg):
+                net(*fargs, None, None, None, None, None)
+            graph_ms, _ = time_steps(hg.replay, args.steps, args.warmup, dev)
+            graph_ms = statistics.mean(graph_ms)
+        except Exception as e:  # reported, never the headline
+            log(f"[bench] graph capture of the forward failed: {e!r}")
     M, k1 = batch.frontier_nbrs.shape
     B, k0 = batch.neigh_map.shape
     edges = batch.sampled_edges
@@ -250,6 +267,7 @@ def run_sage(args, dev):
                       "step": "GraphSAGE.forward (fused gather-mean x2, row gather, 2x SageLayer "
                               "split-K GEMM pairs, classifier) on device-sampled index maps"},
            "forward_ms": statistics.mean(fwd_ms), "sample_ms": statistics.mean(smp_ms),
+           "forward_hipgraph_ms": graph_ms,
            "first_sample_s": t_sample,
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,

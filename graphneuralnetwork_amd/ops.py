@@ -239,8 +239,18 @@ def _check_err(err: torch.Tensor, what: str) -> None:
         raise IndexError(f"{what}: index out of range in self")
 
 
+def _sage_dst(out, M, F, mode, dev):
+    """The caller's output view (any row stride, unit column stride) or a new tensor."""
+    if out is None:
+        return _sage_out(M, F, mode, dev)
+    want = torch.int64 if mode == 1 else torch.float32
+    if out.shape != (M, F) or out.dtype != want or out.stride(1) != 1 or not out.is_cuda:
+        raise ValueError(f"out must be a {want} [{M}, {F}] device view with unit column stride")
+    return out
+
+
 def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str = "MEAN",
-                          check: bool = True) -> torch.Tensor:
+                          check: bool = True, out: torch.Tensor | None = None) -> torch.Tensor:
     """Aggregator(torch.embedding(table, idx)) fused: [M, k] int64 indices into table [n, F]."""
     if agg_func not in SAGE_KINDS:
         raise RuntimeError(f"unknown agg_func {agg_func!r}")
@@ -258,12 +268,12 @@ def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str 
         if mode == 1:
             raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
         return torch.full((M, F), 0.0 if mode == 2 else float("nan"), device=table.device)
-    out = _sage_out(M, F, mode, table.device)
+    out = _sage_dst(out, M, F, mode, table.device)
     err = _err_flag(table.device, check)
     lib = _lib.load()
     _lib.check(lib.gnn_sage_gather_aggregate_f32(
         table.data_ptr(), table.stride(0), table.shape[0], idx.data_ptr(), idx.stride(0), M, k, F,
-        mode, out.data_ptr(), F, err.data_ptr(), _lib.stream_handle(table.device)),
+        mode, out.data_ptr(), out.stride(0), err.data_ptr(), _lib.stream_handle(table.device)),
         "gnn_sage_gather_aggregate_f32")
     if check:
         _check_err(err, "sage_gather_aggregate")
