@@ -43,6 +43,9 @@ SIGNATURES: dict[str, tuple] = {
                                           _vp, _vp, _vp, _vp]),
     "gnn_gat_logits_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64,
                                           _vp]),
+    "gnn_gat_project_supported": (ctypes.c_int, [_i64, _i64, _i64]),
+    "gnn_gat_project_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _i64,
+                                           _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gnn_gat_csr_f32": (ctypes.c_int, [
         _vp, _vp, _i64,                 # rowptr, col, n_rows
         _vp, _i64, _i64, _i64,          # wh, ldw, heads, fh

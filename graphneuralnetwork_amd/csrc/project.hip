@@ -1,0 +1,245 @@
+// project.hip -- GAT feature transform on the matrix cores, attention logits fused.
+//
+// Replaces, for the inference path of every attention layer,
+//   Wh = torch.mm(h, W)                        GAT/models/layers.py:23 / :97 (all heads at
+//                                              once: W = [W_1 | ... | W_H], GAT.py:16)
+//   el = a[:F].Wh_i,  er = a[F:].Wh_j          layers.py:25-26 / :105-108
+// with ONE pass over h: each wave computes a 16-row x 16*NT-column tile of Wh with
+// v_mfma_f32_16x16x4_f32 (exact f32 in / f32 accumulate; gfx950 has no xf32), W held
+// in registers for the whole launch, Wh stored straight from the accumulator layout
+// (16 lanes = 64 contiguous bytes of a row). The logits ride along as one more
+// 16-column MFMA tile: [el | er] = X (W A) with A the block-diagonal [fout, 2 heads]
+// matrix of a_src / a_dst, folded into W once per workgroup (W2 = W A in LDS).
+//
+// MFMA operand maps (16x16x4 f32): lane l holds A[l & 15][k = l >> 4] and
+// B[k = l >> 4][l & 15]; C/D: col = l & 15, row = 4 * (l >> 4) + reg. The kernel
+// computes the transposed tile D = W^T X^T (A = W^T, B = X^T) so that a lane's four
+// accumulators are four consecutive columns of one Wh row (16-B stores). The K axis is
+// permuted so that lane quarter q owns k in [q*S, q*S + S): its X values for all S
+// steps are one contiguous run of h's row, read as float4s from an LDS copy of the
+// wave's 16 rows that was loaded with fully coalesced 16-B-per-lane global loads.
+#include "common.hpp"
+
+namespace gnn {
+
+constexpr int kProjWaves = 4;
+constexpr int kProjBlock = kProjWaves * kWave;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+// w2[k][c] = W[k, head c] . a_src[head c] (c < heads), W[k, head c-heads] . a_dst[head
+// c-heads] (heads <= c < 2 heads), 0 beyond: the logits as a [K, 16] weight tile.
+__global__ __launch_bounds__(256) void gat_project_w2_kernel(const float* __restrict__ w, int k,
+                                                             int fout, const float* __restrict__ a_src,
+                                                             const float* __restrict__ a_dst,
+                                                             int heads, int fh,
+                                                             float* __restrict__ w2) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= k * 16) return;
+  const int kk = e >> 4, c = e & 15;
+  float v = 0.f;
+  if (c < 2 * heads) {
+    const int h = c < heads ? c : c - heads;
+    const float* av = (c < heads ? a_src : a_dst) + h * fh;
+    const float* wr = w + kk * fout + h * fh;
+    for (int f = 0; f < fh; ++f) v = fmaf(wr[f], av[f], v);
+  }
+  w2[e] = v;
+}
+
+template <int K, int NT>
+__global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
+    const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
+    const float* __restrict__ w2, int heads, float* __restrict__ wh, int64_t ldwh,
+    float* __restrict__ el, float* __restrict__ er, int64_t lde) {
+  constexpr int S = K / 4;   // MFMA k-steps
+  constexpr int FO = 16 * NT;
+  constexpr int LDA = K + 4;  // padded LDS row (floats) against bank conflicts
+  __shared__ float atile[kProjWaves][16 * LDA];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int q = lane >> 4, r = lane & 15;
+  const bool vec_logits = heads % 4 == 0 && lde % 4 == 0 &&
+                          ((reinterpret_cast<uintptr_t>(el) | reinterpret_cast<uintptr_t>(er)) & 15) == 0;
+
+  // Logit weights as one more 16-column tile (w2 = W A, gat_project_w2_kernel):
+  // [el | er] = X w2 comes out of the same MFMA k-loop as Wh = X W.
+  __shared__ float w2s[K * 16];
+  for (int e = threadIdx.x; e < K * 16; e += kProjBlock) w2s[e] = w2[e];
+#ifdef GNN_PROJ_B_LDS
+  // B fragments read from LDS at every step (fewer VGPRs, more waves per SIMD)
+  __shared__ float ws[K * FO];
+  for (int e = threadIdx.x; e < K * FO; e += kProjBlock) ws[e] = w[e];
+  __syncthreads();
+#else
+  float b[NT][S];  // B fragments: W[q*S + s][16t + r], resident for the whole launch
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int s = 0; s < S; ++s) b[t][s] = w[(q * S + s) * FO + 16 * t + r];
+  __syncthreads();
+  float b2[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) b2[s] = w2s[(q * S + s) * 16 + r];
+#endif
+
+  // A tiles are staged through LDS: a coalesced 16-B-per-lane copy of the wave's 16 rows,
+  // then each lane reads its row's quarter (row l & 15, k in [q*S, q*S + S)) as float4s
+  float* at = atile[threadIdx.x >> 6];
+  const int64_t n_groups = (n_rows + 16 * kProjWaves - 1) / (16 * kProjWaves);
+  constexpr int V4 = 16 * K / 4;                  // float4s in the wave's tile
+  constexpr int NV = (V4 + kWave - 1) / kWave;    // per lane
+  float4 pre[NV];                                  // the next tile, in flight during the MFMAs
+  auto fetch = [&](int64_t g) {
+    const int64_t r0 = (g * kProjWaves + (threadIdx.x >> 6)) * 16;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int e = v * kWave + lane;
+      const int rr = e / (K / 4), c4 = e - rr * (K / 4);
+      pre[v] = (e < V4 && g < n_groups && r0 + rr < n_rows)
+                   ? *reinterpret_cast<const float4*>(x + (r0 + rr) * ldx + 4 * c4)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  fetch(blockIdx.x);
+  for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {  // uniform over the block
+    const int64_t row0 = (g * kProjWaves + (threadIdx.x >> 6)) * 16;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int e = v * kWave + lane;
+      if (e < V4) {
+        const int rr = e / (K / 4), c4 = e - rr * (K / 4);
+        *reinterpret_cast<float4*>(at + rr * LDA + 4 * c4) = pre[v];
+      }
+    }
+    __syncthreads();
+    fetch(g + gridDim.x);
+    float a[S];
+#pragma unroll
+    for (int v = 0; v < S / 4; ++v) {
+      const float4 t4 = *reinterpret_cast<const float4*>(at + r * LDA + q * S + 4 * v);
+      a[4 * v] = t4.x;
+      a[4 * v + 1] = t4.y;
+      a[4 * v + 2] = t4.z;
+      a[4 * v + 3] = t4.w;
+    }
+    f32x4 acc[NT], acc2 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#ifdef GNN_PROJ_NO_MFMA
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{a[t], a[t + 1], a[t + 2], a[t + 3]};
+    acc2 = f32x4{a[4], a[5], a[6], a[7]};
+#else
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+#ifdef GNN_PROJ_B_LDS
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ws[(q * S + s) * FO + 16 * t + r], a[s],
+                                                     acc[t], 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w2s[(q * S + s) * 16 + r], a[s], acc2, 0, 0, 0);
+#else
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[t][s], a[s], acc[t], 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(b2[s], a[s], acc2, 0, 0, 0);
+#endif
+    }
+#endif
+    // Operands are swapped (D = W^T X^T), so acc[t][i] is Wh[row0 + r][16t + 4q + i]:
+    // one 16-B store per tile, 4 lanes = 64 contiguous bytes of a row; acc2[i] is column
+    // 4q + i of [el | er] for row r
+    const int64_t orow = row0 + r;
+    if (orow < n_rows) {
+#ifndef GNN_PROJ_NO_WH
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        *reinterpret_cast<float4*>(wh + orow * ldwh + 16 * t + 4 * q) =
+            make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+#endif
+      if (vec_logits) {  // heads % 4 == 0: quarter q holds 4 whole logits of el or er
+        const int c = 4 * q;
+        if (c < 2 * heads)
+          *reinterpret_cast<float4*>(c < heads ? el + orow * lde + c : er + orow * lde + c - heads) =
+              make_float4(acc2[0], acc2[1], acc2[2], acc2[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 4 * q + i;
+          if (c < heads)
+            el[orow * lde + c] = acc2[i];
+          else if (c < 2 * heads)
+            er[orow * lde + c - heads] = acc2[i];
+        }
+      }
+    }
+    __syncthreads();  // the next group overwrites the A tile
+  }
+}
+
+template <int K, int NT>
+static int launch_project(const float* x, int64_t ldx, int64_t n_rows, const float* w,
+                          const float* w2, int heads, float* wh, int64_t ldwh, float* el,
+                          float* er, int64_t lde, hipStream_t s) {
+  const int64_t groups = (n_rows + 16 * kProjWaves - 1) / (16 * kProjWaves);
+#ifndef GNN_PROJ_GRID
+#define GNN_PROJ_GRID 1024  // A/B at cfg3: 1024 < 512 < 256 < 2048 < 4096 (ms)
+#endif
+  const int64_t grid = groups < GNN_PROJ_GRID ? groups : GNN_PROJ_GRID;  // W resident across groups
+  hipLaunchKernelGGL((gat_project_kernel<K, NT>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kProjBlock), 0, s, x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er,
+                     lde);
+  return launch_status();
+}
+
+template <int K>
+static int dispatch_project_nt(int64_t fout, const float* x, int64_t ldx, int64_t n_rows,
+                               const float* w, const float* w2, int heads, float* wh,
+                               int64_t ldwh, float* el, float* er, int64_t lde, hipStream_t s) {
+  // B fragments live in registers: (K / 4) * NT <= 64
+  if (fout == 16) return launch_project<K, 1>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, s);
+  if constexpr (K <= 128)
+    if (fout == 32) return launch_project<K, 2>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, s);
+  if constexpr (K <= 64)
+    if (fout == 64) return launch_project<K, 4>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, s);
+  return GNN_E_UNSUPPORTED;
+}
+
+}  // namespace gnn
+
+using namespace gnn;
+
+extern "C" int gnn_gat_project_supported(int64_t k, int64_t fout, int64_t fh) {
+  const bool kk = k == 16 || k == 32 || k == 64 || k == 128 || k == 256;
+  if (!kk || fh < 1 || fout % fh || fout / fh > 8) return 0;  // [el | er] fits one tile
+  if (fout == 16) return 1;
+  if (fout == 32) return k <= 128;
+  if (fout == 64) return k <= 64;
+  return 0;
+}
+
+extern "C" int gnn_gat_project_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                                   const float* w, int64_t fout, const float* a_src,
+                                   const float* a_dst, int64_t heads, int64_t fh, float* wh,
+                                   int64_t ldwh, float* el, float* er, int64_t lde,
+                                   float* w2_scratch, void* stream) {
+  if (n_rows < 0 || heads < 1 || fh < 1 || heads * fh != fout || ldx < k || ldwh < fout ||
+      lde < heads)
+    return GNN_E_ARG;
+  if (!gnn_gat_project_supported(k, fout, fh)) return GNN_E_UNSUPPORTED;
+  if (n_rows == 0) return GNN_OK;
+  if (!x || !w || !a_src || !a_dst || !wh || !el || !er || !w2_scratch) return GNN_E_ARG;
+  if (ldx % 4 || ldwh % 4 || !aligned_to(x, 16) || !aligned_to(wh, 16)) return GNN_E_ALIGN;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int h = static_cast<int>(heads);
+  hipLaunchKernelGGL(gat_project_w2_kernel, dim3(static_cast<unsigned>((k * 16 + 255) / 256)),
+                     dim3(256), 0, s, w, static_cast<int>(k), static_cast<int>(fout), a_src,
+                     a_dst, h, static_cast<int>(fh), w2_scratch);
+  const float* w2 = w2_scratch;
+  switch (k) {
+    case 16: return dispatch_project_nt<16>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
+    case 32: return dispatch_project_nt<32>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
+    case 64: return dispatch_project_nt<64>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
+    case 128: return dispatch_project_nt<128>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
+    default: return dispatch_project_nt<256>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
+  }
+}

@@ -15,9 +15,11 @@ Same class names, constructor arguments, parameter shapes/initialisation and
 
 Where the reference materialises an N x N x 2F tensor per head (dense) or
 E x 2F per head (sparse) and loops over heads in Python, here every
-attention layer is: one GEMM for all heads (X @ [W_1 | ... | W_H], hipBLASLt
-MFMA), one HIP launch for the attention logits, one HIP launch for the fused
-edge-softmax + aggregation (+ ELU) over the CSR adjacency.  ``adj`` may be the
+attention layer is: one pass for the feature transform of all heads
+(X @ [W_1 | ... | W_H]) with the attention logits fused into its epilogue
+(gnn_gat_project_f32, fp32 MFMA; torch.mm + gnn_gat_logits_f32 for shapes it
+does not cover or when autograd needs the GEMM), and one HIP launch for the
+fused edge-softmax + aggregation (+ ELU) over the CSR adjacency.  ``adj`` may be the
 reference's dense tensor, a torch sparse tensor or a ``CsrGraph``.
 
 Training: the aggregation is an autograd Function whose backward is three
@@ -32,7 +34,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
-from .ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_backward, gat_logits
+from .ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_backward, gat_logits, gat_project
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
@@ -70,6 +72,18 @@ class _GatLayerFn(torch.autograd.Function):
         return dwh, da_src, da_dst, None, None, None, None, None, None, None, None
 
 
+def _project(x, W, heads, fh, a_src, a_dst):
+    """(Wh, (el, er) or None): the fused MFMA transform + logits kernel at inference when
+    the shape is covered (gnn_gat_project_f32), else torch.mm (autograd) and logits later."""
+    if not (torch.is_grad_enabled() and (x.requires_grad or W.requires_grad
+                                         or a_src.requires_grad or a_dst.requires_grad)) \
+            and x.is_cuda:
+        r = gat_project(x, W, heads, fh, a_src, a_dst)
+        if r is not None:
+            return r[0], (r[1], r[2])
+    return torch.mm(x, W), None
+
+
 def _dropout_seed() -> int:
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
@@ -83,7 +97,7 @@ class _AttentionBase(nn.Module):
         F_ = self.out_features
         return a[:F_], a[F_:]
 
-    def _aggregate(self, Wh, adj, heads, fh, a_src, a_dst, activation, dropout_p):
+    def _aggregate(self, Wh, adj, heads, fh, a_src, a_dst, activation, dropout_p, logits=None):
         g = as_csr(adj, self.PREDICATE)
         p = dropout_p if self.training else 0.0
         seed = _dropout_seed() if p > 0 else 0
@@ -92,7 +106,7 @@ class _AttentionBase(nn.Module):
             out = _GatLayerFn.apply(Wh, a_src, a_dst, g, heads, fh, self.alpha, self.MODE,
                                     activation, p, seed)
         else:
-            el, er = gat_logits(Wh, heads, fh, a_src, a_dst)
+            el, er = logits if logits is not None else gat_logits(Wh, heads, fh, a_src, a_dst)
             out = gat_aggregate(g, Wh, el, er, heads, fh, self.alpha, self.MODE, activation,
                                 dropout_p=p, seed=seed)
         if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
@@ -102,12 +116,12 @@ class _AttentionBase(nn.Module):
     def forward(self, h, adj, activation: str | None = "__concat__"):
         if activation == "__concat__":
             activation = "elu" if self.concat else None
-        Wh = torch.mm(h, self.W)
+        a_src, a_dst = self._a_parts()
+        Wh, logits = _project(h, self.W, 1, self.out_features, a_src, a_dst)
         if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
             assert not torch.isnan(Wh).any()
-        a_src, a_dst = self._a_parts()
         return self._aggregate(Wh, adj, 1, self.out_features, a_src, a_dst, activation,
-                               self._drop_p())
+                               self._drop_p(), logits)
 
     def __repr__(self):
         return self.__class__.__name__ + ' (' + str(self.in_features) + ' -> ' + str(self.out_features) + ')'
@@ -178,13 +192,14 @@ class GATBase(nn.Module):
             return torch.cat([att(x, adj) for att in heads], dim=1)
         fh = first.out_features
         W = torch.cat([m.W for m in heads], dim=1)          # [in, H*fh]
-        Wh = torch.mm(x, W)                                  # one MFMA GEMM for all heads
-        if first.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
-            assert not torch.isnan(Wh).any()
         parts = [m._a_parts() for m in heads]
         a_src = torch.cat([p[0] for p in parts])
         a_dst = torch.cat([p[1] for p in parts])
-        return first._aggregate(Wh, adj, len(heads), fh, a_src, a_dst, "elu", first._drop_p())
+        Wh, logits = _project(x, W, len(heads), fh, a_src, a_dst)  # one MFMA pass, all heads
+        if first.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
+            assert not torch.isnan(Wh).any()
+        return first._aggregate(Wh, adj, len(heads), fh, a_src, a_dst, "elu", first._drop_p(),
+                                logits)
 
     def forward(self, x, adj):
         x = F.dropout(x, self.dropout, training=self.training)

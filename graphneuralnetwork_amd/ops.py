@@ -124,6 +124,34 @@ def gat_logits(wh: torch.Tensor, heads: int, fh: int, a_src: torch.Tensor,
     return el, er
 
 
+def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: torch.Tensor,
+                a_dst: torch.Tensor):
+    """(Wh = x @ w, el, er) in one MFMA pass (inference; no autograd), or None when the
+    shape is not covered by gnn_gat_project_f32 (the caller then uses torch.mm +
+    gat_logits)."""
+    _require_device(x, w, a_src, a_dst)
+    if (x.dtype != torch.float32 or w.dtype != torch.float32 or x.dim() != 2 or w.dim() != 2
+            or x.shape[1] != w.shape[0] or w.shape[1] != heads * fh):
+        return None
+    lib = _lib.load()
+    k, fout = w.shape
+    if not lib.gnn_gat_project_supported(k, fout, fh):
+        return None
+    if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
+        x = x.contiguous()
+    n = x.shape[0]
+    wh = torch.empty((n, fout), dtype=torch.float32, device=x.device)
+    el = torch.empty((n, heads), dtype=torch.float32, device=x.device)
+    er = torch.empty((n, heads), dtype=torch.float32, device=x.device)
+    w2 = torch.empty((k, 16), dtype=torch.float32, device=x.device)
+    _lib.check(lib.gnn_gat_project_f32(
+        x.data_ptr(), x.stride(0), n, k, w.contiguous().data_ptr(), fout,
+        a_src.contiguous().data_ptr(), a_dst.contiguous().data_ptr(), heads, fh, wh.data_ptr(),
+        fout, el.data_ptr(), er.data_ptr(), heads, w2.data_ptr(), _lib.stream_handle(x.device)),
+        "gnn_gat_project_f32")
+    return wh, el, er
+
+
 def col_mean(x: torch.Tensor) -> torch.Tensor:
     """Mean over rows (double accumulation) -- the dense GAT layer's edgeless-row output."""
     _require_device(x)

@@ -106,6 +106,25 @@ int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t hea
                        void* stream);
 
 /*
+ * GAT feature transform on the matrix cores with the attention logits fused:
+ *   wh[n, :] = x[n, :k] @ w[k, fout]   (w row-major [k, fout], all heads side by side)
+ *   el[n, h] = a_src[h*fh:(h+1)*fh] . wh[n, h*fh:(h+1)*fh], er likewise with a_dst
+ * Replaces torch.mm(h, self.W) + the a-products of GAT/models/layers.py:23-26 /
+ * :97-108 for the inference path (v_mfma_f32_16x16x4_f32, exact f32; the logits are
+ * computed as x (w A) with A the block-diagonal a_src / a_dst matrix, so they match
+ * gnn_gat_logits_f32 on wh to fp32 rounding, not bitwise). Shapes:
+ * gnn_gat_project_supported(k, fout, fh) != 0 (k in {16,32,64,128,256}, fout in
+ * {16,32,64} with (k/4)*(fout/16) <= 64, heads = fout/fh <= 8); otherwise
+ * GNN_E_UNSUPPORTED. x / wh rows 16-B aligned (GNN_E_ALIGN). w2_scratch: k * 16
+ * floats of device memory (the folded logit weights w A).
+ */
+int gnn_gat_project_supported(int64_t k, int64_t fout, int64_t fh);
+int gnn_gat_project_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,
+                        int64_t fout, const float* a_src, const float* a_dst, int64_t heads,
+                        int64_t fh, float* wh, int64_t ldwh, float* el, float* er, int64_t lde,
+                        float* w2_scratch, void* stream);
+
+/*
  * GAT edge-softmax + neighbour aggregation over CSR, all heads in one pass:
  *   out[i, h*fh+f] = act( sum_{j in row i} p_ijh * Wh[j, h*fh+f] / sum_j p_ijh )
  * mode 0 (dense layer, GAT/models/layers.py:22-37):

@@ -284,3 +284,44 @@ def test_gat_dropout_backward_exact(dev, sparse):
     close(Wh.grad.cpu().numpy(), Wt.grad.numpy(), rtol=2e-4)
     close(a_s.grad.cpu().numpy(), ast.grad.numpy(), rtol=2e-4)
     close(a_d.grad.cpu().numpy(), adt.grad.numpy(), rtol=2e-4)
+
+
+@pytest.mark.parametrize("n,k,heads,fh", [(1000, 64, 8, 8), (777, 32, 2, 16), (50, 16, 1, 16),
+                                          (3001, 128, 4, 8), (129, 256, 2, 8), (64, 64, 4, 16),
+                                          (500, 64, 1, 64), (300, 32, 1, 32), (99, 64, 8, 8),
+                                          (70, 16, 8, 2), (40, 32, 4, 4)])
+def test_gat_project_mfma_vs_oracle(dev, n, k, heads, fh):
+    """Fused MFMA transform: Wh = X W within fp32 tolerance of a float64 GEMM; el/er
+    within fp32 tolerance of gnn_gat_logits_f32 run on the produced Wh."""
+    from graphneuralnetwork_amd.ops import gat_logits, gat_project
+    rng = np.random.default_rng(n + k)
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    w = (rng.standard_normal((k, heads * fh)) / np.sqrt(k)).astype(np.float32)
+    a_s = rng.standard_normal(heads * fh).astype(np.float32)
+    a_d = rng.standard_normal(heads * fh).astype(np.float32)
+    r = gat_project(torch.from_numpy(x).to(dev), torch.from_numpy(w).to(dev), heads, fh,
+                    torch.from_numpy(a_s).to(dev), torch.from_numpy(a_d).to(dev))
+    assert r is not None
+    wh, el, er = r
+    close(wh.cpu().numpy(), x.astype(np.float64) @ w.astype(np.float64))
+    el2, er2 = gat_logits(wh, heads, fh, torch.from_numpy(a_s).to(dev), torch.from_numpy(a_d).to(dev))
+    close(el.cpu().numpy(), el2.cpu().numpy())
+    close(er.cpu().numpy(), er2.cpu().numpy())
+    el_o, er_o = O.gat_logits(wh.cpu().numpy(), heads, fh, a_s, a_d)
+    close(el.cpu().numpy(), el_o)
+
+
+def test_gat_project_unsupported_shapes_fall_back(dev):
+    from graphneuralnetwork_amd.ops import gat_project
+    x = torch.randn(10, 48, device=dev)
+    assert gat_project(x, torch.randn(48, 64, device=dev), 8, 8, torch.randn(64, device=dev),
+                       torch.randn(64, device=dev)) is None          # k = 48
+    assert gat_project(torch.randn(10, 64, device=dev), torch.randn(64, 7, device=dev), 1, 7,
+                       torch.randn(7, device=dev), torch.randn(7, device=dev)) is None  # fout = 7
+    assert gat_project(torch.randn(10, 32, device=dev), torch.randn(32, 64, device=dev), 16, 4,
+                       torch.randn(64, device=dev), torch.randn(64, device=dev)) is None  # 16 heads
+    # strided x (not 16-B aligned rows) is copied, still exact
+    big = torch.randn(33, 65, device=dev)
+    w = torch.randn(64, 16, device=dev)
+    wh, _, _ = gat_project(big[:, 1:], w, 2, 8, torch.randn(16, device=dev), torch.randn(16, device=dev))
+    close(wh.cpu().numpy(), big[:, 1:].cpu().double().numpy() @ w.cpu().double().numpy())
