@@ -25,6 +25,7 @@ import os
 import statistics
 import sys
 import time
+import warnings
 from pathlib import Path
 
 import numpy as np
@@ -126,6 +127,45 @@ def load_traffic(name: str):
         return None, None
     return t["traffic_bytes"], (str(path.relative_to(ROOT)) + ": rocprofv3 --pmc FETCH_SIZE x2 + "
                                 "WRITE_SIZE of this command")
+
+
+def cpu_reference_ops(g, X, feat: int, budget_s: float = 25.0):
+    """SURVEY 8(d) CPU lines beside the port: the reference's own operator -- torch.spmm on
+    the uncoalesced COO built as GCN/data_utils.py:63-70 (CSC -> COO order, int64 indices,
+    GCN/GCN.py:43) -- and torch.sparse.mm on CSR, both with every allowed host thread."""
+    threads = min(16, len(os.sched_getaffinity(0)))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        rows = torch.repeat_interleave(torch.arange(g.n_rows, dtype=torch.int64),
+                                       (g.rowptr[1:] - g.rowptr[:-1]).cpu())
+        cols = g.col.cpu().to(torch.int64)
+        order = torch.argsort(cols, stable=True)          # scipy CSC -> COO order
+        idx = torch.stack([rows[order], cols[order]])
+        coo = torch.sparse_coo_tensor(idx, g.val.cpu()[order], (g.n_rows, g.n_cols))  # uncoalesced
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")  # "sparse CSR support is in beta"
+            csr = torch.sparse_csr_tensor(g.rowptr.cpu(), g.col.cpu().to(torch.int64),
+                                          g.val.cpu(), (g.n_rows, g.n_cols))
+        Xc = X.cpu()
+        out = {}
+        for name, fn in (("torch_spmm_coo", lambda: torch.spmm(coo, Xc)),
+                         ("torch_sparse_mm_csr", lambda: torch.sparse.mm(csr, Xc))):
+            t_all = time.perf_counter()
+            fn()                                          # warm-up
+            times = []
+            while not times or (len(times) < 5 and time.perf_counter() - t_all < budget_s / 2):
+                t0 = time.perf_counter()
+                fn()
+                times.append(time.perf_counter() - t0)
+            t = statistics.median(times)
+            out[name] = {"value": g.nnz / t, "unit": "edges/s", "threads": threads,
+                         "seconds_per_step": t, "runs": len(times)}
+        out["note"] = ("torch_spmm_coo is the reference's CPU operator on the reference's tensor "
+                       "layout (effectively single-threaded in ATen); full graph, F=%d" % feat)
+        return out
+    finally:
+        torch.set_num_threads(prev)
 
 
 def time_steps(step, steps: int, warmup: int, dev):
@@ -294,6 +334,8 @@ def main():
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-reference", action="store_true",
+                    help="skip the torch CPU operator lines (torch.spmm COO / sparse.mm CSR)")
     ap.add_argument("--exchange", default="cover", choices=["cover", "gather"],
                     help="N>1 halo exchange: feature rows + remote partial sums (cover) or "
                          "feature rows only (gather)")
@@ -444,6 +486,11 @@ def main():
                 res["cpu_baseline"] = cpu_baseline(g, X, F)
             except Exception as e:  # the baseline is reported, never the target
                 res["cpu_baseline"] = {"value": None, "error": repr(e)}
+            if not args.no_cpu_reference:
+                try:
+                    res["cpu_reference_ops"] = cpu_reference_ops(g, X, F)
+                except Exception as e:
+                    res["cpu_reference_ops"] = {"error": repr(e)}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
