@@ -42,6 +42,11 @@ WORKLOADS = {
                  name="GCN SpMM, RMAT 1M nodes / 10M edges (BASELINE configs[1])"),
     "ns": dict(nodes=10_000_000, edges=100_000_000,
                name="GCN SpMM, RMAT 10M nodes / 100M edges (north star)"),
+    # BASELINE configs[4]: the whole 10M / 100M graph at F=256 edge-cut over the N ranks
+    # (strong scaling: the graph does not grow with N; at N=1 it is the single-GPU reference)
+    "cfg5": dict(nodes=10_000_000, edges=100_000_000, feat=256, strong=True,
+                 name="GCN SpMM, RMAT 10M nodes / 100M edges, F=256, edge-cut over N GPUs "
+                      "(BASELINE configs[4])"),
     "cfg3": dict(nodes=1_000_000, edges=10_000_000,
                  name="GAT 8-head (64->8x8) edge-softmax + aggregate, RMAT 1M / 10M (BASELINE configs[2])"),
     "cfg4": dict(nodes=10_000_000, edges=100_000_000,
@@ -129,7 +134,7 @@ def load_traffic(name: str):
                                 "WRITE_SIZE of this command")
 
 
-def cpu_reference_ops(g, X, feat: int, budget_s: float = 25.0):
+def cpu_reference_ops(g, X, feat: int, budget_s: float = 25.0, max_nnz: int = 21_000_000):
     """SURVEY 8(d) CPU lines beside the port: the reference's own operator -- torch.spmm on
     the uncoalesced COO built as GCN/data_utils.py:63-70 (CSC -> COO order, int64 indices,
     GCN/GCN.py:43) -- and torch.sparse.mm on CSR, both with every allowed host thread."""
@@ -137,20 +142,28 @@ def cpu_reference_ops(g, X, feat: int, budget_s: float = 25.0):
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
-        rows = torch.repeat_interleave(torch.arange(g.n_rows, dtype=torch.int64),
-                                       (g.rowptr[1:] - g.rowptr[:-1]).cpu())
-        cols = g.col.cpu().to(torch.int64)
+        # bounded sample: the leading rows holding at most max_nnz edges (the whole graph at cfg2)
+        rowptr = g.rowptr.cpu()
+        r1 = min(g.n_rows, int(torch.searchsorted(rowptr, max_nnz, right=True)) - 1)
+        r1 = max(r1, 1)
+        e1 = int(rowptr[r1])
+        rows = torch.repeat_interleave(torch.arange(r1, dtype=torch.int64),
+                                       rowptr[1:r1 + 1] - rowptr[:r1])
+        cols = g.col[:e1].cpu().to(torch.int64)
+        vals = g.val[:e1].cpu()
         order = torch.argsort(cols, stable=True)          # scipy CSC -> COO order
         idx = torch.stack([rows[order], cols[order]])
-        coo = torch.sparse_coo_tensor(idx, g.val.cpu()[order], (g.n_rows, g.n_cols))  # uncoalesced
+        coo = torch.sparse_coo_tensor(idx, vals[order], (r1, g.n_cols))  # uncoalesced
         with warnings.catch_warnings():
             warnings.simplefilter("ignore")  # "sparse CSR support is in beta"
-            csr = torch.sparse_csr_tensor(g.rowptr.cpu(), g.col.cpu().to(torch.int64),
-                                          g.val.cpu(), (g.n_rows, g.n_cols))
-        Xc = X.cpu()
+            csr = torch.sparse_csr_tensor(rowptr[:r1 + 1], cols, vals, (r1, g.n_cols))
+        # ATen's CPU sparse kernels index the dense operand with 32-bit offsets: at N*F >= 2^31
+        # (cfg5: 10M x 256) torch.spmm segfaults, so the operand goes in column blocks there
+        n_blk = -(-X.numel() // (2 ** 31 - 1))
+        Xc = [c.contiguous() for c in X.cpu().chunk(n_blk, dim=1)]
         out = {}
-        for name, fn in (("torch_spmm_coo", lambda: torch.spmm(coo, Xc)),
-                         ("torch_sparse_mm_csr", lambda: torch.sparse.mm(csr, Xc))):
+        for name, fn in (("torch_spmm_coo", lambda: [torch.spmm(coo, c) for c in Xc]),
+                         ("torch_sparse_mm_csr", lambda: [torch.sparse.mm(csr, c) for c in Xc])):
             t_all = time.perf_counter()
             fn()                                          # warm-up
             times = []
@@ -159,11 +172,106 @@ def cpu_reference_ops(g, X, feat: int, budget_s: float = 25.0):
                 fn()
                 times.append(time.perf_counter() - t0)
             t = statistics.median(times)
-            out[name] = {"value": g.nnz / t, "unit": "edges/s", "threads": threads,
+            out[name] = {"value": e1 / t, "unit": "edges/s", "threads": threads,
                          "seconds_per_step": t, "runs": len(times)}
+        sample = "full graph" if r1 == g.n_rows else f"rows 0..{r1} ({e1} edges)"
+        if n_blk > 1:
+            sample += f", X in {n_blk} column blocks (N*F >= 2^31 crashes ATen's CPU spmm)"
         out["note"] = ("torch_spmm_coo is the reference's CPU operator on the reference's tensor "
-                       "layout (effectively single-threaded in ATen); full graph, F=%d" % feat)
+                       "layout (effectively single-threaded in ATen); %s, F=%d" % (sample, feat))
         return out
+    finally:
+        torch.set_num_threads(prev)
+
+
+def _cpu_time(fn, budget_s: float):
+    """Median wall seconds of fn() (1 warm-up, up to 5 runs within the budget)."""
+    t_all = time.perf_counter()
+    fn()
+    times = []
+    while not times or (len(times) < 5 and time.perf_counter() - t_all < budget_s):
+        t0 = time.perf_counter()
+        fn()
+        times.append(time.perf_counter() - t0)
+    return statistics.median(times), len(times)
+
+
+def cpu_spgat_ops(g, X, W, a_s, a_d, H: int, Fh: int, max_edges: int = 2_000_000,
+                  budget_s: float = 20.0):
+    """The reference's CPU operator sequence for one SpGAT layer (SpGraphAttentionLayer.forward,
+    GAT/models/layers.py:94-131, one head after another as GAT.py:16 does): h = X W; the E x 2F
+    edge matrix [h_i | h_j]; exp(-LeakyReLU(a . edge_h)); row sums and h' by COO matmuls
+    (SpecialSpmm, layers.py:43-69); h' / rowsum.  Restated with torch CPU ops on the leading
+    rows holding <= max_edges edges, every allowed host thread."""
+    threads = min(16, len(os.sched_getaffinity(0)))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        rowptr = g.rowptr.cpu()
+        r1 = max(1, min(g.n_rows, int(torch.searchsorted(rowptr, max_edges, right=True)) - 1))
+        e1 = int(rowptr[r1])
+        src = torch.repeat_interleave(torch.arange(r1), rowptr[1:r1 + 1] - rowptr[:r1])
+        dst = g.col[:e1].cpu().to(torch.int64)
+        edge = torch.stack([src, dst])
+        ones = torch.ones(g.n_cols, 1)
+        Ws = W.view(-1, H, Fh)
+        a = torch.cat([a_s.view(H, Fh), a_d.view(H, Fh)], 1)  # [H, 2 Fh]
+
+        hs = [X @ Ws[:, hd, :] for hd in range(H)]  # the N x Fh transforms: outside the sample
+
+        def layer():
+            outs = []
+            for hd in range(H):
+                h = hs[hd]
+                edge_h = torch.cat([h[src], h[dst]], 1)
+                e = torch.exp(-torch.nn.functional.leaky_relu(edge_h @ a[hd], 0.2))
+                A = torch.sparse_coo_tensor(edge, e, (r1, g.n_cols))
+                outs.append(torch.sparse.mm(A, h) / torch.sparse.mm(A, ones))
+            return torch.cat(outs, 1)
+
+        t, runs = _cpu_time(layer, budget_s)
+        return {"torch_spgat_layer": {"value": e1 / t, "unit": "edges/s", "threads": threads,
+                                      "seconds_per_step": t, "runs": runs},
+                "note": f"torch CPU restatement of SpGraphAttentionLayer x {H} heads on rows "
+                        f"0..{r1} ({e1} edges), the X W transforms excluded (generous to the CPU); the dense "
+                        f"GraphAttentionLayer is O(N^2) at this size"}
+    finally:
+        torch.set_num_threads(prev)
+
+
+def cpu_sage_ops(table, batch, F: int, H: int, budget_s: float = 20.0):
+    """The reference's CPU GraphSAGE forward for this batch (GraphSAGE/GraphSAGE.py:38-52 with
+    graph_utils.Aggregator MEAN): the collate-side neighbour tensor [M, k1, F]
+    (data_utils.py:141-147) is materialised once outside the timed region, then
+    mean -> Linear(cat) -> ReLU, the torch.embedding re-gathers, mean -> Linear -> ReLU,
+    classifier.  torch CPU ops, every allowed host thread, same shapes, random weights."""
+    threads = min(16, len(os.sched_getaffinity(0)))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        T = torch.from_numpy(table)
+        front = batch.frontier.cpu()
+        nb1 = batch.frontier_nbrs.cpu()
+        cmap, nmap = batch.center_map.cpu(), batch.neigh_map.cpu()
+        self_feats = T[front]
+        neigh_feats = T[nb1]                                   # [M, k1, F]
+        gen = torch.Generator().manual_seed(0)
+        W0 = torch.randn(H, 2 * F, generator=gen) * 0.05
+        W1 = torch.randn(H, 2 * H, generator=gen) * 0.05
+        Wc = torch.randn(3, H, generator=gen) * 0.05
+
+        def forward():
+            h1 = torch.relu(torch.cat([self_feats, neigh_feats.mean(1)], 1) @ W0.T)
+            agg = torch.embedding(h1, nmap).mean(1)
+            h2 = torch.relu(torch.cat([torch.embedding(h1, cmap), agg], 1) @ W1.T)
+            return h2 @ Wc.T
+
+        t, runs = _cpu_time(forward, budget_s)
+        return {"torch_graphsage_forward": {"value": batch.sampled_edges / t, "unit": "edges/s",
+                                            "threads": threads, "seconds_per_step": t,
+                                            "runs": runs},
+                "note": "torch CPU restatement of GraphSAGE.forward (MEAN, 2 layers) on the same "
+                        "sampled batch, neighbour tensor pre-materialised as collate_fn does"}
     finally:
         torch.set_num_threads(prev)
 
@@ -239,6 +347,12 @@ def run_gat(args, dev):
         res["cpu_baseline"] = {"value": float(rp[-1]) / t, "unit": "edges/s", "cores": 1,
                                "kind": "port", "sample": f"oracle gat_csr (numpy) on rows 0..{R} "
                                                         f"({int(rp[-1])} edges)"}
+        if not args.no_cpu_reference:
+            try:
+                res["cpu_reference_ops"] = cpu_spgat_ops(g, X.cpu(), W.cpu(), a_s.cpu(), a_d.cpu(),
+                                                         H, Fh)
+            except Exception as e:
+                res["cpu_reference_ops"] = {"error": repr(e)}
     return res
 
 
@@ -255,7 +369,7 @@ def run_sage(args, dev):
     adj = symmetric_adjacency(s, d, n, device=dev)
     del s, d
     log(f"[bench] sage adjacency nnz={adj.nnz} in {time.time() - t0:.1f}s")
-    F = H = args.feat
+    F = H = args.feat or 128
     gen = torch.Generator(device=dev).manual_seed(0)
     table = torch.randn(n, F, device=dev, generator=gen)
     deg = adj.rowptr[1:] - adj.rowptr[:-1]
@@ -323,6 +437,11 @@ def run_sage(args, dev):
         t = time.perf_counter() - t0
         res["cpu_baseline"] = {"value": idx.size / t, "unit": "edges/s", "cores": 1, "kind": "port",
                                "sample": f"oracle sage_gather_aggregate (numpy) on 50000 frontier rows x {k1}"}
+        if not args.no_cpu_reference:
+            try:
+                res["cpu_reference_ops"] = cpu_sage_ops(tn, batch, F, H)
+            except Exception as e:
+                res["cpu_reference_ops"] = {"error": repr(e)}
     return res
 
 
@@ -332,8 +451,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
-    ap.add_argument("--feat", type=int, default=128)
+    ap.add_argument("--feat", type=int, default=None,
+                    help="feature width (default: the workload's, 128 except cfg5 = 256)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-layer", action="store_true",
+                    help="skip the Graph_conv_layer (GEMM + SpMM) timing beside the aggregation")
     ap.add_argument("--no-cpu-reference", action="store_true",
                     help="skip the torch CPU operator lines (torch.spmm COO / sparse.mm CSR)")
     ap.add_argument("--exchange", default="cover", choices=["cover", "gather"],
@@ -373,8 +495,9 @@ def main():
         return
 
     wl = WORKLOADS[args.workload]
-    nodes, edges = wl["nodes"] * world, wl["edges"] * world
-    F = args.feat
+    grow = 1 if wl.get("strong") else world
+    nodes, edges = wl["nodes"] * grow, wl["edges"] * grow
+    F = args.feat if args.feat is not None else wl.get("feat", 128)
     g = build_graph(nodes, edges, dev, rank, world)
     gen = torch.Generator(device=dev).manual_seed(0)
     bias = torch.randn(F, device=dev, generator=gen)
@@ -448,6 +571,20 @@ def main():
     kern_ms = statistics.mean(step_ms)
     achieved = bytes_local / (kern_ms / 1e3) / 1e9
 
+    layer_ms = None
+    log(f"[bench] aggregation timed: {statistics.mean(step_ms):.3f} ms/launch")
+    if world == 1 and not args.no_layer:
+        # the whole drop-in Graph_conv_layer(F, F).forward (GCN/GCN.py:41-47): dense X W^T on
+        # hipBLASLt + the SpMM with the bias epilogue -- reported beside the aggregation
+        from graphneuralnetwork_amd.gcn import Graph_conv_layer
+        layer = Graph_conv_layer(F, F).to(dev).eval()
+        with torch.no_grad():
+            layer_ms = statistics.mean(time_steps(lambda: layer(X, g), min(args.steps, 10),
+                                                  2, dev)[0])
+        del layer
+        log(f"[bench] Graph_conv_layer timed: {layer_ms:.3f} ms")
+        torch.cuda.empty_cache()
+
     traffic = None
     tpath = Path(args.traffic_json) if args.traffic_json else \
         ROOT / "profiles" / f"traffic_{args.workload}_F{F}.json"
@@ -460,7 +597,8 @@ def main():
         res = {
             "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "strong" if wl.get("strong") else "weak",
+            "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (R-MAT a=.57 b=.19 c=.19 d=.05, seed 0, reference GCN normalisation; "
                     "X ~ N(0,1))",
             "config": {"workload": wl["name"], "nodes": nodes, "directed_edges": edges,
@@ -470,6 +608,7 @@ def main():
                        **({"exchange": args.exchange} if world > 1 else {})},
             "achieved_GBps": achieved,
             "graph_build_s": BUILD_INFO.get("gcn_adjacency_build_s"),
+            **({"gcn_layer_ms": layer_ms} if layer_ms is not None else {}),
             **({"partition_build_s": BUILD_INFO.get("partition_build_s")} if world > 1 else {}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
@@ -482,11 +621,13 @@ def main():
                          "avg_launch_ms": kern_ms, "min_launch_ms": min(step_ms)},
         }
         if world == 1 and not args.no_cpu_baseline:
+            log("[bench] cpu baseline (oracle port) ...")
             try:
                 res["cpu_baseline"] = cpu_baseline(g, X, F)
             except Exception as e:  # the baseline is reported, never the target
                 res["cpu_baseline"] = {"value": None, "error": repr(e)}
             if not args.no_cpu_reference:
+                log("[bench] cpu reference operators ...")
                 try:
                     res["cpu_reference_ops"] = cpu_reference_ops(g, X, F)
                 except Exception as e:
