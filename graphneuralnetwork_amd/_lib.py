@@ -90,6 +90,15 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_gcn_adjacency_fill": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gnn_sample_neighbors": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, ctypes.c_uint64, _vp,
                                             _vp, _vp]),
+    # CPython-exact host sampler (pysample.cpp): host pointers, no stream
+    "gnn_pyadj_build": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
+    "gnn_py_layer_sample": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i32, _i64, _i32, _vp,
+                                           ctypes.POINTER(_vp)]),
+    "gnn_py_layer_result_shape": (ctypes.c_int, [_vp, _vp]),
+    "gnn_py_layer_result_copy": (ctypes.c_int, [_vp, _vp, _vp]),
+    "gnn_py_layer_result_free": (None, [_vp]),
+    "gnn_pyset_order": (ctypes.c_int, [_vp, _i64, _vp, _vp]),
+    "gnn_pyset_union_order": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp]),
 }
 
 EPI_RELU = 1

@@ -43,7 +43,15 @@ def _hipcc() -> str:
 
 
 def sources() -> list[Path]:
-    return sorted(CSRC_DIR.glob("*.hip"))
+    """HIP sources (*.hip, device + host) and host-only C++ (*.cpp, the CPython-exact sampler)."""
+    return sorted(CSRC_DIR.glob("*.hip")) + sorted(CSRC_DIR.glob("*.cpp"))
+
+
+def _compile_cmd(hipcc: str, src: Path, obj: Path, extra=()) -> list[str]:
+    if src.suffix == ".cpp":  # host-only translation unit: the system C++ compiler
+        return ["g++", "-O3", "-fPIC", "-std=c++17", "-Wall", "-pthread", *extra, "-c", str(src),
+                "-o", str(obj)]
+    return [hipcc, *HIPCC_FLAGS, *extra, "-c", str(src), "-o", str(obj)]
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:
@@ -65,7 +73,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         obj = OBJ_DIR / (src.stem + ".o")
         objs.append(obj)
         if force or _stale(obj, [src] + headers):
-            cmd = [hipcc, *HIPCC_FLAGS, "-c", str(src), "-o", str(obj)]
+            cmd = _compile_cmd(hipcc, src, obj)
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE,
@@ -81,7 +89,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         raise RuntimeError("hipcc failed:\n" + "\n".join(failed))
     if force or procs or _stale(LIB_PATH, objs):
         tmp = LIB_PATH.with_suffix(".so.tmp")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp),
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(tmp),
                *map(str, objs)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
@@ -98,14 +106,14 @@ def build_variant(tag: str, defines: list[str]) -> Path:
     out = LIB_DIR / "variants" / f"libgnn_{tag}.so"
     out.parent.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
-    flags = [*HIPCC_FLAGS, *(f"-D{d}" for d in defines)]
-    procs = [(src, subprocess.Popen([hipcc, *flags, "-c", str(src), "-o", str(odir / (src.stem + ".o"))],
+    procs = [(src, subprocess.Popen(_compile_cmd(hipcc, src, odir / (src.stem + ".o"),
+                                                 [f"-D{d}" for d in defines]),
                                     stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
              for src in sources()]
     failed = [f"--- {src.name} ---\n{p.communicate()[0]}" for src, p in procs if p.wait() != 0]
     if failed:
         raise RuntimeError("hipcc failed:\n" + "\n".join(failed))
-    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out),
+    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(out),
                         *(str(odir / (src.stem + ".o")) for src in sources())],
                        capture_output=True, text=True)
     if r.returncode != 0:

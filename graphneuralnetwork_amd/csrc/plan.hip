@@ -216,6 +216,9 @@ extern "C" const char* gnn_error_string(int code) {
     case GNN_E_ARG: return "gnn: invalid argument (null pointer, negative size or bad stride)";
     case GNN_E_ALIGN: return "gnn: misaligned pointer";
     case GNN_E_UNSUPPORTED: return "gnn: shape not supported by this library";
+    case GNN_E_EMPTY: return "Cannot choose from an empty sequence";
+    case GNN_E_RAGGED: return "gnn: index maps of unequal length (ragged nested sequence)";
+    case GNN_E_NOMEM: return "gnn: host allocation failed";
     default: break;
   }
   if (code > 0) return hipGetErrorString(static_cast<hipError_t>(code));

@@ -34,6 +34,11 @@ extern "C" {
 #define GNN_E_ARG (-1)        /* null pointer / negative size / bad stride          */
 #define GNN_E_ALIGN (-2)      /* a pointer is not aligned as the layout requires    */
 #define GNN_E_UNSUPPORTED (-3) /* shape outside what the library implements         */
+#define GNN_E_EMPTY (-4)      /* random.choices on an empty neighbour set (the reference's
+                                 IndexError: Cannot choose from an empty sequence)      */
+#define GNN_E_RAGGED (-5)     /* index maps of unequal length (the reference's torch.tensor
+                                 ValueError)                                           */
+#define GNN_E_NOMEM (-6)      /* host allocation failed                                 */
 
 /* ---- epilogue flags ---- */
 #define GNN_EPI_RELU 1u /* y = max(y, 0) after the bias add                          */
@@ -275,6 +280,40 @@ int gnn_gcn_adjacency_build(const int64_t* src, const int64_t* dst, int64_t n_ed
                             int64_t* nnz_out, void* stream);
 int gnn_gcn_adjacency_fill(const void* workspace, int64_t n_edges, int64_t n_nodes, int64_t nnz,
                            int64_t* rowptr, int32_t* col, float* val, void* stream);
+
+/* ---- CPython-exact host sampler (pysample.cpp; host memory, no stream) ----
+ * Bit-exact restatement of the reference's host-side GraphSAGE sampling, which draws
+ * from CPython's global `random` and iterates Python sets:
+ *   gnn_pyadj_build      adj_lists of read_pubmed_data (GraphSAGE/data_utils.py:29-37):
+ *                        for each pair t in order, adj[src[t]].add(dst[t]);
+ *                        adj[dst[t]].add(src[t]). Writes each node's neighbours in the
+ *                        iteration order of its Python set: rowptr [n_nodes+1],
+ *                        nbr [<= 2 n_pairs]. Ids in [0, n_nodes) (else GNN_E_ARG).
+ *   gnn_py_layer_sample  get_layer_adj_nodes(nodes, adj_lists, num_layers, num_neighs,
+ *                        is_gcn) (data_utils.py:82-124) with the neighbour order
+ *                        (rowptr, nbr) = list(adj_lists[v]). mt_state is CPython's
+ *                        random.getstate()[1] (624 MT words + position, 625 uint32),
+ *                        advanced in place exactly as the reference advances it.
+ *                        On success *result holds the maps; read them with
+ *                        gnn_py_layer_result_shape (dims = {L, pad_len, width}) and
+ *                        gnn_py_layer_result_copy (neigh_map [L, pad_len, width],
+ *                        center_map [L, pad_len], the torch.tensor()s of collate_fn,
+ *                        data_utils.py:158-160), then gnn_py_layer_result_free.
+ *                        GNN_E_EMPTY: a sampled node has no neighbours (IndexError).
+ *   gnn_pyset_order / gnn_pyset_union_order: iteration order of set(keys) and of
+ *                        set(a).union(set(b)) (test hooks for the set restatement).
+ * Keys are node ids in [0, 2^61 - 1). */
+int gnn_pyadj_build(const int64_t* src, const int64_t* dst, int64_t n_pairs, int64_t n_nodes,
+                    int64_t* rowptr, int64_t* nbr);
+int gnn_py_layer_sample(const int64_t* rowptr, const int64_t* nbr, int64_t n_nodes,
+                        const int64_t* nodes, int64_t n_batch, int32_t num_layers,
+                        int64_t num_neighs, int32_t is_gcn, uint32_t* mt_state, void** result);
+int gnn_py_layer_result_shape(const void* result, int64_t* dims);
+int gnn_py_layer_result_copy(const void* result, int64_t* neigh_map, int64_t* center_map);
+void gnn_py_layer_result_free(void* result);
+int gnn_pyset_order(const int64_t* keys, int64_t n, int64_t* out, int64_t* n_out);
+int gnn_pyset_union_order(const int64_t* a, int64_t na, const int64_t* b, int64_t nb,
+                          int64_t* out, int64_t* n_out);
 
 /* ---- developer entry (not part of the drop-in surface) ----
  * gnn_dev_spmm_variant_f32: gnn_spmm_csr_f32 at feat == 128 with a compile-time

@@ -254,6 +254,54 @@ def sage_gather_aggregate(table, idx, agg_func="MEAN"):
     return aggregator(np.asarray(table)[np.asarray(idx)], agg_func)
 
 
+def sage_layer_adj_nodes(nodes, adj_lists, num_layers, num_neighs, is_gcn, rng):
+    """get_layer_adj_nodes (GraphSAGE/data_utils.py:82-124), restated with Python sets and a
+    ``random.Random``-compatible ``rng`` (the draws and set orders ARE CPython's own, so this
+    is exact for small cases; quadratic like the reference's per-node union).
+
+    Per layer i, per node of the layer (a list for i = 0, the previous layer's set after):
+    sample ``k`` of ``list(adj_lists[node])`` (rng.sample if deg > k else rng.choices, :91-94),
+    append the node in gcn mode else add it to the layer set (:95-98), then
+    ``layer = layer.union(set(sample))`` (:100).  Outputs (:104-123), deepest layer first:
+    global ids for the last layer, positions in the next layer's enumeration for the others,
+    -1 padded to the last layer's length.  Returns (neigh [L][P][k'], center [L][P]) lists.
+    """
+    layer_neigh, layer_map = [], []
+    centers = [list(nodes)]
+    cur = nodes
+    for i in range(num_layers):
+        pos, samples, layer = {}, [], set()
+        for idx, node in enumerate(cur):
+            pos[node] = idx
+            nb = list(adj_lists[node])
+            s = rng.sample(nb, k=num_neighs) if len(nb) > num_neighs else \
+                rng.choices(nb, k=num_neighs)
+            if is_gcn:
+                s.append(node)
+            else:
+                layer.add(node)
+            samples.append(s)
+            layer = layer.union(set(s))
+        layer_neigh.append(samples)
+        layer_map.append(pos)
+        cur = layer
+        centers.append(list(cur))
+    neigh_out, center_out = [], []
+    pad = len(layer_neigh[-1])
+    for i in reversed(range(num_layers)):
+        if i == num_layers - 1:
+            neigh_out.append([list(r) for r in layer_neigh[i]])
+            center_out.append(list(centers[i]))
+        else:
+            m = layer_map[i + 1]
+            rows = [[m[v] for v in r] for r in layer_neigh[i]]
+            width = len(rows[0])
+            neigh_out.append(rows + [[-1] * width] * (pad - len(rows)))
+            cm = [m[v] for v in centers[i]]
+            center_out.append(cm + [-1] * (pad - len(cm)))
+    return neigh_out, center_out
+
+
 def gat_csr(rowptr, col, wh, el, er, heads, fh, slope, sparse: bool, empty_fill=None):
     """Edge-list form of both GAT layers for H heads at once, float64.
 

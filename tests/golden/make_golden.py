@@ -387,8 +387,71 @@ def part_sagepy():
     print("sagepy", y.shape)
 
 
+# ------------------------------------------------------- GraphSAGE sampler (index maps)
+def part_pysampler():
+    """The reference's host sampler (get_layer_adj_nodes, GraphSAGE/data_utils.py:82-124)
+    under a seeded global ``random``: pins the CPython-exact native sampler bit for bit.
+    adj_lists is built exactly as read_pubmed_data does (data_utils.py:29-37) from a pair
+    stream that is stored, so the native construction is pinned too."""
+    sys.path.insert(0, str(REF / "GraphSAGE"))
+    import random
+    from collections import defaultdict
+    import data_utils as du  # reference GraphSAGE/data_utils.py
+
+    rng = np.random.default_rng(11)
+    out = {}
+    graphs = {}
+    for name, N, E, hub in (("small", 300, 700, 90), ("mid", 20000, 90000, 700)):
+        ring = np.stack([np.arange(N), (np.arange(N) + 1) % N], 1)  # every node has deg >= 2
+        rnd = rng.integers(0, N, (E, 2))
+        rnd[::97, 1] = rnd[::97, 0]                                   # self pairs
+        hubs = np.stack([np.zeros(hub, np.int64), rng.integers(1, N, hub)], 1)
+        pairs = np.concatenate([ring, rnd, hubs]).astype(np.int64)
+        perm = rng.permutation(len(pairs))
+        pairs = pairs[perm]
+        adj = defaultdict(set)
+        for a, b in pairs.tolist():
+            adj[a].add(b)
+            adj[b].add(a)
+        order = [list(adj[v]) for v in range(N)]
+        out[f"{name}_pairs"] = pairs
+        out[f"{name}_n"] = np.int64(N)
+        out[f"{name}_adj_ptr"] = np.cumsum([0] + [len(o) for o in order]).astype(np.int64)
+        out[f"{name}_adj_nbr"] = np.asarray([u for o in order for u in o], np.int64)
+        graphs[name] = adj
+    cases = [("small", 20, 2, 5, False, 1), ("small", 20, 2, 5, True, 2),
+             ("small", 10, 3, 4, False, 3), ("small", 12, 1, 7, False, 4),
+             ("small", 16, 2, 30, False, 5), ("small", 8, 3, 3, True, 6),
+             ("mid", 256, 2, 10, False, 7), ("mid", 128, 2, 25, False, 8),
+             ("mid", 200, 2, 8, True, 9)]
+    for c, (g, B, L, K, gcn, seed) in enumerate(cases):
+        random.seed(seed)
+        nodes = [int(v) for v in rng.choice(int(out[f"{g}_n"]), B, replace=False)]
+        if c == 3:
+            nodes[3] = nodes[1]  # a repeated batch node (dict position: last one wins)
+        state0 = np.asarray(random.getstate()[1], np.uint32)
+        neigh, center = du.get_layer_adj_nodes(nodes, graphs[g], L, K, gcn)
+        out[f"case{c}_meta"] = np.array([["small", "mid"].index(g), L, K, int(gcn), seed])
+        out[f"case{c}_nodes"] = np.asarray(nodes, np.int64)
+        out[f"case{c}_state0"] = state0
+        out[f"case{c}_neigh"] = np.asarray(neigh, np.int64)
+        out[f"case{c}_center"] = np.asarray(center, np.int64)
+        out[f"case{c}_state1"] = np.asarray(random.getstate()[1], np.uint32)
+        print("pysampler case", c, out[f"case{c}_neigh"].shape)
+    # a node without neighbours: random.choices on [] -> IndexError
+    adj = defaultdict(set, {0: {1}, 1: {0}})
+    random.seed(0)
+    try:
+        du.get_layer_adj_nodes([0, 5], adj, 1, 3, False)
+        out["empty_raises"] = np.int64(0)
+    except IndexError:
+        out["empty_raises"] = np.int64(1)
+    out["empty_state1"] = np.asarray(random.getstate()[1], np.uint32)
+    np.savez_compressed(HERE / "pysampler.npz", **out)
+
+
 PARTS = {"gcn": part_gcn, "gat": part_gat, "sage": part_sage, "han": part_han,
-         "sagepy": part_sagepy}
+         "sagepy": part_sagepy, "pysampler": part_pysampler}
 
 if __name__ == "__main__":
     sys.dont_write_bytecode = True
