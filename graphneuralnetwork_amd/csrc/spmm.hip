@@ -108,6 +108,51 @@ __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ col,
   }
 }
 
+// A/B variant (tools/spmm_ab.py variant 3): the same gather with every neighbour row
+// staged through LDS by LDS-DMA (global_load_lds_dwordx4: per-lane source address, the
+// wave's 1 KiB lands lane-linear at a wave-uniform LDS base) instead of loaded into
+// VGPRs -- the "LDS-staged feature tiles" alternative. Each staged row is read back once
+// by the lane that requested it, so LDS adds a write + read per byte and frees no reuse;
+// measured against the register path in profiles/ (DESIGN.md section 4). VW = 4, NCH = 1.
+template <int LPR, int U>
+__device__ __forceinline__ void gather_rows_lds(const int32_t* __restrict__ col,
+                                                const float* __restrict__ val, int64_t beg,
+                                                int64_t end, const float* __restrict__ x,
+                                                int64_t ldx, int lane, f4& acc, f4* stage) {
+  constexpr int EPI = kWave / LPR;
+  const int sub = lane & (LPR - 1);
+  const int grp = lane / LPR;
+  for (int64_t base = beg; base < end; base += kWave) {
+    const int n = static_cast<int>(min(static_cast<int64_t>(kWave), end - base));
+    int c = 0;
+    float v = 0.f;
+    if (lane < n) {
+      c = __builtin_nontemporal_load(col + base + lane);
+      v = __builtin_nontemporal_load(val + base + lane);
+    }
+    for (int k = 0; k < n; k += EPI * U) {
+      float w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = k + u * EPI + grp;
+        const int ce = __shfl(c, e & (kWave - 1), kWave);
+        const float we = __shfl(v, e & (kWave - 1), kWave);
+        w[u] = we;
+        const float* src = x + static_cast<int64_t>(e < n ? ce : 0) * ldx + sub * 4;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)src,
+            (__attribute__((address_space(3))) void*)(stage + u * kWave), 16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k + u * EPI + grp < n) acc += w[u] * stage[u * kWave + lane];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next DMA
+    }
+  }
+}
+
 // Combine the EPI edge slots of a wave (fixed xor-tree order: deterministic).
 template <int VW, int LPR, int NCH>
 __device__ __forceinline__ void reduce_slots(typename Vec<VW>::T (&acc)[NCH]) {
@@ -142,11 +187,13 @@ __device__ __forceinline__ void store_slot_row(float* __restrict__ out,
   }
 }
 
-template <int VW, int LPR, int NCH, int U, bool NT>
+template <int VW, int LPR, int NCH, int U, bool NT, bool STAGE = false>
 __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
   constexpr int EPI = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+  __shared__ f4 stage_all[STAGE ? kWavesPerBlock * U * kWave : 1];
+  f4* stage = stage_all + (STAGE ? (threadIdx.x >> 6) * U * kWave : 0);
   const int sub = lane & (LPR - 1);
   const int grp = lane / LPR;
   typename Vec<VW>::T acc[NCH];
@@ -158,7 +205,10 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
     const int32_t row = P.seg_row[wave];
     const int64_t beg = P.seg_begin[wave];
     const int64_t end = min(beg + P.seg_len, P.rowptr[row + 1]);
-    gather_rows<VW, LPR, NCH, U>(P.col, P.val, beg, end, P.x, P.ldx, P.feat, lane, acc);
+    if constexpr (STAGE)
+      gather_rows_lds<LPR, U>(P.col, P.val, beg, end, P.x, P.ldx, lane, acc[0], stage);
+    else
+      gather_rows<VW, LPR, NCH, U>(P.col, P.val, beg, end, P.x, P.ldx, P.feat, lane, acc);
     reduce_slots<VW, LPR, NCH>(acc);
     if (lane < LPR) store_slot_row<VW, LPR, NCH, false>(P.partial + wave * P.ldp, nullptr, P.feat,
                                                         0u, sub, acc);
@@ -168,8 +218,12 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
     const int64_t i = wave - P.seg_waves;
     if (i >= P.n_mid) return;
     const int64_t row = P.mid_row ? P.mid_row[i] : i;
-    gather_rows<VW, LPR, NCH, U>(P.col, P.val, P.rowptr[row], P.rowptr[row + 1], P.x, P.ldx,
-                                 P.feat, lane, acc);
+    if constexpr (STAGE)
+      gather_rows_lds<LPR, U>(P.col, P.val, P.rowptr[row], P.rowptr[row + 1], P.x, P.ldx, lane,
+                              acc[0], stage);
+    else
+      gather_rows<VW, LPR, NCH, U>(P.col, P.val, P.rowptr[row], P.rowptr[row + 1], P.x, P.ldx,
+                                   P.feat, lane, acc);
     reduce_slots<VW, LPR, NCH>(acc);
     if (lane < LPR) store_slot_row<VW, LPR, NCH, NT>(P.y + row * P.ldy, P.bias, P.feat, P.flags,
                                                      sub, acc);
@@ -272,7 +326,7 @@ struct SpmmLaunch {
   hipStream_t stream;
 };
 
-template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true>
+template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true, bool STAGE = false>
 static int launch_spmm(const SpmmLaunch& L) {
   constexpr int U = U_OVERRIDE ? U_OVERRIDE : (NCH >= 4 ? 1 : (NCH == 2 ? 2 : 4));
   constexpr int EPI = kWave / LPR;
@@ -286,7 +340,7 @@ static int launch_spmm(const SpmmLaunch& L) {
   const int64_t blocks = seg_blocks + mid_blocks + small_blocks;
   if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   if (blocks > 0) {
-    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT>), dim3(static_cast<unsigned>(blocks)),
+    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT, STAGE>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBlock), 0, L.stream, p);
   }
   if (L.n_long > 0) {
@@ -357,6 +411,8 @@ static int run_spmm(SpmmLaunch L, const float* x, const float* bias, float* y, f
       case 0: return launch_spmm<4, 32, 1, 4, true>(L);  // the shipped configuration
       case 1: return launch_spmm<4, 32, 1, 8, true>(L);
       case 2: return launch_spmm<4, 32, 1, 2, true>(L);
+      case 3: return launch_spmm<4, 32, 1, 4, true, true>(L);   // LDS-DMA staged gather
+      case 4: return launch_spmm<4, 32, 1, 8, true, true>(L);   // LDS-DMA, 8 slots in flight
       case 7: return launch_spmm<4, 32, 1, 4, false>(L);
       default: return GNN_E_ARG;
     }

@@ -317,8 +317,9 @@ int gnn_pyset_union_order(const int64_t* a, int64_t na, const int64_t* b, int64_
 
 /* ---- developer entry (not part of the drop-in surface) ----
  * gnn_dev_spmm_variant_f32: gnn_spmm_csr_f32 at feat == 128 with a compile-time
- * kernel variant (0 shipped: U=4, non-temporal Y stores; 1 U=8; 2 U=2; 7 U=4 with
- * plain Y stores) and no epilogue, for interleaved A/B timing (tools/spmm_ab.py). */
+ * kernel variant (0 shipped: U=4, non-temporal Y stores; 1 U=8; 2 U=2; 3 U=4 and 4 U=8
+ * with the neighbour rows staged through LDS by LDS-DMA; 7 U=4 with plain Y stores) and
+ * no epilogue, for interleaved A/B timing (tools/spmm_ab.py). */
 int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* col, const float* val,
                              int64_t n_rows, const float* x, int64_t ldx, int64_t feat,
                              const float* bias, float* y, int64_t ldy, int64_t seg_len,
