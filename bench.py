@@ -67,6 +67,7 @@ def algorithmic_bytes(nnz: int, n_rows: int, feat: int) -> int:
 
 
 BUILD_INFO = {}
+HUB_INFO = {}
 
 
 def build_graph(nodes: int, edges: int, dev, rank: int, world: int):
@@ -509,6 +510,8 @@ def main():
         rows_local, nnz_local = g.n_rows, g.nnz
         bytes_local = algorithmic_bytes(nnz_local, rows_local, F)
         halo_rows = 0
+        from graphneuralnetwork_amd.ops import hub_rows_for
+        HUB_INFO["hub_rows"] = hub_rows_for(g.n_cols, F)
     else:
         from graphneuralnetwork_amd.distributed import (EdgeCutSpmm, build_cover_exchange,
                                                         build_partition, nnz_balanced_bounds)
@@ -616,7 +619,12 @@ def main():
                          "traffic_source": (str(tpath.relative_to(ROOT)) + ": rocprofv3 --pmc "
                                             "FETCH_SIZE x2 + WRITE_SIZE of this command")
                          if traffic else None,
-                         "kernel": "spmm_csr_kernel (+ spmm_fixup_kernel), per-step HIP events",
+                         "kernel": ("gather_rows_kernel (hub staging: the %d highest-degree rows "
+                                    "of X, %.0f MiB) + spmm_csr_kernel<HUB> + spmm_fixup_kernel, "
+                                    "per-step HIP events" % (HUB_INFO["hub_rows"],
+                                                             HUB_INFO["hub_rows"] * 4 * F / 2**20))
+                         if HUB_INFO.get("hub_rows") else
+                         "spmm_csr_kernel (+ spmm_fixup_kernel), per-step HIP events",
                          "algorithmic_bytes_per_launch": bytes_local,
                          "avg_launch_ms": kern_ms, "min_launch_ms": min(step_ms)},
         }

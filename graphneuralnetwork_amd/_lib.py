@@ -37,6 +37,15 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _vp, _vp, _i64,            # small_row, small_col, small_val, n_small
         _vp, _i64, _vp,                 # mid_row, n_mid, partial
         _u32, _vp]),                    # flags, stream
+    "gnn_spmm_csr_hub_f32": (ctypes.c_int, [
+        _vp, _vp, _vp, _i64,            # rowptr, col_hub, val, n_rows
+        _vp, _i64, _vp, _i64, _i64,     # x, ldx, xh, ldh, feat
+        _vp, _vp, _i64,                 # bias, y, ldy
+        _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
+        _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
+        _vp, _vp, _vp, _i64,            # small_row, small_col, small_val, n_small
+        _vp, _i64, _vp,                 # mid_row, n_mid, partial
+        _u32, _vp]),                    # flags, stream
     "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
     "gnn_spmm_plan_count": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gnn_spmm_plan_fill": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -59,18 +59,26 @@ struct SpmmParams {
   float* partial;
   int64_t ldp;
   uint32_t flags;
+  // hub staging (HUB kernels): col < 0 names row -1-col of the staged hub table xh
+  const float* xh;
+  int64_t ldh;
   // launch geometry (wave index boundaries)
   int64_t seg_waves;
   int64_t mid_waves;
 };
 
 // acc[ch] += sum_{e in [beg, end)} val[e] * x[col[e]][(ch*LPR + sub)*VW .. +VW)
-template <int VW, int LPR, int NCH, int U>
+//
+// HUB: a column id c < 0 names row -1-c of the staged hub table xh (the highest-degree
+// columns of X copied into one compact buffer per call, see gnn_spmm_csr_hub_f32).
+template <int VW, int LPR, int NCH, int U, bool HUB = false>
 __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ col,
                                             const float* __restrict__ val, int64_t beg,
                                             int64_t end, const float* __restrict__ x,
                                             int64_t ldx, int64_t feat, int lane,
-                                            typename Vec<VW>::T (&acc)[NCH]) {
+                                            typename Vec<VW>::T (&acc)[NCH],
+                                            const float* __restrict__ xh = nullptr,
+                                            int64_t ldh = 0) {
   constexpr int EPI = kWave / LPR;
   const int sub = lane & (LPR - 1);
   const int grp = lane / LPR;
@@ -92,7 +100,8 @@ __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ col,
         const int ce = __shfl(c, src, kWave);
         const float we = __shfl(v, src, kWave);
         w[u] = e < n ? we : 0.f;
-        const float* xr = x + static_cast<int64_t>(ce) * ldx;
+        const float* xr = (HUB && ce < 0) ? xh + static_cast<int64_t>(-1 - ce) * ldh
+                                          : x + static_cast<int64_t>(ce) * ldx;
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
           const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
@@ -187,7 +196,7 @@ __device__ __forceinline__ void store_slot_row(float* __restrict__ out,
   }
 }
 
-template <int VW, int LPR, int NCH, int U, bool NT, bool STAGE = false>
+template <int VW, int LPR, int NCH, int U, bool NT, bool STAGE = false, bool HUB = false>
 __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
   constexpr int EPI = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
@@ -208,7 +217,8 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
     if constexpr (STAGE)
       gather_rows_lds<LPR, U>(P.col, P.val, beg, end, P.x, P.ldx, lane, acc[0], stage);
     else
-      gather_rows<VW, LPR, NCH, U>(P.col, P.val, beg, end, P.x, P.ldx, P.feat, lane, acc);
+      gather_rows<VW, LPR, NCH, U, HUB>(P.col, P.val, beg, end, P.x, P.ldx, P.feat, lane, acc,
+                                        P.xh, P.ldh);
     reduce_slots<VW, LPR, NCH>(acc);
     if (lane < LPR) store_slot_row<VW, LPR, NCH, false>(P.partial + wave * P.ldp, nullptr, P.feat,
                                                         0u, sub, acc);
@@ -222,8 +232,8 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
       gather_rows_lds<LPR, U>(P.col, P.val, P.rowptr[row], P.rowptr[row + 1], P.x, P.ldx, lane,
                               acc[0], stage);
     else
-      gather_rows<VW, LPR, NCH, U>(P.col, P.val, P.rowptr[row], P.rowptr[row + 1], P.x, P.ldx,
-                                   P.feat, lane, acc);
+      gather_rows<VW, LPR, NCH, U, HUB>(P.col, P.val, P.rowptr[row], P.rowptr[row + 1], P.x,
+                                        P.ldx, P.feat, lane, acc, P.xh, P.ldh);
     reduce_slots<VW, LPR, NCH>(acc);
     if (lane < LPR) store_slot_row<VW, LPR, NCH, NT>(P.y + row * P.ldy, P.bias, P.feat, P.flags,
                                                      sub, acc);
@@ -326,8 +336,9 @@ struct SpmmLaunch {
   hipStream_t stream;
 };
 
-template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true, bool STAGE = false>
-static int launch_spmm(const SpmmLaunch& L) {
+template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true, bool STAGE = false,
+          bool HUB = false>
+static int launch_spmm_t(const SpmmLaunch& L) {
   constexpr int U = U_OVERRIDE ? U_OVERRIDE : (NCH >= 4 ? 1 : (NCH == 2 ? 2 : 4));
   constexpr int EPI = kWave / LPR;
   SpmmParams p = L.p;
@@ -340,7 +351,7 @@ static int launch_spmm(const SpmmLaunch& L) {
   const int64_t blocks = seg_blocks + mid_blocks + small_blocks;
   if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   if (blocks > 0) {
-    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT, STAGE>), dim3(static_cast<unsigned>(blocks)),
+    hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT, STAGE, HUB>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBlock), 0, L.stream, p);
   }
   if (L.n_long > 0) {
@@ -349,6 +360,12 @@ static int launch_spmm(const SpmmLaunch& L) {
                        p.ldp, p.feat, p.bias, p.y, p.ldy, p.flags);
   }
   return launch_status();
+}
+
+template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true, bool STAGE = false>
+static int launch_spmm(const SpmmLaunch& L) {
+  return L.p.xh ? launch_spmm_t<VW, LPR, NCH, U_OVERRIDE, NT, STAGE, true>(L)
+                : launch_spmm_t<VW, LPR, NCH, U_OVERRIDE, NT, STAGE, false>(L);
 }
 
 // Picks (VW, LPR, NCH) for one column block of width feat (<= 64*8*VW).
@@ -396,8 +413,10 @@ static int check_spmm_args(const int64_t* rowptr, int64_t n_rows, const float* x
 
 static int run_spmm(SpmmLaunch L, const float* x, const float* bias, float* y, float* partial,
                     int64_t feat, int variant) {
+  const float* xh = L.p.xh;
   const bool vec4 = (feat % 4 == 0) && (L.p.ldx % 4 == 0) && (L.p.ldy % 4 == 0) &&
                     aligned_to(x, 16) && aligned_to(y, 16) &&
+                    (xh == nullptr || (aligned_to(xh, 16) && L.p.ldh % 4 == 0)) &&
                     (bias == nullptr || aligned_to(bias, 16)) &&
                     (partial == nullptr || aligned_to(partial, 16));
   if (variant >= 0) {  // developer A/B (feat == 128, vector path only)
@@ -422,6 +441,7 @@ static int run_spmm(SpmmLaunch L, const float* x, const float* bias, float* y, f
   for (int64_t c0 = 0; c0 < feat; c0 += blk) {
     L.p.feat = feat - c0 < blk ? feat - c0 : blk;
     L.p.x = x + c0;
+    L.p.xh = xh ? xh + c0 : nullptr;
     L.p.y = y + c0;
     L.p.bias = bias ? bias + c0 : nullptr;
     L.p.partial = partial ? partial + c0 : nullptr;
@@ -438,11 +458,12 @@ static int spmm_entry(const int64_t* rowptr, const int32_t* col, const float* va
                       const int32_t* long_seg_ptr, int64_t n_long, const int32_t* small_row,
                       const int32_t* small_col, const float* small_val, int64_t n_small,
                       const int32_t* mid_row, int64_t n_mid, float* partial, uint32_t flags,
-                      void* stream, int variant) {
+                      void* stream, int variant, const float* xh = nullptr, int64_t ldh = 0) {
   int rc = check_spmm_args(rowptr, n_rows, x, ldx, feat, y, ldy, seg_len, n_seg, n_long, n_small,
                            n_mid, seg_row, seg_begin, long_row, long_seg_ptr, small_row, small_col,
                            small_val, mid_row, partial, flags);
   if (rc != GNN_OK) return rc;
+  if (xh != nullptr && ldh < feat) return GNN_E_ARG;
   if (n_rows == 0 || feat == 0) return GNN_OK;
   const bool plan = mid_row != nullptr;
   SpmmLaunch L{};
@@ -464,6 +485,8 @@ static int spmm_entry(const int64_t* rowptr, const int32_t* col, const float* va
   L.p.n_small = plan ? n_small : 0;
   L.p.ldp = feat;
   L.p.flags = flags;
+  L.p.xh = xh;
+  L.p.ldh = ldh;
   L.long_row = long_row;
   L.long_seg_ptr = long_seg_ptr;
   L.n_long = plan ? n_long : 0;
@@ -486,6 +509,22 @@ extern "C" int gnn_spmm_csr_f32(const int64_t* rowptr, const int32_t* col, const
   return spmm_entry(rowptr, col, val, n_rows, x, ldx, feat, bias, y, ldy, seg_len, seg_row,
                     seg_begin, n_seg, long_row, long_seg_ptr, n_long, small_row, small_col,
                     small_val, n_small, mid_row, n_mid, partial, flags, stream, -1);
+}
+
+extern "C" int gnn_spmm_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub,
+                                    const float* val, int64_t n_rows, const float* x, int64_t ldx,
+                                    const float* xh, int64_t ldh, int64_t feat, const float* bias,
+                                    float* y, int64_t ldy, int64_t seg_len, const int32_t* seg_row,
+                                    const int64_t* seg_begin, int64_t n_seg,
+                                    const int32_t* long_row, const int32_t* long_seg_ptr,
+                                    int64_t n_long, const int32_t* small_row,
+                                    const int32_t* small_col, const float* small_val,
+                                    int64_t n_small, const int32_t* mid_row, int64_t n_mid,
+                                    float* partial, uint32_t flags, void* stream) {
+  if (xh == nullptr) return GNN_E_ARG;
+  return spmm_entry(rowptr, col_hub, val, n_rows, x, ldx, feat, bias, y, ldy, seg_len, seg_row,
+                    seg_begin, n_seg, long_row, long_seg_ptr, n_long, small_row, small_col,
+                    small_val, n_small, mid_row, n_mid, partial, flags, stream, -1, xh, ldh);
 }
 
 // ---- developer entry: kernel-variant A/B at one shape (tools/spmm_ab.py) ----

@@ -101,6 +101,20 @@ class RowSplitPlan:
 
 
 @dataclass
+class HubPlan:
+    """Hub staging of a graph's columns (gnn_spmm_csr_hub_f32): the k highest-degree
+    columns, hottest first, and the column array with hub columns renamed -1-rank."""
+
+    hub_ids: torch.Tensor   # int64 [k]
+    col_hub: torch.Tensor   # int32 [nnz]
+    err: torch.Tensor       # int32 [1] (gather index check flag)
+
+    @property
+    def k(self) -> int:
+        return int(self.hub_ids.numel())
+
+
+@dataclass
 class CsrGraph:
     """Adjacency in CSR: row = output node, col = gathered node (torch.spmm orientation)."""
 
@@ -141,6 +155,15 @@ class CsrGraph:
         if p is None:
             p = _build_plan(self, seg_len)
             self._plans[seg_len] = p
+        return p
+
+    def hub_plan(self, k: int) -> HubPlan:
+        """Hub staging plan for the k highest-degree columns (built once per k, cached)."""
+        key = ("_hub", k)
+        p = self._plans.get(key)
+        if p is None:
+            p = _build_hub_plan(self, k)
+            self._plans[key] = p
         return p
 
     def transpose(self) -> "CsrGraph":
@@ -207,6 +230,23 @@ def _build_plan(g: CsrGraph, seg_len: int) -> RowSplitPlan:
                                       stream), "gnn_spmm_plan_fill")
     return RowSplitPlan(seg_len, seg_row, seg_begin, long_row, long_seg_ptr, small_row,
                         small_col, small_val, mid_row)
+
+
+def _build_hub_plan(g: CsrGraph, k: int) -> HubPlan:
+    """Column in-degrees -> the k hottest columns (ties: lower id first, torch.topk order
+    is not relied on for results: any hub set gives the same sums, only the speed)."""
+    dev = g.device
+    k = max(0, min(int(k), g.n_cols))
+    col64 = g.col.to(torch.int64)
+    deg = torch.bincount(col64, minlength=g.n_cols)
+    hub_ids = torch.topk(deg, k, sorted=True).indices.contiguous() if k else \
+        torch.empty(0, dtype=torch.int64, device=dev)
+    rank = torch.full((g.n_cols,), -1, dtype=torch.int32, device=dev)
+    rank[hub_ids] = torch.arange(k, dtype=torch.int32, device=dev)
+    r = rank[col64]
+    del col64
+    col_hub = torch.where(r >= 0, -1 - r, g.col).contiguous()
+    return HubPlan(hub_ids, col_hub, torch.zeros(1, dtype=torch.int32, device=dev))
 
 
 # ---------------------------------------------------------------- builders

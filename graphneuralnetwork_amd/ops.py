@@ -31,9 +31,23 @@ def _rows_f32(x: torch.Tensor, name: str) -> torch.Tensor:
     return x
 
 
+# Hub staging (gnn_spmm_csr_hub_f32): when X is too large to stay in the Infinity Cache,
+# the HUB_BYTES of its highest-degree rows are copied into one compact table per call.
+HUB_MIN_X_BYTES = 256 << 20
+HUB_BYTES = 64 << 20
+
+
+def hub_rows_for(n_cols: int, feat: int) -> int:
+    """Default number of staged hub rows for an X of n_cols x feat fp32 (0 = no staging)."""
+    if n_cols * 4 * feat < HUB_MIN_X_BYTES:
+        return 0
+    return min(n_cols, max(1, HUB_BYTES // (4 * feat)))
+
+
 def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
                  activation: str | None = None, out: torch.Tensor | None = None,
-                 seg_len: int | None = None, accumulate: bool = False) -> torch.Tensor:
+                 seg_len: int | None = None, accumulate: bool = False,
+                 hubs: int | None = None) -> torch.Tensor:
     """Y = A.X (+ bias) (act) with A in CSR -- the GCN aggregation (GCN/GCN.py:43-45).
 
     ``accumulate=True`` adds into ``out`` (Y = out + A.X ...): the halo pass of
@@ -41,6 +55,9 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
 
     ``seg_len`` overrides the long-row threshold (rows with more edges are split
     across wavefronts); by default it is sized from the feature width.
+
+    ``hubs`` = number of highest-degree rows of X staged into a compact table before
+    the gather (0: none; default ``hub_rows_for``). It changes speed, not results.
     """
     _require_device(g.rowptr, x, bias, out)
     x = _rows_f32(x, "X")
@@ -66,12 +83,26 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
     if x.numel() == 0:  # no column to gather from (e.g. an empty halo): never read
         x = torch.empty((1, feat), dtype=torch.float32, device=x.device)
     lib = _lib.load()
+    flags = _ACT_FLAGS[activation] | (_lib.EPI_ACCUMULATE if accumulate else 0)
+    stream = _lib.stream_handle(x.device)
+    k = hub_rows_for(g.n_cols, feat) if hubs is None else min(int(hubs), g.n_cols)
+    if k > 0 and g.nnz:
+        hp = g.hub_plan(k)
+        xh = torch.empty((hp.k, feat), dtype=torch.float32, device=x.device)
+        _lib.check(lib.gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0],
+                                           hp.hub_ids.data_ptr(), hp.k, feat, xh.data_ptr(), feat,
+                                           hp.err.data_ptr(), stream), "gnn_gather_rows_f32")
+        rc = lib.gnn_spmm_csr_hub_f32(
+            g.rowptr.data_ptr(), hp.col_hub.data_ptr(), g.val.data_ptr(), g.n_rows,
+            x.data_ptr(), x.stride(0), xh.data_ptr(), feat, feat, _lib.ptr(bias),
+            out.data_ptr(), out.stride(0), plan.seg_len, *plan.args(), _lib.ptr(partial), flags,
+            stream)
+        _lib.check(rc, "gnn_spmm_csr_hub_f32")
+        return out
     rc = lib.gnn_spmm_csr_f32(
         g.rowptr.data_ptr(), g.col.data_ptr(), g.val.data_ptr(), g.n_rows,
         x.data_ptr(), x.stride(0), feat, _lib.ptr(bias), out.data_ptr(), out.stride(0),
-        plan.seg_len, *plan.args(), _lib.ptr(partial),
-        _ACT_FLAGS[activation] | (_lib.EPI_ACCUMULATE if accumulate else 0),
-        _lib.stream_handle(x.device))
+        plan.seg_len, *plan.args(), _lib.ptr(partial), flags, stream)
     _lib.check(rc, "gnn_spmm_csr_f32")
     return out
 

@@ -81,6 +81,26 @@ int gnn_spmm_csr_f32(const int64_t* rowptr, const int32_t* col, const float* val
                      int64_t n_mid, float* partial, uint32_t flags, void* stream);
 
 /*
+ * gnn_spmm_csr_f32 with hub staging (same aggregation, same plan arguments).
+ * The K highest-degree columns of X ("hubs") are copied by the caller into one
+ * compact table xh [K, ldh] (gnn_gather_rows_f32 with the hub id list) once per
+ * call, and the column array is the graph's hub-remapped copy col_hub: a
+ * hub column c with rank k is stored as -1-k, every other column as itself.
+ * Hub gathers then hit a few MiB-GiB of contiguous rows instead of rows spread
+ * over the whole of X (address-translation reach and Infinity Cache locality).
+ * small_col keeps the unremapped ids. Results equal gnn_spmm_csr_f32's.
+ * Replaces the same call site: GCN/GCN.py:43-45.
+ */
+int gnn_spmm_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub, const float* val,
+                         int64_t n_rows, const float* x, int64_t ldx, const float* xh,
+                         int64_t ldh, int64_t feat, const float* bias, float* y, int64_t ldy,
+                         int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin,
+                         int64_t n_seg, const int32_t* long_row, const int32_t* long_seg_ptr,
+                         int64_t n_long, const int32_t* small_row, const int32_t* small_col,
+                         const float* small_val, int64_t n_small, const int32_t* mid_row,
+                         int64_t n_mid, float* partial, uint32_t flags, void* stream);
+
+/*
  * Row-class plan for gnn_spmm_csr_f32 / gnn_gat_csr_f32 (built once per graph).
  *
  * gnn_spmm_plan_count: classifies the rows and writes four int64 counters into

@@ -232,7 +232,9 @@ def test_rmat_1m_parity_vs_c_oracle(dev):
     assert g.nnz == 20_073_500
     F = 128
     X = torch.randn(n, F, generator=torch.Generator().manual_seed(0)).to(dev)
-    Y = spmm_forward(g, X).cpu().numpy()
+    Yd = spmm_forward(g, X)  # X is 512 MB: the default path stages hub rows
+    assert torch.equal(Yd, spmm_forward(g, X, hubs=0))
+    Y = Yd.cpu().numpy()
     rowptr, col, val = g.rowptr.cpu().numpy(), g.col.cpu().numpy(), g.val.cpu().numpy()
     deg = np.diff(rowptr)
     rows = np.unique(np.concatenate([np.random.default_rng(0).choice(n, 4000, replace=False),
@@ -244,3 +246,48 @@ def test_rmat_1m_parity_vs_c_oracle(dev):
     colsum_a = np.bincount(col, weights=val.astype(np.float64), minlength=n)
     np.testing.assert_allclose(Y.astype(np.float64).sum(0), colsum_a @ Xn.astype(np.float64),
                                rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("F", [3, 64, 128, 256, 600])
+def test_hub_staging_bitexact(dev, F):
+    """gnn_spmm_csr_hub_f32: staging the hottest rows of X into a compact table changes no
+    bit of Y (same edge order; the gathered values are copies) for any hub count, with
+    bias / activation / accumulate epilogues, long-row segments and strided X."""
+    from graphneuralnetwork_amd.ops import spmm_forward
+    n = 900
+    rowptr, col, val = _rand_graph(n, 12 * n, 40 + F, hub_deg=4000)
+    g = _graph(rowptr, col, val, n, dev)
+    Xw = torch.randn(n, F + 5, device=dev)
+    for X in (Xw[:, :F].contiguous(), Xw[:, 1:F + 1]):   # vector path and strided/misaligned
+        b = torch.randn(F, device=dev)
+        base = torch.randn(n, F, device=dev)
+        for seg_len in (None, 16):
+            ref = spmm_forward(g, X, b, activation="relu", seg_len=seg_len, hubs=0)
+            acc_ref = spmm_forward(g, X, None, out=base.clone(), accumulate=True, seg_len=seg_len,
+                                   hubs=0)
+            for k in (1, 17, 300, n):
+                y = spmm_forward(g, X, b, activation="relu", seg_len=seg_len, hubs=k)
+                assert torch.equal(y, ref), (F, seg_len, k)
+                y = spmm_forward(g, X, None, out=base.clone(), accumulate=True, seg_len=seg_len,
+                                 hubs=k)
+                assert torch.equal(y, acc_ref), (F, seg_len, k, "accumulate")
+    close(ref.cpu().numpy(), np.maximum(O.spmm_csr(rowptr, col, val, X.cpu().numpy(),
+                                                   b.cpu().numpy()), 0))
+
+
+def test_hub_plan_structure(dev):
+    """col_hub decodes back to col; the hub set is the k highest column degrees."""
+    n = 3000
+    rowptr, col, val = _rand_graph(n, 20 * n, 77, hub_deg=9000)
+    g = _graph(rowptr, col, val, n, dev)
+    k = 123
+    hp = g.hub_plan(k)
+    ch = hp.col_hub.cpu().numpy().astype(np.int64)
+    hub = hp.hub_ids.cpu().numpy()
+    assert hp.k == k and len(np.unique(hub)) == k
+    dec = np.where(ch < 0, hub[np.clip(-1 - ch, 0, k - 1)], ch)
+    np.testing.assert_array_equal(dec, col)
+    assert ((ch < 0) == np.isin(col, hub)).all()
+    deg = np.bincount(col, minlength=n)
+    assert deg[hub].min() >= np.delete(deg, hub).max()
+    assert (np.diff(deg[hub]) <= 0).all()  # hottest first

@@ -1,3 +1,4 @@
-bash tools/gpu_check.sh prof pmc && \
-BENCH_ARGS="--workload ns" OUT=gpurun_out/ns bash tools/gpu_check.sh pmc && \
-bash tools/gpu_check.sh bench_ns bench_sage
+K="hub or spmm" bash tools/gpu_check.sh testsk && \
+PTAG=_cfg2 BENCH_ARGS="--no-layer --no-cpu-reference" bash tools/gpu_check.sh prof pmc && \
+PTAG=_ns BENCH_ARGS="--workload ns --no-layer --no-cpu-reference" bash tools/gpu_check.sh prof pmc && \
+bash tools/gpu_check.sh bench bench_ns
