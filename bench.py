@@ -319,6 +319,8 @@ def run_gat(args, dev):
     layer_ms, wall = time_steps(layer, args.steps, args.warmup, dev)
     agg_ms = {m: time_steps(f, args.steps, args.warmup, dev)[0] for m, f in agg.items()}
     nnz, n = g.nnz, g.n_rows
+    from graphneuralnetwork_amd.ops import hub_rows_for
+    hub_k = hub_rows_for(g.n_cols, H * Fh + H)
     bytes_agg = nnz * (4 + 4 * H + 4 * H * Fh) + n * (8 + 4 * H + 4 * H * Fh)
     k_ms = statistics.mean(agg_ms[GAT_DENSE])
     achieved = bytes_agg / (k_ms / 1e3) / 1e9
@@ -334,7 +336,9 @@ def run_gat(args, dev):
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                         "traffic_source": tsrc,
-                        "kernel": "gat_csr_kernel<dense> + gat_short_kernel + gat_fixup_kernel",
+                        "kernel": ("gather_rows_kernel x2 (hub staging: Wh / er rows of the %d "
+                                   "highest-degree columns) + " % hub_k if hub_k else "") +
+                                  "gat_csr_kernel<dense> + gat_short_kernel + gat_fixup_kernel",
                         "algorithmic_bytes_per_launch": bytes_agg, "avg_launch_ms": k_ms}}
     if not args.no_cpu_baseline:
         from oracle import gnn_oracle as O

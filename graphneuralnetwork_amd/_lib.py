@@ -68,6 +68,20 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _i64, _vp, _i64,           # mid_row, n_mid, short_row, n_short
         _vp, _vp,                       # partial, stats
         _u32, _vp]),                    # flags, stream
+    "gnn_gat_csr_hub_f32": (ctypes.c_int, [
+        _vp, _vp, _i64,                 # rowptr, col_hub, n_rows
+        _vp, _i64, _i64, _i64,          # wh, ldw, heads, fh
+        _vp, _vp, _i64,                 # el, er, lde
+        ctypes.c_float, _i32, _vp,      # negative_slope, mode, empty_row_fill
+        ctypes.c_float, ctypes.c_uint64,  # dropout_p, dropout_seed
+        _vp, _i64,                      # out, ldo
+        _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
+        _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
+        _vp, _vp, _i64,                 # small_row, small_col, n_small
+        _vp, _i64, _vp, _i64,           # mid_row, n_mid, short_row, n_short
+        _vp, _vp,                       # partial, stats
+        _u32, _vp,                      # flags, stream
+        _vp, _i64, _vp, _i64]),         # whh, ldwh, erh, ldeh
     "gnn_gat_backward_prep_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp,
                                                  _vp]),
     "gnn_gat_backward_edges_f32": (ctypes.c_int, [

@@ -100,7 +100,24 @@ struct GatParams {
   uint32_t flags;
   float* stats;    // optional [n_rows, lds]: per-head log-sum-exp of the row (backward)
   int64_t lds;
+  // hub staging (gnn_gat_csr_hub_f32): a column id c < 0 names row -1-c of the staged
+  // tables whh [K, ldwh] / erh [K, ldeh] (the highest-degree columns' Wh and er rows)
+  const float* whh;
+  int64_t ldwh;
+  const float* erh;
+  int64_t ldeh;
 };
+
+// Wh row / er entry of column c (hub-staged when c < 0). Without staging no column id is
+// negative and the select never picks the hub tables.
+__device__ __forceinline__ const float* wh_row(const GatParams& P, int c) {
+  return c < 0 ? P.whh + static_cast<int64_t>(-1 - c) * P.ldwh
+               : P.wh + static_cast<int64_t>(c) * P.ldw;
+}
+__device__ __forceinline__ float er_at(const GatParams& P, int c, int h) {
+  return c < 0 ? P.erh[static_cast<int64_t>(-1 - c) * P.ldeh + h]
+               : P.er[static_cast<int64_t>(c) * P.lde + h];
+}
 
 constexpr int kGatSmallUnroll = 4;
 #ifndef GNN_GAT_U
@@ -219,11 +236,11 @@ __device__ __forceinline__ void gat_short_rows(const GatParams& P, int64_t wave,
     for (int e = 0; e < K; ++e) {
       z[e] = -INFINITY;
       if (e < n) {
-        const float sv = eli + P.er[static_cast<int64_t>(c[e]) * P.lde + h];
+        const float sv = eli + er_at(P, c[e], h);
         const float x = sv > 0.f ? sv : P.slope * sv;
         z[e] = SPARSE ? -x : x;
       }
-      xv[e] = e < n ? vload<VW>(P.wh + static_cast<int64_t>(c[e]) * P.ldw + f) : vzero<VW>();
+      xv[e] = e < n ? vload<VW>(wh_row(P, c[e]) + f) : vzero<VW>();
     }
     if (!SPARSE) {
       float cm = z[0];
@@ -338,7 +355,7 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
       const bool live = j * EPP + ae < np && head_ok;
       zj[j] = -INFINITY;
       if (live) {
-        const float sv = eli + P.er[static_cast<int64_t>(cj[j]) * P.lde + ah];
+        const float sv = eli + er_at(P, cj[j], ah);
         const float x = sv > 0.f ? sv : P.slope * sv;
         zj[j] = SPARSE ? -x : x;
       }
@@ -386,7 +403,7 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
         for (int jj = 1; jj < J; ++jj)
           if (jj == j) { cv = cj[jj]; pv = pj[jj]; }
         const int ce = __shfl(cv, es, kWave);
-        const float* xr = P.wh + static_cast<int64_t>(ce) * P.ldw;
+        const float* xr = wh_row(P, ce);
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
           const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
@@ -756,17 +773,18 @@ extern "C" int gnn_col_mean_f32(const float* x, int64_t ldx, int64_t n_rows, int
   return launch_status();
 }
 
-extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
-                               const float* wh, int64_t ldw, int64_t heads, int64_t fh,
-                               const float* el, const float* er, int64_t lde, float negative_slope,
-                               int32_t mode, const float* empty_row_fill, float dropout_p,
-                               uint64_t dropout_seed, float* out, int64_t ldo, int64_t seg_len,
-                               const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
-                               const int32_t* long_row, const int32_t* long_seg_ptr,
-                               int64_t n_long, const int32_t* small_row, const int32_t* small_col,
-                               int64_t n_small, const int32_t* mid_row, int64_t n_mid,
-                               const int32_t* short_row, int64_t n_short,
-                               float* partial, float* stats, uint32_t flags, void* stream) {
+static int gat_entry(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                     const float* wh, int64_t ldw, int64_t heads, int64_t fh,
+                     const float* el, const float* er, int64_t lde, float negative_slope,
+                     int32_t mode, const float* empty_row_fill, float dropout_p,
+                     uint64_t dropout_seed, float* out, int64_t ldo, int64_t seg_len,
+                     const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
+                     const int32_t* long_row, const int32_t* long_seg_ptr,
+                     int64_t n_long, const int32_t* small_row, const int32_t* small_col,
+                     int64_t n_small, const int32_t* mid_row, int64_t n_mid,
+                     const int32_t* short_row, int64_t n_short,
+                     float* partial, float* stats, uint32_t flags, void* stream,
+                     const float* whh, int64_t ldwh, const float* erh, int64_t ldeh) {
   if (n_rows < 0 || heads < 1 || fh < 1 || seg_len < 1 || n_seg < 0 || n_long < 0 || n_small < 0)
     return GNN_E_ARG;
   const bool plan = mid_row != nullptr;
@@ -785,6 +803,8 @@ extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_
   if ((n_seg > 0 || n_long > 0) &&
       (!seg_row || !seg_begin || !long_row || !long_seg_ptr || !partial || n_seg == 0 || n_long == 0))
     return GNN_E_ARG;
+  if ((whh == nullptr) != (erh == nullptr)) return GNN_E_ARG;
+  if (whh && (ldwh < feat_all || ldeh < heads)) return GNN_E_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   // partial row layout per segment: [heads*fh acc | heads l | heads m] of the WHOLE layer;
   // each head group writes its own slice (the host allocates ldp = heads*fh + 2*heads).
@@ -833,7 +853,12 @@ extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_
     P.flags = flags;
     P.stats = stats ? stats + h0 : nullptr;
     P.lds = heads;
+    P.whh = whh ? whh + h0 * fh : nullptr;
+    P.ldwh = ldwh;
+    P.erh = erh ? erh + h0 : nullptr;
+    P.ldeh = ldeh;
     const bool vec4 = (fh % 4 == 0) && (ldw % 4 == 0) && (ldo % 4 == 0) && aligned_to(P.wh, 16) &&
+                      (P.whh == nullptr || (aligned_to(P.whh, 16) && ldwh % 4 == 0)) &&
                       aligned_to(P.out, 16) &&
                       (P.empty_fill == nullptr || aligned_to(P.empty_fill, 16)) &&
                       (P.partial == nullptr || (aligned_to(P.partial, 16) && ldp % 4 == 0));
@@ -845,4 +870,45 @@ extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_
     if (rc != GNN_OK) return rc;
   }
   return GNN_OK;
+}
+
+extern "C" int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                               const float* wh, int64_t ldw, int64_t heads, int64_t fh,
+                               const float* el, const float* er, int64_t lde, float negative_slope,
+                               int32_t mode, const float* empty_row_fill, float dropout_p,
+                               uint64_t dropout_seed, float* out, int64_t ldo, int64_t seg_len,
+                               const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
+                               const int32_t* long_row, const int32_t* long_seg_ptr,
+                               int64_t n_long, const int32_t* small_row, const int32_t* small_col,
+                               int64_t n_small, const int32_t* mid_row, int64_t n_mid,
+                               const int32_t* short_row, int64_t n_short,
+                               float* partial, float* stats, uint32_t flags, void* stream) {
+  return gat_entry(rowptr, col, n_rows, wh, ldw, heads, fh, el, er, lde, negative_slope, mode,
+                   empty_row_fill, dropout_p, dropout_seed, out, ldo, seg_len, seg_row, seg_begin,
+                   n_seg, long_row, long_seg_ptr, n_long, small_row, small_col, n_small, mid_row,
+                   n_mid, short_row, n_short, partial, stats, flags, stream, nullptr, 0, nullptr,
+                   0);
+}
+
+extern "C" int gnn_gat_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub, int64_t n_rows,
+                                   const float* wh, int64_t ldw, int64_t heads, int64_t fh,
+                                   const float* el, const float* er, int64_t lde,
+                                   float negative_slope, int32_t mode,
+                                   const float* empty_row_fill, float dropout_p,
+                                   uint64_t dropout_seed, float* out, int64_t ldo,
+                                   int64_t seg_len, const int32_t* seg_row,
+                                   const int64_t* seg_begin, int64_t n_seg,
+                                   const int32_t* long_row, const int32_t* long_seg_ptr,
+                                   int64_t n_long, const int32_t* small_row,
+                                   const int32_t* small_col, int64_t n_small,
+                                   const int32_t* mid_row, int64_t n_mid,
+                                   const int32_t* short_row, int64_t n_short, float* partial,
+                                   float* stats, uint32_t flags, void* stream, const float* whh,
+                                   int64_t ldwh, const float* erh, int64_t ldeh) {
+  if (whh == nullptr || erh == nullptr) return GNN_E_ARG;
+  return gat_entry(rowptr, col_hub, n_rows, wh, ldw, heads, fh, el, er, lde, negative_slope,
+                   mode, empty_row_fill, dropout_p, dropout_seed, out, ldo, seg_len, seg_row,
+                   seg_begin, n_seg, long_row, long_seg_ptr, n_long, small_row, small_col,
+                   n_small, mid_row, n_mid, short_row, n_short, partial, stats, flags, stream,
+                   whh, ldwh, erh, ldeh);
 }

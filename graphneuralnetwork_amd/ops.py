@@ -31,17 +31,25 @@ def _rows_f32(x: torch.Tensor, name: str) -> torch.Tensor:
     return x
 
 
-# Hub staging (gnn_spmm_csr_hub_f32): when X is too large to stay in the Infinity Cache,
-# the HUB_BYTES of its highest-degree rows are copied into one compact table per call.
-HUB_MIN_X_BYTES = 256 << 20
+# Hub staging (gnn_spmm_csr_hub_f32 / gnn_gat_csr_hub_f32): when the gathered table is
+# too large to stay in the Infinity Cache, its highest-degree rows (at most HUB_ROWS rows,
+# at most HUB_BYTES) are copied into one compact table per call. A/B on MI355X
+# (tools/hub_ab.py, profiles/r01f_hub_ab_*.log): SpMM 10M/207M F=128 20.9 -> 14.4 ms
+# (best 64-128 Ki rows), F=256 40.0 -> 30.0 ms (flat 32-128 Ki rows); 1M/20M F=128
+# 1.57 -> 1.16 ms (flat 8-128 Ki rows), F=64 0.71 -> 0.59 ms (best 64 Ki rows); GAT
+# 8x8 heads on 1M/20M 1.00 -> 0.94-0.95 ms (best 16-64 Ki rows); a 128 MB table (F=32)
+# gains ~1 % and a 64 MB one (F=16) loses ~2 %, hence the size threshold.
+HUB_MIN_X_BYTES = 192 << 20
 HUB_BYTES = 64 << 20
+HUB_ROWS = 131072
 
 
 def hub_rows_for(n_cols: int, feat: int) -> int:
-    """Default number of staged hub rows for an X of n_cols x feat fp32 (0 = no staging)."""
+    """Default number of staged hub rows for a gathered table of n_cols x feat fp32
+    (0 = no staging)."""
     if n_cols * 4 * feat < HUB_MIN_X_BYTES:
         return 0
-    return min(n_cols, max(1, HUB_BYTES // (4 * feat)))
+    return min(n_cols, HUB_ROWS, max(1, HUB_BYTES // (4 * feat)))
 
 
 def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
@@ -204,8 +212,11 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
                   fh: int, negative_slope: float, mode: int, activation: str | None = None,
                   dropout_p: float = 0.0, seed: int = 0, seg_len: int | None = None,
                   out: torch.Tensor | None = None,
-                  stats: torch.Tensor | None = None) -> torch.Tensor:
-    """Fused edge-softmax + neighbour aggregation for all heads (one HIP launch + fix-up)."""
+                  stats: torch.Tensor | None = None, hubs: int | None = None) -> torch.Tensor:
+    """Fused edge-softmax + neighbour aggregation for all heads (one HIP launch + fix-up).
+
+    ``hubs``: Wh / er rows of the highest-degree columns staged into compact tables first
+    (gnn_gat_csr_hub_f32; 0 = none, default ``hub_rows_for``); same output bits."""
     _require_device(g.rowptr, wh, el, er, out)
     wh = _rows_f32(wh, "Wh")
     n = g.n_rows
@@ -232,14 +243,28 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
     pa = plan.args()  # (seg_row, seg_begin, n_seg, long_row, long_seg_ptr, n_long,
     #                    small_row, small_col, small_val, n_small, mid_row, n_mid)
     mid, short = plan.gat_split(g.rowptr, GAT_SHORT_MAX_DEG)
-    rc = lib.gnn_gat_csr_f32(
-        g.rowptr.data_ptr(), g.col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
-        el.data_ptr(), er.data_ptr(), heads, float(negative_slope), int(mode), _lib.ptr(fill),
-        float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), out.stride(0),
-        plan.seg_len, *pa[:6], pa[6], pa[7], pa[9],
-        mid.data_ptr() if mid.numel() else pa[10], mid.numel(),
-        short.data_ptr() if short.numel() else None, short.numel(), _lib.ptr(partial),
-        _lib.ptr(stats), _ACT_FLAGS[activation], _lib.stream_handle(wh.device))
+    stream = _lib.stream_handle(wh.device)
+    args = (n, wh.data_ptr(), wh.stride(0), heads, fh,
+            el.data_ptr(), er.data_ptr(), heads, float(negative_slope), int(mode), _lib.ptr(fill),
+            float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), out.stride(0),
+            plan.seg_len, *pa[:6], pa[6], pa[7], pa[9],
+            mid.data_ptr() if mid.numel() else pa[10], mid.numel(),
+            short.data_ptr() if short.numel() else None, short.numel(), _lib.ptr(partial),
+            _lib.ptr(stats), _ACT_FLAGS[activation], stream)
+    k = hub_rows_for(g.n_cols, feat + heads) if hubs is None else min(int(hubs), g.n_cols)
+    if k > 0 and g.nnz:
+        hp = g.hub_plan(k)
+        whh = torch.empty((hp.k, feat), dtype=torch.float32, device=wh.device)
+        erh = torch.empty((hp.k, heads), dtype=torch.float32, device=wh.device)
+        for src, dst, w in ((wh, whh, feat), (er, erh, heads)):
+            _lib.check(lib.gnn_gather_rows_f32(src.data_ptr(), src.stride(0), src.shape[0],
+                                               hp.hub_ids.data_ptr(), hp.k, w, dst.data_ptr(), w,
+                                               hp.err.data_ptr(), stream), "gnn_gather_rows_f32")
+        rc = lib.gnn_gat_csr_hub_f32(g.rowptr.data_ptr(), hp.col_hub.data_ptr(), *args,
+                                     whh.data_ptr(), feat, erh.data_ptr(), heads)
+        _lib.check(rc, "gnn_gat_csr_hub_f32")
+        return out
+    rc = lib.gnn_gat_csr_f32(g.rowptr.data_ptr(), g.col.data_ptr(), *args)
     _lib.check(rc, "gnn_gat_csr_f32")
     return out
 

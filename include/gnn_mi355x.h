@@ -184,6 +184,25 @@ int gnn_gat_csr_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows, c
                     float* stats, uint32_t flags, void* stream);
 
 /*
+ * gnn_gat_csr_f32 with hub staging (same outputs, bit for bit): col_hub is the graph's
+ * hub-remapped column array (hub column of rank k stored as -1-k, as for
+ * gnn_spmm_csr_hub_f32) and whh [K, ldwh] / erh [K, ldeh] hold the Wh rows and er
+ * entries of the K hub columns, copied by the caller (gnn_gather_rows_f32) per call.
+ * small_col keeps the unremapped ids. Replaces the same call sites as gnn_gat_csr_f32.
+ */
+int gnn_gat_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub, int64_t n_rows,
+                        const float* wh, int64_t ldw, int64_t heads, int64_t fh, const float* el,
+                        const float* er, int64_t lde, float negative_slope, int32_t mode,
+                        const float* empty_row_fill, float dropout_p, uint64_t dropout_seed,
+                        float* out, int64_t ldo, int64_t seg_len, const int32_t* seg_row,
+                        const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
+                        const int32_t* long_seg_ptr, int64_t n_long, const int32_t* small_row,
+                        const int32_t* small_col, int64_t n_small, const int32_t* mid_row,
+                        int64_t n_mid, const int32_t* short_row, int64_t n_short, float* partial,
+                        float* stats, uint32_t flags, void* stream, const float* whh,
+                        int64_t ldwh, const float* erh, int64_t ldeh);
+
+/*
  * Column mean of x[n_rows, feat] (double accumulation, deterministic): the dense
  * GAT layer's output for an edgeless row (uniform softmax over all N nodes,
  * GAT/models/layers.py:29-32). scratch: gnn_col_mean_scratch_bytes(n_rows, feat).

@@ -115,6 +115,34 @@ def test_gat_aggregate_vs_oracle(dev, heads, fh, sparse, seg_len):
     close(out, ref)
 
 
+@pytest.mark.parametrize("heads,fh", [(8, 8), (3, 5), (12, 4)])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gat_hub_staging_bitexact(dev, heads, fh, sparse):
+    """gnn_gat_csr_hub_f32 (staged Wh / er rows of the hub columns) reproduces the unstaged
+    kernel bit for bit: outputs, log-sum-exp stats and dropout masks, in every row class
+    (small, short, mid, long-row segments) and head group (12 heads = two launches)."""
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.ops import GAT_DENSE, GAT_SPARSE, gat_aggregate
+    n = 2000
+    rowptr, col = _rand_csr(n, 6 * n, heads + fh, hub=1500)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.ones(col.size, device=dev), n, n)
+    wh = torch.randn(n, heads * fh, device=dev) * 0.5
+    el, er = torch.randn(n, heads, device=dev), torch.randn(n, heads, device=dev)
+    mode = GAT_SPARSE if sparse else GAT_DENSE
+    for seg_len, p in ((None, 0.0), (24, 0.0), (24, 0.4)):
+        st0 = torch.empty(n, heads, device=dev)
+        ref = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, activation="elu", seg_len=seg_len,
+                            dropout_p=p, seed=5, stats=st0, hubs=0)
+        for k in (1, 50, n):
+            st = torch.empty(n, heads, device=dev)
+            out = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, activation="elu",
+                                seg_len=seg_len, dropout_p=p, seed=5, stats=st, hubs=k)
+            assert torch.equal(out, ref) or (torch.isnan(ref).any() and torch.equal(
+                torch.nan_to_num(out, 1.5), torch.nan_to_num(ref, 1.5))), (seg_len, p, k)
+            assert torch.equal(torch.nan_to_num(st, 1.5), torch.nan_to_num(st0, 1.5))
+
+
 @pytest.mark.parametrize("heads,fh,ld,off", [(8, 8, 80, 0), (8, 8, 67, 0), (4, 16, 64, 1),
                                               (3, 12, 40, 4)])
 def test_gat_logits_strided_and_unaligned(dev, heads, fh, ld, off):

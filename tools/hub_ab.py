@@ -1,6 +1,9 @@
 """Interleaved A/B of the SpMM hub-staging size (ops.spmm_forward(hubs=K)) at one shape.
 
-    python tools/hub_ab.py [--workload cfg2|ns] [--feat 128] [--ks 0,16384,65536,...]
+    python tools/hub_ab.py [--workload cfg2|ns] [--feat 128] [--ks 0,16384,65536,...] [--op spmm|gat]
+
+--op gat: the GAT aggregation (ops.gat_aggregate, dense softmax + ELU, 8 heads x feat/8)
+with staged Wh and er rows.
 
 K = 0 is the unstaged kernel; every K must give bit-identical output (same edge order,
 the gathered values are copies). Times include the per-call hub-row copy.
@@ -22,9 +25,10 @@ def main():
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--ks", default="0,16384,32768,65536,131072,262144,1048576")
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--op", default="spmm", choices=["spmm", "gat"])
     args = ap.parse_args()
     from graphneuralnetwork_amd import _lib
-    from graphneuralnetwork_amd.ops import spmm_forward
+    from graphneuralnetwork_amd.ops import gat_aggregate, spmm_forward
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     from graphneuralnetwork_amd.rmat import rmat_edges
     _lib.load()
@@ -37,15 +41,23 @@ def main():
     X = torch.randn(n, F, device=dev)
     b = torch.randn(F, device=dev)
     Y = torch.empty(n, F, device=dev)
-    ref = spmm_forward(g, X, b, hubs=0).clone()
     nbytes = g.nnz * (8 + 4 * F) + n * (8 + 4 * F)
+    if args.op == "gat":
+        H = 8
+        el, er = torch.randn(n, H, device=dev), torch.randn(n, H, device=dev)
+        nbytes = g.nnz * (4 + 4 * H + 4 * F) + n * (8 + 4 * H + 4 * F)
+
+        def spmm_forward(g, X, b, out, hubs):  # noqa: F811 -- same harness, GAT op
+            return gat_aggregate(g, X, el, er, H, F // H, 0.2, 0, activation="elu", out=out,
+                                 hubs=hubs)
+    ref = spmm_forward(g, X, b, out=torch.empty_like(Y), hubs=0).clone()
     stream = torch.cuda.current_stream(dev)
     ks = [int(k) for k in args.ks.split(",")]
     for k in ks:
         spmm_forward(g, X, b, out=Y, hubs=k)
         torch.cuda.synchronize()
         assert torch.equal(Y, ref), f"hubs={k}: output differs from the unstaged kernel"
-    print(json.dumps({"workload": args.workload, "feat": F, "nnz": g.nnz, "bitexact": True}),
+    print(json.dumps({"op": args.op, "workload": args.workload, "feat": F, "nnz": g.nnz, "bitexact": True}),
           flush=True)
     times = {k: [] for k in ks}
     for _ in range(args.rounds):
