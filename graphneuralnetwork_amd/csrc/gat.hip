@@ -123,6 +123,9 @@ constexpr int kGatSmallUnroll = 4;
 #ifndef GNN_GAT_U
 #define GNN_GAT_U 2  // feature-row gathers in flight per lane in phase B (A/B: tools/gat_ab.py)
 #endif
+#ifndef GNN_GAT_PIPE
+#define GNN_GAT_PIPE 1  // pipelined chunk loop in gat_csr_kernel (A/B: tools/gat_ab.py)
+#endif
 #ifndef GNN_GAT_CHUNK
 #define GNN_GAT_CHUNK 8  // edges per phase-A chunk (A/B at cfg3 with the short-row path: 8 > 16 > 32 > 64)
 #endif
@@ -337,6 +340,62 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
     acc[ch] = vzero<VW>();
   }
 
+  constexpr int CE = (C + EPI - 1) / EPI;  // gather slots per chunk
+  if constexpr (GNN_GAT_PIPE && J == 1 && NCH == 1 && CE <= 4) {
+    // Pipelined chunk loop: the next chunk's column ids are loaded while this chunk is
+    // processed, and this chunk's er entries and Wh rows are issued together, before the
+    // softmax arithmetic -- one memory round trip per chunk instead of col -> er -> Wh.
+    // Same arithmetic in the same order as the loop below (bit-identical results).
+    int c_next = ae < end - beg ? P.col[beg + ae] : 0;
+    for (int64_t b = beg; b < end; b += C) {
+      const int np = static_cast<int>(min(static_cast<int64_t>(C), end - b));
+      const int cj = c_next;
+      if (b + C < end) c_next = b + C + ae < end ? P.col[b + C + ae] : 0;
+      const bool live = ae < np && head_ok;
+      const float erv = live ? er_at(P, cj, ah) : 0.f;
+      const int64_t f0 = static_cast<int64_t>(sub) * VW;
+      typename Vec<VW>::T xv[CE];
+#pragma unroll
+      for (int q = 0; q < CE; ++q) {
+        const int e = q * EPI + grp;
+        const int ce = __shfl(cj, (e < EPP ? e : 0) * HP, kWave);
+        xv[q] = (e < np && f0 < P.feat) ? vload<VW>(wh_row(P, ce) + f0) : vzero<VW>();
+      }
+      float z = -INFINITY;
+      if (live) {
+        const float sv = eli + erv;
+        const float x = sv > 0.f ? sv : P.slope * sv;
+        z = SPARSE ? -x : x;
+      }
+      float pv;
+      if (!SPARSE) {
+        float pm = z;
+#pragma unroll
+        for (int o = HP; o < kWave; o <<= 1) pm = fmaxf(pm, __shfl_xor(pm, o, kWave));
+        const float mn = fmaxf(m, pm);
+        const float scale = __expf(m - mn);  // 0 on the first chunk (m = -inf)
+        m = mn;
+        pv = z == -INFINITY ? 0.f : __expf(z - mn);
+        lsum = lsum * scale + pv;
+        acc[0] *= __shfl(scale, hid[0], kWave);
+      } else {
+        pv = z == -INFINITY ? 0.f : expf(z);  // exp(-LeakyReLU), no max subtraction
+        lsum += pv;
+      }
+#pragma unroll
+      for (int q = 0; q < CE; ++q) {
+        const int e = q * EPI + grp;
+        const bool ok = e < np && f0 < P.feat;
+        float wv = __shfl(pv, (e < EPP ? e : 0) * HP + hid[0], kWave);
+        if (P.drop_p > 0.f && ok) {
+          const uint32_t r = hash3(P.drop_seed, b + e, P.head0 + hid[0]);
+          wv = (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f
+                                                                               : wv * P.drop_scale;
+        }
+        acc[0] += (ok ? wv : 0.f) * xv[q];
+      }
+    }
+  } else
   // A chunk is J phase-A passes (C = J * EPP edges): every lane issues its J column
   // and J er loads at once, then the whole chunk's feature rows are gathered in
   // C / EPI slots -- one dependent round trip per chunk instead of per pass.

@@ -20,6 +20,8 @@ VARIANTS = {
     "c16u2": ["GNN_GAT_CHUNK=16", "GNN_GAT_U=2"],
     "c16u2w8": ["GNN_GAT_CHUNK=16", "GNN_GAT_U=2", "GNN_GAT_WAVES_PER_EU=8"],
     "c8u2": ["GNN_GAT_CHUNK=8", "GNN_GAT_U=2"],
+    "nopipe": ["GNN_GAT_PIPE=0"],
+    "pipe": ["GNN_GAT_PIPE=1"],
 }
 
 
