@@ -628,6 +628,10 @@ def main():
                                     "per-step HIP events" % (HUB_INFO["hub_rows"],
                                                              HUB_INFO["hub_rows"] * 4 * F / 2**20))
                          if HUB_INFO.get("hub_rows") else
+                         ("EdgeCutSpmm step: send-side SpMM + 2 RCCL all-to-all-v (comm stream) "
+                          "overlapping the interior SpMM (hub-staged when its X is >= 192 MiB), "
+                          "then the halo SpMMs; per-step HIP events, max over ranks")
+                         if world > 1 else
                          "spmm_csr_kernel (+ spmm_fixup_kernel), per-step HIP events",
                          "algorithmic_bytes_per_launch": bytes_local,
                          "avg_launch_ms": kern_ms, "min_launch_ms": min(step_ms)},
