@@ -335,6 +335,7 @@ def run_gat(args, dev):
            "aggregate_ms": {"dense": k_ms, "sparse": statistics.mean(agg_ms[GAT_SPARSE])},
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                        "traffic_GBps": traffic / (k_ms / 1e3) / 1e9 if traffic else None,
                         "traffic_source": tsrc,
                         "kernel": ("gather_rows_kernel x2 (hub staging: Wh / er rows of the %d "
                                    "highest-degree columns) + " % hub_k if hub_k else "") +
@@ -620,6 +621,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic["traffic_bytes"] if traffic else None,
+                         # L2-miss bytes per second (Infinity Cache hits included): the rate the
+                         # memory side actually served; "achieved" counts algorithmic bytes
+                         "traffic_GBps": traffic["traffic_bytes"] / (kern_ms / 1e3) / 1e9
+                         if traffic else None,
                          "traffic_source": (str(tpath.relative_to(ROOT)) + ": rocprofv3 --pmc "
                                             "FETCH_SIZE x2 + WRITE_SIZE of this command")
                          if traffic else None,

@@ -47,6 +47,8 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _i64, _vp,                 # mid_row, n_mid, partial
         _u32, _vp]),                    # flags, stream
     "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
+    "gnn_hub_plan_workspace_bytes": (_i64, [_i64]),
+    "gnn_hub_plan_build": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "gnn_spmm_plan_count": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gnn_spmm_plan_fill": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _vp, _vp]),

@@ -233,20 +233,20 @@ def _build_plan(g: CsrGraph, seg_len: int) -> RowSplitPlan:
 
 
 def _build_hub_plan(g: CsrGraph, k: int) -> HubPlan:
-    """Column in-degrees -> the k hottest columns (ties: lower id first, torch.topk order
-    is not relied on for results: any hub set gives the same sums, only the speed)."""
+    """The k hottest columns (in-degree descending, ties by ascending id) and the renamed
+    column array, built on the device by gnn_hub_plan_build (hub.hip)."""
+    lib = _lib.load()
     dev = g.device
-    k = max(0, min(int(k), g.n_cols))
-    col64 = g.col.to(torch.int64)
-    deg = torch.bincount(col64, minlength=g.n_cols)
-    hub_ids = torch.topk(deg, k, sorted=True).indices.contiguous() if k else \
-        torch.empty(0, dtype=torch.int64, device=dev)
-    rank = torch.full((g.n_cols,), -1, dtype=torch.int32, device=dev)
-    rank[hub_ids] = torch.arange(k, dtype=torch.int32, device=dev)
-    r = rank[col64]
-    del col64
-    col_hub = torch.where(r >= 0, -1 - r, g.col).contiguous()
-    return HubPlan(hub_ids, col_hub, torch.zeros(1, dtype=torch.int32, device=dev))
+    k = max(1, min(int(k), g.n_cols))
+    hub_ids = torch.empty(k, dtype=torch.int64, device=dev)
+    col_hub = torch.empty_like(g.col)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = torch.empty(int(lib.gnn_hub_plan_workspace_bytes(g.n_cols)), dtype=torch.uint8,
+                     device=dev)
+    _lib.check(lib.gnn_hub_plan_build(_lib.ptr(g.col), g.nnz, g.n_cols, k, hub_ids.data_ptr(),
+                                      _lib.ptr(col_hub), err.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), _lib.stream_handle(dev)), "gnn_hub_plan_build")
+    return HubPlan(hub_ids, col_hub, err)
 
 
 # ---------------------------------------------------------------- builders

@@ -101,6 +101,22 @@ int gnn_spmm_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub, const fl
                          int64_t n_mid, float* partial, uint32_t flags, void* stream);
 
 /*
+ * Hub-staging plan for gnn_spmm_csr_hub_f32 / gnn_gat_csr_hub_f32 (built once per graph
+ * and hub count k, 1 <= k <= n_cols):
+ *   hub_ids[r] (int64 [k]) = the column of in-degree rank r (degree descending, ties by
+ *                            ascending column id: deterministic);
+ *   col_hub[e] (int32 [nnz]) = -1 - rank(col[e]) for a hub column, col[e] otherwise.
+ * A column id outside [0, n_cols) sets *err_flag |= 1 (device int32) and is copied as is.
+ * workspace: gnn_hub_plan_workspace_bytes(n_cols) bytes of device memory.
+ * New in this library (the reference has no such plan); it serves GCN/GCN.py:43-45 and
+ * GAT/models/layers.py:22-37 / :94-131 through the two hub kernels.
+ */
+int64_t gnn_hub_plan_workspace_bytes(int64_t n_cols);
+int gnn_hub_plan_build(const int32_t* col, int64_t nnz, int64_t n_cols, int64_t k,
+                       int64_t* hub_ids, int32_t* col_hub, int32_t* err_flag, void* workspace,
+                       int64_t workspace_bytes, void* stream);
+
+/*
  * Row-class plan for gnn_spmm_csr_f32 / gnn_gat_csr_f32 (built once per graph).
  *
  * gnn_spmm_plan_count: classifies the rows and writes four int64 counters into

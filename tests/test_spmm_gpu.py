@@ -291,3 +291,6 @@ def test_hub_plan_structure(dev):
     deg = np.bincount(col, minlength=n)
     assert deg[hub].min() >= np.delete(deg, hub).max()
     assert (np.diff(deg[hub]) <= 0).all()  # hottest first
+    # deterministic: exactly the stable order (degree descending, ties by ascending id)
+    np.testing.assert_array_equal(hub, np.lexsort((np.arange(n), -deg))[:k])
+    assert int(hp.err.item()) == 0

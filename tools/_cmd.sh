@@ -1,4 +1,5 @@
-bash tools/gpu_check.sh tests && \
-PTAG=_cfg3 BENCH_ARGS="--workload cfg3" bash tools/gpu_check.sh prof pmc && \
-bash tools/gpu_check.sh bench_gat && \
-step_cfg5() { timeout -k 10 900 python bench.py --workload cfg5 --steps 10 --warmup 3 > gpurun_out/bench_cfg5.log 2>&1; } && step_cfg5 && tail -2 gpurun_out/bench_cfg5.log
+set -e
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider -k "hub or spmm or gat or distributed or fullsize" --timeout 300 --timeout-method thread > gpurun_out/pytest_hub.log 2>&1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+timeout -k 10 400 python -u bench.py --workload ns --no-cpu-baseline --no-layer > gpurun_out/bench_ns_quick.log 2>&1
