@@ -518,17 +518,19 @@ def main():
         from graphneuralnetwork_amd.ops import hub_rows_for
         HUB_INFO["hub_rows"] = hub_rows_for(g.n_cols, F)
     else:
-        from graphneuralnetwork_amd.distributed import (EdgeCutSpmm, build_cover_exchange,
+        from graphneuralnetwork_amd.distributed import (EdgeCutSpmm,
+                                                        build_cover_exchange_balanced,
                                                         build_partition, nnz_balanced_bounds)
         t0 = time.time()
-        bounds = nnz_balanced_bounds(g.rowptr, world)
         if args.exchange == "cover":
-            part = build_cover_exchange(g, rank, world, bounds=bounds)
+            # row blocks re-cut for the work the cover moves (cost model, 2 refinements)
+            part, hist = build_cover_exchange_balanced(g, rank, world)
+            BUILD_INFO["balance_max_mean_cost"] = hist
             work = (f"interior {part.interior.nnz}, partial {part.send_p.nnz}, halo "
                     f"{part.halo_x.nnz} + {part.halo_p.nnz}; "
                     f"recv {part.n_partial_recv} partial + {part.n_feature_recv} feature rows")
         else:
-            part = build_partition(g, rank, world, bounds=bounds)
+            part = build_partition(g, rank, world, bounds=nnz_balanced_bounds(g.rowptr, world))
             work = f"interior {part.interior.nnz}, halo {part.halo.nnz}"
         BUILD_INFO["partition_build_s"] = time.time() - t0
         X = torch.randn(part.n_own, F, device=dev, generator=gen)
@@ -617,7 +619,10 @@ def main():
             "achieved_GBps": achieved,
             "graph_build_s": BUILD_INFO.get("gcn_adjacency_build_s"),
             **({"gcn_layer_ms": layer_ms} if layer_ms is not None else {}),
-            **({"partition_build_s": BUILD_INFO.get("partition_build_s")} if world > 1 else {}),
+            **({"partition_build_s": BUILD_INFO.get("partition_build_s"),
+                "row_bounds": part.bounds,
+                "balance_max_mean_cost": BUILD_INFO.get("balance_max_mean_cost")}
+               if world > 1 else {}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic["traffic_bytes"] if traffic else None,

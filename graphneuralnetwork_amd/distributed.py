@@ -41,6 +41,28 @@ import torch.distributed as dist
 from .graph import CsrGraph, from_coo
 
 
+def weighted_bounds(rowptr: torch.Tensor, world: int, weights=None, old_bounds=None) -> torch.Tensor:
+    """Row boundaries [world+1] balancing  sum_i w_block(i) * (deg_i + 1)  per block, where
+    ``weights[b]`` is a cost density for the rows of block b of ``old_bounds`` (all 1.0:
+    plain edges + rows balance)."""
+    n = rowptr.numel() - 1
+    dev = rowptr.device
+    c = (rowptr[1:] - rowptr[:-1]).to(torch.float64) + 1.0
+    if weights is not None:
+        ob = torch.as_tensor(old_bounds, dtype=torch.int64, device=dev)
+        blk = torch.bucketize(torch.arange(n, device=dev), ob[1:-1], right=True)
+        c = c * torch.as_tensor(weights, dtype=torch.float64, device=dev)[blk]
+    cost = torch.zeros(n + 1, dtype=torch.float64, device=dev)
+    torch.cumsum(c, 0, out=cost[1:])
+    total = float(cost[-1])
+    targets = torch.tensor([total * k / world for k in range(world + 1)], dtype=torch.float64,
+                           device=dev)
+    b = torch.searchsorted(cost, targets).clamp_(0, n)
+    b[0] = 0
+    b[-1] = n
+    return torch.cummax(b, 0).values.to(torch.int64)
+
+
 def nnz_balanced_bounds(rowptr: torch.Tensor, world: int) -> torch.Tensor:
     """Row boundaries [world+1] so each block holds ~nnz/world stored edges (+ rows as a tiebreak)."""
     n = rowptr.numel() - 1
@@ -305,6 +327,73 @@ def build_cover_exchange(g: CsrGraph, rank: int, world: int, group=None,
                          halo_p, [t[0] for t in theirs_l], [t[1] for t in theirs_l],
                          [int(v) for v in nx.cpu().tolist()], [int(v) for v in np_.cpu().tolist()],
                          any_x, any_p)
+
+
+def _all_gather_floats(v: list, world: int, device, group=None) -> torch.Tensor:
+    """[world, len(v)] float64: every rank's ``v`` (an all-to-all-v of the same row)."""
+    on_dev = torch.device(device).type == "cuda" and dist.get_backend(group) != "gloo"
+    dev = device if on_dev else "cpu"
+    inp = torch.tensor(v, dtype=torch.float64, device=dev).repeat(world)
+    out = torch.empty(world * len(v), dtype=torch.float64, device=dev)
+    _all_to_all_v(out, inp, [len(v)] * world, [len(v)] * world, group)
+    return out.view(world, len(v)).cpu()
+
+
+# cost of a row of 4F bytes moved over xGMI (RCCL all-to-all) relative to HBM (one
+# gathered or written row): ~6 TB/s HBM vs ~0.4-0.5 TB/s of all-to-all per GPU, halved
+# because the interior SpMM overlaps the exchange
+XGMI_ROW_COST = 8.0
+
+
+def cover_cost(part: CoverExchange, alpha: float = XGMI_ROW_COST) -> float:
+    """Modelled per-aggregation cost of one rank, in units of one 4F-byte row through HBM:
+    edges gathered + rows written (read-modify-written by the accumulate passes, only the
+    rows with edges) + alpha x the rows this rank sends or receives, whichever is larger."""
+    def touched(g: CsrGraph) -> int:
+        return int(((g.rowptr[1:] - g.rowptr[:-1]) > 0).sum()) if g.n_rows else 0
+    n_sx, n_sp = sum(part.send_x_counts), sum(part.send_p_counts)
+    compute = (part.interior.nnz + part.n_own + part.send_p.nnz + n_sp + 2 * n_sx
+               + part.halo_x.nnz + 2 * touched(part.halo_x)
+               + part.halo_p.nnz + 2 * touched(part.halo_p))
+    exchange = max(n_sx + n_sp, sum(part.recv_counts))
+    return float(compute + alpha * exchange)
+
+
+def build_cover_exchange_balanced(g: CsrGraph, rank: int, world: int, group=None,
+                                  iters: int = 2, alpha: float = XGMI_ROW_COST):
+    """``build_cover_exchange`` with row blocks re-cut for the work the cover moves.
+
+    The cover shifts work between ranks (partial sums are computed by the column
+    owners; high-id R-MAT blocks hold millions of degree-1 rows), so edges + rows
+    balanced blocks end up far apart in cost (8 ranks: 0.8 vs 2.4 ms of compute,
+    173 vs 549 MB sent, tools/rank_sim.py). Each iteration gathers every rank's
+    ``cover_cost``, turns it into a cost density per block (cost / (edges + rows)) and
+    re-cuts with those densities; the partition with the lowest maximum cost is kept
+    (the same choice on every rank: they all see the same costs). Returns
+    (partition, per-iteration max/mean costs).
+    """
+    bounds = nnz_balanced_bounds(g.rowptr, world)
+    best, best_max, history = None, None, []
+    deg1 = (g.rowptr[1:] - g.rowptr[:-1]).to(torch.float64) + 1.0
+    for it in range(iters + 1):
+        part = build_cover_exchange(g, rank, world, group, bounds=bounds)
+        costs = _all_gather_floats([cover_cost(part, alpha)], world, g.device, group)[:, 0]
+        mx, mean = float(costs.max()), float(costs.mean())
+        history.append((mx, mean))
+        if best_max is None or mx < best_max:
+            best, best_max = part, mx
+        else:
+            del part
+        if it == iters:
+            break
+        b = [int(v) for v in bounds.cpu().tolist()]
+        cum = torch.zeros(deg1.numel() + 1, dtype=torch.float64, device=deg1.device)
+        torch.cumsum(deg1, 0, out=cum[1:])
+        units = torch.tensor([float(cum[b[k + 1]] - cum[b[k]]) for k in range(world)],
+                             dtype=torch.float64)
+        dens = (costs / units.clamp(min=1.0)).tolist()
+        bounds = weighted_bounds(g.rowptr, world, dens, b)
+    return best, history
 
 
 class EdgeCutSpmm:

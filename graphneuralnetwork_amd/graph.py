@@ -89,12 +89,27 @@ class RowSplitPlan:
                                   self.mid_row[short].contiguous())
         return cache[max_deg]
 
-    def args(self):
-        """The plan arguments of gnn_spmm_csr_f32 / gnn_gat_csr_f32 (after seg_len)."""
+    def nonempty_small(self):
+        """(small_row, small_col, small_val) without the edgeless rows (cached): an
+        accumulate pass with no bias and no activation leaves those rows unchanged, so it
+        need not read-modify-write them (the halo passes of the edge-cut SpMM, where most
+        owned rows have no halo edge)."""
+        if not hasattr(self, "_nonempty_small"):
+            keep = self.small_col >= 0
+            self._nonempty_small = (self.small_row[keep].contiguous(),
+                                    self.small_col[keep].contiguous(),
+                                    self.small_val[keep].contiguous())
+        return self._nonempty_small
+
+    def args(self, skip_empty: bool = False):
+        """The plan arguments of gnn_spmm_csr_f32 / gnn_gat_csr_f32 (after seg_len);
+        ``skip_empty`` drops the edgeless rows (see ``nonempty_small``)."""
         from ._lib import ptr
+        small_row, small_col, small_val = (self.nonempty_small() if skip_empty else
+                                           (self.small_row, self.small_col, self.small_val))
         return (ptr(self.seg_row), ptr(self.seg_begin), self.n_seg, ptr(self.long_row),
-                self.long_seg_ptr.data_ptr(), self.n_long, ptr(self.small_row),
-                ptr(self.small_col), ptr(self.small_val), self.n_small,
+                self.long_seg_ptr.data_ptr(), self.n_long, ptr(small_row),
+                ptr(small_col), ptr(small_val), int(small_row.numel()),
                 # mid_row must be non-NULL whenever a plan is used (NULL = "no plan")
                 self.mid_row.data_ptr() if self.n_mid else self.long_seg_ptr.data_ptr(),
                 self.n_mid)

@@ -93,6 +93,8 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
     lib = _lib.load()
     flags = _ACT_FLAGS[activation] | (_lib.EPI_ACCUMULATE if accumulate else 0)
     stream = _lib.stream_handle(x.device)
+    # out += A.X with no bias / activation: rows without edges stay as they are
+    pargs = plan.args(skip_empty=accumulate and bias is None and activation is None)
     k = hub_rows_for(g.n_cols, feat) if hubs is None else min(int(hubs), g.n_cols)
     if k > 0 and g.nnz:
         hp = g.hub_plan(k)
@@ -103,14 +105,13 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
         rc = lib.gnn_spmm_csr_hub_f32(
             g.rowptr.data_ptr(), hp.col_hub.data_ptr(), g.val.data_ptr(), g.n_rows,
             x.data_ptr(), x.stride(0), xh.data_ptr(), feat, feat, _lib.ptr(bias),
-            out.data_ptr(), out.stride(0), plan.seg_len, *plan.args(), _lib.ptr(partial), flags,
-            stream)
+            out.data_ptr(), out.stride(0), plan.seg_len, *pargs, _lib.ptr(partial), flags, stream)
         _lib.check(rc, "gnn_spmm_csr_hub_f32")
         return out
     rc = lib.gnn_spmm_csr_f32(
         g.rowptr.data_ptr(), g.col.data_ptr(), g.val.data_ptr(), g.n_rows,
         x.data_ptr(), x.stride(0), feat, _lib.ptr(bias), out.data_ptr(), out.stride(0),
-        plan.seg_len, *plan.args(), _lib.ptr(partial), flags, stream)
+        plan.seg_len, *pargs, _lib.ptr(partial), flags, stream)
     _lib.check(rc, "gnn_spmm_csr_f32")
     return out
 

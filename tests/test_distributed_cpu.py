@@ -69,10 +69,15 @@ def _worker(rank, world, port, n, F, q, kind="gather"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from graphneuralnetwork_amd.distributed import (EdgeCutSpmm, build_cover_exchange,
+                                                        build_cover_exchange_balanced,
                                                         build_partition)
         g = _graph(n, 3)
-        if kind == "cover":
-            part = build_cover_exchange(g, rank, world)
+        if kind in ("cover", "balanced"):
+            if kind == "cover":
+                part = build_cover_exchange(g, rank, world)
+            else:
+                part, hist = build_cover_exchange_balanced(g, rank, world)
+                assert len(hist) == 3 and min(h[0] for h in hist) <= hist[0][0]
             # cut edges reduced here: halo column entries + partial edges computed for peers
             edges = part.interior.nnz + part.halo_x.nnz + part.send_p.nnz
         else:
@@ -88,7 +93,8 @@ def _worker(rank, world, port, n, F, q, kind="gather"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind", [(2, "gather"), (3, "gather"), (2, "cover"), (3, "cover")])
+@pytest.mark.parametrize("world,kind", [(2, "gather"), (3, "gather"), (2, "cover"), (3, "cover"),
+                                        (3, "balanced")])
 def test_edge_cut_matches_single_device(world, kind):
     n, F = 3000, 16
     ctx = mp.get_context("spawn")
@@ -161,6 +167,22 @@ def test_cover_exchange_without_cut_edges():
         nxt = (rr + 1) % 20 + (rr // 20) * 20
         ref = np.maximum(-0.5 * (X[rr] + X[nxt]), 0)
         np.testing.assert_allclose(y, ref, rtol=1e-6, atol=1e-6)
+
+
+def test_weighted_bounds():
+    from graphneuralnetwork_amd.distributed import nnz_balanced_bounds, weighted_bounds
+    rng = np.random.default_rng(1)
+    deg = rng.zipf(1.8, 5000).clip(0, 3000)
+    rowptr = torch.from_numpy(np.concatenate([[0], np.cumsum(deg)]))
+    for w in (2, 3, 8):
+        assert torch.equal(weighted_bounds(rowptr, w), nnz_balanced_bounds(rowptr, w))
+    b0 = nnz_balanced_bounds(rowptr, 4).tolist()
+    # block 0 three times as costly per edge/row: it shrinks, the others grow
+    b1 = weighted_bounds(rowptr, 4, [3.0, 1.0, 1.0, 1.0], b0).tolist()
+    assert b1[0] == 0 and b1[-1] == 5000 and b1 == sorted(b1) and b1[1] < b0[1]
+    c = np.concatenate([[0], np.cumsum((deg + 1) * np.where(np.arange(5000) < b0[1], 3.0, 1.0))])
+    part = [c[b1[k + 1]] - c[b1[k]] for k in range(4)]
+    assert max(part) - min(part) <= 2 * (deg.max() + 1) * 3
 
 
 def test_nnz_balanced_bounds():

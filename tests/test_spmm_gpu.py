@@ -248,7 +248,7 @@ def test_rmat_1m_parity_vs_c_oracle(dev):
                                rtol=1e-4, atol=1e-2)
 
 
-@pytest.mark.parametrize("F", [3, 64, 128, 256, 600])
+@pytest.mark.parametrize("F", [3, 64, 128, 256, 600, 2100])
 def test_hub_staging_bitexact(dev, F):
     """gnn_spmm_csr_hub_f32: staging the hottest rows of X into a compact table changes no
     bit of Y (same edge order; the gathered values are copies) for any hub count, with
