@@ -1,0 +1,75 @@
+"""Interleaved A/B of whole-library builds (lib/variants/libgnn_<tag>.so, built by
+build.build_variant) on the default SpMM path (ops.spmm_forward) at one workload.
+
+    python tools/lib_ab.py --build --variants base,ntcold      (CPU side)
+    python tools/lib_ab.py --variants base,ntcold [--workload cfg2|ns] [--feat 128]
+"""
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+# tag -> -D flags. Tried and dropped (profiles/r01f_lib_ab_ntcold_*.log): non-temporal
+# loads for the cold (non-hub) gathers, "ntcold" = GNN_SPMM_NT_COLD=1: no change at cfg2
+# (1.162 vs 1.161 ms) or the north star (14.32 vs 14.32 ms).
+VARIANTS = {
+    "base": [],
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--workload", default="cfg2")
+    ap.add_argument("--feat", type=int, default=128)
+    ap.add_argument("--rounds", type=int, default=6)
+    args = ap.parse_args()
+    names = args.variants.split(",")
+    if args.build:
+        from graphneuralnetwork_amd.build import build_variant
+        for n in names:
+            print(build_variant(n, VARIANTS[n]))
+        return
+    import torch
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd.ops import spmm_forward
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    dev = torch.device("cuda:0")
+    n, e = (1_000_000, 10_000_000) if args.workload == "cfg2" else (10_000_000, 100_000_000)
+    s, d = rmat_edges(n, e, 0)
+    g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n, device=dev)
+    F = args.feat
+    X = torch.randn(n, F, device=dev)
+    Y = torch.empty(n, F, device=dev)
+    ref = spmm_forward(g, X).clone()
+    nbytes = g.nnz * (8 + 4 * F) + n * (8 + 4 * F)
+    libs = {v: ROOT / "graphneuralnetwork_amd" / "lib" / "variants" / f"libgnn_{v}.so" for v in names}
+    times = {v: [] for v in names}
+    for r in range(args.rounds):
+        for v in names:
+            _lib.use_variant(libs[v])
+            spmm_forward(g, X, out=Y)
+            torch.cuda.synchronize()
+            if r == 0:
+                assert torch.equal(Y, ref), v
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(5):
+                spmm_forward(g, X, out=Y)
+            b.record()
+            torch.cuda.synchronize()
+            times[v].append(a.elapsed_time(b) / 5)
+    for v, t in times.items():
+        m = statistics.median(t)
+        print(json.dumps({"variant": v, "workload": args.workload, "feat": F, "median_ms": m,
+                          "algo_GBps": nbytes / m / 1e6}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
