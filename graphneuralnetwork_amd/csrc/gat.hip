@@ -14,8 +14,10 @@
 //   phase A (lane = edge, 64 edges per chunk): s_ijh = LeakyReLU(el_ih + er_jh);
 //     dense : online softmax -- chunk max per head by a wave reduction, running
 //             max m_h, rescale of the lane-local denominators and of acc;
-//     sparse: p = exp(-s) with NO max subtraction (bit-for-bit the reference's
-//             arithmetic, including its overflow to inf / NaN);
+//     sparse: p = exp(-s) with NO max subtraction (the reference's arithmetic,
+//             including its overflow to inf / NaN; v_exp_f32-based __expf, within
+//             ~1e-6 relative of the correctly rounded exp and overflowing at the
+//             same argument to within rounding);
 //     p[e][h] goes to a 64 x HP LDS tile private to the wave.
 //   phase B (lanes = features): acc[f] += p[e][head(f)] * Wh[col_e][f] with the
 //     same wide-gather geometry as the SpMM (EPI edge slots x LPR lanes x VW).
@@ -182,7 +184,7 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
       } else if (SPARSE) {
         const int h = static_cast<int>(f / P.fh);
         const float sv = P.el[rows[u] * P.lde + h] + P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
-        const float p = expf(-(sv > 0.f ? sv : P.slope * sv));
+        const float p = __expf(-(sv > 0.f ? sv : P.slope * sv));
         float wv = p;
         if (P.drop_p > 0.f) {
           const uint32_t rr = hash3(P.drop_seed, P.rowptr[rows[u]], P.head0 + h);
@@ -258,7 +260,7 @@ __device__ __forceinline__ void gat_short_rows(const GatParams& P, int64_t wave,
 #pragma unroll
     for (int e = 0; e < K; ++e) {
       if (e >= n) continue;
-      const float p = SPARSE ? expf(z[e]) : (z[e] == -INFINITY ? 0.f : __expf(z[e] - m));
+      const float p = SPARSE ? __expf(z[e]) : (z[e] == -INFINITY ? 0.f : __expf(z[e] - m));
       l += p;
       float w = p;
       if (P.drop_p > 0.f) {
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
         lsum = lsum * scale + pv;
         acc[0] *= __shfl(scale, hid[0], kWave);
       } else {
-        pv = z == -INFINITY ? 0.f : expf(z);  // exp(-LeakyReLU), no max subtraction
+        pv = z == -INFINITY ? 0.f : __expf(z);  // exp(-LeakyReLU), no max subtraction
         lsum += pv;
       }
 #pragma unroll
@@ -441,7 +443,7 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
     } else {
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        pj[j] = zj[j] == -INFINITY ? 0.f : expf(zj[j]);  // exp(-LeakyReLU), no max subtraction
+        pj[j] = zj[j] == -INFINITY ? 0.f : __expf(zj[j]);  // exp(-LeakyReLU), no max subtraction
         lsum += pj[j];
       }
     }
