@@ -73,6 +73,8 @@ def main():
     ap.add_argument("world", nargs="?", type=int, default=8)
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--exchange", default="cover", choices=["cover", "gather", "balanced"])
+    ap.add_argument("--strong", action="store_true",
+                    help="cfg5: the fixed 10M / 100M graph cut W ways (default: W x 1M / 10M)")
     args = ap.parse_args()
     import graphneuralnetwork_amd.distributed as D
     from graphneuralnetwork_amd import _lib
@@ -82,9 +84,9 @@ def main():
     _lib.load()
     dev = torch.device("cuda:0")
     W, F = args.world, args.feat
-    s, d = rmat_edges(1_000_000 * W, 10_000_000 * W, 0)
-    g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), 1_000_000 * W,
-                      device=dev)
+    nodes, edges = (10_000_000, 100_000_000) if args.strong else (1_000_000 * W, 10_000_000 * W)
+    s, d = rmat_edges(nodes, edges, 0)
+    g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), nodes, device=dev)
     del s, d
     sim = _Sim(W)
     D._all_to_all_v = sim.a2a
