@@ -9,8 +9,9 @@ exactly like GCN/GCN.py:23, which is why the layer class keeps the name
 
 The aggregation ``torch.spmm(adj, support) + bias`` (GCN/GCN.py:43-45) runs
 as ONE gfx950 kernel launch (CSR SpMM with the bias fused into its epilogue);
-the feature transform ``support = dense(X)`` stays an MFMA GEMM (hipBLASLt via
-torch).  ``adj`` may be the reference's sparse COO tensor, a sparse CSR
+the feature transform ``support = dense(X)`` is an fp32 MFMA GEMM: the hand-written
+``gnn_gcn_transform_f32`` at inference for the shapes it covers (F_in/F_out 64-256),
+otherwise (training, other shapes) nn.Linear on hipBLASLt.  ``adj`` may be the reference's sparse COO tensor, a sparse CSR
 tensor, a dense tensor or a prebuilt ``CsrGraph``; the CSR form is cached on
 the adjacency tensor.
 """
@@ -20,7 +21,7 @@ import torch
 from torch import nn
 
 from .graph import as_csr
-from .ops import spmm
+from .ops import gcn_transform, spmm
 
 
 class GCN_Model(nn.Module):
@@ -64,7 +65,12 @@ class Graph_conv_layer(nn.Module):
             self.register_parameter('bias', None)
 
     def forward(self, X_input, adj):
-        support = self.dense(X_input)
+        support = None
+        if X_input.is_cuda and not (torch.is_grad_enabled() and
+                                    (X_input.requires_grad or self.dense.weight.requires_grad)):
+            support = gcn_transform(X_input, self.dense.weight)  # MFMA kernel (inference)
+        if support is None:
+            support = self.dense(X_input)
         return spmm(as_csr(adj), support, self.bias)
 
     def __repr__(self):

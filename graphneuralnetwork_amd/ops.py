@@ -192,6 +192,28 @@ def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: to
     return wh, el, er
 
 
+def gcn_transform(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None:
+    """support = x @ weight^T on fp32 MFMA (gnn_gcn_transform_f32), the dense half of
+    Graph_conv_layer.forward (GCN/GCN.py:42); inference only (no autograd). None when the
+    shape is not covered (the caller then uses nn.Linear / hipBLASLt)."""
+    _require_device(x, weight)
+    if (x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 2
+            or weight.dim() != 2 or x.shape[1] != weight.shape[1]):
+        return None
+    lib = _lib.load()
+    fout, k = weight.shape
+    if not lib.gnn_gcn_transform_supported(k, fout):
+        return None
+    if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
+        x = x.contiguous()
+    w = weight.contiguous()
+    y = torch.empty((x.shape[0], fout), dtype=torch.float32, device=x.device)
+    _lib.check(lib.gnn_gcn_transform_f32(x.data_ptr(), x.stride(0), x.shape[0], k, w.data_ptr(),
+                                         fout, y.data_ptr(), fout, _lib.stream_handle(x.device)),
+               "gnn_gcn_transform_f32")
+    return y
+
+
 def col_mean(x: torch.Tensor) -> torch.Tensor:
     """Mean over rows (double accumulation) -- the dense GAT layer's edgeless-row output."""
     _require_device(x)

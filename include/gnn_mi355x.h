@@ -147,6 +147,19 @@ int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t hea
                        void* stream);
 
 /*
+ * GCN feature transform on the matrix cores: y[n, :fout] = x[n, :k] @ w^T with w the
+ * nn.Linear weight [fout, k] (row-major), fp32 in / fp32 accumulate
+ * (v_mfma_f32_16x16x4_f32). Replaces `support = self.dense(X_input)` at GCN/GCN.py:42
+ * (inference path). Shapes covered: gnn_gcn_transform_supported(k, fout) != 0
+ * (k in {16, 32, 64, 128, 256}; fout 64, or 128 with k <= 128, or 256 with k <= 64);
+ * other shapes return GNN_E_UNSUPPORTED (the caller uses a library GEMM). x, w, y
+ * 16-B aligned, ldx and ldy multiples of 4 (else GNN_E_ALIGN).
+ */
+int gnn_gcn_transform_supported(int64_t k, int64_t fout);
+int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,
+                          int64_t fout, float* y, int64_t ldy, void* stream);
+
+/*
  * GAT feature transform on the matrix cores with the attention logits fused:
  *   wh[n, :] = x[n, :k] @ w[k, fout]   (w row-major [k, fout], all heads side by side)
  *   el[n, h] = a_src[h*fh:(h+1)*fh] . wh[n, h*fh:(h+1)*fh], er likewise with a_dst

@@ -294,3 +294,40 @@ def test_hub_plan_structure(dev):
     # deterministic: exactly the stable order (degree descending, ties by ascending id)
     np.testing.assert_array_equal(hub, np.lexsort((np.arange(n), -deg))[:k])
     assert int(hp.err.item()) == 0
+
+
+@pytest.mark.parametrize("k,fout", [(16, 64), (32, 128), (64, 64), (64, 256), (128, 128),
+                                    (256, 64)])
+@pytest.mark.parametrize("n", [1, 63, 1000, 4097])
+def test_gcn_transform_mfma(dev, k, fout, n):
+    """gnn_gcn_transform_f32 (fp32 MFMA, W [fout, k] as nn.Linear) vs a float64 matmul."""
+    from graphneuralnetwork_amd.ops import gcn_transform
+    rng = np.random.default_rng(k * 7 + fout + n)
+    X = rng.standard_normal((n, k + 4)).astype(np.float32)
+    W = (rng.standard_normal((fout, k)) / np.sqrt(k)).astype(np.float32)
+    ref = X[:, :k].astype(np.float64) @ W.astype(np.float64).T
+    Xd = torch.from_numpy(X).to(dev)
+    for x in (Xd[:, :k].contiguous(), Xd[:, :k]):   # packed and ldx = k + 4
+        y = gcn_transform(x, torch.from_numpy(W).to(dev))
+        assert y is not None and y.shape == (n, fout)
+        close(y.cpu().numpy(), ref)
+
+
+def test_gcn_transform_fallback_and_training(dev):
+    """Uncovered shapes return None (nn.Linear runs); with autograd the layer uses nn.Linear."""
+    from graphneuralnetwork_amd.gcn import Graph_conv_layer
+    from graphneuralnetwork_amd.ops import gcn_transform
+    x = torch.randn(100, 7, device=dev)
+    assert gcn_transform(x, torch.randn(5, 7, device=dev)) is None
+    assert gcn_transform(torch.randn(100, 256, device=dev), torch.randn(256, 256, device=dev)) is None
+    n = 300
+    rowptr, col, val = _rand_graph(n, 3000, 8)
+    g = _graph(rowptr, col, val, n, dev)
+    layer = Graph_conv_layer(128, 128).to(dev)
+    X = torch.randn(n, 128, device=dev, requires_grad=True)
+    y = layer(X, g)
+    y.sum().backward()
+    assert X.grad is not None and layer.dense.weight.grad is not None
+    with torch.no_grad():
+        y2 = layer(X, g)  # MFMA transform path
+    close(y2.cpu().numpy(), y.detach().cpu().numpy())
