@@ -16,8 +16,13 @@ sys.path.insert(0, str(ROOT))
 # tag -> -D flags. Tried and dropped (profiles/r01f_lib_ab_ntcold_*.log): non-temporal
 # loads for the cold (non-hub) gathers, "ntcold" = GNN_SPMM_NT_COLD=1: no change at cfg2
 # (1.162 vs 1.161 ms) or the north star (14.32 vs 14.32 ms).
+# GCN transform grid (tools/transform_ab.py --variants, profiles/r01f_transform_grid_ab.log):
+# 512 workgroups 0.294 ms at 1M x 128 x 128, 256: 0.340, 768: 0.314, 1024: 0.304.
 VARIANTS = {
     "base": [],
+    "tf256": ["GNN_TF_GRID=256"],
+    "tf768": ["GNN_TF_GRID=768"],
+    "tf1024": ["GNN_TF_GRID=1024"],
 }
 
 
