@@ -1,5 +1,2 @@
-set -e
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_spmm_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_tf.log 2>&1
-timeout -k 10 300 python -u tools/transform_ab.py > gpurun_out/transform_ab.log 2>&1
-timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/bench_tf.log 2>&1
+OUT=gpurun_out/r01g bash tools/gpu_check.sh tests smoke bench bench_ns bench_gat bench_sage && \
+timeout -k 10 900 python bench.py --workload cfg5 --steps 10 --warmup 3 > gpurun_out/r01g/bench_cfg5.log 2>&1 && tail -1 gpurun_out/r01g/bench_cfg5.log | cut -c1-300
