@@ -283,6 +283,9 @@ __global__ __launch_bounds__(kGatBlock) void gat_short_kernel(GatParams P) {
                                   threadIdx.x & (kWave - 1));
 }
 
+#ifndef GNN_GAT_LDS_PAD
+#define GNN_GAT_LDS_PAD 0  // A/B: dynamic LDS per workgroup to cap workgroups per CU
+#endif
 #ifdef GNN_GAT_WAVES_PER_EU
 #define GNN_GAT_OCC __attribute__((amdgpu_waves_per_eu(GNN_GAT_WAVES_PER_EU)))
 #else
@@ -665,7 +668,7 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
   const int64_t blocks = seg_blocks + mid_blocks + short_blocks + small_blocks;
   if (blocks > 0)
     hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U, J>),
-                       dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), 0, s, Q);
+                       dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), GNN_GAT_LDS_PAD, s, Q);
   if constexpr (NCH == 1) {
     if (P.n_short > 0) {
       const int64_t sw = (P.n_short + EPI - 1) / EPI;

@@ -23,6 +23,9 @@
 namespace gnn {
 
 constexpr int kSageBlock = 256;
+#ifndef GNN_SAGE_LDS_PAD
+#define GNN_SAGE_LDS_PAD 0  // A/B: dynamic LDS per workgroup to cap workgroups per CU
+#endif
 constexpr int kSageWaves = kSageBlock / kWave;
 
 enum SageMode : int32_t { kMean = 0, kArgmax = 1, kSum = 2 };
@@ -179,7 +182,7 @@ static int launch_sage(const SageArgs& a) {
   const int64_t blocks = (a.M + kSageWaves - 1) / kSageWaves;
   if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   hipLaunchKernelGGL((sage_aggregate_kernel<VW, LPR, NCH, MODE, GATHER, U>),
-                     dim3(static_cast<unsigned>(blocks)), dim3(kSageBlock), 0, a.s, a.src, a.ld_row,
+                     dim3(static_cast<unsigned>(blocks)), dim3(kSageBlock), GNN_SAGE_LDS_PAD, a.s, a.src, a.ld_row,
                      a.ld_m, a.n_table, a.idx, a.ldi, a.M, a.k, a.feat, a.out, a.ldo, a.err);
   return launch_status();
 }

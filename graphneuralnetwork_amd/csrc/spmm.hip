@@ -33,7 +33,32 @@ namespace gnn {
 
 constexpr int kBlock = 256;                 // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kSmallUnroll = 4;             // small rows per slot per wave
+#ifndef GNN_SPMM_SMALL_UNROLL
+// small rows per slot per wave at NCH = 1 (halved per doubling of NCH). A/B with hub
+// staging (tools/lib_ab.py, profiles/r01f_lib_ab_*): 16 vs 4 took cfg2 1.164 -> 1.082 ms,
+// the north star 14.54 -> 13.76 ms, F=256 29.7 -> 28.3 ms (with the longer segments)
+#define GNN_SPMM_SMALL_UNROLL 16
+#endif
+#ifndef GNN_SPMM_U
+#define GNN_SPMM_U 4  // slot loads in flight per lane for one-chunk rows (A/B: tools/lib_ab.py)
+#endif
+#ifndef GNN_SPMM_SMALL_SPLIT
+#define GNN_SPMM_SMALL_SPLIT 0
+#endif
+#ifndef GNN_SPMM_SMALL_SPLIT_UNROLL
+#define GNN_SPMM_SMALL_SPLIT_UNROLL 16
+#endif
+#ifndef GNN_SPMM_LDS_PAD
+#define GNN_SPMM_LDS_PAD 0  // A/B: dynamic LDS per workgroup to cap workgroups per CU
+#endif
+constexpr int kSmallUnroll = GNN_SPMM_SMALL_UNROLL;  // small rows per slot per wave (NCH = 1)
+// per column-chunk count: the unrolled loads stay at ~16 x 16 B per lane
+template <int NCH>
+constexpr int small_unroll() {
+  return kSmallUnroll / NCH >= 2 ? kSmallUnroll / NCH : 2;
+}
+constexpr bool kSmallSplit = GNN_SPMM_SMALL_SPLIT;   // small rows in their own launch
+constexpr int kSmallSplitUnroll = GNN_SPMM_SMALL_SPLIT_UNROLL;
 
 struct SpmmParams {
   const int64_t* rowptr;
@@ -196,6 +221,41 @@ __device__ __forceinline__ void store_slot_row(float* __restrict__ out,
   }
 }
 
+// Rows with at most one edge, pre-resolved by the plan (small_col -1 = no edge): EPI x SU
+// rows per wave, one per slot and unroll step, all SU loads issued before the stores.
+template <int VW, int LPR, int NCH, bool NT, int SU>
+__device__ __forceinline__ void small_rows(const SpmmParams& P, int64_t swave, int lane) {
+  constexpr int EPI = kWave / LPR;
+  const int sub = lane & (LPR - 1);
+  const int grp = lane / LPR;
+  const int64_t i0 = swave * (EPI * SU);
+  typename Vec<VW>::T xv[SU][NCH];
+  float w[SU];
+  int64_t rows[SU];
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int64_t i = i0 + u * EPI + grp;
+    const bool ok = i < P.n_small;
+    const int c = ok ? P.small_col[i] : -1;
+    rows[u] = ok ? P.small_row[i] : -1;
+    w[u] = c >= 0 ? P.small_val[i] : 0.f;
+    const float* xr = P.x + static_cast<int64_t>(c < 0 ? 0 : c) * P.ldx;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+      xv[u][ch] = (c >= 0 && f < P.feat) ? vload<VW>(xr + f) : vzero<VW>();
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    if (rows[u] < 0) continue;
+    typename Vec<VW>::T r[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) r[ch] = w[u] * xv[u][ch];
+    store_slot_row<VW, LPR, NCH, NT>(P.y + rows[u] * P.ldy, P.bias, P.feat, P.flags, sub, r);
+  }
+}
+
 template <int VW, int LPR, int NCH, int U, bool NT, bool STAGE = false, bool HUB = false>
 __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
   constexpr int EPI = kWave / LPR;
@@ -239,33 +299,18 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
                                                      sub, acc);
     return;
   }
-  // ---- packed small rows: EPI x kSmallUnroll rows per wave, one per slot and unroll step
-  const int64_t i0 = (wave - P.seg_waves - P.mid_waves) * (EPI * kSmallUnroll);
-  typename Vec<VW>::T xv[kSmallUnroll][NCH];
-  float w[kSmallUnroll];
-  int64_t rows[kSmallUnroll];
-#pragma unroll
-  for (int u = 0; u < kSmallUnroll; ++u) {
-    const int64_t i = i0 + u * EPI + grp;
-    const bool ok = i < P.n_small;
-    const int c = ok ? P.small_col[i] : -1;
-    rows[u] = ok ? P.small_row[i] : -1;
-    w[u] = c >= 0 ? P.small_val[i] : 0.f;
-    const float* xr = P.x + static_cast<int64_t>(c < 0 ? 0 : c) * P.ldx;
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-      const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
-      xv[u][ch] = (c >= 0 && f < P.feat) ? vload<VW>(xr + f) : vzero<VW>();
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kSmallUnroll; ++u) {
-    if (rows[u] < 0) continue;
-    typename Vec<VW>::T r[NCH];
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) r[ch] = w[u] * xv[u][ch];
-    store_slot_row<VW, LPR, NCH, NT>(P.y + rows[u] * P.ldy, P.bias, P.feat, P.flags, sub, r);
-  }
+  // ---- packed small rows (unless they have their own launch, spmm_small_kernel)
+  if constexpr (!kSmallSplit)
+    small_rows<VW, LPR, NCH, NT, small_unroll<NCH>()>(P, wave - P.seg_waves - P.mid_waves, lane);
+}
+
+// Packed small rows as their own launch: their unrolled loads then do not set the
+// register budget (and so the occupancy) of the segment / mid-row waves.
+template <int VW, int LPR, int NCH, bool NT>
+__global__ __launch_bounds__(kBlock) void spmm_small_kernel(SpmmParams P) {
+  small_rows<VW, LPR, NCH, NT, kSmallSplitUnroll>(
+      P, static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6),
+      threadIdx.x & (kWave - 1));
 }
 
 // y[long_row[i]] = act(sum_{s in segs(i)} partial[s] + bias).
@@ -339,19 +384,24 @@ struct SpmmLaunch {
 template <int VW, int LPR, int NCH, int U_OVERRIDE = 0, bool NT = true, bool STAGE = false,
           bool HUB = false>
 static int launch_spmm_t(const SpmmLaunch& L) {
-  constexpr int U = U_OVERRIDE ? U_OVERRIDE : (NCH >= 4 ? 1 : (NCH == 2 ? 2 : 4));
+  constexpr int U = U_OVERRIDE ? U_OVERRIDE : (NCH >= 4 ? 1 : (NCH == 2 ? 2 : GNN_SPMM_U));
   constexpr int EPI = kWave / LPR;
   SpmmParams p = L.p;
   const int64_t seg_blocks = (p.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
   const int64_t mid_blocks = (p.n_mid + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int64_t small_waves = (p.n_small + EPI * kSmallUnroll - 1) / (EPI * kSmallUnroll);
+  constexpr int SU = kSmallSplit ? kSmallSplitUnroll : small_unroll<NCH>();
+  const int64_t small_waves = (p.n_small + EPI * SU - 1) / (EPI * SU);
   const int64_t small_blocks = (small_waves + kWavesPerBlock - 1) / kWavesPerBlock;
   p.seg_waves = seg_blocks * kWavesPerBlock;
   p.mid_waves = mid_blocks * kWavesPerBlock;
-  const int64_t blocks = seg_blocks + mid_blocks + small_blocks;
-  if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
+  const int64_t blocks = seg_blocks + mid_blocks + (kSmallSplit ? 0 : small_blocks);
+  if (blocks > 0x7fffffffLL || small_blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   if (blocks > 0) {
     hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, U, NT, STAGE, HUB>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), GNN_SPMM_LDS_PAD, L.stream, p);
+  }
+  if (kSmallSplit && small_blocks > 0) {
+    hipLaunchKernelGGL((spmm_small_kernel<VW, LPR, NCH, NT>), dim3(static_cast<unsigned>(small_blocks)),
                        dim3(kBlock), 0, L.stream, p);
   }
   if (L.n_long > 0) {

@@ -26,16 +26,18 @@ import torch
 
 from . import _lib
 
-# Long-row segment size: ~96 KiB of gathered feature rows per wavefront. A/B on
-# MI355X (tools/spmm_ab.py, F=128): 192 edges is within 1 % of the best setting on
-# both the 1M-node graph (best 64-192) and the 10M-node graph (best 192-256);
-# 512+ leaves single-wave tails, 64 over-splits the large graph.
-SEG_BYTES = 96 * 1024
+# Long-row segment size: ~192 KiB of gathered feature rows per wavefront. A/B on
+# MI355X with hub staging (tools/lib_ab.py): 384 edges at F=128 beats 192 by 2.6 %
+# (1M-node graph) and 1 % (10M-node graph); 288-512 are within 1 % of each other, and at
+# F=256 192 edges beat 96 by 1 %. (Before hub staging 192 was best at F=128.)
+SEG_BYTES = 192 * 1024
+# the GAT passes keep the 96 KiB segments they were tuned with (tools/gat_ab.py)
+GAT_SEG_BYTES = 96 * 1024
 MIN_SEG_LEN = 64
 
 
-def seg_len_for(feat: int) -> int:
-    return max(MIN_SEG_LEN, SEG_BYTES // max(1, 4 * feat))
+def seg_len_for(feat: int, seg_bytes: int = SEG_BYTES) -> int:
+    return max(MIN_SEG_LEN, seg_bytes // max(1, 4 * feat))
 
 
 @dataclass

@@ -8,7 +8,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .graph import CsrGraph, seg_len_for
+from .graph import GAT_SEG_BYTES, CsrGraph, seg_len_for
 
 _ACT_FLAGS = {None: 0, "relu": _lib.EPI_RELU, "elu": _lib.EPI_ELU}
 
@@ -257,7 +257,7 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
     fill = None
     if mode == GAT_DENSE and g.has_empty_rows():
         fill = col_mean(wh)
-    plan = g.plan(seg_len if seg_len is not None else seg_len_for(feat))
+    plan = g.plan(seg_len if seg_len is not None else seg_len_for(feat, GAT_SEG_BYTES))
     partial = None
     if plan.n_seg:
         partial = torch.empty((plan.n_seg, feat + 2 * heads), dtype=torch.float32,
@@ -428,7 +428,7 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
     _lib.check(lib.gnn_gat_backward_prep_f32(dy.data_ptr(), y.data_ptr(), feat, n, heads, fh,
                                              int(elu), dout.data_ptr(), D.data_ptr(), stream),
                "gnn_gat_backward_prep_f32")
-    sl = seg_len if seg_len is not None else seg_len_for(feat)
+    sl = seg_len if seg_len is not None else seg_len_for(feat, GAT_SEG_BYTES)
     plan = g.plan(sl)
     E = g.nnz
     w_edge = torch.empty((max(E, 1), heads), dtype=torch.float32, device=dev)

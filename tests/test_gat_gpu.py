@@ -220,7 +220,7 @@ def test_gat_backward_vs_torch(dev, heads, fh, sparse, seg_len):
     R = torch.randn(n, feat, dtype=torch.float64)
     old = graph_mod.seg_len_for
     if seg_len is not None:
-        graph_mod.seg_len_for = lambda f: seg_len
+        graph_mod.seg_len_for = lambda f, *a: seg_len
         import graphneuralnetwork_amd.ops as ops_mod
         ops_mod.seg_len_for = graph_mod.seg_len_for
     try:

@@ -1,2 +1,13 @@
-OUT=gpurun_out/r01g bash tools/gpu_check.sh tests smoke bench bench_ns bench_gat bench_sage && \
-timeout -k 10 900 python bench.py --workload cfg5 --steps 10 --warmup 3 > gpurun_out/r01g/bench_cfg5.log 2>&1 && tail -1 gpurun_out/r01g/bench_cfg5.log | cut -c1-300
+mkdir -p gpurun_out
+{
+python -c "
+import torch, time
+p = torch.cuda.get_device_properties(0); print(p)
+x = torch.empty(2**28, device='cuda'); y = torch.empty_like(x)
+for _ in range(3): y.copy_(x)
+torch.cuda.synchronize(); t=time.time()
+for _ in range(20): y.copy_(x)
+torch.cuda.synchronize(); dt=(time.time()-t)/20; print('copy 1 GiB -> GB/s', 2*2**30/dt/1e9)
+"
+rocm-smi --showcomputepartition --showmemorypartition --showclocks 2>&1 | head -40
+} > gpurun_out/boxinfo.log 2>&1

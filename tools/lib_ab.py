@@ -23,6 +23,23 @@ VARIANTS = {
     "tf256": ["GNN_TF_GRID=256"],
     "tf768": ["GNN_TF_GRID=768"],
     "tf1024": ["GNN_TF_GRID=1024"],
+    "u2": ["GNN_SPMM_U=2"],
+    "u8": ["GNN_SPMM_U=8"],
+    "small2": ["GNN_SPMM_SMALL_UNROLL=2"],
+    "small8": ["GNN_SPMM_SMALL_UNROLL=8"],
+    "small16": ["GNN_SPMM_SMALL_UNROLL=16"],
+    "split8": ["GNN_SPMM_SMALL_SPLIT=1", "GNN_SPMM_SMALL_SPLIT_UNROLL=8"],
+    "split16": ["GNN_SPMM_SMALL_SPLIT=1", "GNN_SPMM_SMALL_SPLIT_UNROLL=16"],
+    "split32": ["GNN_SPMM_SMALL_SPLIT=1", "GNN_SPMM_SMALL_SPLIT_UNROLL=32"],
+    # occupancy caps by dynamic LDS (160 KiB per CU): at most 6 / 4 / 3 / 2 workgroups per CU
+    "wg6": ["GNN_SPMM_LDS_PAD=26624", "GNN_GAT_LDS_PAD=26624", "GNN_SAGE_LDS_PAD=26624"],
+    "wg4": ["GNN_SPMM_LDS_PAD=40960", "GNN_GAT_LDS_PAD=40960", "GNN_SAGE_LDS_PAD=40960"],
+    "wg3": ["GNN_SPMM_LDS_PAD=53248", "GNN_GAT_LDS_PAD=53248", "GNN_SAGE_LDS_PAD=53248"],
+    "wg2": ["GNN_SPMM_LDS_PAD=65536", "GNN_GAT_LDS_PAD=65536", "GNN_SAGE_LDS_PAD=65536"],
+    "s16u8": ["GNN_SPMM_SMALL_UNROLL=16", "GNN_SPMM_U=8"],
+    "s16u2": ["GNN_SPMM_SMALL_UNROLL=16", "GNN_SPMM_U=2"],
+    "small32": ["GNN_SPMM_SMALL_UNROLL=32"],
+    "small4": ["GNN_SPMM_SMALL_UNROLL=4"],
 }
 
 
@@ -33,11 +50,12 @@ def main():
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--seg-lens", default="", help="also time the default build at these seg_len")
     args = ap.parse_args()
-    names = args.variants.split(",")
+    names = args.variants.split(",")  # "tag" or "tag@seg_len"
     if args.build:
         from graphneuralnetwork_amd.build import build_variant
-        for n in names:
+        for n in {n.split("@")[0] for n in names}:
             print(build_variant(n, VARIANTS[n]))
         return
     import torch
@@ -54,19 +72,24 @@ def main():
     Y = torch.empty(n, F, device=dev)
     ref = spmm_forward(g, X).clone()
     nbytes = g.nnz * (8 + 4 * F) + n * (8 + 4 * F)
-    libs = {v: ROOT / "graphneuralnetwork_amd" / "lib" / "variants" / f"libgnn_{v}.so" for v in names}
+    libs = {v: ROOT / "graphneuralnetwork_amd" / "lib" / "variants" /
+            f"libgnn_{v.split('@')[0]}.so" for v in names}
+    seg = {v: int(v.split("@")[1]) for v in names if "@" in v}
+    seg.update({f"seg{sl}": int(sl) for sl in args.seg_lens.split(",") if sl})
+    names = names + [k for k in seg if k not in names]
     times = {v: [] for v in names}
     for r in range(args.rounds):
         for v in names:
-            _lib.use_variant(libs[v])
-            spmm_forward(g, X, out=Y)
+            _lib.use_variant(libs[v] if v in libs and libs[v].exists() else None)
+            sl = seg.get(v)
+            spmm_forward(g, X, out=Y, seg_len=sl)
             torch.cuda.synchronize()
-            if r == 0:
+            if r == 0 and sl is None:
                 assert torch.equal(Y, ref), v
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             for _ in range(5):
-                spmm_forward(g, X, out=Y)
+                spmm_forward(g, X, out=Y, seg_len=sl)
             b.record()
             torch.cuda.synchronize()
             times[v].append(a.elapsed_time(b) / 5)
