@@ -121,7 +121,16 @@ __device__ __forceinline__ float er_at(const GatParams& P, int c, int h) {
                : P.er[static_cast<int64_t>(c) * P.lde + h];
 }
 
-constexpr int kGatSmallUnroll = 4;
+#ifndef GNN_GAT_SMALL_UNROLL
+// edgeless / one-edge rows per slot per wave at NCH = 1 (halved per doubling of NCH);
+// A/B at cfg3 (tools/gat_ab.py, profiles/r01h_gat_small_ab.log): 16 vs 4: 0.797 -> 0.766 ms
+#define GNN_GAT_SMALL_UNROLL 16
+#endif
+constexpr int kGatSmallUnroll = GNN_GAT_SMALL_UNROLL;
+template <int NCH>
+constexpr int gat_small_unroll() {
+  return kGatSmallUnroll / NCH >= 2 ? kGatSmallUnroll / NCH : 2;
+}
 #ifndef GNN_GAT_U
 #define GNN_GAT_U 2  // feature-row gathers in flight per lane in phase B (A/B: tools/gat_ab.py)
 #endif
@@ -142,12 +151,13 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
   constexpr int EPI = kWave / LPR;
   const int sub = lane & (LPR - 1);
   const int grp = lane / LPR;
-  const int64_t i0 = wave * (EPI * kGatSmallUnroll);
-  typename Vec<VW>::T xv[kGatSmallUnroll][NCH];
-  int64_t rows[kGatSmallUnroll];
-  int cols[kGatSmallUnroll];
+  constexpr int SU = gat_small_unroll<NCH>();
+  const int64_t i0 = wave * (EPI * SU);
+  typename Vec<VW>::T xv[SU][NCH];
+  int64_t rows[SU];
+  int cols[SU];
 #pragma unroll
-  for (int u = 0; u < kGatSmallUnroll; ++u) {
+  for (int u = 0; u < SU; ++u) {
     const int64_t i = i0 + u * EPI + grp;
     const bool ok = i < P.n_small;
     const int c = ok ? P.small_col[i] : -1;
@@ -161,7 +171,7 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
     }
   }
 #pragma unroll
-  for (int u = 0; u < kGatSmallUnroll; ++u) {
+  for (int u = 0; u < SU; ++u) {
     if (rows[u] < 0) continue;
     float* orow = P.out + rows[u] * P.ldo;
 #pragma unroll
@@ -659,7 +669,8 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
   // NCH == 1: short rows in their own launch, EPI rows per wave; else one wave per row here
   const int64_t short_waves = NCH == 1 ? 0 : P.n_short;
   const int64_t short_blocks = (short_waves + kGatWaves - 1) / kGatWaves;
-  const int64_t small_waves = (P.n_small + EPI * kGatSmallUnroll - 1) / (EPI * kGatSmallUnroll);
+  constexpr int SU = gat_small_unroll<NCH>();
+  const int64_t small_waves = (P.n_small + EPI * SU - 1) / (EPI * SU);
   const int64_t small_blocks = (small_waves + kGatWaves - 1) / kGatWaves;
   GatParams Q = P;
   Q.seg_waves = seg_blocks * kGatWaves;

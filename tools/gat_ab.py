@@ -22,6 +22,9 @@ VARIANTS = {
     "c8u2": ["GNN_GAT_CHUNK=8", "GNN_GAT_U=2"],
     "nopipe": ["GNN_GAT_PIPE=0"],
     "pipe": ["GNN_GAT_PIPE=1"],
+    "base": [],
+    "gs8": ["GNN_GAT_SMALL_UNROLL=8"],
+    "gs16": ["GNN_GAT_SMALL_UNROLL=16"],
 }
 
 
