@@ -23,6 +23,11 @@
 namespace gnn {
 
 constexpr int kSageBlock = 256;
+#ifndef GNN_SAGE_U
+// neighbour-slot loads in flight per lane. A/B (tools/lib_ab.py --op sage, 10M-row table,
+// k = 10, profiles/r01h_sage_u_ab.log): 2: 37.1 us, 4: 35.5, 8: 33.7, 16: 45.8
+#define GNN_SAGE_U 8
+#endif
 #ifndef GNN_SAGE_LDS_PAD
 #define GNN_SAGE_LDS_PAD 0  // A/B: dynamic LDS per workgroup to cap workgroups per CU
 #endif
@@ -178,7 +183,7 @@ struct SageArgs {
 
 template <int VW, int LPR, int NCH, int MODE, bool GATHER>
 static int launch_sage(const SageArgs& a) {
-  constexpr int U = NCH >= 2 ? 2 : 4;
+  constexpr int U = NCH >= 2 ? 2 : GNN_SAGE_U;
   const int64_t blocks = (a.M + kSageWaves - 1) / kSageWaves;
   if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   hipLaunchKernelGGL((sage_aggregate_kernel<VW, LPR, NCH, MODE, GATHER, U>),

@@ -40,6 +40,9 @@ VARIANTS = {
     "s16u2": ["GNN_SPMM_SMALL_UNROLL=16", "GNN_SPMM_U=2"],
     "small32": ["GNN_SPMM_SMALL_UNROLL=32"],
     "small4": ["GNN_SPMM_SMALL_UNROLL=4"],
+    "su2": ["GNN_SAGE_U=2"],
+    "su8": ["GNN_SAGE_U=8"],
+    "su16": ["GNN_SAGE_U=16"],
 }
 
 
@@ -51,6 +54,9 @@ def main():
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--seg-lens", default="", help="also time the default build at these seg_len")
+    ap.add_argument("--op", default="spmm", choices=["spmm", "sage"],
+                    help="sage: the fused gather-mean over [M=62,401, k=10] uniform-degree-weighted "
+                         "samples of the workload's graph (the cfg4 layer-0 shape)")
     args = ap.parse_args()
     names = args.variants.split(",")  # "tag" or "tag@seg_len"
     if args.build:
@@ -70,8 +76,20 @@ def main():
     F = args.feat
     X = torch.randn(n, F, device=dev)
     Y = torch.empty(n, F, device=dev)
-    ref = spmm_forward(g, X).clone()
     nbytes = g.nnz * (8 + 4 * F) + n * (8 + 4 * F)
+    if args.op == "sage":
+        from graphneuralnetwork_amd.ops import sage_gather_aggregate
+        from graphneuralnetwork_amd.sampler import sample_neighbors
+        deg = g.rowptr[1:] - g.rowptr[:-1]
+        cand = torch.nonzero(deg > 0).view(-1)
+        nodes = cand[torch.randperm(cand.numel(), device=dev)[:62401]]
+        idx = sample_neighbors(g, nodes, 10, 0)
+        Y = torch.empty(idx.shape[0], F, device=dev)
+        nbytes = idx.numel() * (4 * F + 8) + idx.shape[0] * 4 * F
+
+        def spmm_forward(g_, X_, out=None, seg_len=None):  # noqa: F811 -- same harness
+            return sage_gather_aggregate(X_, idx, "MEAN", check=False, out=out)
+    ref = spmm_forward(g, X, out=torch.empty_like(Y)).clone()
     libs = {v: ROOT / "graphneuralnetwork_amd" / "lib" / "variants" /
             f"libgnn_{v.split('@')[0]}.so" for v in names}
     seg = {v: int(v.split("@")[1]) for v in names if "@" in v}
@@ -88,14 +106,14 @@ def main():
                 assert torch.equal(Y, ref), v
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            for _ in range(5):
+            for _ in range(20 if args.op == "sage" else 5):
                 spmm_forward(g, X, out=Y, seg_len=sl)
             b.record()
             torch.cuda.synchronize()
-            times[v].append(a.elapsed_time(b) / 5)
+            times[v].append(a.elapsed_time(b) / (20 if args.op == "sage" else 5))
     for v, t in times.items():
         m = statistics.median(t)
-        print(json.dumps({"variant": v, "workload": args.workload, "feat": F, "median_ms": m,
+        print(json.dumps({"variant": v, "op": args.op, "workload": args.workload, "feat": F, "median_ms": m,
                           "algo_GBps": nbytes / m / 1e6}), flush=True)
 
 
