@@ -50,11 +50,15 @@ def _worker(rank, world, port, n, F, q, kind="gather"):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from graphneuralnetwork_amd.distributed import (EdgeCutSpmm, build_cover_exchange,
+                                                        build_cover_exchange_balanced,
                                                         build_partition)
         dev = torch.device("cuda:0")
         g = _graph(n, dev)
-        build = build_cover_exchange if kind == "cover" else build_partition
-        part = build(g, rank, world)
+        if kind == "balanced":  # what bench.py --gpus N uses
+            part, _ = build_cover_exchange_balanced(g, rank, world)
+        else:
+            build = build_cover_exchange if kind == "cover" else build_partition
+            part = build(g, rank, world)
         X = torch.from_numpy(np.random.default_rng(1).standard_normal((n, F)).astype(np.float32)).to(dev)
         b = torch.linspace(-1, 1, F, device=dev)
         r0, r1 = part.bounds[rank], part.bounds[rank + 1]
@@ -67,7 +71,8 @@ def _worker(rank, world, port, n, F, q, kind="gather"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind", [(2, "gather"), (2, "cover"), (3, "cover")])
+@pytest.mark.parametrize("world,kind", [(2, "gather"), (2, "cover"), (3, "cover"),
+                                        (2, "balanced")])
 def test_edge_cut_hip_path_matches_single_gpu(dev, world, kind):
     from graphneuralnetwork_amd.ops import spmm_forward
     n, F = 20000, 64
