@@ -25,6 +25,7 @@ VARIANTS = {
     "base": [],
     "gs8": ["GNN_GAT_SMALL_UNROLL=8"],
     "gs16": ["GNN_GAT_SMALL_UNROLL=16"],
+    "gs4": ["GNN_GAT_SMALL_UNROLL=4"],
 }
 
 
