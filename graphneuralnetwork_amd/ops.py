@@ -165,10 +165,13 @@ def gat_logits(wh: torch.Tensor, heads: int, fh: int, a_src: torch.Tensor,
 
 
 def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: torch.Tensor,
-                a_dst: torch.Tensor):
+                a_dst: torch.Tensor, packed: bool = False):
     """(Wh = x @ w, el, er) in one MFMA pass (inference; no autograd), or None when the
     shape is not covered by gnn_gat_project_f32 (the caller then uses torch.mm +
-    gat_logits)."""
+    gat_logits). ``packed``: the three are views of ONE [n, H*Fh + 2H] buffer, rows
+    [Wh | er | el], so the aggregation's er gather lands next to the Wh row it also
+    gathers. Same output bits; measured neutral at cfg3 on a slow box (1.297 vs 1.298 ms,
+    profiles/r01i_gat_pack_ab_slow.log), so it is not the default."""
     _require_device(x, w, a_src, a_dst)
     if (x.dtype != torch.float32 or w.dtype != torch.float32 or x.dim() != 2 or w.dim() != 2
             or x.shape[1] != w.shape[0] or w.shape[1] != heads * fh):
@@ -180,15 +183,19 @@ def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: to
     if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
         x = x.contiguous()
     n = x.shape[0]
-    wh = torch.empty((n, fout), dtype=torch.float32, device=x.device)
-    el = torch.empty((n, heads), dtype=torch.float32, device=x.device)
-    er = torch.empty((n, heads), dtype=torch.float32, device=x.device)
+    if packed:
+        buf = torch.empty((n, fout + 2 * heads), dtype=torch.float32, device=x.device)
+        wh, er, el = buf[:, :fout], buf[:, fout:fout + heads], buf[:, fout + heads:]
+    else:
+        wh = torch.empty((n, fout), dtype=torch.float32, device=x.device)
+        el = torch.empty((n, heads), dtype=torch.float32, device=x.device)
+        er = torch.empty((n, heads), dtype=torch.float32, device=x.device)
     w2 = torch.empty((k, 16), dtype=torch.float32, device=x.device)
     _lib.check(lib.gnn_gat_project_f32(
         x.data_ptr(), x.stride(0), n, k, w.contiguous().data_ptr(), fout,
         a_src.contiguous().data_ptr(), a_dst.contiguous().data_ptr(), heads, fh, wh.data_ptr(),
-        fout, el.data_ptr(), er.data_ptr(), heads, w2.data_ptr(), _lib.stream_handle(x.device)),
-        "gnn_gat_project_f32")
+        wh.stride(0), el.data_ptr(), er.data_ptr(), el.stride(0), w2.data_ptr(),
+        _lib.stream_handle(x.device)), "gnn_gat_project_f32")
     return wh, el, er
 
 
@@ -245,10 +252,15 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
     n = g.n_rows
     if wh.shape[0] != g.n_cols or wh.shape[1] != heads * fh:
         raise ValueError("Wh must be [n_cols, heads * fh]")
-    el = el.contiguous()
-    er = er.contiguous()
     if el.shape != (n, heads) or er.shape != (g.n_cols, heads):
         raise ValueError("el must be [n_rows, heads] and er [n_cols, heads]")
+    # el / er share one row stride in the C-ABI: strided views of one buffer (gat_project
+    # packed=True) pass as they are, anything else is made contiguous
+    if not (el.stride(1) == 1 and er.stride(1) == 1 and el.stride(0) == er.stride(0)
+            and el.stride(0) >= heads):
+        el = el.contiguous()
+        er = er.contiguous()
+    lde = el.stride(0)
     feat = heads * fh
     if out is None:
         out = torch.empty((n, feat), dtype=torch.float32, device=wh.device)
@@ -268,7 +280,7 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
     mid, short = plan.gat_split(g.rowptr, GAT_SHORT_MAX_DEG)
     stream = _lib.stream_handle(wh.device)
     args = (n, wh.data_ptr(), wh.stride(0), heads, fh,
-            el.data_ptr(), er.data_ptr(), heads, float(negative_slope), int(mode), _lib.ptr(fill),
+            el.data_ptr(), er.data_ptr(), lde, float(negative_slope), int(mode), _lib.ptr(fill),
             float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), out.stride(0),
             plan.seg_len, *pa[:6], pa[6], pa[7], pa[9],
             mid.data_ptr() if mid.numel() else pa[10], mid.numel(),

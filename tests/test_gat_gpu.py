@@ -339,6 +339,30 @@ def test_gat_project_mfma_vs_oracle(dev, n, k, heads, fh):
     close(el.cpu().numpy(), el_o)
 
 
+def test_gat_project_packed_layout_bitexact(dev):
+    """gat_project(packed=True): Wh / er / el as views of one [n, H*Fh + 2H] buffer; the
+    aggregation over them (el / er row stride H*Fh + 2H) gives the same bits."""
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_project
+    n, H, fh, k = 3000, 8, 8, 64
+    rowptr, col = _rand_csr(n, 8 * n, 11, hub=2000)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.ones(col.size, device=dev), n, n)
+    x = torch.randn(n, k, device=dev)
+    w = torch.randn(k, H * fh, device=dev) * 0.2
+    a_s, a_d = torch.randn(H * fh, device=dev) * 0.3, torch.randn(H * fh, device=dev) * 0.3
+    p0 = gat_project(x, w, H, fh, a_s, a_d)
+    p1 = gat_project(x, w, H, fh, a_s, a_d, packed=True)
+    assert p1[0].stride(0) == H * fh + 2 * H and p1[1].stride(0) == H * fh + 2 * H
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)
+    for mode in (GAT_DENSE, GAT_SPARSE):
+        for hubs in (0, 100):
+            r0 = gat_aggregate(g, *p0, H, fh, 0.2, mode, "elu", seg_len=32, hubs=hubs)
+            r1 = gat_aggregate(g, *p1, H, fh, 0.2, mode, "elu", seg_len=32, hubs=hubs)
+            assert torch.equal(r0, r1), (mode, hubs)
+
+
 def test_gat_project_unsupported_shapes_fall_back(dev):
     from graphneuralnetwork_amd.ops import gat_project
     x = torch.randn(10, 48, device=dev)
