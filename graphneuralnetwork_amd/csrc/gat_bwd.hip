@@ -256,13 +256,6 @@ __global__ __launch_bounds__(kBw) void gat_bwd_node_kernel(BwdNodeParams P) {
     hid[ch] = f < P.feat ? static_cast<int>(f / P.fh) : 0;
     acc[ch] = vzero<VW>();
   }
-  // der_j: lanes = (edge, head)
-  float dsum = 0.f;
-  if (ah < P.H) {
-    for (int64_t b = beg + ae; b < end; b += EPP) dsum += P.ds_edge[P.eid_t[b] * P.H + ah];
-  }
-#pragma unroll
-  for (int o = HP; o < kWave; o <<= 1) dsum += __shfl_xor(dsum, o, kWave);
   // sum_i w_ij dout_i: lanes = features, EPI edge slots
   for (int64_t b = beg; b < end; b += EPI * U) {
     typename Vec<VW>::T xv[U][NCH];
@@ -293,11 +286,33 @@ __global__ __launch_bounds__(kBw) void gat_bwd_node_kernel(BwdNodeParams P) {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) acc[ch] += shfl_xor_f(acc[ch], o);
   }
+  // der_j = sum_i ds_ij: lanes = (edge, head), HP heads per pass (any head count)
+  float* pr = is_seg ? P.part + wave * P.ldp : nullptr;
   float derh[NCH];
 #pragma unroll
-  for (int ch = 0; ch < NCH; ++ch) derh[ch] = __shfl(dsum, hid[ch], kWave);
+  for (int ch = 0; ch < NCH; ++ch) derh[ch] = 0.f;
+  for (int64_t h0 = 0; h0 < P.H; h0 += HP) {
+    const int64_t hh = h0 + ah;
+    float dsum = 0.f;
+    if (hh < P.H) {
+      for (int64_t b = beg + ae; b < end; b += EPP) dsum += P.ds_edge[P.eid_t[b] * P.H + hh];
+    }
+#pragma unroll
+    for (int o = HP; o < kWave; o <<= 1) dsum += __shfl_xor(dsum, o, kWave);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int64_t rel = hid[ch] - h0;
+      const float v = __shfl(dsum, static_cast<int>(rel & (HP - 1)), kWave);
+      if (rel >= 0 && rel < HP) derh[ch] = v;
+    }
+    if (lane < HP && hh < P.H) {
+      if (is_seg)
+        pr[P.feat + hh] = dsum;
+      else
+        P.der[j * P.H + hh] = dsum;
+    }
+  }
   if (is_seg) {
-    float* pr = P.part + wave * P.ldp;
     if (lane < LPR) {
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
@@ -305,10 +320,8 @@ __global__ __launch_bounds__(kBw) void gat_bwd_node_kernel(BwdNodeParams P) {
         if (f < P.feat) vstore<VW>(pr + f, acc[ch]);
       }
     }
-    if (lane < HP && ah < P.H) pr[P.feat + ah] = dsum;
     return;
   }
-  if (lane < HP && ah < P.H) P.der[j * P.H + ah] = dsum;
   if (lane < LPR) node_epilogue<VW, LPR, NCH>(P, j, sub, hid, acc, derh);
 }
 
@@ -509,9 +522,9 @@ extern "C" int gnn_gat_backward_nodes_f32(
     int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
     const int32_t* long_row, const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows,
     int64_t n_rows_list, float* part, void* stream) {
-  if (n_nodes < 0 || heads < 1 || heads > 8 || fh < 1 || n_seg < 0 || n_long < 0 ||
-      n_rows_list < 0 || seg_len < 1)
-    return heads > 8 ? GNN_E_UNSUPPORTED : GNN_E_ARG;
+  if (n_nodes < 0 || heads < 1 || fh < 1 || n_seg < 0 || n_long < 0 || n_rows_list < 0 ||
+      seg_len < 1)
+    return GNN_E_ARG;
   if (n_nodes == 0) return GNN_OK;
   if (!rowptr_t || !dout || !w_edge || !ds_edge || !del || !a_src || !a_dst || !dwh || !der)
     return GNN_E_ARG;

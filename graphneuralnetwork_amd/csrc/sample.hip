@@ -5,9 +5,11 @@
 //   deg <= k : random.choices(neighs, k)  -- k draws with replacement
 //   deg == 0 : the reference raises IndexError (random.choices of an empty list)
 // for a whole frontier at once, one thread per frontier node, with a
-// counter-based hash RNG keyed by (seed, node, draw) instead of CPython's
-// Mersenne Twister (the reference sampler is unseeded, so only the
-// distribution -- not the exact draw -- is reproducible).
+// counter-based hash RNG keyed by (seed, position in `nodes`, draw) instead of
+// CPython's Mersenne Twister (the reference sampler is unseeded, so only the
+// distribution -- not the exact draw -- is reproducible). Keying by position, not
+// node id, makes a node listed twice draw two independent neighbour lists, as the
+// reference's sequential draws do; the host derives `seed` per (batch seed, layer).
 // Without replacement uses Robert Floyd's algorithm: k iterations, each a
 // uniform draw and a membership test against the <= k picks so far.
 #include "common.hpp"
@@ -22,8 +24,8 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 }
 
 // uniform integer in [0, n) (n < 2^32 on this path; Lemire's multiply-shift)
-__device__ __forceinline__ int64_t uniform_below(uint64_t seed, int64_t node, int64_t draw, int64_t n) {
-  const uint64_t r = mix64(seed ^ mix64(static_cast<uint64_t>(node) * 0x100000001b3ull +
+__device__ __forceinline__ int64_t uniform_below(uint64_t seed, int64_t pos, int64_t draw, int64_t n) {
+  const uint64_t r = mix64(seed ^ mix64(static_cast<uint64_t>(pos) * 0x100000001b3ull +
                                         static_cast<uint64_t>(draw)));
   if (n <= 0xffffffffll) return static_cast<int64_t>(((r >> 32) * static_cast<uint64_t>(n)) >> 32);
   return static_cast<int64_t>(r % static_cast<uint64_t>(n));
@@ -55,13 +57,13 @@ __global__ __launch_bounds__(256) void sample_kernel(const int64_t* __restrict__
     return;
   }
   if (deg <= k) {  // random.choices: k independent draws
-    for (int64_t j = 0; j < k; ++j) o[j] = col[b + uniform_below(seed, v, j, deg)];
+    for (int64_t j = 0; j < k; ++j) o[j] = col[b + uniform_below(seed, i, j, deg)];
     return;
   }
   // random.sample: Floyd -- positions chosen so far live in o[] (as offsets, then mapped)
   int64_t cnt = 0;
   for (int64_t j = deg - k; j < deg; ++j) {
-    const int64_t t = uniform_below(seed, v, j, j + 1);
+    const int64_t t = uniform_below(seed, i, j, j + 1);
     bool seen = false;
     for (int64_t q = 0; q < cnt; ++q) seen |= (o[q] == t);
     o[cnt++] = seen ? j : t;

@@ -396,6 +396,20 @@ def build_cover_exchange_balanced(g: CsrGraph, rank: int, world: int, group=None
     return best, history
 
 
+def _overlaps(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Whether the byte ranges spanned by the views a and b intersect."""
+    if a.device != b.device:
+        return False
+
+    def span(t):
+        last = sum((n - 1) * st for n, st in zip(t.shape, t.stride()))
+        return t.data_ptr(), t.data_ptr() + (last + 1) * t.element_size()
+
+    a0, a1 = span(a)
+    b0, b1 = span(b)
+    return a0 < b1 and b0 < a1
+
+
 class EdgeCutSpmm:
     """Y_own = (A X)[own rows] (+ bias) for one rank of the edge-cut, halo exchange overlapped.
 
@@ -425,7 +439,10 @@ class EdgeCutSpmm:
         else:
             self.send_buf = torch.empty((sum(part.send_counts), feat), **f32)
             self.recv_buf = torch.empty((part.n_halo, feat), **f32)
-        self.out = torch.empty((part.n_own, feat), **f32)
+        # two output buffers used in turn, so a result fed back as the next call's x
+        # (stacked layers of one width) is never the buffer that call writes
+        self._outs = [torch.empty((part.n_own, feat), **f32) for _ in range(2)]
+        self._turn = 0
         self.cuda = self.device.type == "cuda"
         self.comm_stream = torch.cuda.Stream(self.device) if self.cuda else None
 
@@ -446,11 +463,26 @@ class EdgeCutSpmm:
         if ev is not None:
             cur.wait_event(ev)
 
+    @property
+    def out(self) -> torch.Tensor:
+        """The buffer the most recent call wrote."""
+        return self._outs[self._turn ^ 1]
+
     def __call__(self, x: torch.Tensor, bias: torch.Tensor | None = None,
-                 activation: str | None = None) -> torch.Tensor:
+                 activation: str | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Returns ``out`` if given, else one of two internal buffers used in turn: an
+        internal result stays valid until the call after next overwrites it."""
         p = self.part
         if x.shape != (p.n_own, self.feat):
             raise ValueError("x must be this rank's [n_own, feat] feature rows")
+        if out is None:
+            out = self._outs[self._turn]
+            self._turn ^= 1
+        elif out.shape != (p.n_own, self.feat) or out.dtype != torch.float32:
+            raise ValueError("out must be float32 [n_own, feat]")
+        if x.numel() and out.numel() and _overlaps(x, out):
+            raise ValueError("x and the output buffer overlap: the interior SpMM would read "
+                             "rows it is writing")
         cur = torch.cuda.current_stream(self.device) if self.cuda else None
         if self.cover:
             ev_x = ev_p = None
@@ -464,28 +496,28 @@ class EdgeCutSpmm:
                     self._spmm(p.send_p, x, None, out=self.send_p)  # partial sums for peers
                 ev_p = self._exchange(self.recv_p, self.send_p, p.recv_p_counts,
                                       p.send_p_counts, cur)
-            self._spmm(p.interior, x, bias, out=self.out)           # overlaps both exchanges
+            self._spmm(p.interior, x, bias, out=out)           # overlaps both exchanges
             last = "p" if p.any_p else ("x" if p.any_x else None)
             if p.any_x:
                 self._wait(ev_x, cur)
-                self._spmm(p.halo_x, self.recv_x, None, out=self.out, accumulate=True,
+                self._spmm(p.halo_x, self.recv_x, None, out=out, accumulate=True,
                            activation=activation if last == "x" else None)
             if p.any_p:
                 self._wait(ev_p, cur)
-                self._spmm(p.halo_p, self.recv_p, None, out=self.out, accumulate=True,
+                self._spmm(p.halo_p, self.recv_p, None, out=out, accumulate=True,
                            activation=activation)
             if last is None and activation is not None:
-                self._spmm(p.halo_x, self.recv_x, None, out=self.out, accumulate=True,
+                self._spmm(p.halo_x, self.recv_x, None, out=out, accumulate=True,
                            activation=activation)
-            return self.out
+            return out
         if p.send_idx.numel():
             self._gather(x, p.send_idx, self.send_buf)
         ev = self._exchange(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts, cur)
-        self._spmm(p.interior, x, bias, out=self.out)               # overlaps the exchange
+        self._spmm(p.interior, x, bias, out=out)               # overlaps the exchange
         self._wait(ev, cur)
-        self._spmm(p.halo, self.recv_buf, None, activation=activation, out=self.out,
+        self._spmm(p.halo, self.recv_buf, None, activation=activation, out=out,
                    accumulate=True)
-        return self.out
+        return out
 
 
 def extended_graph(part: EdgeCutPartition) -> CsrGraph:

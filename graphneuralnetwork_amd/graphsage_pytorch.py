@@ -160,5 +160,5 @@ def multihop_sampling(src_nodes, sample_nums, adj: CsrGraph, seed: int = 0):
     from .sampler import sample_neighbors
     hops = [torch.as_tensor(src_nodes, dtype=torch.int64, device=adj.device).reshape(-1)]
     for k, n in enumerate(sample_nums):
-        hops.append(sample_neighbors(adj, hops[k], int(n), seed + k).reshape(-1))
+        hops.append(sample_neighbors(adj, hops[k], int(n), seed, layer=k).reshape(-1))
     return hops

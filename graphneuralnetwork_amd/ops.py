@@ -67,6 +67,8 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
     ``hubs`` = number of highest-degree rows of X staged into a compact table before
     the gather (0: none; default ``hub_rows_for``). It changes speed, not results.
     """
+    if accumulate and out is None:  # checked first: it is a usage error on any device
+        raise ValueError("accumulate=True needs `out` (it adds into the caller's buffer)")
     _require_device(g.rowptr, x, bias, out)
     x = _rows_f32(x, "X")
     if x.shape[0] != g.n_cols:
@@ -80,8 +82,6 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
         out = torch.empty((g.n_rows, feat), dtype=torch.float32, device=x.device)
     elif out.shape != (g.n_rows, feat) or out.stride(1) != 1 or out.dtype != torch.float32:
         raise ValueError("out must be float32 [n_rows, features] with unit column stride")
-    if accumulate and out is None:
-        raise ValueError("accumulate=True needs `out`")
     if g.n_rows == 0 or feat == 0:
         return out
     plan = g.plan(seg_len if seg_len is not None else seg_len_for(feat))
@@ -309,6 +309,14 @@ SAGE_MODES = {"MEAN": 0, "MAX": 1}   # GraphSAGE/graph_utils.py Aggregator
 SAGE_KINDS = {"MEAN": 0, "MAX": 1, "SUM": 2}   # + NeighborAggregator 'sum' (GraphSAGE_Pytorch)
 
 
+_EMPTY_FILL = {0: float("nan"), 2: 0.0}  # k == 0: torch.mean -> NaN, torch.sum -> 0
+
+
+def _empty_reduction(mode: int) -> None:
+    if mode == 1:  # torch.argmax over an empty dim raises
+        raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
+
+
 def _sage_out(M, F, mode, dev):
     dt = torch.int64 if mode == 1 else torch.float32
     return torch.empty((M, F), dtype=dt, device=dev)
@@ -327,9 +335,8 @@ def sage_aggregate(neigh: torch.Tensor, agg_func: str = "MEAN") -> torch.Tensor:
     M, k, F = neigh.shape
     mode = SAGE_KINDS[agg_func]
     if k == 0:
-        if mode == 1:
-            raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
-        return torch.full((M, F), 0.0 if mode == 2 else float("nan"), device=neigh.device)
+        _empty_reduction(mode)
+        return torch.full((M, F), _EMPTY_FILL[mode], device=neigh.device)
     out = _sage_out(M, F, mode, neigh.device)
     lib = _lib.load()
     _lib.check(lib.gnn_sage_aggregate_f32(neigh.data_ptr(), neigh.stride(1), neigh.stride(0), M, k,
@@ -383,11 +390,10 @@ def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str 
     M, k = idx.shape
     F = table.shape[1]
     mode = SAGE_KINDS[agg_func]
-    if k == 0:
-        if mode == 1:
-            raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
-        return torch.full((M, F), 0.0 if mode == 2 else float("nan"), device=table.device)
     out = _sage_dst(out, M, F, mode, table.device)
+    if k == 0:  # torch.mean over an empty dim is NaN, sum is 0; the caller's view is filled
+        _empty_reduction(mode)
+        return out.fill_(_EMPTY_FILL[mode])
     err = _err_flag(table.device, check)
     lib = _lib.load()
     _lib.check(lib.gnn_sage_gather_aggregate_f32(
@@ -464,15 +470,12 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
     part = torch.empty((max(pt.n_seg, 1), feat + heads), dtype=torch.float32, device=dev)
     a_src = a_src.contiguous().float()
     a_dst = a_dst.contiguous().float()
-    for h0 in range(0, heads, 8):  # the node pass takes <= 8 heads per call
-        hg = min(8, heads - h0)
-        if hg != heads:
-            raise NotImplementedError("GAT backward with more than 8 heads")
-        _lib.check(lib.gnn_gat_backward_nodes_f32(
-            rowptr_t.data_ptr(), src_t.data_ptr(), eid_t.data_ptr(), n, heads, fh,
-            dout.data_ptr(), w_edge.data_ptr(), ds_edge.data_ptr(), dl.data_ptr(),
-            a_src.data_ptr(), a_dst.data_ptr(), dwh.data_ptr(), der.data_ptr(), pt.seg_len,
-            _lib.ptr(pt.seg_row), _lib.ptr(pt.seg_begin), pt.n_seg, _lib.ptr(pt.long_row),
-            pt.long_seg_ptr.data_ptr(), pt.n_long, _lib.ptr(rows_t), rows_t.numel(),
-            part.data_ptr(), stream), "gnn_gat_backward_nodes_f32")
+    # one node pass for every head (the kernel sums der over groups of 8 heads itself)
+    _lib.check(lib.gnn_gat_backward_nodes_f32(
+        rowptr_t.data_ptr(), src_t.data_ptr(), eid_t.data_ptr(), n, heads, fh,
+        dout.data_ptr(), w_edge.data_ptr(), ds_edge.data_ptr(), dl.data_ptr(),
+        a_src.data_ptr(), a_dst.data_ptr(), dwh.data_ptr(), der.data_ptr(), pt.seg_len,
+        _lib.ptr(pt.seg_row), _lib.ptr(pt.seg_begin), pt.n_seg, _lib.ptr(pt.long_row),
+        pt.long_seg_ptr.data_ptr(), pt.n_long, _lib.ptr(rows_t), rows_t.numel(),
+        part.data_ptr(), stream), "gnn_gat_backward_nodes_f32")
     return dwh, dout, dl, der

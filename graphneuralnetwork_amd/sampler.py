@@ -28,8 +28,30 @@ from .graph import CsrGraph
 from .graphsage import Gathered, trust_map
 
 
-def sample_neighbors(adj: CsrGraph, nodes: torch.Tensor, k: int, seed: int = 0) -> torch.Tensor:
-    """[len(nodes), k] int64 sampled neighbour ids (random.sample / random.choices rule)."""
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z: int) -> int:
+    """splitmix64 finaliser (the same mix the device RNG applies)."""
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def stream_seed(seed: int, layer: int) -> int:
+    """The device RNG key of one (batch seed, layer) pair: hashed, so batch s's layer 1
+    and batch s+1's layer 0 draw independently (seed + layer would collide)."""
+    return _mix64(_mix64(int(seed) & _M64) ^ ((int(layer) * 0xD1B54A32D192ED03) & _M64))
+
+
+def sample_neighbors(adj: CsrGraph, nodes: torch.Tensor, k: int, seed: int = 0,
+                     layer: int = 0) -> torch.Tensor:
+    """[len(nodes), k] int64 sampled neighbour ids (random.sample / random.choices rule).
+
+    Draws are keyed by (stream_seed(seed, layer), position in ``nodes``, draw): a node
+    listed twice gets two independent neighbour lists, like the reference's sequential
+    draws from one generator (GraphSAGE/data_utils.py:89-94)."""
     if not adj.rowptr.is_cuda:
         raise RuntimeError("sampling runs on the ROCm device only (no CPU fallback)")
     nodes = nodes.to(device=adj.device, dtype=torch.int64).contiguous()
@@ -38,7 +60,7 @@ def sample_neighbors(adj: CsrGraph, nodes: torch.Tensor, k: int, seed: int = 0) 
     lib = _lib.load()
     _lib.check(lib.gnn_sample_neighbors(adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.n_rows,
                                         nodes.data_ptr(), nodes.numel(), k,
-                                        int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(),
+                                        stream_seed(seed, layer), out.data_ptr(),
                                         err.data_ptr(), _lib.stream_handle(adj.device)),
                "gnn_sample_neighbors")
     e = int(err.item())
@@ -73,11 +95,11 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
     if len(fanouts) != 2:
         raise NotImplementedError("two-layer sampling (the reference's num_layers=2 runs)")
     seeds = seeds.to(device=adj.device, dtype=torch.int64)
-    nb0 = sample_neighbors(adj, seeds, fanouts[0], seed)
+    nb0 = sample_neighbors(adj, seeds, fanouts[0], seed, layer=0)
     if gcn:  # the reference appends the node itself (data_utils.py:95-96)
         nb0 = torch.cat([nb0, seeds[:, None]], dim=1)
     s1 = torch.unique(torch.cat([seeds, nb0.reshape(-1)]))
-    nb1 = sample_neighbors(adj, s1, fanouts[1], seed + 1)
+    nb1 = sample_neighbors(adj, s1, fanouts[1], seed, layer=1)
     if gcn:
         nb1 = torch.cat([nb1, s1[:, None]], dim=1)
     return SampledBatch(seeds, s1, nb1, torch.searchsorted(s1, seeds),

@@ -253,7 +253,7 @@ int gnn_col_mean_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t feat, 
  * nodes: over the transposed CSR (rowptr_t, src_t = source row, eid_t = CSR edge id)
  *        with its own plan: dwh[j] = sum_e w_edge[e,h] dout_i + der_j a_dst + del_j a_src,
  *        der[j,h] = sum_e ds_edge[e,h] (part [n_seg_t, heads*fh + heads] workspace);
- *        heads <= 8 per call.
+ *        any head count (der is reduced 8 heads per pass inside the kernel).
  * The dropout mask is recomputed from (dropout_seed, edge, head) exactly as the forward drew it.
  */
 int gnn_gat_backward_prep_f32(const float* dy, const float* y, int64_t ldo, int64_t n_rows,
@@ -322,8 +322,10 @@ int gnn_gather_rows_f32(const float* x, int64_t ldx, int64_t n_x, const int64_t*
  *     deg <= k: k draws with replacement (random.choices);
  *     deg == 0: row of -1 and *err_flag |= 1 (the reference raises IndexError);
  *   node id outside [0, n_graph): row of -1, *err_flag |= 2.
- * Draws come from a counter-based hash RNG keyed by (seed, node, draw): a
- * frontier is reproducible for a given seed. k <= 256.
+ * Draws come from a counter-based hash RNG keyed by (seed, i, draw), i = the position
+ * in `nodes`: a frontier is reproducible for a given seed, and a node listed twice
+ * draws independently. Callers derive `seed` per (batch seed, layer) with a hash
+ * (sampler.stream_seed), never seed + layer. k <= 256.
  */
 int gnn_sample_neighbors(const int64_t* rowptr, const int32_t* col, int64_t n_graph,
                          const int64_t* nodes, int64_t n, int64_t k, uint64_t seed, int64_t* out,

@@ -87,8 +87,19 @@ def _worker(rank, world, port, n, F, q, kind="gather"):
         b = torch.arange(F, dtype=torch.float32) / F
         r0, r1 = part.bounds[rank], part.bounds[rank + 1]
         run = EdgeCutSpmm(part, F, "cpu", spmm=_cpu_spmm, gather=_cpu_gather)
-        y = run(X[r0:r1].contiguous(), b, activation="relu").clone()
-        q.put((rank, r0, r1, y.numpy(), edges, part.n_halo, part.send_counts, part.recv_counts))
+        y_t = run(X[r0:r1].contiguous(), b, activation="relu")
+        y = y_t.clone()
+        # stacked layers: the result fed straight back as x lands in the other buffer
+        y2 = run(y_t, b, activation="relu").clone()
+        assert torch.equal(y_t, y), "the previous result was overwritten by the next call"
+        try:
+            run(y_t, b, out=y_t)
+            aliased = False
+        except ValueError:
+            aliased = True
+        assert aliased, "x aliasing the output buffer must be rejected"
+        q.put((rank, r0, r1, (y.numpy(), y2.numpy()), edges, part.n_halo, part.send_counts,
+               part.recv_counts))
     finally:
         dist.destroy_process_group()
 
@@ -110,14 +121,17 @@ def test_edge_cut_matches_single_device(world, kind):
         assert p.exitcode == 0
     g = _graph(n, 3)
     X = np.random.default_rng(0).standard_normal((n, F)).astype(np.float32)
-    ref = np.maximum(O.spmm_csr(g.rowptr.numpy(), g.col.numpy(), g.val.numpy(), X,
-                                np.arange(F, dtype=np.float32) / F), 0)
-    res.sort()
+    bias = np.arange(F, dtype=np.float32) / F
+    ref = np.maximum(O.spmm_csr(g.rowptr.numpy(), g.col.numpy(), g.val.numpy(), X, bias), 0)
+    ref2 = np.maximum(O.spmm_csr(g.rowptr.numpy(), g.col.numpy(), g.val.numpy(),
+                                 ref.astype(np.float32), bias), 0)
+    res.sort(key=lambda t: t[0])
     covered = 0
     tot_nnz = 0
     sends = {}
-    for rank, r0, r1, y, nnz, n_halo, sc, rc in res:
+    for rank, r0, r1, (y, y2), nnz, n_halo, sc, rc in res:
         np.testing.assert_allclose(y, ref[r0:r1], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(y2, ref2[r0:r1], rtol=1e-4, atol=1e-5)
         covered += r1 - r0
         tot_nnz += nnz
         sends[rank] = (sc, rc)

@@ -41,3 +41,22 @@ def test_graphsage_aggregator_rejects_unknown_mode(capsys):
     with pytest.raises(RuntimeError):
         Aggregator(torch.randn(2, 3, 4), "SUM")
     assert "请选择合适的聚合函数" in capsys.readouterr().out
+
+
+def test_sampler_stream_seeds_do_not_collide():
+    """Per-(batch seed, layer) RNG keys are hashed: seed + layer would make batch s's
+    layer 1 equal batch s+1's layer 0."""
+    from graphneuralnetwork_amd.sampler import stream_seed
+    keys = {stream_seed(s, layer) for s in range(200) for layer in range(4)}
+    assert len(keys) == 800
+
+
+def test_spmm_accumulate_needs_out():
+    """accumulate=True adds into the caller's buffer: without one it is a usage error
+    (the check sat after the allocation and never fired)."""
+    import torch
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.ops import spmm_forward
+    g = CsrGraph(torch.tensor([0, 1]), torch.tensor([0], dtype=torch.int32), torch.ones(1), 1, 1)
+    with pytest.raises(ValueError, match="accumulate"):
+        spmm_forward(g, torch.ones(1, 4), accumulate=True)

@@ -196,10 +196,12 @@ def _torch_gat(Wh, a_src, a_dst, mask, H, fh, slope, sparse, elu):
     return torch.nn.functional.elu(out) if elu else out
 
 
-@pytest.mark.parametrize("heads,fh", [(8, 8), (1, 7), (3, 4), (2, 16)])
+@pytest.mark.parametrize("heads,fh", [(8, 8), (1, 7), (3, 4), (2, 16), (12, 4), (17, 2)])
 @pytest.mark.parametrize("sparse", [False, True])
 @pytest.mark.parametrize("seg_len", [None, 16])
 def test_gat_backward_vs_torch(dev, heads, fh, sparse, seg_len):
+    """Every head count trains: more than 8 heads run the edge pass in groups of 8 and
+    reduce der 8 heads per pass inside the node kernel (>8 heads used to raise)."""
     from graphneuralnetwork_amd.gat import _GatLayerFn
     from graphneuralnetwork_amd.graph import CsrGraph
     from graphneuralnetwork_amd import graph as graph_mod

@@ -72,3 +72,22 @@ def test_batch_maps_and_gathered_forward(dev):
         e2, c2 = net(*pre, None, None, None, None, None)
     torch.testing.assert_close(e1, e2, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(c1, c2, rtol=1e-5, atol=1e-5)
+
+
+def test_duplicate_nodes_and_layers_draw_independently(dev):
+    """A node listed twice gets two independent neighbour lists, and batch s's layer 1
+    does not replay batch s+1's layer 0 (the RNG was keyed by node and
+    seed + layer)."""
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.sampler import sample_neighbors
+    deg = 1000
+    rowptr = torch.tensor([0, deg], dtype=torch.int64, device=dev)
+    col = torch.arange(deg, dtype=torch.int32, device=dev)
+    g = CsrGraph(rowptr, col, torch.ones(deg, device=dev), 1, deg)
+    nodes = torch.zeros(4, dtype=torch.int64, device=dev)
+    out = sample_neighbors(g, nodes, 10, seed=5).cpu().numpy()
+    rows = {tuple(r) for r in out.tolist()}
+    assert len(rows) == 4  # 10 of 1000: identical rows by chance have probability ~1e-30
+    a = sample_neighbors(g, nodes[:1], 10, seed=5, layer=1).cpu().numpy()
+    b = sample_neighbors(g, nodes[:1], 10, seed=6, layer=0).cpu().numpy()
+    assert not np.array_equal(a, b)
