@@ -54,6 +54,18 @@ def _compile_cmd(hipcc: str, src: Path, obj: Path, extra=()) -> list[str]:
     return [hipcc, *HIPCC_FLAGS, *extra, "-c", str(src), "-o", str(obj)]
 
 
+# Only the C-ABI (gnn_*) leaves the library. Everything else -- the kernels' host stubs
+# above all, which are weak template instantiations -- binds inside the library, so a
+# second build of the same sources loaded into the process (build_variant, the A/B tools)
+# launches its OWN kernels instead of being interposed by the first library's.
+EXPORT_MAP = CSRC_DIR / "exports.map"
+
+
+def _link_cmd(hipcc: str, out: Path, objs) -> list[str]:
+    return [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread",
+            f"-Wl,--version-script={EXPORT_MAP}", "-o", str(out), *map(str, objs)]
+
+
 def _stale(target: Path, deps: list[Path]) -> bool:
     if not target.exists():
         return True
@@ -87,35 +99,43 @@ def build(force: bool = False, verbose: bool = False) -> Path:
             print(out, file=sys.stderr)
     if failed:
         raise RuntimeError("hipcc failed:\n" + "\n".join(failed))
-    if force or procs or _stale(LIB_PATH, objs):
+    if force or procs or _stale(LIB_PATH, objs + [EXPORT_MAP]):
         tmp = LIB_PATH.with_suffix(".so.tmp")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(tmp),
-               *map(str, objs)]
-        r = subprocess.run(cmd, capture_output=True, text=True)
+        r = subprocess.run(_link_cmd(hipcc, tmp, objs), capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
         os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
 
-def build_variant(tag: str, defines: list[str]) -> Path:
-    """Kernel-tuning build: every source with extra ``-D`` flags, linked into
-    ``lib/variants/libgnn_<tag>.so`` (same C-ABI; used by tools/*_ab.py only)."""
+def build_variant(tag: str, defines: list[str], only: list[str] | None = None) -> Path:
+    """Kernel-tuning build: the sources with extra ``-D`` flags, linked into
+    ``lib/variants/libgnn_<tag>.so`` (same C-ABI; used by tools/*_ab.py only).
+    ``only``: compile just these csrc file names with the defines and link the main
+    build's objects for the rest (the main library must be built)."""
+    if only:
+        build()
     odir = OBJ_DIR / "variants" / tag
     odir.mkdir(parents=True, exist_ok=True)
     out = LIB_DIR / "variants" / f"libgnn_{tag}.so"
     out.parent.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
+    headers = sorted(CSRC_DIR.glob("*.hpp")) + [HEADER]
+    stamp = odir / "defines.txt"
+    same = stamp.exists() and stamp.read_text() == "\n".join(defines)
     procs = [(src, subprocess.Popen(_compile_cmd(hipcc, src, odir / (src.stem + ".o"),
                                                  [f"-D{d}" for d in defines]),
                                     stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
-             for src in sources()]
+             for src in sources()
+             if (not only or src.name in only)
+             and (not same or _stale(odir / (src.stem + ".o"), [src] + headers))]
     failed = [f"--- {src.name} ---\n{p.communicate()[0]}" for src, p in procs if p.wait() != 0]
     if failed:
         raise RuntimeError("hipcc failed:\n" + "\n".join(failed))
-    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(out),
-                        *(str(odir / (src.stem + ".o")) for src in sources())],
-                       capture_output=True, text=True)
+    stamp.write_text("\n".join(defines))
+    objs = [(odir if not only or src.name in only else OBJ_DIR) / (src.stem + ".o")
+            for src in sources()]
+    r = subprocess.run(_link_cmd(hipcc, out, objs), capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
     return out

@@ -117,14 +117,23 @@ __device__ __forceinline__ const float* wh_row(const GatParams& P, int c) {
                : P.wh + static_cast<int64_t>(c) * P.ldw;
 }
 __device__ __forceinline__ float er_at(const GatParams& P, int c, int h) {
+#if defined(GNN_GAT_ER_PROBE)
+  // timing probe only (tools/gat_ab.py "erprobe"): every er read hits row 0 -- the cost of
+  // the per-edge er gather, measured by its absence; results are wrong by construction
+  (void)c;
+  return P.er[h];
+#else
   return c < 0 ? P.erh[static_cast<int64_t>(-1 - c) * P.ldeh + h]
                : P.er[static_cast<int64_t>(c) * P.lde + h];
+#endif
 }
 
 #ifndef GNN_GAT_SMALL_UNROLL
-// edgeless / one-edge rows per slot per wave at NCH = 1 (halved per doubling of NCH);
-// A/B at cfg3 (tools/gat_ab.py, profiles/r01h_gat_small_ab.log): 16 vs 4: 0.797 -> 0.766 ms
-#define GNN_GAT_SMALL_UNROLL 16
+// edgeless / one-edge rows per slot per wave at NCH = 1 (halved per doubling of NCH). The
+// unrolled loads set the register budget of the whole gat_csr_kernel: 16 took 129 VGPRs
+// (3 waves/SIMD), 4 takes 58-66 (7-8). A/B with isolated variant libraries at cfg3
+// (tools/gat_ab.py, profiles/r02f_gat_ab.log): 1.295 -> 0.791 ms (with GNN_GAT_U = 4).
+#define GNN_GAT_SMALL_UNROLL 4
 #endif
 constexpr int kGatSmallUnroll = GNN_GAT_SMALL_UNROLL;
 template <int NCH>
@@ -132,7 +141,7 @@ constexpr int gat_small_unroll() {
   return kGatSmallUnroll / NCH >= 2 ? kGatSmallUnroll / NCH : 2;
 }
 #ifndef GNN_GAT_U
-#define GNN_GAT_U 2  // feature-row gathers in flight per lane in phase B (A/B: tools/gat_ab.py)
+#define GNN_GAT_U 4  // feature-row gathers in flight per lane in phase B (capped at the chunk's slots)
 #endif
 #ifndef GNN_GAT_PIPE
 #define GNN_GAT_PIPE 1  // pipelined chunk loop in gat_csr_kernel (A/B: tools/gat_ab.py)

@@ -34,10 +34,12 @@ namespace gnn {
 constexpr int kBlock = 256;                 // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
 #ifndef GNN_SPMM_SMALL_UNROLL
-// small rows per slot per wave at NCH = 1 (halved per doubling of NCH). A/B with hub
-// staging (tools/lib_ab.py, profiles/r01f_lib_ab_*): 16 vs 4 took cfg2 1.164 -> 1.082 ms,
-// the north star 14.54 -> 13.76 ms, F=256 29.7 -> 28.3 ms (with the longer segments)
-#define GNN_SPMM_SMALL_UNROLL 16
+// small rows per slot per wave at NCH = 1 (halved per doubling of NCH). The unrolled loads
+// set the register budget of the WHOLE kernel (one launch for every row class): 16 took
+// 134 VGPRs = 3 waves/SIMD, 4 takes 48 = 8 waves/SIMD. A/B with isolated variant libraries
+// (tools/lib_ab.py, profiles/r02e_lib_ab_*): cfg2 1.574 -> 1.128 ms, the north star
+// 18.73 -> 14.55 ms; 2 is the same, 32 spills (4x slower).
+#define GNN_SPMM_SMALL_UNROLL 4
 #endif
 #ifndef GNN_SPMM_U
 #define GNN_SPMM_U 4  // slot loads in flight per lane for one-chunk rows (A/B: tools/lib_ab.py)

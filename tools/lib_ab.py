@@ -40,9 +40,19 @@ VARIANTS = {
     "s16u2": ["GNN_SPMM_SMALL_UNROLL=16", "GNN_SPMM_U=2"],
     "small32": ["GNN_SPMM_SMALL_UNROLL=32"],
     "small4": ["GNN_SPMM_SMALL_UNROLL=4"],
+    "s2": ["GNN_SPMM_SMALL_UNROLL=2"],
+    "s4u8": ["GNN_SPMM_SMALL_UNROLL=4", "GNN_SPMM_U=8"],
+    "s2u8": ["GNN_SPMM_SMALL_UNROLL=2", "GNN_SPMM_U=8"],
+    "s4u6": ["GNN_SPMM_SMALL_UNROLL=4", "GNN_SPMM_U=6"],
+    "s4u12": ["GNN_SPMM_SMALL_UNROLL=4", "GNN_SPMM_U=12"],
+    "s4u16": ["GNN_SPMM_SMALL_UNROLL=4", "GNN_SPMM_U=16"],
+    "sp4u8": ["GNN_SPMM_SMALL_SPLIT=1", "GNN_SPMM_SMALL_SPLIT_UNROLL=4", "GNN_SPMM_U=8"],
+    "sp8u8": ["GNN_SPMM_SMALL_SPLIT=1", "GNN_SPMM_SMALL_SPLIT_UNROLL=8", "GNN_SPMM_U=8"],
+    "sp16u8": ["GNN_SPMM_SMALL_SPLIT=1", "GNN_SPMM_SMALL_SPLIT_UNROLL=16", "GNN_SPMM_U=8"],
     "su2": ["GNN_SAGE_U=2"],
     "su8": ["GNN_SAGE_U=8"],
     "su16": ["GNN_SAGE_U=16"],
+    "su4": ["GNN_SAGE_U=4"],
 }
 
 
@@ -53,6 +63,9 @@ def main():
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--only", default="spmm.hip,sage.hip",
+                    help="--build: csrc files compiled with the variant's defines (the rest "
+                         "link from the main build)")
     ap.add_argument("--seg-lens", default="", help="also time the default build at these seg_len")
     ap.add_argument("--op", default="spmm", choices=["spmm", "sage"],
                     help="sage: the fused gather-mean over [M=62,401, k=10] uniform-degree-weighted "
@@ -62,7 +75,7 @@ def main():
     if args.build:
         from graphneuralnetwork_amd.build import build_variant
         for n in {n.split("@")[0] for n in names}:
-            print(build_variant(n, VARIANTS[n]))
+            print(build_variant(n, VARIANTS[n], only=[f for f in args.only.split(",") if f]))
         return
     import torch
     from graphneuralnetwork_amd import _lib
