@@ -117,15 +117,8 @@ __device__ __forceinline__ const float* wh_row(const GatParams& P, int c) {
                : P.wh + static_cast<int64_t>(c) * P.ldw;
 }
 __device__ __forceinline__ float er_at(const GatParams& P, int c, int h) {
-#if defined(GNN_GAT_ER_PROBE)
-  // timing probe only (tools/gat_ab.py "erprobe"): every er read hits row 0 -- the cost of
-  // the per-edge er gather, measured by its absence; results are wrong by construction
-  (void)c;
-  return P.er[h];
-#else
   return c < 0 ? P.erh[static_cast<int64_t>(-1 - c) * P.ldeh + h]
                : P.er[static_cast<int64_t>(c) * P.lde + h];
-#endif
 }
 
 #ifndef GNN_GAT_SMALL_UNROLL

@@ -26,13 +26,11 @@ VARIANTS = {
     "gs8": ["GNN_GAT_SMALL_UNROLL=8"],
     "gs16": ["GNN_GAT_SMALL_UNROLL=16"],
     "gs4": ["GNN_GAT_SMALL_UNROLL=4"],
-    "erprobe": ["GNN_GAT_ER_PROBE=1"],  # timing probe: er reads from one row (wrong results)
     "gs2": ["GNN_GAT_SMALL_UNROLL=2"],
     "gs4u4": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_U=4"],
     "gs4c16": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_CHUNK=16"],
     "gs4c16u4": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_CHUNK=16", "GNN_GAT_U=4"],
     "gs4np": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_PIPE=0"],
-    "gs4er": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_ER_PROBE=1"],
 }
 
 
