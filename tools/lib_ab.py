@@ -16,8 +16,14 @@ sys.path.insert(0, str(ROOT))
 # tag -> -D flags. Tried and dropped (profiles/r01f_lib_ab_ntcold_*.log): non-temporal
 # loads for the cold (non-hub) gathers, "ntcold" = GNN_SPMM_NT_COLD=1: no change at cfg2
 # (1.162 vs 1.161 ms) or the north star (14.32 vs 14.32 ms).
-# GCN transform grid (tools/transform_ab.py --variants, profiles/r01f_transform_grid_ab.log):
-# 512 workgroups 0.294 ms at 1M x 128 x 128, 256: 0.340, 768: 0.314, 1024: 0.304.
+# Prefetching the next 64-edge (col, val) chunk during the current one: no change (cfg2
+# 1.133 vs 1.134 ms, ns 14.21 vs 14.23 ms, profiles/r02o_pf_*.log), not kept.
+# Short rows (2..16 edges) in their own launch, 64/LPS rows per wave (LPS lanes x 4 16-B
+# chunks, 2 edges in flight per lane): slower at every threshold (cfg2 1.136 ms off, 1.144
+# at <= 4, 1.168 at <= 16, 1.211 at <= 64; ns 14.35 off vs 14.41), profiles/r02p_short_*.log;
+# not kept: the one-wave-per-row mid path already overlaps those rows' latency.
+# GCN transform grid (tools/transform_ab.py --variants, profiles/r02m_transform_ab.log):
+# 512 workgroups 0.300 ms at 1M x 128 x 128, 256: 0.333, 768: 0.316, 1024: 0.30x.
 VARIANTS = {
     "base": [],
     "tf256": ["GNN_TF_GRID=256"],

@@ -26,7 +26,7 @@ def main():
     if args.build:
         from graphneuralnetwork_amd.build import build_variant
         for n in names:
-            print(build_variant("proj_" + n, VARIANTS[n]))
+            print(build_variant("proj_" + n, VARIANTS[n], only=["project.hip"]))
         return
     import torch
     from graphneuralnetwork_amd import _lib
