@@ -27,6 +27,9 @@ VARIANTS = {
     "gs16": ["GNN_GAT_SMALL_UNROLL=16"],
     "gs4": ["GNN_GAT_SMALL_UNROLL=4"],
     "gs2": ["GNN_GAT_SMALL_UNROLL=2"],
+    "c16": ["GNN_GAT_CHUNK=16"],
+    "c32": ["GNN_GAT_CHUNK=32"],
+    "u2": ["GNN_GAT_U=2"],
     "gs4u4": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_U=4"],
     "gs4c16": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_CHUNK=16"],
     "gs4c16u4": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_CHUNK=16", "GNN_GAT_U=4"],

@@ -13,9 +13,12 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
-# tag -> -D flags. Tried and dropped (profiles/r01f_lib_ab_ntcold_*.log): non-temporal
-# loads for the cold (non-hub) gathers, "ntcold" = GNN_SPMM_NT_COLD=1: no change at cfg2
-# (1.162 vs 1.161 ms) or the north star (14.32 vs 14.32 ms).
+# tag -> -D flags. Variant libraries export only the C-ABI (build.EXPORT_MAP), so each
+# one launches its own kernels; before round 2 they did not (the kernels' weak template
+# symbols bound to the main library), and every round-1 library A/B compared the main
+# build with itself.
+# Non-temporal loads for the cold (non-hub) gathers, so they leave the hub rows in L2:
+# no change (cfg2 1.134 vs 1.136 ms, ns 14.37 vs 14.37 ms, profiles/r02q_nt_*.log).
 # Prefetching the next 64-edge (col, val) chunk during the current one: no change (cfg2
 # 1.133 vs 1.134 ms, ns 14.21 vs 14.23 ms, profiles/r02o_pf_*.log), not kept.
 # Short rows (2..16 edges) in their own launch, 64/LPS rows per wave (LPS lanes x 4 16-B
