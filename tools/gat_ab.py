@@ -12,6 +12,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
+# Measured and not kept (profiles/r02x_gat_pipe2.log): a depth-2 chunk pipeline (chunk
+# k+1's er / Wh loads in flight while chunk k is reduced, two register buffers) -- 0.98 ms
+# against 0.80: 84 VGPRs (5 waves/SIMD) cost more than the deeper pipeline gains.
 VARIANTS = {
     "j1u2": ["GNN_GAT_CHUNK=1", "GNN_GAT_U=2"],     # one pass per chunk (previous kernel)
     "c32u2": ["GNN_GAT_CHUNK=32", "GNN_GAT_U=2"],
