@@ -277,6 +277,24 @@ def cpu_sage_ops(table, batch, F: int, H: int, budget_s: float = 20.0):
         torch.set_num_threads(prev)
 
 
+def describe_path(g, feat: int):
+    """The kernels one single-GPU step launched (read from the plans the warm-up built)."""
+    xp = next((v for k, v in g._plans.items()
+               if isinstance(k, tuple) and k[0] == "_xcd" and v is not None), None)
+    if xp is not None:
+        return ("gather_rows_kernel (hub staging: the %d highest-degree rows of X, %.0f MiB) + "
+                "spmm_csr_kernel<HUB> pass 1 (%d XCD-sliced hub items of rows with >= %d edges, "
+                "workgroup w on XCD w %% 8) + spmm_csr_kernel<HUB> pass 2 (remaining edges + "
+                "partial refs) + spmm_fixup_kernel, per-step HIP events"
+                % (xp.k, xp.k * 4 * feat / 2**20, xp.n_items, xp.min_deg))
+    hub = next((v for k, v in g._plans.items() if isinstance(k, tuple) and k[0] == "_hub"), None)
+    if hub is not None:
+        return ("gather_rows_kernel (hub staging: the %d highest-degree rows of X, %.0f MiB) + "
+                "spmm_csr_kernel<HUB> + spmm_fixup_kernel, per-step HIP events"
+                % (hub.k, hub.k * 4 * feat / 2**20))
+    return "spmm_csr_kernel (+ spmm_fixup_kernel), per-step HIP events"
+
+
 def time_steps(step, steps: int, warmup: int, dev):
     """Per-step HIP-event times (ms) on the current stream + wall seconds for `steps` steps."""
     stream = torch.cuda.current_stream(dev)
@@ -541,8 +559,7 @@ def main():
         rows_local, nnz_local = g.n_rows, g.nnz
         bytes_local = algorithmic_bytes(nnz_local, rows_local, F)
         halo_rows = 0
-        from graphneuralnetwork_amd.ops import hub_rows_for
-        HUB_INFO["hub_rows"] = hub_rows_for(g.n_cols, F)
+        HUB_INFO["graph"] = g
     else:
         from graphneuralnetwork_amd.distributed import (EdgeCutSpmm,
                                                         build_cover_exchange_balanced,
@@ -576,6 +593,8 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    if HUB_INFO.get("graph") is not None:
+        HUB_INFO["kernel"] = describe_path(HUB_INFO.pop("graph"), F)
     if world > 1:
         dist.barrier()
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -659,11 +678,7 @@ def main():
                          "traffic_source": (str(tpath.relative_to(ROOT)) + ": rocprofv3 --pmc "
                                             "FETCH_SIZE x2 + WRITE_SIZE of this command")
                          if traffic else None,
-                         "kernel": ("gather_rows_kernel (hub staging: the %d highest-degree rows "
-                                    "of X, %.0f MiB) + spmm_csr_kernel<HUB> + spmm_fixup_kernel, "
-                                    "per-step HIP events" % (HUB_INFO["hub_rows"],
-                                                             HUB_INFO["hub_rows"] * 4 * F / 2**20))
-                         if HUB_INFO.get("hub_rows") else
+                         "kernel": HUB_INFO["kernel"] if HUB_INFO.get("kernel") else
                          ("EdgeCutSpmm step: send-side SpMM + 2 RCCL all-to-all-v (comm stream) "
                           "overlapping the interior SpMM (hub-staged when its X is >= 192 MiB), "
                           "then the halo SpMMs; per-step HIP events, max over ranks")

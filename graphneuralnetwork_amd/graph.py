@@ -131,6 +131,110 @@ class HubPlan:
         return int(self.hub_ids.numel())
 
 
+# gfx950: 8 XCDs with one 4 MiB L2 each; the workgroups of a launch are dealt to them
+# round-robin (workgroup w runs on XCD w % 8), and the SpMM kernel runs 4 waves per
+# workgroup (spmm.hip kBlock = 256), one row per wave.
+XCDS = 8
+SPMM_WAVES_PER_WG = 4
+
+
+@dataclass
+class XcdHubPlan:
+    """XCD-sliced hub staging (built once per graph, hub count and row threshold).
+
+    The staged hub ranks are dealt to the 8 XCDs (rank % 8). For every row of degree
+    >= ``min_deg``, the hub edges that fall in one slice form an *item* (chunked to at
+    most ``chunk`` edges). Pass 1 (``items``) reduces each item into one partial row;
+    its rows are laid out so that workgroup w holds only items of slice w % 8, so each
+    XCD's L2 serves 1/8 of the hub table. Pass 2 (``rest``) is every row's remaining
+    edges followed by one edge of value 1.0 per partial row of that row.
+
+    Both passes run the hub kernel (gnn_spmm_csr_hub_f32) over one staged buffer
+    [hub table (k rows) | partial rows (n_pos rows)]: column c < 0 names its row -1-c.
+    The row sums are regrouped (same terms, another order), so the result equals the
+    unstaged kernel's to fp32 rounding, and is bitwise reproducible.
+    """
+
+    hub: HubPlan
+    items: CsrGraph     # rows: item positions; cols: -1-rank (hub table rows)
+    rest: CsrGraph      # rows: graph rows; cols: X rows, -1-rank, -1-(k + position)
+    n_items: int        # real items (the other positions are 2-edge zero-valued pads)
+    min_deg: int
+    chunk: int
+
+    @property
+    def k(self) -> int:
+        return self.hub.k
+
+    @property
+    def n_pos(self) -> int:
+        return self.items.n_rows
+
+
+def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, k: int,
+                min_deg: int, chunk: int, xcds: int = XCDS,
+                waves_per_wg: int = SPMM_WAVES_PER_WG):
+    """The two COO edge lists of ``XcdHubPlan`` (torch ops on any device; the CPU tests
+    check them against the oracle SpMM).
+
+    Returns ``None`` when no row has two hub edges in one slice, else
+    ``((item_rows, item_cols, item_vals, n_pos, n_items), (rest_rows, rest_cols, rest_vals))``.
+    Item edges keep their CSR order; rest rows list their unmoved edges in CSR order,
+    then their partial refs in (slice, chunk) order."""
+    if chunk < 4 or k < xcds:  # balanced chunks of a >= 2-edge item then hold >= 2 edges
+        raise ValueError("xcd hub staging needs chunk >= 4 and k >= the XCD count")
+    dev = rowptr.device
+    i64 = torch.int64
+    n = rowptr.numel() - 1
+    deg = rowptr[1:] - rowptr[:-1]
+    rows_e = torch.repeat_interleave(torch.arange(n, device=dev, dtype=i64), deg)
+    c = col_hub.to(i64)
+    eid = torch.nonzero((c < 0) & (deg[rows_e] >= min_deg)).view(-1)
+    s_e = (-1 - c[eid]) % xcds
+    key = rows_e[eid] * xcds + s_e
+    order = torch.argsort(key, stable=True)                  # by (row, slice), CSR order kept
+    eid, key, s_e = eid[order], key[order], s_e[order]
+    _, inv, m = torch.unique_consecutive(key, return_inverse=True, return_counts=True)
+    moved = m >= 2                                           # a 1-edge item saves nothing
+    if not bool(moved.any()):
+        return None
+    em = moved[inv]
+    eid, s_e, inv = eid[em], s_e[em], inv[em]
+    grp = (torch.cumsum(moved.to(i64), 0) - 1)[inv]          # item group of each moved edge
+    mg = m[moved]
+    nch = (mg + chunk - 1) // chunk                          # balanced chunks of <= chunk edges
+    pos_in = torch.arange(eid.numel(), device=dev, dtype=i64) - (torch.cumsum(mg, 0) - mg)[grp]
+    item = (torch.cumsum(nch, 0) - nch)[grp] + pos_in * nch[grp] // mg[grp]
+    n_items = int(nch.sum())
+    it_slice = torch.empty(n_items, dtype=i64, device=dev)
+    it_slice[item] = s_e
+    it_row = torch.empty(n_items, dtype=i64, device=dev)
+    it_row[item] = rows_e[eid]
+    # position of an item: the j-th item of slice s goes to workgroup (j // W) * xcds + s
+    by_slice = torch.argsort(it_slice, stable=True)
+    cnt = torch.bincount(it_slice, minlength=xcds)
+    j = torch.empty(n_items, dtype=i64, device=dev)
+    j[by_slice] = torch.arange(n_items, device=dev, dtype=i64) - (torch.cumsum(cnt, 0) - cnt)[
+        it_slice[by_slice]]
+    W = waves_per_wg
+    per = -(-int(cnt.max()) // W) * W
+    pos = ((j // W) * xcds + it_slice) * W + j % W
+    n_pos = per * xcds
+    filled = torch.zeros(n_pos, dtype=torch.bool, device=dev)
+    filled[pos] = True
+    pad = torch.nonzero(~filled).view(-1)                    # 2 zero-valued edges of its slice
+    pad_col = -1 - (pad // W) % xcds
+    items = (torch.cat([pos[item], pad, pad]), torch.cat([c[eid], pad_col, pad_col]),
+             torch.cat([val[eid], torch.zeros(2 * pad.numel(), dtype=val.dtype, device=dev)]),
+             n_pos, n_items)
+    keep = torch.ones(c.numel(), dtype=torch.bool, device=dev)
+    keep[eid] = False
+    kid = torch.nonzero(keep).view(-1)
+    rest = (torch.cat([rows_e[kid], it_row]), torch.cat([c[kid], -1 - (k + pos)]),
+            torch.cat([val[kid], torch.ones(n_items, dtype=val.dtype, device=dev)]))
+    return items, rest
+
+
 @dataclass
 class CsrGraph:
     """Adjacency in CSR: row = output node, col = gathered node (torch.spmm orientation)."""
@@ -182,6 +286,14 @@ class CsrGraph:
             p = _build_hub_plan(self, k)
             self._plans[key] = p
         return p
+
+    def xcd_hub_plan(self, k: int, min_deg: int, chunk: int) -> "XcdHubPlan | None":
+        """XCD-sliced hub staging plan (built once per (k, min_deg, chunk), cached);
+        None when no row has two hub edges in one slice."""
+        key = ("_xcd", k, min_deg, chunk)
+        if key not in self._plans:
+            self._plans[key] = _build_xcd_hub_plan(self, k, min_deg, chunk)
+        return self._plans[key]
 
     def transpose(self) -> "CsrGraph":
         """CSR of A^T (used by the SpMM backward: dX = A^T dY)."""
@@ -264,6 +376,21 @@ def _build_hub_plan(g: CsrGraph, k: int) -> HubPlan:
                                       _lib.ptr(col_hub), err.data_ptr(), ws.data_ptr(),
                                       ws.numel(), _lib.stream_handle(dev)), "gnn_hub_plan_build")
     return HubPlan(hub_ids, col_hub, err)
+
+
+def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int) -> "XcdHubPlan | None":
+    hub = g.hub_plan(k)
+    if hub.k < XCDS or g.nnz == 0:
+        return None
+    coo = xcd_hub_coo(g.rowptr, hub.col_hub, g.val, hub.k, min_deg, chunk)
+    if coo is None:
+        return None
+    (ir, ic, iv, n_pos, n_items), (rr, rc, rv) = coo
+    if hub.k + n_pos > 0x7fffffff:
+        return None  # partial refs must fit int32 column ids
+    items = from_coo(ir, ic, iv, n_pos, hub.k, check=False)
+    rest = from_coo(rr, rc, rv, g.n_rows, g.n_cols, check=False)
+    return XcdHubPlan(hub, items, rest, n_items, min_deg, chunk)
 
 
 # ---------------------------------------------------------------- builders

@@ -52,10 +52,39 @@ def hub_rows_for(n_cols: int, feat: int) -> int:
     return min(n_cols, HUB_ROWS, max(1, HUB_BYTES // (4 * feat)))
 
 
+# XCD-sliced hub staging (graph.XcdHubPlan): on graphs with at least XCD_MIN_NNZ stored
+# entries whose X would be hub-staged, the hub edges of rows of degree >= XCD_MIN_DEG are
+# reduced per (row, XCD slice) first, so each XCD's L2 serves 1/8 of the hub table.
+# Measured with tools/workingset_probe.py and tools/xcd_hub_probe.py (profiles/r02y_*):
+# a gather set that fits one XCD's L2 runs at ~50 G rows/s, 16-256 MiB sets at 14-19 (the
+# Infinity Cache hardly beats HBM's 12); emulated, cfg2 1.14 -> 0.96 ms and the north star
+# 14.4 -> 12.4 ms at 256 Ki hub rows, degree >= 128, items of <= 128 edges.
+XCD_MIN_NNZ = 4_000_000
+XCD_HUB_BYTES = 128 << 20
+XCD_HUB_ROWS = 262144
+XCD_MIN_DEG = 128
+XCD_CHUNK = 128
+
+
+def xcd_hub_rows_for(n_cols: int, feat: int) -> int:
+    """Default hub rows of the XCD-sliced staging (0 = X too small to stage)."""
+    if n_cols * 4 * feat < HUB_MIN_X_BYTES:
+        return 0
+    return min(n_cols, XCD_HUB_ROWS, max(64, XCD_HUB_BYTES // (4 * feat)))
+
+
+def _spmm_hub_call(lib, g: CsrGraph, col: torch.Tensor, plan, pargs, x, xh, feat, bias, y, ldy,
+                   partial, flags, stream, what):
+    _lib.check(lib.gnn_spmm_csr_hub_f32(
+        g.rowptr.data_ptr(), col.data_ptr(), g.val.data_ptr(), g.n_rows, x.data_ptr(),
+        x.stride(0), xh.data_ptr(), feat, feat, _lib.ptr(bias), y.data_ptr(), ldy, plan.seg_len,
+        *pargs, _lib.ptr(partial), flags, stream), what)
+
+
 def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
                  activation: str | None = None, out: torch.Tensor | None = None,
                  seg_len: int | None = None, accumulate: bool = False,
-                 hubs: int | None = None) -> torch.Tensor:
+                 hubs: int | None = None, xcd: bool | None = None) -> torch.Tensor:
     """Y = A.X (+ bias) (act) with A in CSR -- the GCN aggregation (GCN/GCN.py:43-45).
 
     ``accumulate=True`` adds into ``out`` (Y = out + A.X ...): the halo pass of
@@ -65,7 +94,12 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
     across wavefronts); by default it is sized from the feature width.
 
     ``hubs`` = number of highest-degree rows of X staged into a compact table before
-    the gather (0: none; default ``hub_rows_for``). It changes speed, not results.
+    the gather (0: none; default ``hub_rows_for``). It changes speed, not results: the
+    output is bit-identical to the unstaged kernel's.
+
+    ``xcd`` = XCD-sliced hub staging (``graph.XcdHubPlan``; default: on for graphs of at
+    least XCD_MIN_NNZ entries whose X is staged and no explicit ``hubs``). Same sums,
+    regrouped: equal to the unstaged result to fp32 rounding, bitwise reproducible.
     """
     if accumulate and out is None:  # checked first: it is a usage error on any device
         raise ValueError("accumulate=True needs `out` (it adds into the caller's buffer)")
@@ -84,17 +118,28 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
         raise ValueError("out must be float32 [n_rows, features] with unit column stride")
     if g.n_rows == 0 or feat == 0:
         return out
-    plan = g.plan(seg_len if seg_len is not None else seg_len_for(feat))
-    partial = None
-    if plan.n_seg:
-        partial = torch.empty((plan.n_seg, feat), dtype=torch.float32, device=x.device)
+    seg = seg_len if seg_len is not None else seg_len_for(feat)
     if x.numel() == 0:  # no column to gather from (e.g. an empty halo): never read
         x = torch.empty((1, feat), dtype=torch.float32, device=x.device)
     lib = _lib.load()
     flags = _ACT_FLAGS[activation] | (_lib.EPI_ACCUMULATE if accumulate else 0)
     stream = _lib.stream_handle(x.device)
     # out += A.X with no bias / activation: rows without edges stay as they are
-    pargs = plan.args(skip_empty=accumulate and bias is None and activation is None)
+    skip_empty = accumulate and bias is None and activation is None
+    if xcd is None:
+        xcd = hubs is None and g.nnz >= XCD_MIN_NNZ and xcd_hub_rows_for(g.n_cols, feat) > 0
+    if xcd and g.nnz:
+        kx = xcd_hub_rows_for(g.n_cols, feat) if hubs is None else min(int(hubs), g.n_cols)
+        chunk = min(XCD_CHUNK, seg)
+        xp = g.xcd_hub_plan(kx, XCD_MIN_DEG, chunk) if kx >= 8 and chunk >= 4 else None
+        if xp is not None:
+            _spmm_xcd(lib, g, xp, x, feat, bias, out, seg, skip_empty, flags, stream)
+            return out
+    plan = g.plan(seg)
+    partial = None
+    if plan.n_seg:
+        partial = torch.empty((plan.n_seg, feat), dtype=torch.float32, device=x.device)
+    pargs = plan.args(skip_empty=skip_empty)
     k = hub_rows_for(g.n_cols, feat) if hubs is None else min(int(hubs), g.n_cols)
     if k > 0 and g.nnz:
         hp = g.hub_plan(k)
@@ -114,6 +159,30 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
         plan.seg_len, *pargs, _lib.ptr(partial), flags, stream)
     _lib.check(rc, "gnn_spmm_csr_f32")
     return out
+
+
+def _spmm_xcd(lib, g: CsrGraph, xp, x, feat, bias, out, seg, skip_empty, flags, stream):
+    """The XCD-sliced hub SpMM: hub rows -> staged buffer, pass 1 (items -> partial rows of
+    the same buffer, workgroup w on XCD w % 8 holds only slice w % 8), pass 2 (remaining
+    edges + partial refs, with the epilogue). Three launches on one stream."""
+    k, n_pos = xp.k, xp.n_pos
+    buf = torch.empty((k + n_pos, feat), dtype=torch.float32, device=x.device)
+    hp = xp.hub
+    _lib.check(lib.gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0],
+                                       hp.hub_ids.data_ptr(), k, feat, buf.data_ptr(), feat,
+                                       hp.err.data_ptr(), stream), "gnn_gather_rows_f32")
+    p1 = xp.items.plan(seg)
+    if p1.n_seg or p1.n_small:  # by construction every item is a 2..chunk-edge row
+        raise RuntimeError("XCD hub plan: item rows outside the mid-row class")
+    _spmm_hub_call(lib, xp.items, xp.items.col, p1, p1.args(), x, buf, feat, None, buf[k:], feat,
+                   None, 0, stream, "gnn_spmm_csr_hub_f32 (xcd items)")
+    p2 = xp.rest.plan(seg)
+    partial = None
+    if p2.n_seg:
+        partial = torch.empty((p2.n_seg, feat), dtype=torch.float32, device=x.device)
+    _spmm_hub_call(lib, xp.rest, xp.rest.col, p2, p2.args(skip_empty=skip_empty), x, buf, feat,
+                   bias, out, out.stride(0), partial, flags, stream,
+                   "gnn_spmm_csr_hub_f32 (xcd rest)")
 
 
 class _SpmmFn(torch.autograd.Function):

@@ -232,8 +232,12 @@ def test_rmat_1m_parity_vs_c_oracle(dev):
     assert g.nnz == 20_073_500
     F = 128
     X = torch.randn(n, F, generator=torch.Generator().manual_seed(0)).to(dev)
-    Yd = spmm_forward(g, X)  # X is 512 MB: the default path stages hub rows
-    assert torch.equal(Yd, spmm_forward(g, X, hubs=0))
+    Yd = spmm_forward(g, X)  # X is 512 MB: the default path is the XCD-sliced hub staging
+    assert any(isinstance(k, tuple) and k[0] == "_xcd" and v is not None
+               for k, v in g._plans.items())
+    assert torch.equal(Yd, spmm_forward(g, X))           # reproducible
+    close(Yd.cpu().numpy(), spmm_forward(g, X, hubs=0).cpu().numpy(), rtol=1e-5)
+    assert torch.equal(spmm_forward(g, X, hubs=131072), spmm_forward(g, X, hubs=0))
     Y = Yd.cpu().numpy()
     rowptr, col, val = g.rowptr.cpu().numpy(), g.col.cpu().numpy(), g.val.cpu().numpy()
     deg = np.diff(rowptr)
@@ -273,6 +277,63 @@ def test_hub_staging_bitexact(dev, F):
                 assert torch.equal(y, acc_ref), (F, seg_len, k, "accumulate")
     close(ref.cpu().numpy(), np.maximum(O.spmm_csr(rowptr, col, val, X.cpu().numpy(),
                                                    b.cpu().numpy()), 0))
+
+
+@pytest.mark.parametrize("F", [3, 64, 128, 256, 600])
+def test_xcd_hub_staging(dev, F, monkeypatch):
+    """XCD-sliced hub staging (graph.XcdHubPlan, two hub-kernel passes over [table |
+    partials]): equal to the unstaged kernel within fp32 rounding, bitwise reproducible,
+    with bias / activation / accumulate epilogues, long-row segments and strided X."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.ops import spmm_forward
+    monkeypatch.setattr(ops, "XCD_MIN_DEG", 4)     # many small items on a small graph
+    monkeypatch.setattr(ops, "XCD_CHUNK", 8)
+    n = 1500
+    rowptr, col, val = _rand_graph(n, 16 * n, 90 + F, hub_deg=5000)
+    g = _graph(rowptr, col, val, n, dev)
+    Xw = torch.randn(n, F + 5, device=dev)
+    for X in (Xw[:, :F].contiguous(), Xw[:, 1:F + 1]):
+        b = torch.randn(F, device=dev)
+        base = torch.randn(n, F, device=dev)
+        for seg_len in (None, 16):
+            ref = spmm_forward(g, X, b, activation="elu", seg_len=seg_len, hubs=0)
+            acc_ref = spmm_forward(g, X, None, out=base.clone(), accumulate=True, seg_len=seg_len,
+                                   hubs=0)
+            for k in (8, 200, n):
+                y = spmm_forward(g, X, b, activation="elu", seg_len=seg_len, hubs=k, xcd=True)
+                key = ("_xcd", k, 4, min(8, seg_len or 10 ** 9))
+                assert g._plans.get(key) is not None, key
+                close(y.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5)
+                assert torch.equal(y, spmm_forward(g, X, b, activation="elu", seg_len=seg_len,
+                                                   hubs=k, xcd=True))
+                y = spmm_forward(g, X, None, out=base.clone(), accumulate=True, seg_len=seg_len,
+                                 hubs=k, xcd=True)
+                close(y.cpu().numpy(), acc_ref.cpu().numpy(), rtol=1e-5)
+    Xn = X.cpu().numpy()
+    y = spmm_forward(g, X, b, hubs=n, xcd=True).cpu().numpy()
+    close(y, O.spmm_csr(rowptr, col, val, Xn, b.cpu().numpy()))
+
+
+def test_xcd_hub_default_policy(dev, monkeypatch):
+    """The default: XCD slicing on graphs of >= XCD_MIN_NNZ entries whose X is staged; an
+    explicit ``hubs`` keeps the bit-exact single-pass staging; no item -> single pass."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.ops import spmm_forward
+    n, F = 2000, 128
+    rowptr, col, val = _rand_graph(n, 30 * n, 5, hub_deg=6000)
+    g = _graph(rowptr, col, val, n, dev)
+    X = torch.randn(n, F, device=dev)
+    monkeypatch.setattr(ops, "HUB_MIN_X_BYTES", 0)
+    monkeypatch.setattr(ops, "XCD_MIN_NNZ", 1)
+    y = spmm_forward(g, X)
+    assert any(isinstance(k, tuple) and k[0] == "_xcd" for k in g._plans)
+    close(y.cpu().numpy(), O.spmm_csr(rowptr, col, val, X.cpu().numpy()))
+    g2 = _graph(rowptr, col, val, n, dev)
+    assert torch.equal(spmm_forward(g2, X, hubs=64), spmm_forward(g2, X, hubs=0))
+    assert not any(isinstance(k, tuple) and k[0] == "_xcd" for k in g2._plans)
+    monkeypatch.setattr(ops, "XCD_MIN_DEG", 10 ** 9)   # no row qualifies: plan is None
+    g3 = _graph(rowptr, col, val, n, dev)
+    assert torch.equal(spmm_forward(g3, X), spmm_forward(g3, X, hubs=ops.hub_rows_for(n, F)))
 
 
 def test_hub_plan_structure(dev):

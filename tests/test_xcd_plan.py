@@ -1,0 +1,110 @@
+"""XCD-sliced hub staging plan (graph.xcd_hub_coo): host-side structure and algebra.
+
+The plan regroups each row's sum A_i. X into [edges left in place] + [one partial row per
+(row, XCD slice) item]; here the two edge lists are checked on the CPU against the oracle
+SpMM (float64), and their layout against what the GPU launch relies on (item positions
+dealt to XCDs in workgroups of 4, 2..chunk edges per item, refs after the row's own edges).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gnn_oracle as O
+
+XCDS, W = 8, 4
+
+
+def _hub_rename(col, n, k):
+    """col_hub as hub.hip builds it: the k highest in-degree columns (ties by ascending id)
+    renamed -1-rank."""
+    deg = np.bincount(col, minlength=n)
+    hub = np.lexsort((np.arange(n), -deg))[:k]
+    rank = np.full(n, -1, np.int64)
+    rank[hub] = np.arange(k)
+    ch = np.where(rank[col] >= 0, -1 - rank[col], col)
+    return hub, ch
+
+
+def _graph(n=3000, e=60000, seed=0):
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    s, d = rmat_edges(n, e, seed)
+    return O.gcn_adjacency(s, d, n)
+
+
+def _decode(cols, X, B):
+    return np.where(cols[:, None] >= 0, X[np.maximum(cols, 0)], B[np.maximum(-1 - cols, 0)])
+
+
+def _csr_spmm(rows, cols, vals, n_rows, src):
+    """sum over edges of vals * src-row, per row (float64)."""
+    out = np.zeros((n_rows, src.shape[1]))
+    np.add.at(out, rows, vals[:, None].astype(np.float64) * src)
+    return out
+
+
+@pytest.mark.parametrize("k,min_deg,chunk", [(64, 16, 8), (200, 2, 4), (500, 64, 128),
+                                             (3000, 1, 4), (3000, 1, 5)])
+def test_xcd_plan_algebra_and_layout(k, min_deg, chunk):
+    from graphneuralnetwork_amd.graph import xcd_hub_coo
+    rowptr, col, val = _graph()
+    n = rowptr.size - 1
+    hub, ch = _hub_rename(col, n, k)
+    res = xcd_hub_coo(torch.from_numpy(rowptr), torch.from_numpy(ch.astype(np.int32)),
+                      torch.from_numpy(val), k, min_deg, chunk)
+    assert res is not None
+    (ir, ic, iv, n_pos, n_items), (rr, rc, rv) = res
+    ir, ic, iv, rr, rc, rv = (t.numpy() for t in (ir, ic, iv, rr, rc, rv))
+    # layout: positions fill whole workgroups of every XCD; an item only reads its slice
+    assert n_pos % (XCDS * W) == 0
+    assert ((ic < 0) & (ic >= -k)).all()
+    np.testing.assert_array_equal(((-1 - ic) % XCDS), (ir // W) % XCDS)
+    cnt = np.bincount(ir, minlength=n_pos)
+    assert cnt.min() >= 2 and cnt.max() <= chunk
+    pads = (iv == 0) & (np.bincount(ir, weights=(iv != 0), minlength=n_pos)[ir] == 0)
+    assert n_pos - n_items == len(np.unique(ir[pads]))
+    # refs point at partial rows k .. k + n_pos - 1, one per real item
+    refs = rc < -k
+    assert refs.sum() == n_items and (rv[refs] == 1.0).all()
+    assert (-1 - rc[refs] - k < n_pos).all()
+    # every original edge appears exactly once (in an item or left in place), CSR order kept
+    deg = np.diff(rowptr)
+    rows_e = np.repeat(np.arange(n), deg)
+    kept = ~refs
+    moved_rows = np.empty(ir.size, np.int64)
+    pos_row = np.full(n_pos, -1, np.int64)
+    pos_row[-1 - rc[refs] - k] = rr[refs]
+    moved_rows = pos_row[ir[~pads]]
+    both = np.concatenate([np.stack([rr[kept], rc[kept]]), np.stack([moved_rows, ic[~pads]])], 1)
+    orig = np.stack([rows_e, ch])
+    np.testing.assert_array_equal(np.lexsort(both[::-1]).size, orig.shape[1])
+    np.testing.assert_array_equal(both[:, np.lexsort(both[::-1])], orig[:, np.lexsort(orig[::-1])])
+    # rest rows: own edges in CSR order before the partial refs
+    order = np.argsort(rr, kind="stable")
+    rs, rcs = rr[order], rc[order]
+    for r in np.unique(rs[rcs < -k])[:50]:
+        seg = rcs[rs == r]
+        is_ref = seg < -k
+        assert not (is_ref[:-1] & ~is_ref[1:]).any()
+    # algebra: pass 1 over the staged table, pass 2 over [table | partials] and X == A . X
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((n, 5))
+    T = X[hub]
+    P = _csr_spmm(ir, ic, iv, n_pos, _decode(ic, X, T))
+    B = np.concatenate([T, P])
+    Y = _csr_spmm(rr, rc, rv, n, _decode(rc, X, B))
+    np.testing.assert_allclose(Y, O.spmm_csr(rowptr, col, val, X), rtol=1e-12, atol=1e-12)
+
+
+def test_xcd_plan_none_without_items():
+    from graphneuralnetwork_amd.graph import xcd_hub_coo
+    rowptr, col, val = _graph(500, 3000, 2)
+    n = rowptr.size - 1
+    _, ch = _hub_rename(col, n, 16)
+    assert xcd_hub_coo(torch.from_numpy(rowptr), torch.from_numpy(ch.astype(np.int32)),
+                       torch.from_numpy(val), 16, 10 ** 9, 8) is None
+    with pytest.raises(ValueError):
+        xcd_hub_coo(torch.from_numpy(rowptr), torch.from_numpy(ch.astype(np.int32)),
+                    torch.from_numpy(val), 4, 2, 8)
+    with pytest.raises(ValueError):
+        xcd_hub_coo(torch.from_numpy(rowptr), torch.from_numpy(ch.astype(np.int32)),
+                    torch.from_numpy(val), 16, 2, 3)

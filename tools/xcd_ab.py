@@ -1,0 +1,86 @@
+"""Interleaved A/B of the XCD-sliced hub staging (ops.spmm_forward xcd=True) against the
+single-pass hub staging, at one shape, over (hub rows K, min row degree, item chunk).
+
+    python tools/xcd_ab.py [--workload cfg2|ns] [--feat 128] [--ks 131072,262144]
+                           [--degs 64,128,256] [--chunks 128]
+
+Every variant is checked against the unstaged kernel (fp32 rounding) before timing. Times
+include the per-call hub-row copy and both passes.
+"""
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="cfg2")
+    ap.add_argument("--feat", type=int, default=128)
+    ap.add_argument("--ks", default="131072,262144")
+    ap.add_argument("--degs", default="64,128,256")
+    ap.add_argument("--chunks", default="128")
+    ap.add_argument("--rounds", type=int, default=6)
+    args = ap.parse_args()
+    from graphneuralnetwork_amd import _lib, ops
+    from graphneuralnetwork_amd.ops import hub_rows_for, spmm_forward
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    _lib.load()
+    dev = torch.device("cuda:0")
+    n, e = (1_000_000, 10_000_000) if args.workload == "cfg2" else (10_000_000, 100_000_000)
+    s, d = rmat_edges(n, e, 0)
+    g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n, device=dev)
+    del s, d
+    F = args.feat
+    X = torch.randn(n, F, device=dev)
+    b = torch.randn(F, device=dev)
+    Y = torch.empty(n, F, device=dev)
+    nbytes = g.nnz * (8 + 4 * F) + n * (8 + 4 * F)
+    ref = spmm_forward(g, X, b, hubs=0)
+    k0 = hub_rows_for(n, F)
+    variants = {f"single K={k0}": dict(hubs=k0, xcd=False)}
+    for k in (int(v) for v in args.ks.split(",")):
+        for dg in (int(v) for v in args.degs.split(",")):
+            for ch in (int(v) for v in args.chunks.split(",")):
+                variants[f"xcd K={k} deg>={dg} chunk={ch}"] = dict(hubs=k, xcd=True, deg=dg, chunk=ch)
+
+    def call(v):
+        if v.get("xcd"):
+            ops.XCD_MIN_DEG, ops.XCD_CHUNK = v["deg"], v["chunk"]
+        return spmm_forward(g, X, b, out=Y, hubs=v["hubs"], xcd=v["xcd"])
+
+    scale = float(ref.abs().max())
+    for name, v in variants.items():
+        call(v)
+        torch.cuda.synchronize()
+        err = float((Y - ref).abs().max()) / scale
+        assert err < 1e-5, (name, err)
+        v["err"] = err
+    print(json.dumps({"workload": args.workload, "feat": F, "nnz": g.nnz}), flush=True)
+    stream = torch.cuda.current_stream(dev)
+    times = {k: [] for k in variants}
+    for _ in range(args.rounds):
+        for name, v in variants.items():
+            a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            call(v)
+            a.record(stream)
+            for _ in range(3):
+                call(v)
+            c.record(stream)
+            torch.cuda.synchronize()
+            times[name].append(a.elapsed_time(c) / 3)
+    for name, t in times.items():
+        med = statistics.median(t)
+        print(json.dumps({"variant": name, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
+                          "algo_GBps": round(nbytes / (med / 1e3) / 1e9),
+                          "max_rel_err": variants[name]["err"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
