@@ -161,6 +161,7 @@ class XcdHubPlan:
     n_items: int        # real items (the other positions are 2-edge zero-valued pads)
     min_deg: int
     chunk: int
+    item_row: torch.Tensor  # int64 [n_pos]: the graph row of each item position (pads: 0)
 
     @property
     def k(self) -> int:
@@ -170,6 +171,30 @@ class XcdHubPlan:
     def n_pos(self) -> int:
         return self.items.n_rows
 
+    def rest_plan(self, seg_len: int) -> RowSplitPlan:
+        """The row-class plan of ``rest`` for the hub kernels (cached per seg_len).
+
+        The packed small-row class reads its one pre-resolved column straight from X and
+        treats a negative id as "no edge"; a one-edge row of ``rest`` whose edge is a hub
+        or a partial row (negative id) therefore goes to the mid-row class instead, whose
+        gather resolves negative ids through the staged buffer."""
+        cache = self.__dict__.setdefault("_rest_plans", {})
+        if seg_len not in cache:
+            p = self.rest.plan(seg_len)
+            rp = self.rest.rowptr
+            if p.n_small:
+                r = p.small_row.to(torch.int64)
+                staged = (p.small_col < 0) & ((rp[r + 1] - rp[r]) == 1)
+                if bool(staged.any()):
+                    keep = ~staged
+                    p = RowSplitPlan(p.seg_len, p.seg_row, p.seg_begin, p.long_row,
+                                     p.long_seg_ptr, p.small_row[keep].contiguous(),
+                                     p.small_col[keep].contiguous(),
+                                     p.small_val[keep].contiguous(),
+                                     torch.cat([p.mid_row, p.small_row[staged]]).contiguous())
+            cache[seg_len] = p
+        return cache[seg_len]
+
 
 def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, k: int,
                 min_deg: int, chunk: int, xcds: int = XCDS,
@@ -178,7 +203,8 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     check them against the oracle SpMM).
 
     Returns ``None`` when no row has two hub edges in one slice, else
-    ``((item_rows, item_cols, item_vals, n_pos, n_items), (rest_rows, rest_cols, rest_vals))``.
+    ``((item_rows, item_cols, item_vals, n_pos, n_items), (rest_rows, rest_cols, rest_vals),
+    pos_row)`` where ``pos_row[p]`` is the graph row of item position p (pads: 0).
     Item edges keep their CSR order; rest rows list their unmoved edges in CSR order,
     then their partial refs in (slice, chunk) order."""
     if chunk < 4 or k < xcds:  # balanced chunks of a >= 2-edge item then hold >= 2 edges
@@ -232,7 +258,9 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     kid = torch.nonzero(keep).view(-1)
     rest = (torch.cat([rows_e[kid], it_row]), torch.cat([c[kid], -1 - (k + pos)]),
             torch.cat([val[kid], torch.ones(n_items, dtype=val.dtype, device=dev)]))
-    return items, rest
+    pos_row = torch.zeros(n_pos, dtype=i64, device=dev)
+    pos_row[pos] = it_row
+    return items, rest, pos_row
 
 
 @dataclass
@@ -385,12 +413,12 @@ def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int) -> "XcdHu
     coo = xcd_hub_coo(g.rowptr, hub.col_hub, g.val, hub.k, min_deg, chunk)
     if coo is None:
         return None
-    (ir, ic, iv, n_pos, n_items), (rr, rc, rv) = coo
+    (ir, ic, iv, n_pos, n_items), (rr, rc, rv), pos_row = coo
     if hub.k + n_pos > 0x7fffffff:
         return None  # partial refs must fit int32 column ids
     items = from_coo(ir, ic, iv, n_pos, hub.k, check=False)
     rest = from_coo(rr, rc, rv, g.n_rows, g.n_cols, check=False)
-    return XcdHubPlan(hub, items, rest, n_items, min_deg, chunk)
+    return XcdHubPlan(hub, items, rest, n_items, min_deg, chunk, pos_row)
 
 
 # ---------------------------------------------------------------- builders

@@ -176,7 +176,7 @@ def _spmm_xcd(lib, g: CsrGraph, xp, x, feat, bias, out, seg, skip_empty, flags, 
         raise RuntimeError("XCD hub plan: item rows outside the mid-row class")
     _spmm_hub_call(lib, xp.items, xp.items.col, p1, p1.args(), x, buf, feat, None, buf[k:], feat,
                    None, 0, stream, "gnn_spmm_csr_hub_f32 (xcd items)")
-    p2 = xp.rest.plan(seg)
+    p2 = xp.rest_plan(seg)
     partial = None
     if p2.n_seg:
         partial = torch.empty((p2.n_seg, feat), dtype=torch.float32, device=x.device)
@@ -305,17 +305,82 @@ def col_mean(x: torch.Tensor) -> torch.Tensor:
 
 
 GAT_SHORT_MAX_DEG = 16  # rows with 2..16 edges take the short-row path (A/B at cfg3: 16 best)
+# XCD-sliced hub staging for GAT (``_gat_xcd``) is built and tested but not the default: at
+# cfg3 it loses or ties at every setting (tools/xcd_ab.py --op gat, profiles/r02z_xcd_ab_gat_*:
+# single pass 0.79 ms; rows of >= 128 edges 0.88, >= 256 0.86, >= 1024 0.79). The edge
+# softmax (8 exps per edge, phase A/B through LDS) hides the gathers that the SpMM waits on.
+GAT_XCD = False
+
+
+def _gat_call(lib, g_rowptr, col, n, wh, el, er, lde, heads, fh, slope, mode, fill, out, ldo,
+              seg_len, plan, mid, short, partial, stats, flags, stream, whh, erh, what):
+    pa = plan.args()
+    _lib.check(lib.gnn_gat_csr_hub_f32(
+        g_rowptr.data_ptr(), col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
+        el.data_ptr(), er.data_ptr(), lde, float(slope), int(mode), _lib.ptr(fill), 0.0, 0,
+        out.data_ptr(), ldo, seg_len, *pa[:6], pa[6], pa[7], pa[9],
+        mid.data_ptr() if mid.numel() else pa[10], mid.numel(),
+        short.data_ptr() if short is not None and short.numel() else None,
+        short.numel() if short is not None else 0, _lib.ptr(partial), _lib.ptr(stats), flags,
+        stream, whh.data_ptr(), whh.stride(0), erh.data_ptr(), erh.stride(0)), what)
+
+
+def _gat_xcd(lib, g: CsrGraph, xp, wh, el, er, heads, fh, slope, mode, fill, out, seg, flags,
+             stream):
+    """GAT over the XCD-sliced hub plan (graph.XcdHubPlan), inference.
+
+    Pass 1 runs each item (a row's hub edges in one XCD slice) as a row of its own, on XCD
+    w % 8 like the SpMM, writing the item's softmax-weighted mean of Wh (no activation) and
+    its per-head log-sum-exp L. Pass 2 runs every row's remaining edges plus one pseudo-edge
+    per item whose Wh row is that mean and whose logit is L: an edge's logit is
+    LeakyReLU(el_i + er_j) (dense; its negation for sparse), so the item's er entry is set
+    to LeakyReLU^-1(+-L) - el_i. The online softmax then merges the items exactly as the
+    fix-up merges segments (log-sum-exp rule). Both passes are gnn_gat_csr_hub_f32 over
+    the staged buffers [hub rows | item rows]."""
+    k, n_pos = xp.k, xp.n_pos
+    feat = heads * fh
+    dev = wh.device
+    whb = torch.empty((k + n_pos, feat), dtype=torch.float32, device=dev)
+    erb = torch.empty((k + n_pos, heads), dtype=torch.float32, device=dev)
+    hp = xp.hub
+    for src, dst, w in ((wh, whb, feat), (er, erb, heads)):
+        _lib.check(lib.gnn_gather_rows_f32(src.data_ptr(), src.stride(0), src.shape[0],
+                                           hp.hub_ids.data_ptr(), k, w, dst.data_ptr(), w,
+                                           hp.err.data_ptr(), stream), "gnn_gather_rows_f32")
+    el_items = el.index_select(0, xp.item_row)
+    lse = torch.empty((n_pos, heads), dtype=torch.float32, device=dev)
+    p1 = xp.items.plan(seg)
+    if p1.n_seg or p1.n_small:
+        raise RuntimeError("XCD hub plan: item rows outside the mid-row class")
+    # er is never read in pass 1 (every column is staged): erb stands in with its stride
+    _gat_call(lib, xp.items.rowptr, xp.items.col, n_pos, wh, el_items, erb, heads, heads, fh,
+              slope, mode, None, whb[k:], feat, seg, p1, p1.mid_row, None, None, lse, 0, stream,
+              whb, erb, "gnn_gat_csr_hub_f32 (xcd items)")
+    y = lse if mode == GAT_DENSE else -lse
+    torch.sub(torch.where(y >= 0, y, y / slope), el_items, out=erb[k:])
+    p2 = xp.rest_plan(seg)
+    mid, short = p2.gat_split(xp.rest.rowptr, GAT_SHORT_MAX_DEG)
+    partial = None
+    if p2.n_seg:
+        partial = torch.empty((p2.n_seg, feat + 2 * heads), dtype=torch.float32, device=dev)
+    _gat_call(lib, xp.rest.rowptr, xp.rest.col, g.n_rows, wh, el, er, el.stride(0), heads, fh,
+              slope, mode, fill, out, out.stride(0), seg, p2, mid, short, partial, None, flags,
+              stream, whb, erb, "gnn_gat_csr_hub_f32 (xcd rest)")
 
 
 def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tensor, heads: int,
                   fh: int, negative_slope: float, mode: int, activation: str | None = None,
                   dropout_p: float = 0.0, seed: int = 0, seg_len: int | None = None,
                   out: torch.Tensor | None = None,
-                  stats: torch.Tensor | None = None, hubs: int | None = None) -> torch.Tensor:
+                  stats: torch.Tensor | None = None, hubs: int | None = None,
+                  xcd: bool | None = None) -> torch.Tensor:
     """Fused edge-softmax + neighbour aggregation for all heads (one HIP launch + fix-up).
 
     ``hubs``: Wh / er rows of the highest-degree columns staged into compact tables first
-    (gnn_gat_csr_hub_f32; 0 = none, default ``hub_rows_for``); same output bits."""
+    (gnn_gat_csr_hub_f32; 0 = none, default ``hub_rows_for``); same output bits.
+
+    ``xcd``: XCD-sliced hub staging (``_gat_xcd``; default GAT_XCD and the same size rule
+    as the SpMM, inference only: no dropout, no stats, a positive LeakyReLU slope)."""
     _require_device(g.rowptr, wh, el, er, out)
     wh = _rows_f32(wh, "Wh")
     n = g.n_rows
@@ -338,12 +403,26 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
     fill = None
     if mode == GAT_DENSE and g.has_empty_rows():
         fill = col_mean(wh)
-    plan = g.plan(seg_len if seg_len is not None else seg_len_for(feat, GAT_SEG_BYTES))
+    seg = seg_len if seg_len is not None else seg_len_for(feat, GAT_SEG_BYTES)
+    lib = _lib.load()
+    if xcd is None:
+        xcd = (GAT_XCD and hubs is None and g.nnz >= XCD_MIN_NNZ
+               and xcd_hub_rows_for(g.n_cols, feat + heads) > 0)
+    if (xcd and g.nnz and dropout_p == 0 and stats is None and negative_slope > 0
+            and mode in (GAT_DENSE, GAT_SPARSE)):
+        kx = (xcd_hub_rows_for(g.n_cols, feat + heads) if hubs is None
+              else min(int(hubs), g.n_cols))
+        chunk = min(XCD_CHUNK, seg)
+        xp = g.xcd_hub_plan(kx, XCD_MIN_DEG, chunk) if kx >= 8 and chunk >= 4 else None
+        if xp is not None:
+            _gat_xcd(lib, g, xp, wh, el, er, heads, fh, negative_slope, mode, fill, out, seg,
+                     _ACT_FLAGS[activation], _lib.stream_handle(wh.device))
+            return out
+    plan = g.plan(seg)
     partial = None
     if plan.n_seg:
         partial = torch.empty((plan.n_seg, feat + 2 * heads), dtype=torch.float32,
                               device=wh.device)
-    lib = _lib.load()
     pa = plan.args()  # (seg_row, seg_begin, n_seg, long_row, long_seg_ptr, n_long,
     #                    small_row, small_col, small_val, n_small, mid_row, n_mid)
     mid, short = plan.gat_split(g.rowptr, GAT_SHORT_MAX_DEG)

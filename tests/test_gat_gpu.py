@@ -143,6 +143,68 @@ def test_gat_hub_staging_bitexact(dev, heads, fh, sparse):
             assert torch.equal(torch.nan_to_num(st, 1.5), torch.nan_to_num(st0, 1.5))
 
 
+def _xcd_gat_graph(n, seed):
+    """Edge set with hub columns 0..79 of strictly decreasing in-degree (hub rank = id), a
+    hub row, one-edge rows into hub 0 (rows 0-99), edgeless rows (100-109), and rows whose
+    edges all go to hubs of one XCD slice (110-119 -> columns 8, 16, ..., 64)."""
+    rng = np.random.default_rng(seed)
+    s = [rng.integers(130, n, 8 * n), np.full(1500, 1)]
+    d = [rng.integers(0, n, 8 * n), rng.integers(0, n, 1500)]
+    for c in range(80):
+        s.append(rng.choice(np.arange(130, n), 1000 - 10 * c, replace=False))
+        d.append(np.full(1000 - 10 * c, c))
+    s += [np.arange(100), np.repeat(np.arange(110, 120), 8)]
+    d += [np.zeros(100, np.int64), np.tile(np.arange(8, 72, 8), 10)]
+    s, d = np.concatenate(s), np.concatenate(d)
+    key = np.unique(s * n + d)
+    rowptr, col, _ = O.coo_to_csr(key // n, key % n, np.ones(key.size, np.float32), n)
+    return rowptr, col
+
+
+@pytest.mark.parametrize("heads,fh", [(8, 8), (3, 5), (12, 4)])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gat_xcd_hub_staging(dev, heads, fh, sparse, monkeypatch):
+    """XCD-sliced GAT (items per (row, XCD slice) merged as pseudo-edges with their
+    log-sum-exp logit): equal to the single-pass kernel within fp32 rounding in every row
+    class and head group, reproducible; dropout / stats requests keep the bit-exact path."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.ops import GAT_DENSE, GAT_SPARSE, gat_aggregate
+    monkeypatch.setattr(ops, "XCD_MIN_DEG", 4)
+    monkeypatch.setattr(ops, "XCD_CHUNK", 8)
+    n = 2000
+    rowptr, col = _xcd_gat_graph(n, heads + fh)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.ones(col.size, device=dev), n, n)
+    wh = torch.randn(n, heads * fh, device=dev) * 0.5
+    el, er = torch.randn(n, heads, device=dev), torch.randn(n, heads, device=dev)
+    mode = GAT_SPARSE if sparse else GAT_DENSE
+    for seg_len in (None, 24):
+        ref = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, "elu", seg_len=seg_len, hubs=0)
+        for k in (64, 200, n):  # (k = 8: one hub per slice, an edge set has no 2-edge item)
+            out = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, "elu", seg_len=seg_len,
+                                hubs=k, xcd=True)
+            assert any(isinstance(key, tuple) and key[0] == "_xcd" and key[1] == k and v
+                       for key, v in g._plans.items()), k
+            close(out.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5)
+            again = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, "elu", seg_len=seg_len,
+                                  hubs=k, xcd=True)
+            assert torch.equal(torch.nan_to_num(out, 1.5), torch.nan_to_num(again, 1.5))
+    whn, eln, ern = (t.cpu().numpy().astype(np.float64) for t in (wh, el, er))
+    o = O.gat_csr(rowptr, col, whn, eln, ern, heads, fh, 0.2, sparse)
+    o = np.where(o > 0, o, np.expm1(np.minimum(o, 0)))
+    ok = ~np.isnan(o).any(1)
+    out = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, "elu", hubs=n, xcd=True)
+    close(out.cpu().numpy()[ok], o[ok])
+    # training requests (dropout, stats for the backward) take the bit-exact single pass
+    st0, st1 = torch.empty(n, heads, device=dev), torch.empty(n, heads, device=dev)
+    a = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, "elu", dropout_p=0.3, seed=2,
+                      stats=st0, hubs=64, xcd=True)
+    b = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, "elu", dropout_p=0.3, seed=2,
+                      stats=st1, hubs=0)
+    assert torch.equal(torch.nan_to_num(a, 1.5), torch.nan_to_num(b, 1.5))
+
+
 @pytest.mark.parametrize("heads,fh,ld,off", [(8, 8, 80, 0), (8, 8, 67, 0), (4, 16, 64, 1),
                                               (3, 12, 40, 4)])
 def test_gat_logits_strided_and_unaligned(dev, heads, fh, ld, off):

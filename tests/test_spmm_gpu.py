@@ -279,6 +279,24 @@ def test_hub_staging_bitexact(dev, F):
                                                    b.cpu().numpy()), 0))
 
 
+def _xcd_graph(n, seed):
+    """Random rows with hubs, plus the corner rows of the XCD-sliced plan: one-edge rows
+    whose edge is a hub column (rows 0-99), edgeless rows (100-109), and rows whose every
+    edge is a duplicate of one hub column (110-119: a single partial ref left in pass 2)."""
+    rng = np.random.default_rng(seed)
+    src = rng.integers(120, n, 16 * n)
+    dst = rng.integers(0, n, 16 * n)
+    hub = np.concatenate([np.full(5000, 3), np.full(2500, n - 1)])
+    src = np.concatenate([src, hub, np.arange(100), np.repeat(np.arange(110, 120), 8)])
+    dst = np.concatenate([dst, rng.integers(0, n, hub.size), np.full(100, 7),
+                          np.full(80, 11)])
+    # columns 7 and 11 become the two hottest
+    src = np.concatenate([src, rng.integers(120, n, 6000)])
+    dst = np.concatenate([dst, np.repeat([7, 11], 3000)])
+    val = rng.standard_normal(src.size).astype(np.float32)
+    return O.coo_to_csr(src, dst, val, n)
+
+
 @pytest.mark.parametrize("F", [3, 64, 128, 256, 600])
 def test_xcd_hub_staging(dev, F, monkeypatch):
     """XCD-sliced hub staging (graph.XcdHubPlan, two hub-kernel passes over [table |
@@ -289,7 +307,7 @@ def test_xcd_hub_staging(dev, F, monkeypatch):
     monkeypatch.setattr(ops, "XCD_MIN_DEG", 4)     # many small items on a small graph
     monkeypatch.setattr(ops, "XCD_CHUNK", 8)
     n = 1500
-    rowptr, col, val = _rand_graph(n, 16 * n, 90 + F, hub_deg=5000)
+    rowptr, col, val = _xcd_graph(n, 90 + F)
     g = _graph(rowptr, col, val, n, dev)
     Xw = torch.randn(n, F + 5, device=dev)
     for X in (Xw[:, :F].contiguous(), Xw[:, 1:F + 1]):

@@ -52,7 +52,7 @@ def test_xcd_plan_algebra_and_layout(k, min_deg, chunk):
     res = xcd_hub_coo(torch.from_numpy(rowptr), torch.from_numpy(ch.astype(np.int32)),
                       torch.from_numpy(val), k, min_deg, chunk)
     assert res is not None
-    (ir, ic, iv, n_pos, n_items), (rr, rc, rv) = res
+    (ir, ic, iv, n_pos, n_items), (rr, rc, rv), pos_row = res
     ir, ic, iv, rr, rc, rv = (t.numpy() for t in (ir, ic, iv, rr, rc, rv))
     # layout: positions fill whole workgroups of every XCD; an item only reads its slice
     assert n_pos % (XCDS * W) == 0
@@ -71,8 +71,8 @@ def test_xcd_plan_algebra_and_layout(k, min_deg, chunk):
     rows_e = np.repeat(np.arange(n), deg)
     kept = ~refs
     moved_rows = np.empty(ir.size, np.int64)
-    pos_row = np.full(n_pos, -1, np.int64)
-    pos_row[-1 - rc[refs] - k] = rr[refs]
+    pos_row = pos_row.numpy()
+    np.testing.assert_array_equal(pos_row[-1 - rc[refs] - k], rr[refs])
     moved_rows = pos_row[ir[~pads]]
     both = np.concatenate([np.stack([rr[kept], rc[kept]]), np.stack([moved_rows, ic[~pads]])], 1)
     orig = np.stack([rows_e, ch])

@@ -32,9 +32,12 @@ def main():
     ap.add_argument("--nnz", type=int, default=20_000_000)
     ap.add_argument("--table", type=int, default=10_000_000)
     ap.add_argument("--sizes", default="4096,8192,32768,65536,131072,524288,2097152,10000000")
+    ap.add_argument("--op", default="spmm", choices=["spmm", "gat"],
+                    help="gat: the GAT aggregation (dense softmax + ELU, 8 heads x feat/8; "
+                         "gathers a Wh row and an er entry per edge)")
     args = ap.parse_args()
     from graphneuralnetwork_amd.graph import CsrGraph
-    from graphneuralnetwork_amd.ops import spmm_forward
+    from graphneuralnetwork_amd.ops import gat_aggregate, spmm_forward
     dev = torch.device("cuda:0")
     F, D = args.feat, args.deg
     R = args.nnz // D
@@ -47,16 +50,27 @@ def main():
     xcd_of_edge = xcd_of_row.repeat_interleave(D)
     gen = torch.Generator(device=dev).manual_seed(0)
 
+    if args.op == "gat":
+        H = 8
+        el = torch.randn(R, H, device=dev)
+        er = torch.randn(args.table, H, device=dev)
+
+        def run(g):
+            gat_aggregate(g, X, el, er, H, F // H, 0.2, 0, "elu", out=Y, hubs=0)
+    else:
+        def run(g):
+            spmm_forward(g, X, out=Y, hubs=0)
+
     def timed(g, reps=10):
         for _ in range(3):
-            spmm_forward(g, X, out=Y, hubs=0)
+            run(g)
         torch.cuda.synchronize()
         ts = []
         for _ in range(5):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             for _ in range(reps):
-                spmm_forward(g, X, out=Y, hubs=0)
+                run(g)
             b.record()
             torch.cuda.synchronize()
             ts.append(a.elapsed_time(b) / reps)

@@ -26,9 +26,11 @@ def main():
     ap.add_argument("--degs", default="64,128,256")
     ap.add_argument("--chunks", default="128")
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--op", default="spmm", choices=["spmm", "gat"],
+                    help="gat: the cfg3 GAT aggregation (dense softmax + ELU, 8 heads x F/8)")
     args = ap.parse_args()
     from graphneuralnetwork_amd import _lib, ops
-    from graphneuralnetwork_amd.ops import hub_rows_for, spmm_forward
+    from graphneuralnetwork_amd.ops import gat_aggregate, hub_rows_for, spmm_forward
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     from graphneuralnetwork_amd.rmat import rmat_edges
     _lib.load()
@@ -42,8 +44,17 @@ def main():
     b = torch.randn(F, device=dev)
     Y = torch.empty(n, F, device=dev)
     nbytes = g.nnz * (8 + 4 * F) + n * (8 + 4 * F)
-    ref = spmm_forward(g, X, b, hubs=0)
     k0 = hub_rows_for(n, F)
+    if args.op == "gat":
+        H = 8
+        el, er = torch.randn(n, H, device=dev), torch.randn(n, H, device=dev)
+        nbytes = g.nnz * (4 + 4 * H + 4 * F) + n * (8 + 4 * H + 4 * F)
+        k0 = hub_rows_for(n, F + H)
+
+        def spmm_forward(g, X, b, out=None, hubs=None, xcd=None):  # noqa: F811 -- GAT op
+            return gat_aggregate(g, X, el, er, H, F // H, 0.2, 0, activation="elu", out=out,
+                                 hubs=hubs, xcd=xcd)
+    ref = spmm_forward(g, X, b, hubs=0)
     variants = {f"single K={k0}": dict(hubs=k0, xcd=False)}
     for k in (int(v) for v in args.ks.split(",")):
         for dg in (int(v) for v in args.degs.split(",")):
@@ -62,7 +73,8 @@ def main():
         err = float((Y - ref).abs().max()) / scale
         assert err < 1e-5, (name, err)
         v["err"] = err
-    print(json.dumps({"workload": args.workload, "feat": F, "nnz": g.nnz}), flush=True)
+    print(json.dumps({"op": args.op, "workload": args.workload, "feat": F, "nnz": g.nnz}),
+          flush=True)
     stream = torch.cuda.current_stream(dev)
     times = {k: [] for k in variants}
     for _ in range(args.rounds):
