@@ -108,6 +108,9 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_sage_gather_aggregate_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
                                                      _i32, _vp, _i64, _vp, _vp]),
     "gnn_gather_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
+    "gnn_sage_layer_supported": (ctypes.c_int, [_i64, _i64]),
+    "gnn_sage_layer_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _i64,
+                                          _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp]),
     "gnn_dev_spmm_variant_f32": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _i64,
                                                 _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp,
                                                 _vp, _i64, _vp, _i64, _vp, _i32, _vp]),

@@ -24,7 +24,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import from_coo
-from .ops import gather_rows, sage_aggregate, sage_gather_aggregate, spmm_forward
+from .ops import gather_rows, sage_aggregate, sage_gather_aggregate, sage_layer, spmm_forward
 
 
 class Gathered(NamedTuple):
@@ -171,12 +171,25 @@ class SageLayer(nn.Module):
 
 
 def _fused_sage_layer(block, center, neigh: Gathered):
-    """Inference SageLayer on a (table, index map) aggregate: the centre rows and the
-    fused gather-mean write the two halves of ONE [M, 2F] buffer (the reference's
-    torch.cat, never copied), then a single K=2F GEMM with the ReLU in the hipBLASLt
-    epilogue: GraphSAGE.py:18-20 + the gathers of :47-49 as 3 launches instead of 7."""
+    """Inference SageLayer on a (table, index map) aggregate.
+
+    Covered shapes (``ops.sage_layer``): ONE launch gathers the centre rows and the
+    neighbour mean into an LDS tile and multiplies it by W on the matrix cores, ReLU fused.
+    Otherwise the centre rows and the fused gather-mean write the two halves of ONE
+    [M, 2F] buffer (the reference's torch.cat, never copied), then a single K=2F GEMM with
+    the ReLU in the hipBLASLt epilogue: GraphSAGE.py:18-20 + the gathers of :47-49 as 3
+    launches instead of 7."""
+    if isinstance(center, Gathered):
+        self_src, self_idx, trusted = center.table, center.index, center.trusted
+    else:
+        self_src, self_idx, trusted = center, None, True
+    y = sage_layer(neigh.table, neigh.index, block.weight.weight, self_src, self_idx,
+                   check=not (trusted and neigh.trusted))
+    if y is not None:
+        return y
     M, n = neigh.index.shape[0], block.input_size
-    buf = torch.empty((M, 2 * n), dtype=torch.float32, device=neigh.table.device)
+    dev = neigh.table.device
+    buf = torch.empty((M, 2 * n), dtype=torch.float32, device=dev)
     if isinstance(center, Gathered):
         gather_rows(center.table, center.index, out=buf[:, :n], check=not center.trusted)
     else:

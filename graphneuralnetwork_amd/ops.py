@@ -553,6 +553,58 @@ def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str 
     return out
 
 
+# The fused layer pays only on a large frontier (its W stays in registers for a persistent
+# grid): cfg4 layer 0 (62,479 rows) 108 vs 111 us unfused; the 8,192-row layer 1 is faster
+# unfused (tools/sage_layer_ab.py, profiles/r02z_sage_layer_ab*.log).
+SAGE_FUSED_MIN_ROWS = 32768
+
+
+def _rows16(t: torch.Tensor) -> bool:
+    return (t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1
+            and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0)
+
+
+def sage_layer(table: torch.Tensor, nbr_idx: torch.Tensor, weight: torch.Tensor,
+               self_src: torch.Tensor, self_idx: torch.Tensor | None = None,
+               check: bool = True) -> torch.Tensor | None:
+    """relu(W . cat[self, mean_j table[nbr_idx[:, j]]]) in ONE launch (gnn_sage_layer_f32):
+    the inference SageLayer (GraphSAGE/GraphSAGE.py:15-20) fused with its MEAN Aggregator and
+    input gathers (graph_utils.py:6, GraphSAGE.py:47-49). self = self_src[self_idx] or, with
+    no index, self_src itself. None when the shape is not covered (the caller then runs the
+    gather-mean + GEMM launches)."""
+    _require_device(table, nbr_idx, weight, self_src, self_idx)
+    if nbr_idx.dim() != 2 or weight.dim() != 2 or not (_rows16(table) and _rows16(self_src)):
+        return None
+    M, k = nbr_idx.shape
+    feat = table.shape[1]
+    H = weight.shape[0]
+    if k == 0 or self_src.shape[1] != feat or weight.shape[1] != 2 * feat or M < SAGE_FUSED_MIN_ROWS:
+        return None
+    if self_idx is None and self_src.shape[0] != M:
+        return None
+    lib = _lib.load()
+    if not lib.gnn_sage_layer_supported(feat, H):
+        return None
+    w = weight.detach().to(torch.float32).contiguous()
+    nbr_idx = nbr_idx.to(torch.int64)
+    if nbr_idx.stride(1) != 1:
+        nbr_idx = nbr_idx.contiguous()
+    if self_idx is not None:
+        self_idx = self_idx.to(torch.int64).contiguous().view(-1)
+        if self_idx.numel() != M:
+            raise ValueError("self_idx must hold one index per output row")
+    out = torch.empty((M, H), dtype=torch.float32, device=table.device)
+    err = _err_flag(table.device, check)
+    _lib.check(lib.gnn_sage_layer_f32(
+        table.data_ptr(), table.stride(0), table.shape[0], self_src.data_ptr(),
+        self_src.stride(0), self_src.shape[0], _lib.ptr(self_idx), nbr_idx.data_ptr(),
+        nbr_idx.stride(0), M, k, feat, w.data_ptr(), H, out.data_ptr(), H, err.data_ptr(),
+        _lib.stream_handle(table.device)), "gnn_sage_layer_f32")
+    if check:
+        _check_err(err, "sage_layer")
+    return out
+
+
 def gather_rows(x: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = None,
                 check: bool = True) -> torch.Tensor:
     """out[i] = x[idx[i]] (torch.embedding semantics, one HIP launch)."""

@@ -308,6 +308,25 @@ int gnn_sage_gather_aggregate_f32(const float* table, int64_t ldt, int64_t n_tab
                                   int32_t* err_flag, void* stream);
 
 /*
+ * One fused GraphSAGE inference layer (MEAN, not gcn):
+ *   out[m] = relu(W . cat[self[m], mean_j table[nbr_idx[m, j]]])
+ * Replaces SageLayer.forward(self, Aggregator(neigh, 'MEAN')) -- GraphSAGE/GraphSAGE.py:15-20,
+ * graph_utils.py:6 -- plus the torch.embedding gathers of its inputs (GraphSAGE.py:47-49).
+ * self[m] = self_src[self_idx[m]] (self_idx int64 [M], rows of a [n_self, lds] matrix) or,
+ * with self_idx NULL, row m of self_src. nbr_idx int64 [M, ldi], k >= 1 neighbours per row;
+ * table [n_table, ldt]. W fp32 [out_features, 2*feat] row-major (nn.Linear's weight).
+ * out fp32 [M, ldo]. Shapes: gnn_sage_layer_supported(feat, out_features) != 0; 16-B
+ * aligned rows. An index out of range sets *err_flag (the caller raises IndexError).
+ * One persistent launch: gathers into an LDS tile, then v_mfma_f32_16x16x4_f32.
+ */
+int gnn_sage_layer_supported(int64_t feat, int64_t out_features);
+int gnn_sage_layer_f32(const float* table, int64_t ldt, int64_t n_table, const float* self_src,
+                       int64_t lds, int64_t n_self, const int64_t* self_idx,
+                       const int64_t* nbr_idx, int64_t ldi, int64_t M, int64_t k, int64_t feat,
+                       const float* w, int64_t out_features, float* out, int64_t ldo,
+                       int32_t* err_flag, void* stream);
+
+/*
  * Row gather out[i, :] = x[idx[i], :] (torch.embedding at GraphSAGE/GraphSAGE.py:47-48;
  * also packs halo send buffers for the multi-GPU edge-cut). Out-of-range index ->
  * *err_flag |= 1, row skipped.

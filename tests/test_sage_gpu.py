@@ -129,3 +129,76 @@ def test_gather_backward_is_the_transposed_aggregation(dev, M, k, n, F):
     ref = t64.grad.numpy()
     got = t.grad.cpu().numpy()
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=2e-5 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("F,H", [(128, 128), (64, 128), (128, 256), (64, 256)])
+@pytest.mark.parametrize("M,k", [(1, 1), (31, 3), (33, 10), (1000, 25), (4100, 10)])
+def test_fused_sage_layer_vs_oracle(dev, F, H, M, k, monkeypatch):
+    """gnn_sage_layer_f32: relu(W . cat[self, mean of k table rows]) in one launch (gathers
+    into an LDS tile, v_mfma_f32_16x16x4_f32), with and without a centre index."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.ops import sage_layer
+    monkeypatch.setattr(ops, "SAGE_FUSED_MIN_ROWS", 1)
+    rng = np.random.default_rng(F + H + M + k)
+    n = 5000
+    table = rng.standard_normal((n, F)).astype(np.float32)
+    idx = rng.integers(0, n, (M, k))
+    cidx = rng.integers(0, n, M)
+    W = (rng.standard_normal((H, 2 * F)) * 0.1).astype(np.float32)
+    T, Wd = torch.from_numpy(table).to(dev), torch.from_numpy(W).to(dev)
+    agg = table[idx].astype(np.float64).mean(1)
+    for self_idx in (cidx, None):
+        selfm = table[self_idx] if self_idx is not None else table[:M]
+        ref = np.maximum(np.concatenate([selfm, agg], 1) @ W.T.astype(np.float64), 0)
+        out = sage_layer(T, torch.from_numpy(idx).to(dev), Wd,
+                         T if self_idx is not None else T[:M],
+                         None if self_idx is None else torch.from_numpy(self_idx).to(dev))
+        assert out is not None and out.shape == (M, H)
+        np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-4,
+                                   atol=1e-5 * max(1.0, np.abs(ref).max()))
+
+
+def test_fused_sage_layer_checks_and_fallbacks(dev, monkeypatch):
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.ops import sage_layer
+    monkeypatch.setattr(ops, "SAGE_FUSED_MIN_ROWS", 1)
+    T = torch.randn(100, 128, device=dev)
+    W = torch.randn(128, 256, device=dev)
+    idx = torch.randint(0, 100, (10, 4), device=dev)
+    bad = idx.clone()
+    bad[3, 2] = 100
+    with pytest.raises(IndexError):
+        sage_layer(T, bad, W, T, torch.arange(10, device=dev))
+    with pytest.raises(IndexError):
+        sage_layer(T, idx, W, T, torch.full((10,), -1, device=dev))
+    assert sage_layer(T, idx, torch.randn(96, 256, device=dev), T[:10]) is None   # H = 96
+    assert sage_layer(T[:, :100], idx, torch.randn(128, 200, device=dev), T[:10, :100]) is None
+    assert sage_layer(T, idx[:, :0], W, T[:10]) is None                            # k = 0
+
+
+def test_graphsage_forward_fused_matches_unfused(dev, monkeypatch):
+    """The eval-mode forward on device-sampler maps (Gathered inputs) gives the same
+    embeddings and logits through the fused layer kernel as through gather-mean + GEMM."""
+    from graphneuralnetwork_amd import graphsage as GS
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.graph import from_coo
+    from graphneuralnetwork_amd.sampler import sample_batch
+    monkeypatch.setattr(ops, "SAGE_FUSED_MIN_ROWS", 1)
+    rng = np.random.default_rng(7)
+    n, F = 3000, 128
+    s, d = rng.integers(0, n, 40000), rng.integers(0, n, 40000)
+    adj = from_coo(torch.from_numpy(np.concatenate([s, d])).to(dev),
+                   torch.from_numpy(np.concatenate([d, s])).to(dev),
+                   torch.ones(80000, device=dev), n, n)
+    table = torch.randn(n, F, device=dev)
+    deg = adj.rowptr[1:] - adj.rowptr[:-1]
+    seeds = torch.nonzero(deg > 0).view(-1)[:500]
+    batch = sample_batch(adj, seeds, (25, 10), seed=3)
+    net = GS.GraphSAGE(2, F, F, False, agg_func="MEAN", Unsupervised=False,
+                       class_size=3).to(dev).eval()
+    with torch.no_grad():
+        emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+        monkeypatch.setattr(GS, "sage_layer", lambda *a, **kw: None)
+        emb0, logits0 = net(*batch.forward_args(table), None, None, None, None, None)
+    np.testing.assert_allclose(emb.cpu().numpy(), emb0.cpu().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(logits.cpu().numpy(), logits0.cpu().numpy(), rtol=1e-4, atol=1e-5)

@@ -1,3 +1,4 @@
 set -o pipefail
 O=gpurun_out/r02z; mkdir -p $O; export PYTHONUNBUFFERED=1
-timeout -k 10 300 python tools/xcd_ab.py --op gat --workload cfg2 --feat 64 --ks 131072,262144 --degs 512,1024,2048 --chunks 128,384 > $O/xcd_ab_gat_cfg3b.log 2>&1 || exit $?
+timeout -k 10 400 python -u -m pytest tests/test_sage_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_sage_fused.log 2>&1 || exit $?
+timeout -k 10 300 python tools/sage_layer_ab.py > $O/sage_layer_ab.log 2>&1 || exit $?
