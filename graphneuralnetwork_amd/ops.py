@@ -553,10 +553,13 @@ def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str 
     return out
 
 
-# The fused layer pays only on a large frontier (its W stays in registers for a persistent
-# grid): cfg4 layer 0 (62,479 rows) 108 vs 111 us unfused; the 8,192-row layer 1 is faster
-# unfused (tools/sage_layer_ab.py, profiles/r02z_sage_layer_ab*.log).
-SAGE_FUSED_MIN_ROWS = 32768
+# The fused layer is opt-in (set SAGE_FUSED_MIN_ROWS to the smallest frontier to fuse): at
+# cfg4 it gains 2-3 % on layer 0 (62,479 rows: 110 vs 112 us) and loses on the 8,192-row
+# layer 1 (33 vs 25 us) -- its gathers and MFMAs do not overlap, so it costs about their
+# sum, while the unfused gather-mean and hipBLASLt GEMM each run near their own roofline.
+# A producer/consumer form (8 gather + 8 MFMA waves, double-buffered LDS tiles) was slower
+# still (129 us). tools/sage_layer_ab.py, profiles/r02z_sage_layer_ab*.log.
+SAGE_FUSED_MIN_ROWS = None
 
 
 def _rows16(t: torch.Tensor) -> bool:
@@ -578,7 +581,8 @@ def sage_layer(table: torch.Tensor, nbr_idx: torch.Tensor, weight: torch.Tensor,
     M, k = nbr_idx.shape
     feat = table.shape[1]
     H = weight.shape[0]
-    if k == 0 or self_src.shape[1] != feat or weight.shape[1] != 2 * feat or M < SAGE_FUSED_MIN_ROWS:
+    if (SAGE_FUSED_MIN_ROWS is None or M < SAGE_FUSED_MIN_ROWS or k == 0
+            or self_src.shape[1] != feat or weight.shape[1] != 2 * feat):
         return None
     if self_idx is None and self_src.shape[0] != M:
         return None

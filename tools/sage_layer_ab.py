@@ -99,6 +99,7 @@ def main():
         b = layer0()
         err = float((a - b).abs().max() / b.abs().max())
         assert err < 1e-5, err
+        forced()
         assert real_sage_layer(table, batch.frontier_nbrs, blk.weight.weight, table,
                                batch.frontier, check=False) is not None
         # each variant replayed from a HIP graph of REP calls: GPU time, no Python pacing
