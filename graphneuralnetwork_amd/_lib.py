@@ -120,6 +120,10 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_gcn_adjacency_fill": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "gnn_sample_neighbors": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, ctypes.c_uint64, _vp,
                                             _vp, _vp]),
+    "gnn_frontier_workspace_bytes": (ctypes.c_int64, [_i64]),
+    "gnn_frontier_build": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "gnn_frontier_emit": (ctypes.c_int, [_i64, _vp, _vp, _vp]),
+    "gnn_frontier_rank": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     # CPython-exact host sampler (pysample.cpp): host pointers, no stream
     "gnn_pyadj_build": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "gnn_py_layer_sample": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i32, _i64, _i32, _vp,

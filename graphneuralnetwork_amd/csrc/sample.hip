@@ -33,6 +33,59 @@ __device__ __forceinline__ int64_t uniform_below(uint64_t seed, int64_t pos, int
 
 constexpr int kMaxFanout = 256;
 
+// Fanouts up to KMAX: Floyd's picks stay in registers (both loops unrolled over KMAX with
+// a k predicate, so every array index is a compile-time constant) and the k column loads
+// are issued together at the end. Same draws and picks as the generic path below.
+template <int KMAX>
+__global__ __launch_bounds__(256) void sample_reg_kernel(const int64_t* __restrict__ rowptr,
+                                                         const int32_t* __restrict__ col,
+                                                         int64_t n_graph,
+                                                         const int64_t* __restrict__ nodes,
+                                                         int64_t n, int k, uint64_t seed,
+                                                         int64_t* __restrict__ out,
+                                                         int32_t* __restrict__ err) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t v = nodes[i];
+  int64_t* o = out + i * k;
+  if (v < 0 || v >= n_graph) {
+    atomicOr(err, 2);
+    for (int j = 0; j < k; ++j) o[j] = -1;
+    return;
+  }
+  const int64_t b = rowptr[v];
+  const int64_t deg = rowptr[v + 1] - b;
+  if (deg == 0) {
+    atomicOr(err, 1);
+    for (int j = 0; j < k; ++j) o[j] = -1;
+    return;
+  }
+  int64_t pick[KMAX];
+  if (deg <= k) {  // random.choices: k independent draws
+#pragma unroll
+    for (int j = 0; j < KMAX; ++j)
+      pick[j] = j < k ? uniform_below(seed, i, j, deg) : 0;
+  } else {         // random.sample: Floyd, draw j over [0, deg - k + jj]
+#pragma unroll
+    for (int jj = 0; jj < KMAX; ++jj) {
+      if (jj < k) {
+        const int64_t j = deg - k + jj;
+        const int64_t t = uniform_below(seed, i, j, j + 1);
+        bool seen = false;
+#pragma unroll
+        for (int q = 0; q < jj; ++q) seen |= (pick[q] == t);
+        pick[jj] = seen ? j : t;
+      }
+    }
+  }
+  int64_t c[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) c[j] = j < k ? col[b + pick[j]] : 0;
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j)
+    if (j < k) o[j] = c[j];
+}
+
 __global__ __launch_bounds__(256) void sample_kernel(const int64_t* __restrict__ rowptr,
                                                      const int32_t* __restrict__ col,
                                                      int64_t n_graph,
@@ -83,8 +136,17 @@ extern "C" int gnn_sample_neighbors(const int64_t* rowptr, const int32_t* col, i
   if (!rowptr || !col || !nodes || !out || !err_flag) return GNN_E_ARG;
   const int64_t blocks = (n + 255) / 256;
   if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
-  hipLaunchKernelGGL(sample_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
-                     static_cast<hipStream_t>(stream), rowptr, col, n_graph, nodes, n, k, seed, out,
-                     err_flag);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 g(static_cast<unsigned>(blocks)), t(256);
+  const int kk = static_cast<int>(k);
+  if (k <= 16)
+    hipLaunchKernelGGL(sample_reg_kernel<16>, g, t, 0, s, rowptr, col, n_graph, nodes, n, kk, seed,
+                       out, err_flag);
+  else if (k <= 32)
+    hipLaunchKernelGGL(sample_reg_kernel<32>, g, t, 0, s, rowptr, col, n_graph, nodes, n, kk, seed,
+                       out, err_flag);
+  else
+    hipLaunchKernelGGL(sample_kernel, g, t, 0, s, rowptr, col, n_graph, nodes, n, k, seed, out,
+                       err_flag);
   return launch_status();
 }

@@ -351,6 +351,27 @@ int gnn_sample_neighbors(const int64_t* rowptr, const int32_t* col, int64_t n_gr
                          int32_t* err_flag, void* stream);
 
 /*
+ * Batch frontier (sampler.sample_batch): the sorted distinct ids of two id lists and the
+ * position of listed ids among them -- collate_fn's set union and index remap
+ * (GraphSAGE/data_utils.py:100-116), i.e. torch.unique(cat[a, b]) + torch.searchsorted.
+ * A node bitmap marked with atomics and an exclusive scan of its word popcounts; no sort.
+ *   gnn_frontier_build: clears the bitmap, marks ids_a and ids_b (an id outside
+ *     [0, n_nodes) sets *err_flag |= 2), scans; writes the distinct count to *count
+ *     (device int64). n_a + n_b < 2^32.
+ *   gnn_frontier_emit:  frontier[0 .. count) = the distinct ids, ascending.
+ *   gnn_frontier_rank:  pos[i] = position of ids[i] in the frontier (ids must be marked;
+ *     an id outside [0, n_nodes) gives -1).
+ * workspace: gnn_frontier_workspace_bytes(n_nodes) bytes, kept between the three calls.
+ */
+int64_t gnn_frontier_workspace_bytes(int64_t n_nodes);
+int gnn_frontier_build(const int64_t* ids_a, int64_t n_a, const int64_t* ids_b, int64_t n_b,
+                       int64_t n_nodes, void* workspace, int64_t workspace_bytes, int64_t* count,
+                       int32_t* err_flag, void* stream);
+int gnn_frontier_emit(int64_t n_nodes, const void* workspace, int64_t* frontier, void* stream);
+int gnn_frontier_rank(const int64_t* ids, int64_t n, int64_t n_nodes, const void* workspace,
+                      int64_t* pos, void* stream);
+
+/*
  * Reference GCN adjacency on the device: D^-1/2 (max(A, A^T) + I)^T D^-1/2 as fp32 CSR
  * (GCN/data_utils.py:32-35 symmetrise, :78 + sp.eye, :54-60 normalize_adj, :63-70 fp32),
  * from a directed edge list (src -> dst, int64, duplicates allowed). Bit-identical to

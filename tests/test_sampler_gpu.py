@@ -14,14 +14,14 @@ def _adj(dev, n=3000, e=20000, seed=0):
     return symmetric_adjacency(s, d, n, device=dev)
 
 
-def test_sample_rules(dev):
+@pytest.mark.parametrize("k", [1, 10, 16, 25, 32, 40])  # register paths (<= 16, <= 32), generic
+def test_sample_rules(dev, k):
     from graphneuralnetwork_amd.sampler import sample_neighbors
     adj = _adj(dev)
     rowptr = adj.rowptr.cpu().numpy()
     col = adj.col.cpu().numpy()
     deg = np.diff(rowptr)
     nodes = np.nonzero(deg > 0)[0]
-    k = 10
     out = sample_neighbors(adj, torch.from_numpy(nodes), k, seed=3).cpu().numpy()
     again = sample_neighbors(adj, torch.from_numpy(nodes), k, seed=3).cpu().numpy()
     np.testing.assert_array_equal(out, again)
@@ -37,7 +37,8 @@ def test_sample_rules(dev):
         sample_neighbors(adj, torch.from_numpy(iso[:1]), k)
 
 
-def test_sample_is_uniform(dev):
+@pytest.mark.parametrize("k", [10, 25, 36])
+def test_sample_is_uniform(dev, k):
     from graphneuralnetwork_amd.graph import CsrGraph
     from graphneuralnetwork_amd.sampler import sample_neighbors
     deg = 40
@@ -47,8 +48,8 @@ def test_sample_is_uniform(dev):
     nodes = torch.zeros(1, dtype=torch.int64, device=dev)
     counts = np.zeros(deg)
     for s in range(400):
-        counts += np.bincount(sample_neighbors(g, nodes, 10, seed=s).cpu().numpy()[0], minlength=deg)
-    expected = 400 * 10 / deg
+        counts += np.bincount(sample_neighbors(g, nodes, k, seed=s).cpu().numpy()[0], minlength=deg)
+    expected = 400 * k / deg
     chi2 = ((counts - expected) ** 2 / expected).sum()
     assert chi2 < 90  # 39 dof: p ~ 1e-5 threshold
 
@@ -91,3 +92,43 @@ def test_duplicate_nodes_and_layers_draw_independently(dev):
     a = sample_neighbors(g, nodes[:1], 10, seed=5, layer=1).cpu().numpy()
     b = sample_neighbors(g, nodes[:1], 10, seed=6, layer=0).cpu().numpy()
     assert not np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("n_nodes,n_a,n_b", [(1, 1, 0), (31, 5, 40), (33, 33, 33),
+                                             (100_000, 512, 12_800), (10_000_000, 8192, 204_800)])
+def test_frontier_matches_unique_and_searchsorted(dev, n_nodes, n_a, n_b):
+    """gnn_frontier_* (node bitmap + popcount scan) == torch.unique(cat) + searchsorted,
+    bit for bit, incl. repeated ids, ids on word edges and a near-empty bitmap."""
+    from graphneuralnetwork_amd.sampler import build_frontier
+    g = torch.Generator(device=dev).manual_seed(n_nodes + n_a)
+    a = torch.randint(0, n_nodes, (n_a,), device=dev, generator=g)
+    b = torch.randint(0, n_nodes, (n_b,), device=dev, generator=g)
+    if n_nodes > 64:
+        b[:3] = torch.tensor([0, 31, n_nodes - 1], device=dev)
+        a = torch.cat([a, a[:7]])  # duplicates inside one list
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    s1, rank = build_frontier(a, b.view(-1, 1) if n_b else b, n_nodes, err)
+    ref = torch.unique(torch.cat([a, b]))
+    assert torch.equal(s1, ref)
+    assert torch.equal(rank(a), torch.searchsorted(ref, a))
+    assert torch.equal(rank(b), torch.searchsorted(ref, b))
+
+
+def test_batch_errors_and_frontier_out_of_range(dev):
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.sampler import build_frontier, sample_batch
+    # node 2 has no neighbour: the reference's random.choices([]) IndexError
+    rowptr = torch.tensor([0, 2, 3, 3], dtype=torch.int64, device=dev)
+    col = torch.tensor([1, 0, 0], dtype=torch.int32, device=dev)
+    g = CsrGraph(rowptr, col, torch.ones(3, device=dev), 3, 3)
+    with pytest.raises(IndexError, match="empty sequence"):
+        sample_batch(g, torch.tensor([0, 2], device=dev), (4, 2))
+    with pytest.raises(IndexError, match="out of range"):
+        sample_batch(g, torch.tensor([0, 7], device=dev), (4, 2))
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    with pytest.raises(IndexError, match="out of range"):
+        build_frontier(torch.tensor([0, 5], device=dev), torch.tensor([1], device=dev), 3, err)
+    b = sample_batch(g, torch.tensor([0, 1], device=dev), (4, 2), seed=3)
+    assert torch.equal(b.frontier[b.center_map], torch.tensor([0, 1], device=dev))
+    nb = b.frontier[b.neigh_map].cpu().numpy()   # every sampled id is a true neighbour
+    assert set(nb[0]) <= {0, 1} and set(nb[1]) == {0}

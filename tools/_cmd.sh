@@ -1,7 +1,4 @@
 set -o pipefail
-O=gpurun_out/r02zf; mkdir -p $O; export PYTHONUNBUFFERED=1
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || exit $?
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || exit $?
-timeout -k 10 300 python bench.py --workload cfg3 > $O/bench_gat.log 2>&1 || exit $?
-timeout -k 10 400 python bench.py --workload cfg4 > $O/bench_sage.log 2>&1 || exit $?
+O=gpurun_out/r02z; mkdir -p $O; export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest tests/test_sampler_gpu.py tests/test_sage_gpu.py tests/test_han_sagepy_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_frontier.log 2>&1 || exit $?
+timeout -k 10 400 python bench.py --workload cfg4 --no-cpu-baseline > $O/bench_sage_frontier.log 2>&1 || exit $?
