@@ -295,6 +295,12 @@ def describe_path(g, feat: int):
     return "spmm_csr_kernel (+ spmm_fixup_kernel), per-step HIP events"
 
 
+def _all_gather_phase_values(v: list, world: int, dev):
+    """[world, len(v)] float64 of every rank's phase times (an all-to-all-v of one row)."""
+    from graphneuralnetwork_amd.distributed import _all_gather_floats
+    return _all_gather_floats(v, world, dev)
+
+
 def time_steps(step, steps: int, warmup: int, dev):
     """Per-step HIP-event times (ms) on the current stream + wall seconds for `steps` steps."""
     stream = torch.cuda.current_stream(dev)
@@ -633,6 +639,19 @@ def main():
     kern_ms = statistics.mean(step_ms)
     achieved = bytes_local / (kern_ms / 1e3) / 1e9
 
+    phases = None
+    if world > 1 and dev.type == "cuda":
+        # one more (untimed) step with events at every phase boundary: per-rank compute
+        # phases, the compute stream's waits on the exchanges, and the all-to-all-v times
+        prof = runner.profile(X, bias)
+        names = sorted(prof)
+        vals = _all_gather_phase_values([prof[k] for k in names], world, dev)
+        phases = {"rank0": {k: round(v, 4) for k, v in prof.items()},
+                  "max_over_ranks": {k: round(float(vals[:, i].max()), 4)
+                                     for i, k in enumerate(names)},
+                  "exchange_MB_rank0": {
+                      "send": round(sum(part.send_counts) * 4 * F / 1e6, 1),
+                      "recv": round(sum(part.recv_counts) * 4 * F / 1e6, 1)}}
     layer_ms = None
     log(f"[bench] aggregation timed: {statistics.mean(step_ms):.3f} ms/launch")
     if world == 1 and not args.no_layer:
@@ -674,7 +693,8 @@ def main():
             **({"gcn_layer_ms": layer_ms} if layer_ms is not None else {}),
             **({"partition_build_s": BUILD_INFO.get("partition_build_s"),
                 "row_bounds": part.bounds,
-                "balance_max_mean_cost": BUILD_INFO.get("balance_max_mean_cost")}
+                "balance_max_mean_cost": BUILD_INFO.get("balance_max_mean_cost"),
+                "phases_ms": phases}
                if world > 1 else {}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,

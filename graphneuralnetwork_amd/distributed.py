@@ -445,8 +445,15 @@ class EdgeCutSpmm:
         self._turn = 0
         self.cuda = self.device.type == "cuda"
         self.comm_stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self._marks = None  # [(name, event)] while profile() runs
 
-    def _exchange(self, recv, send, recv_counts, send_counts, cur):
+    def _mark(self, name, stream):
+        if self._marks is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            self._marks.append((name, ev))
+
+    def _exchange(self, recv, send, recv_counts, send_counts, cur, tag="a2a"):
         """All-to-all-v on the communication stream after the work queued on ``cur``;
         returns an event marking its completion (None off-GPU: done on return)."""
         if not self.cuda:
@@ -454,10 +461,41 @@ class EdgeCutSpmm:
             return None
         self.comm_stream.wait_stream(cur)
         with torch.cuda.stream(self.comm_stream):
+            self._mark(tag + ">", self.comm_stream)
             _all_to_all_v(recv, send, recv_counts, send_counts, self.group)
+            self._mark(tag + "<", self.comm_stream)
             ev = torch.cuda.Event()
             ev.record(self.comm_stream)
         return ev
+
+    def profile(self, x, bias=None, activation=None) -> dict:
+        """One call with timing events at every phase boundary (GPU only): milliseconds of
+        each compute-stream phase in issue order (a "wait_*" phase is the time the compute
+        stream stalled on an exchange), of each all-to-all-v on the communication stream,
+        and of the whole call. For the multi-GPU bench's per-rank breakdown."""
+        if not self.cuda:
+            raise RuntimeError("profile() needs the GPU path")
+        self._marks = []
+        cur = torch.cuda.current_stream(self.device)
+        try:
+            self._mark("start", cur)
+            self(x, bias, activation)
+            self._mark("end", cur)
+            torch.cuda.synchronize(self.device)
+        finally:
+            marks, self._marks = self._marks, None
+        res, prev, opened = {}, None, {}
+        for name, ev in marks:
+            if name.endswith(">"):
+                opened[name[:-1]] = ev
+            elif name.endswith("<"):
+                res[name[:-1] + "_ms"] = opened.pop(name[:-1]).elapsed_time(ev)
+            else:
+                if prev is not None and name != "end":
+                    res[name + "_ms"] = prev.elapsed_time(ev)
+                prev = ev if name != "end" else prev
+        res["total_ms"] = marks[0][1].elapsed_time(marks[-1][1])
+        return res
 
     def _wait(self, ev, cur):
         if ev is not None:
@@ -489,34 +527,45 @@ class EdgeCutSpmm:
             if p.any_x:
                 if self.send_x.shape[0]:
                     self._gather(x, p.send_x_idx, self.send_x)
+                self._mark("gather_send_x", cur)
                 ev_x = self._exchange(self.recv_x, self.send_x, p.recv_x_counts,
-                                      p.send_x_counts, cur)
+                                      p.send_x_counts, cur, "a2a_x")
             if p.any_p:
                 if self.send_p.shape[0]:
                     self._spmm(p.send_p, x, None, out=self.send_p)  # partial sums for peers
+                self._mark("spmm_send_p", cur)
                 ev_p = self._exchange(self.recv_p, self.send_p, p.recv_p_counts,
-                                      p.send_p_counts, cur)
+                                      p.send_p_counts, cur, "a2a_p")
             self._spmm(p.interior, x, bias, out=out)           # overlaps both exchanges
+            self._mark("spmm_interior", cur)
             last = "p" if p.any_p else ("x" if p.any_x else None)
             if p.any_x:
                 self._wait(ev_x, cur)
+                self._mark("wait_x", cur)
                 self._spmm(p.halo_x, self.recv_x, None, out=out, accumulate=True,
                            activation=activation if last == "x" else None)
+                self._mark("spmm_halo_x", cur)
             if p.any_p:
                 self._wait(ev_p, cur)
+                self._mark("wait_p", cur)
                 self._spmm(p.halo_p, self.recv_p, None, out=out, accumulate=True,
                            activation=activation)
+                self._mark("spmm_halo_p", cur)
             if last is None and activation is not None:
                 self._spmm(p.halo_x, self.recv_x, None, out=out, accumulate=True,
                            activation=activation)
             return out
         if p.send_idx.numel():
             self._gather(x, p.send_idx, self.send_buf)
+        self._mark("gather_send", cur)
         ev = self._exchange(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts, cur)
         self._spmm(p.interior, x, bias, out=out)               # overlaps the exchange
+        self._mark("spmm_interior", cur)
         self._wait(ev, cur)
+        self._mark("wait", cur)
         self._spmm(p.halo, self.recv_buf, None, activation=activation, out=out,
                    accumulate=True)
+        self._mark("spmm_halo", cur)
         return out
 
 

@@ -68,7 +68,10 @@ def _worker(rank, world, port, n, F, q, kind="gather"):
         r0, r1 = part.bounds[rank], part.bounds[rank + 1]
         run = EdgeCutSpmm(part, F, dev)
         y = run(X[r0:r1].contiguous(), b, activation="relu")
-        y = run(X[r0:r1].contiguous(), b, activation="relu")  # second call reuses buffers
+        prof = run.profile(X[r0:r1].contiguous(), b, activation="relu")  # bench.py's breakdown
+        assert prof["total_ms"] > 0 and prof["spmm_interior_ms"] >= 0
+        assert any(k.startswith("a2a") for k in prof) and any(k.startswith("wait") for k in prof)
+        y = run(X[r0:r1].contiguous(), b, activation="relu")  # later calls reuse buffers
         torch.cuda.synchronize()
         q.put((rank, r0, r1, y.cpu().numpy()))
     finally:
