@@ -149,3 +149,28 @@ def test_graphsage_pytorch_sampled_gathered_path(dev):
     (g1,) = torch.autograd.grad((y_g * gy).sum(), table)
     (g2,) = torch.autograd.grad((y_d * gy).sum(), table)
     close(g1.cpu().numpy(), g2.cpu().numpy())
+
+
+def test_han_layer_batched_metapaths_match(golden, dev, monkeypatch):
+    """The inference HANLayer runs all metapaths as ONE block-diagonal aggregation launch;
+    it equals the per-metapath GATConv path (and so the reference), and a metapath graph
+    with an edgeless row falls back to the per-metapath path."""
+    from graphneuralnetwork_amd import han
+    d, net, gs, h = _han(golden, dev)
+    net.eval()
+    with torch.no_grad():
+        batched = net(gs, h)
+        assert net.layers[0]._block_cache[1] is not None
+        monkeypatch.setattr(han, "BATCH_METAPATHS", False)
+        single = net(gs, h)
+    close(batched.cpu().numpy(), single.cpu().numpy(), rtol=1e-5)
+    close(batched.cpu().numpy(), d["logits"])
+    monkeypatch.setattr(han, "BATCH_METAPATHS", True)
+    g0 = gs[0].clone()
+    g0[5, :] = 0                                  # an edgeless row in metapath 0
+    with torch.no_grad():
+        y = net.layers[0]([g0] + gs[1:], h)
+        assert net.layers[0]._block_cache[1] is None
+        monkeypatch.setattr(han, "BATCH_METAPATHS", False)
+        y0 = net.layers[0]([g0] + gs[1:], h)
+    close(y.cpu().numpy(), y0.cpu().numpy(), rtol=1e-5)
