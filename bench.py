@@ -573,7 +573,10 @@ def main():
         t0 = time.time()
         if args.exchange == "cover":
             # row blocks re-cut for the work the cover moves (cost model, 2 refinements)
-            part, hist = build_cover_exchange_balanced(g, rank, world)
+            part, hist = build_cover_exchange_balanced(
+                g, rank, world, progress=lambda it, mx, mean, s: log(
+                    f"[bench] cover partition, build {it}: max/mean cost {mx / mean:.3f} "
+                    f"({s:.1f}s)"))
             BUILD_INFO["balance_max_mean_cost"] = hist
             work = (f"interior {part.interior.nnz}, partial {part.send_p.nnz}, halo "
                     f"{part.halo_x.nnz} + {part.halo_p.nnz}; "
@@ -603,6 +606,7 @@ def main():
     step()
     torch.cuda.synchronize(dev)
     BUILD_INFO["first_step_s"] = time.perf_counter() - t_first
+    log(f"[bench] first step (builds the per-graph plans) {BUILD_INFO['first_step_s']:.2f}s")
     for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize(dev)

@@ -360,7 +360,7 @@ def cover_cost(part: CoverExchange, alpha: float = XGMI_ROW_COST) -> float:
 
 
 def build_cover_exchange_balanced(g: CsrGraph, rank: int, world: int, group=None,
-                                  iters: int = 2, alpha: float = XGMI_ROW_COST):
+                                  iters: int = 2, alpha: float = XGMI_ROW_COST, progress=None):
     """``build_cover_exchange`` with row blocks re-cut for the work the cover moves.
 
     The cover shifts work between ranks (partial sums are computed by the column
@@ -370,16 +370,21 @@ def build_cover_exchange_balanced(g: CsrGraph, rank: int, world: int, group=None
     ``cover_cost``, turns it into a cost density per block (cost / (edges + rows)) and
     re-cuts with those densities; the partition with the lowest maximum cost is kept
     (the same choice on every rank: they all see the same costs). Returns
-    (partition, per-iteration max/mean costs).
+    (partition, per-iteration max/mean costs). ``progress(it, max_cost, mean_cost, seconds)``
+    is called after each build.
     """
+    import time
     bounds = nnz_balanced_bounds(g.rowptr, world)
     best, best_max, history = None, None, []
     deg1 = (g.rowptr[1:] - g.rowptr[:-1]).to(torch.float64) + 1.0
     for it in range(iters + 1):
+        t0 = time.perf_counter()
         part = build_cover_exchange(g, rank, world, group, bounds=bounds)
         costs = _all_gather_floats([cover_cost(part, alpha)], world, g.device, group)[:, 0]
         mx, mean = float(costs.max()), float(costs.mean())
         history.append((mx, mean))
+        if progress is not None:
+            progress(it, mx, mean, time.perf_counter() - t0)
         if best_max is None or mx < best_max:
             best, best_max = part, mx
         else:

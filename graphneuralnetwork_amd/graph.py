@@ -198,7 +198,7 @@ class XcdHubPlan:
 
 def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, k: int,
                 min_deg: int, chunk: int, xcds: int = XCDS,
-                waves_per_wg: int = SPMM_WAVES_PER_WG):
+                waves_per_wg: int = SPMM_WAVES_PER_WG, phases: int = 1):
     """The two COO edge lists of ``XcdHubPlan`` (torch ops on any device; the CPU tests
     check them against the oracle SpMM).
 
@@ -206,9 +206,14 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     ``((item_rows, item_cols, item_vals, n_pos, n_items), (rest_rows, rest_cols, rest_vals),
     pos_row)`` where ``pos_row[p]`` is the graph row of item position p (pads: 0).
     Item edges keep their CSR order; rest rows list their unmoved edges in CSR order,
-    then their partial refs in (slice, chunk) order."""
-    if chunk < 4 or k < xcds:  # balanced chunks of a >= 2-edge item then hold >= 2 edges
-        raise ValueError("xcd hub staging needs chunk >= 4 and k >= the XCD count")
+    then their partial refs in (slice, chunk) order.
+
+    ``phases`` > 1 deals the hub ranks to xcds * phases slices (rank % S); the items of
+    slice s run on XCD s % xcds in phase s // xcds, the phases one after another in the
+    launch order, so each XCD's L2 holds 1 / (xcds * phases) of the table at a time."""
+    S = xcds * phases
+    if chunk < 4 or k < S or phases < 1:  # balanced chunks of a >= 2-edge item hold >= 2 edges
+        raise ValueError("xcd hub staging needs chunk >= 4 and k >= xcds * phases")
     dev = rowptr.device
     i64 = torch.int64
     n = rowptr.numel() - 1
@@ -216,8 +221,8 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     rows_e = torch.repeat_interleave(torch.arange(n, device=dev, dtype=i64), deg)
     c = col_hub.to(i64)
     eid = torch.nonzero((c < 0) & (deg[rows_e] >= min_deg)).view(-1)
-    s_e = (-1 - c[eid]) % xcds
-    key = rows_e[eid] * xcds + s_e
+    s_e = (-1 - c[eid]) % S
+    key = rows_e[eid] * S + s_e
     order = torch.argsort(key, stable=True)                  # by (row, slice), CSR order kept
     eid, key, s_e = eid[order], key[order], s_e[order]
     _, inv, m = torch.unique_consecutive(key, return_inverse=True, return_counts=True)
@@ -236,20 +241,26 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     it_slice[item] = s_e
     it_row = torch.empty(n_items, dtype=i64, device=dev)
     it_row[item] = rows_e[eid]
-    # position of an item: the j-th item of slice s goes to workgroup (j // W) * xcds + s
+    # position of an item: the j-th item of slice s (phase p = s // xcds) goes to workgroup
+    # base[p] + (j // W) * xcds + s % xcds
     by_slice = torch.argsort(it_slice, stable=True)
-    cnt = torch.bincount(it_slice, minlength=xcds)
+    cnt = torch.bincount(it_slice, minlength=S)
     j = torch.empty(n_items, dtype=i64, device=dev)
     j[by_slice] = torch.arange(n_items, device=dev, dtype=i64) - (torch.cumsum(cnt, 0) - cnt)[
         it_slice[by_slice]]
     W = waves_per_wg
-    per = -(-int(cnt.max()) // W) * W
-    pos = ((j // W) * xcds + it_slice) * W + j % W
-    n_pos = per * xcds
+    per = [-(-int(v) // W) * W for v in cnt.view(phases, xcds).max(1).values.tolist()]
+    base_l = [0]
+    for v in per:
+        base_l.append(base_l[-1] + v * xcds)                 # positions before each phase
+    base = torch.tensor(base_l, dtype=i64, device=dev)
+    pos = base[it_slice // xcds] + ((j // W) * xcds + it_slice % xcds) * W + j % W
+    n_pos = base_l[-1]
     filled = torch.zeros(n_pos, dtype=torch.bool, device=dev)
     filled[pos] = True
     pad = torch.nonzero(~filled).view(-1)                    # 2 zero-valued edges of its slice
-    pad_col = -1 - (pad // W) % xcds
+    pad_phase = torch.searchsorted(base, pad, right=True) - 1
+    pad_col = -1 - (pad_phase * xcds + ((pad - base[pad_phase]) // W) % xcds)
     items = (torch.cat([pos[item], pad, pad]), torch.cat([c[eid], pad_col, pad_col]),
              torch.cat([val[eid], torch.zeros(2 * pad.numel(), dtype=val.dtype, device=dev)]),
              n_pos, n_items)
@@ -315,12 +326,13 @@ class CsrGraph:
             self._plans[key] = p
         return p
 
-    def xcd_hub_plan(self, k: int, min_deg: int, chunk: int) -> "XcdHubPlan | None":
-        """XCD-sliced hub staging plan (built once per (k, min_deg, chunk), cached);
+    def xcd_hub_plan(self, k: int, min_deg: int, chunk: int,
+                     phases: int = 1) -> "XcdHubPlan | None":
+        """XCD-sliced hub staging plan (built once per (k, min_deg, chunk, phases), cached);
         None when no row has two hub edges in one slice."""
-        key = ("_xcd", k, min_deg, chunk)
+        key = ("_xcd", k, min_deg, chunk, phases)
         if key not in self._plans:
-            self._plans[key] = _build_xcd_hub_plan(self, k, min_deg, chunk)
+            self._plans[key] = _build_xcd_hub_plan(self, k, min_deg, chunk, phases)
         return self._plans[key]
 
     def transpose(self) -> "CsrGraph":
@@ -406,11 +418,12 @@ def _build_hub_plan(g: CsrGraph, k: int) -> HubPlan:
     return HubPlan(hub_ids, col_hub, err)
 
 
-def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int) -> "XcdHubPlan | None":
+def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int,
+                        phases: int = 1) -> "XcdHubPlan | None":
     hub = g.hub_plan(k)
-    if hub.k < XCDS or g.nnz == 0:
+    if hub.k < XCDS * phases or g.nnz == 0:
         return None
-    coo = xcd_hub_coo(g.rowptr, hub.col_hub, g.val, hub.k, min_deg, chunk)
+    coo = xcd_hub_coo(g.rowptr, hub.col_hub, g.val, hub.k, min_deg, chunk, phases=phases)
     if coo is None:
         return None
     (ir, ic, iv, n_pos, n_items), (rr, rc, rv), pos_row = coo

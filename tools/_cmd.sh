@@ -1,6 +1,7 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_han_sagepy_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/han_t.log 2>&1
-timeout -k 10 200 python -u tools/han_ab.py > gpurun_out/han_ab.log 2>&1
-timeout -k 10 200 python -u tools/han_ab.py --n 20000 --deg 32 >> gpurun_out/han_ab.log 2>&1
-timeout -k 10 200 python -u tools/han_ab.py --n 3025 --deg 40 --fin 1870 >> gpurun_out/han_ab.log 2>&1
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest tests/test_spmm_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k xcd > gpurun_out/t_xcd.log 2>&1
+timeout -k 10 300 python -u tools/xcd_ab.py --workload cfg2 --ks 262144 --degs 128,256,512 --phases 1,2,4 > gpurun_out/xcd_phase_cfg2.log 2>&1
+timeout -k 10 300 python -u tools/xcd_ab.py --workload ns --ks 262144 --degs 128,512 --phases 1,2,4 --rounds 4 > gpurun_out/xcd_phase_ns.log 2>&1
+NP=8 RT=540 bash tools/gpu_check.sh rehearse

@@ -18,7 +18,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for MODE in "$@"; do
   case $MODE in
-    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) step pytest_gpu ${TT:-1200} python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     testsk) step pytest_gpu_k 900 python -m pytest tests -m gpu -v -p no:cacheprovider -k "${K:-spmm}" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 5 ;;
@@ -31,6 +31,7 @@ for MODE in "$@"; do
     pmc) step pmc_fetch${PTAG:-} 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch${PTAG:-}" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}
          step pmc_write${PTAG:-} 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write${PTAG:-}" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
     rehearse2) GNN_BENCH_DEVICE=0 step rehearse2 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 ;;
+    rehearse) GNN_BENCH_DEVICE=0 step rehearse${NP:-4} ${RT:-600} python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NP:-4} --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus ${NP:-4} --backend gloo --steps 3 --warmup 1 ${BENCH_ARGS:-} ;;
     *) echo "unknown mode $MODE"; exit 2 ;;
   esac
 done

@@ -2,7 +2,7 @@
 single-pass hub staging, at one shape, over (hub rows K, min row degree, item chunk).
 
     python tools/xcd_ab.py [--workload cfg2|ns] [--feat 128] [--ks 131072,262144]
-                           [--degs 64,128,256] [--chunks 128]
+                           [--degs 64,128,256] [--chunks 128] [--phases 1,2,4]
 
 Every variant is checked against the unstaged kernel (fp32 rounding) before timing. Times
 include the per-call hub-row copy and both passes.
@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--ks", default="131072,262144")
     ap.add_argument("--degs", default="64,128,256")
     ap.add_argument("--chunks", default="128")
+    ap.add_argument("--phases", default="1",
+                    help="slices per XCD run one after another (ops.XCD_PHASES)")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--op", default="spmm", choices=["spmm", "gat"],
                     help="gat: the cfg3 GAT aggregation (dense softmax + ELU, 8 heads x F/8)")
@@ -59,11 +61,14 @@ def main():
     for k in (int(v) for v in args.ks.split(",")):
         for dg in (int(v) for v in args.degs.split(",")):
             for ch in (int(v) for v in args.chunks.split(",")):
-                variants[f"xcd K={k} deg>={dg} chunk={ch}"] = dict(hubs=k, xcd=True, deg=dg, chunk=ch)
+                for ph in (int(v) for v in args.phases.split(",")):
+                    variants[f"xcd K={k} deg>={dg} chunk={ch} phases={ph}"] = dict(
+                        hubs=k, xcd=True, deg=dg, chunk=ch, phases=ph)
 
     def call(v):
         if v.get("xcd"):
             ops.XCD_MIN_DEG, ops.XCD_CHUNK = v["deg"], v["chunk"]
+            ops.XCD_PHASES = v["phases"]
         return spmm_forward(g, X, b, out=Y, hubs=v["hubs"], xcd=v["xcd"])
 
     scale = float(ref.abs().max())
@@ -73,6 +78,10 @@ def main():
         err = float((Y - ref).abs().max()) / scale
         assert err < 1e-5, (name, err)
         v["err"] = err
+        if v.get("xcd") and args.op == "spmm":
+            xp = g.xcd_hub_plan(min(v["hubs"], n), v["deg"], min(v["chunk"], ops.seg_len_for(F)),
+                                v["phases"])
+            v["items"] = xp.n_items if xp is not None else 0
     print(json.dumps({"op": args.op, "workload": args.workload, "feat": F, "nnz": g.nnz}),
           flush=True)
     stream = torch.cuda.current_stream(dev)
@@ -91,7 +100,8 @@ def main():
         med = statistics.median(t)
         print(json.dumps({"variant": name, "median_ms": round(med, 4), "min_ms": round(min(t), 4),
                           "algo_GBps": round(nbytes / (med / 1e3) / 1e9),
-                          "max_rel_err": variants[name]["err"]}), flush=True)
+                          "max_rel_err": variants[name]["err"],
+                          "items": variants[name].get("items")}), flush=True)
 
 
 if __name__ == "__main__":
