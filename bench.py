@@ -522,6 +522,9 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default profiles/traffic_<workload>_F<feat>.json")
     args = ap.parse_args()
+    if os.environ.get("GNN_BENCH_STACKS"):  # rehearsals: every rank dumps its stack periodically
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["GNN_BENCH_STACKS"]), repeat=True)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

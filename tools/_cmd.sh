@@ -1,7 +1,3 @@
-set -e
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest tests/test_spmm_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k xcd > gpurun_out/t_xcd.log 2>&1
-timeout -k 10 300 python -u tools/xcd_ab.py --workload cfg2 --ks 262144 --degs 128,256,512 --phases 1,2,4 > gpurun_out/xcd_phase_cfg2.log 2>&1
-timeout -k 10 300 python -u tools/xcd_ab.py --workload ns --ks 262144 --degs 128,512 --phases 1,2,4 --rounds 4 > gpurun_out/xcd_phase_ns.log 2>&1
-NP=8 RT=540 bash tools/gpu_check.sh rehearse
+GNN_BENCH_STACKS=90 NP=8 RT=560 bash tools/gpu_check.sh rehearse
