@@ -519,6 +519,9 @@ def main():
                          "feature rows only (gather)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = multi-rank rehearsal (host-staged exchange), never for numbers")
+    ap.add_argument("--scale", type=float, default=1.0,
+                    help="graph size factor (rehearsals of the N-rank path on one GPU only; the "
+                         "JSON config reports the nodes / edges actually used)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default profiles/traffic_<workload>_F<feat>.json")
     args = ap.parse_args()
@@ -555,7 +558,7 @@ def main():
 
     wl = WORKLOADS[args.workload]
     grow = 1 if wl.get("strong") else world
-    nodes, edges = wl["nodes"] * grow, wl["edges"] * grow
+    nodes, edges = int(wl["nodes"] * grow * args.scale), int(wl["edges"] * grow * args.scale)
     F = args.feat if args.feat is not None else wl.get("feat", 128)
     g = build_graph(nodes, edges, dev, rank, world)
     gen = torch.Generator(device=dev).manual_seed(0)
