@@ -198,7 +198,8 @@ class XcdHubPlan:
 
 def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, k: int,
                 min_deg: int, chunk: int, xcds: int = XCDS,
-                waves_per_wg: int = SPMM_WAVES_PER_WG, phases: int = 1):
+                waves_per_wg: int = SPMM_WAVES_PER_WG, phases: int = 1,
+                item_k: int | None = None):
     """The two COO edge lists of ``XcdHubPlan`` (torch ops on any device; the CPU tests
     check them against the oracle SpMM).
 
@@ -210,7 +211,10 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
 
     ``phases`` > 1 deals the hub ranks to xcds * phases slices (rank % S); the items of
     slice s run on XCD s % xcds in phase s // xcds, the phases one after another in the
-    launch order, so each XCD's L2 holds 1 / (xcds * phases) of the table at a time."""
+    launch order, so each XCD's L2 holds 1 / (xcds * phases) of the table at a time.
+
+    ``item_k`` < k limits the items to the item_k hottest hub rows (a smaller set per XCD
+    slice); the edges to the other hub rows stay in ``rest`` and read the whole table."""
     S = xcds * phases
     if chunk < 4 or k < S or phases < 1:  # balanced chunks of a >= 2-edge item hold >= 2 edges
         raise ValueError("xcd hub staging needs chunk >= 4 and k >= xcds * phases")
@@ -220,7 +224,10 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     deg = rowptr[1:] - rowptr[:-1]
     rows_e = torch.repeat_interleave(torch.arange(n, device=dev, dtype=i64), deg)
     c = col_hub.to(i64)
-    eid = torch.nonzero((c < 0) & (deg[rows_e] >= min_deg)).view(-1)
+    ik = k if item_k is None else min(int(item_k), k)
+    if ik < S:
+        raise ValueError("xcd hub staging needs item_k >= xcds * phases")
+    eid = torch.nonzero((c < 0) & (c >= -ik) & (deg[rows_e] >= min_deg)).view(-1)
     s_e = (-1 - c[eid]) % S
     key = rows_e[eid] * S + s_e
     order = torch.argsort(key, stable=True)                  # by (row, slice), CSR order kept
@@ -326,13 +333,13 @@ class CsrGraph:
             self._plans[key] = p
         return p
 
-    def xcd_hub_plan(self, k: int, min_deg: int, chunk: int,
-                     phases: int = 1) -> "XcdHubPlan | None":
-        """XCD-sliced hub staging plan (built once per (k, min_deg, chunk, phases), cached);
-        None when no row has two hub edges in one slice."""
-        key = ("_xcd", k, min_deg, chunk, phases)
+    def xcd_hub_plan(self, k: int, min_deg: int, chunk: int, phases: int = 1,
+                     item_k: int | None = None) -> "XcdHubPlan | None":
+        """XCD-sliced hub staging plan (built once per (k, min_deg, chunk, phases, item_k),
+        cached); None when no row has two hub edges in one slice."""
+        key = ("_xcd", k, min_deg, chunk, phases, item_k)
         if key not in self._plans:
-            self._plans[key] = _build_xcd_hub_plan(self, k, min_deg, chunk, phases)
+            self._plans[key] = _build_xcd_hub_plan(self, k, min_deg, chunk, phases, item_k)
         return self._plans[key]
 
     def transpose(self) -> "CsrGraph":
@@ -418,12 +425,15 @@ def _build_hub_plan(g: CsrGraph, k: int) -> HubPlan:
     return HubPlan(hub_ids, col_hub, err)
 
 
-def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int,
-                        phases: int = 1) -> "XcdHubPlan | None":
+def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int, phases: int = 1,
+                        item_k: int | None = None) -> "XcdHubPlan | None":
     hub = g.hub_plan(k)
     if hub.k < XCDS * phases or g.nnz == 0:
         return None
-    coo = xcd_hub_coo(g.rowptr, hub.col_hub, g.val, hub.k, min_deg, chunk, phases=phases)
+    if item_k is not None and min(int(item_k), hub.k) < XCDS * phases:
+        return None
+    coo = xcd_hub_coo(g.rowptr, hub.col_hub, g.val, hub.k, min_deg, chunk, phases=phases,
+                      item_k=item_k)
     if coo is None:
         return None
     (ir, ic, iv, n_pos, n_items), (rr, rc, rv), pos_row = coo

@@ -65,6 +65,7 @@ XCD_HUB_ROWS = 262144
 XCD_MIN_DEG = 128
 XCD_CHUNK = 128
 XCD_PHASES = 1  # slices per XCD, run one after another (graph.xcd_hub_coo ``phases``)
+XCD_ITEM_ROWS = None  # items read only the hottest XCD_ITEM_ROWS hub rows (None: all K)
 
 
 def xcd_hub_rows_for(n_cols: int, feat: int) -> int:
@@ -132,7 +133,7 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
     if xcd and g.nnz:
         kx = xcd_hub_rows_for(g.n_cols, feat) if hubs is None else min(int(hubs), g.n_cols)
         chunk = min(XCD_CHUNK, seg)
-        xp = (g.xcd_hub_plan(kx, XCD_MIN_DEG, chunk, XCD_PHASES)
+        xp = (g.xcd_hub_plan(kx, XCD_MIN_DEG, chunk, XCD_PHASES, XCD_ITEM_ROWS)
               if kx >= 8 * XCD_PHASES and chunk >= 4 else None)
         if xp is not None:
             _spmm_xcd(lib, g, xp, x, feat, bias, out, seg, skip_empty, flags, stream)

@@ -317,10 +317,12 @@ def test_xcd_hub_staging(dev, F, monkeypatch):
             ref = spmm_forward(g, X, b, activation="elu", seg_len=seg_len, hubs=0)
             acc_ref = spmm_forward(g, X, None, out=base.clone(), accumulate=True, seg_len=seg_len,
                                    hubs=0)
-            for k, ph in ((8, 1), (200, 1), (n, 1), (200, 2), (n, 4)):
+            for k, ph, ik in ((8, 1, None), (200, 1, None), (n, 1, None), (200, 2, None),
+                              (n, 4, None), (n, 1, 64), (200, 2, 100)):
                 monkeypatch.setattr(ops, "XCD_PHASES", ph)  # slices per XCD, in launch order
+                monkeypatch.setattr(ops, "XCD_ITEM_ROWS", ik)  # items from the ik hottest rows
                 y = spmm_forward(g, X, b, activation="elu", seg_len=seg_len, hubs=k, xcd=True)
-                key = ("_xcd", k, 4, min(8, seg_len or 10 ** 9), ph)
+                key = ("_xcd", k, 4, min(8, seg_len or 10 ** 9), ph, ik)
                 assert g._plans.get(key) is not None, key
                 close(y.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5)
                 assert torch.equal(y, spmm_forward(g, X, b, activation="elu", seg_len=seg_len,
@@ -329,6 +331,7 @@ def test_xcd_hub_staging(dev, F, monkeypatch):
                                  hubs=k, xcd=True)
                 close(y.cpu().numpy(), acc_ref.cpu().numpy(), rtol=1e-5)
     monkeypatch.setattr(ops, "XCD_PHASES", 1)
+    monkeypatch.setattr(ops, "XCD_ITEM_ROWS", None)
     Xn = X.cpu().numpy()
     y = spmm_forward(g, X, b, hubs=n, xcd=True).cpu().numpy()
     close(y, O.spmm_csr(rowptr, col, val, Xn, b.cpu().numpy()))

@@ -42,24 +42,24 @@ def _csr_spmm(rows, cols, vals, n_rows, src):
     return out
 
 
-@pytest.mark.parametrize("k,min_deg,chunk,phases", [(64, 16, 8, 1), (200, 2, 4, 1),
-                                                    (500, 64, 128, 1), (3000, 1, 4, 1),
-                                                    (3000, 1, 5, 1), (500, 16, 8, 2),
-                                                    (3000, 2, 4, 4)])
-def test_xcd_plan_algebra_and_layout(k, min_deg, chunk, phases):
+@pytest.mark.parametrize("k,min_deg,chunk,phases,item_k", [
+    (64, 16, 8, 1, None), (200, 2, 4, 1, None), (500, 64, 128, 1, None),
+    (3000, 1, 4, 1, None), (3000, 1, 5, 1, None), (500, 16, 8, 2, None),
+    (3000, 2, 4, 4, None), (3000, 2, 8, 1, 100), (500, 16, 8, 2, 64)])
+def test_xcd_plan_algebra_and_layout(k, min_deg, chunk, phases, item_k):
     from graphneuralnetwork_amd.graph import xcd_hub_coo
     rowptr, col, val = _graph()
     n = rowptr.size - 1
     hub, ch = _hub_rename(col, n, k)
     res = xcd_hub_coo(torch.from_numpy(rowptr), torch.from_numpy(ch.astype(np.int32)),
-                      torch.from_numpy(val), k, min_deg, chunk, phases=phases)
+                      torch.from_numpy(val), k, min_deg, chunk, phases=phases, item_k=item_k)
     assert res is not None
     (ir, ic, iv, n_pos, n_items), (rr, rc, rv), pos_row = res
     ir, ic, iv, rr, rc, rv = (t.numpy() for t in (ir, ic, iv, rr, rc, rv))
     # layout: positions fill whole workgroups of every XCD; an item only reads its slice
     # (slice = rank % (XCDS * phases), on XCD slice % XCDS), the phases in launch order
     assert n_pos % (XCDS * W) == 0
-    assert ((ic < 0) & (ic >= -k)).all()
+    assert ((ic < 0) & (ic >= -(item_k or k))).all()
     sl = (-1 - ic) % (XCDS * phases)
     np.testing.assert_array_equal(sl % XCDS, (ir // W) % XCDS)
     o = np.argsort(ir, kind="stable")
