@@ -360,6 +360,8 @@ def run_gat(args, dev):
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                         "traffic_GBps": traffic / (k_ms / 1e3) / 1e9 if traffic else None,
+                        "traffic_frac": traffic / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBPS
+                        if traffic else None,
                         "traffic_source": tsrc,
                         "kernel": ("gather_rows_kernel x2 (hub staging: Wh / er rows of the %d "
                                    "highest-degree columns) + " % hub_k if hub_k else "") +
@@ -478,6 +480,9 @@ def run_sage(args, dev):
            "first_sample_s": t_sample,
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                        "traffic_GBps": traffic / (k_ms / 1e3) / 1e9 if traffic else None,
+                        "traffic_frac": traffic / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBPS
+                        if traffic else None,
                         "traffic_source": tsrc,
                         "kernel": "sage_aggregate_kernel<gather, mean> (layer 0: |S1| x 10 from the 10M table)"
                                   + (", %d launches per HIP-graph replay" % REP if agg_graph_ms else
@@ -713,6 +718,10 @@ def main():
                          # memory side actually served; "achieved" counts algorithmic bytes
                          "traffic_GBps": traffic["traffic_bytes"] / (kern_ms / 1e3) / 1e9
                          if traffic else None,
+                         # the same rate as a fraction of the 8 TB/s peak: what the memory
+                         # side served (frac above counts algorithmic, no-reuse bytes)
+                         "traffic_frac": traffic["traffic_bytes"] / (kern_ms / 1e3) / 1e9
+                         / HBM_PEAK_GBPS if traffic else None,
                          "traffic_source": (str(tpath.relative_to(ROOT)) + ": rocprofv3 --pmc "
                                             "FETCH_SIZE x2 + WRITE_SIZE of this command")
                          if traffic else None,
