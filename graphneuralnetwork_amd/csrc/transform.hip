@@ -1,7 +1,9 @@
 // transform.hip -- the GCN feature transform on the matrix cores: Y = X W^T (fp32).
 //
 // Replaces `support = self.dense(X_input)` (nn.Linear, no bias) at GCN/GCN.py:42, the
-// dense half of Graph_conv_layer.forward, for the inference path (no autograd).
+// dense half of Graph_conv_layer.forward, for the inference path (no autograd); with the
+// ReLU epilogue (gnn_linear_relu_f32) the SageLayer's relu(weight(cat[self, agg])) at
+// GraphSAGE/GraphSAGE.py:18-20.
 // Shapes: X [n, K] row-major, W [FO, K] (nn.Linear's [out, in]), Y [n, FO].
 //
 // One workgroup = 4 waves; the X tile (64 rows x K) is staged in LDS once by all four
@@ -15,25 +17,35 @@
 // reads, rows padded by 4 floats so the 16 rows of a read hit distinct banks).
 #include "common.hpp"
 
+extern "C" int gnn_gcn_transform_supported(int64_t k, int64_t fout);
+
 namespace gnn {
 
 constexpr int kTfWaves = 4;
-constexpr int kTfBlock = kTfWaves * kWave;
 constexpr int kTfRows = 64;  // rows per tile (4 MFMA row blocks)
 using tf32x4 = __attribute__((ext_vector_type(4))) float;
 
-template <int K, int CB>
-__global__ __launch_bounds__(kTfBlock) void gcn_transform_kernel(const float* __restrict__ x,
-                                                                 int64_t ldx, int64_t n_rows,
-                                                                 const float* __restrict__ w,
-                                                                 float* __restrict__ y,
-                                                                 int64_t ldy) {
+// NW waves per workgroup, each owning CB 16-column blocks of W (FO = NW * CB * 16).
+// K = 256 (the SageLayer's cat[self, agg]) runs 8 waves x 1 block: its 64 W values per lane
+// stay resident, the X fragment is read from LDS in chunks of XC k-steps, and the four
+// 16-row blocks of a tile run as four independent MFMA chains (one chain of 64 dependent
+// MFMAs per wave would leave the matrix core waiting on its own results).
+template <int K, int CB, int NW, bool RELU>
+__global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* __restrict__ x,
+                                                                   int64_t ldx, int64_t n_rows,
+                                                                   const float* __restrict__ w,
+                                                                   float* __restrict__ y,
+                                                                   int64_t ldy) {
+  constexpr int kTfBlock = NW * kWave;
   constexpr int S = K / 4;           // MFMA k-steps
-  constexpr int FO = kTfWaves * CB * 16;
+  constexpr int XC = S <= 32 ? S : 16;  // k-steps of X held in registers at a time
+  constexpr int RB = CB == 1 && S > 32 ? 4 : 1;  // 16-row blocks computed together
+  constexpr int FO = NW * CB * 16;
   constexpr int LDA = K + 4;         // padded LDS row (floats)
   constexpr int V4 = kTfRows * K / 4;  // float4s per tile
   constexpr int NV = V4 / kTfBlock;    // per thread
   static_assert(V4 % kTfBlock == 0, "tile must split evenly over the workgroup");
+  static_assert(S % XC == 0 && XC % 4 == 0, "X chunks of whole float4s");
   __shared__ float xt[kTfRows * LDA];
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = threadIdx.x >> 6;
@@ -79,33 +91,55 @@ __global__ __launch_bounds__(kTfBlock) void gcn_transform_kernel(const float* __
     fetch(g + gridDim.x);
     const int64_t row0 = g * kTfRows;
 #pragma unroll
-    for (int rb = 0; rb < kTfRows / 16; ++rb) {
-      float xb[S];
-      const float* xr = xt + (rb * 16 + r) * LDA + q * S;
+    for (int rb0 = 0; rb0 < kTfRows / 16; rb0 += RB) {
+      // RB row blocks at once: RB * CB independent accumulation chains per wave
+      tf32x4 acc[RB][CB];
 #pragma unroll
-      for (int v = 0; v < S / 4; ++v) {
-        const float4 t = *reinterpret_cast<const float4*>(xr + 4 * v);
-        xb[4 * v] = t.x;
-        xb[4 * v + 1] = t.y;
-        xb[4 * v + 2] = t.z;
-        xb[4 * v + 3] = t.w;
+      for (int j = 0; j < RB; ++j)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) acc[j][cb] = tf32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c0 = 0; c0 < S; c0 += XC) {
+        float xb[RB][XC];
+#pragma unroll
+        for (int j = 0; j < RB; ++j) {
+          const float* xr = xt + ((rb0 + j) * 16 + r) * LDA + q * S + c0;
+#pragma unroll
+          for (int v = 0; v < XC / 4; ++v) {
+            const float4 t = *reinterpret_cast<const float4*>(xr + 4 * v);
+            xb[j][4 * v] = t.x;
+            xb[j][4 * v + 1] = t.y;
+            xb[j][4 * v + 2] = t.z;
+            xb[j][4 * v + 3] = t.w;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < XC; ++s) {
+#pragma unroll
+          for (int j = 0; j < RB; ++j)
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb)
+              acc[j][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[cb][c0 + s], xb[j][s],
+                                                                acc[j][cb], 0, 0, 0);
+        }
       }
-      tf32x4 acc[CB];
 #pragma unroll
-      for (int cb = 0; cb < CB; ++cb) acc[cb] = tf32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < RB; ++j) {
+        // acc[j][cb][i] = Y[row0 + 16 (rb0 + j) + r][(wv*CB + cb)*16 + 4q + i]
+        const int64_t orow = row0 + (rb0 + j) * 16 + r;
+        if (orow < n_rows) {
 #pragma unroll
-      for (int s = 0; s < S; ++s) {
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
-          acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[cb][s], xb[s], acc[cb], 0, 0, 0);
-      }
-      // acc[cb][i] = Y[row0 + 16 rb + r][(wv*CB + cb)*16 + 4q + i]
-      const int64_t orow = row0 + rb * 16 + r;
-      if (orow < n_rows) {
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
-          *reinterpret_cast<float4*>(y + orow * ldy + (wv * CB + cb) * 16 + 4 * q) =
-              make_float4(acc[cb][0], acc[cb][1], acc[cb][2], acc[cb][3]);
+          for (int cb = 0; cb < CB; ++cb) {
+            float4 o = make_float4(acc[j][cb][0], acc[j][cb][1], acc[j][cb][2], acc[j][cb][3]);
+            if constexpr (RELU) {
+              o.x = fmaxf(o.x, 0.f);
+              o.y = fmaxf(o.y, 0.f);
+              o.z = fmaxf(o.z, 0.f);
+              o.w = fmaxf(o.w, 0.f);
+            }
+            *reinterpret_cast<float4*>(y + orow * ldy + (wv * CB + cb) * 16 + 4 * q) = o;
+          }
+        }
       }
     }
     __syncthreads();  // the next tile overwrites xt
@@ -113,28 +147,53 @@ __global__ __launch_bounds__(kTfBlock) void gcn_transform_kernel(const float* __
   (void)FO;
 }
 
-template <int K, int CB>
+template <int K, int CB, int NW, bool RELU>
 static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const float* w,
                             float* y, int64_t ldy, hipStream_t s) {
   const int64_t tiles = (n_rows + kTfRows - 1) / kTfRows;
 #ifndef GNN_TF_GRID
 #define GNN_TF_GRID 512  // persistent grid: 2 workgroups per CU
 #endif
-  const int64_t grid = tiles < GNN_TF_GRID ? tiles : GNN_TF_GRID;
-  hipLaunchKernelGGL((gcn_transform_kernel<K, CB>), dim3(static_cast<unsigned>(grid)),
-                     dim3(kTfBlock), 0, s, x, ldx, n_rows, w, y, ldy);
+  constexpr int64_t kGrid = GNN_TF_GRID * kTfWaves / NW;  // 8-wave workgroups: 1 per CU
+  const int64_t grid = tiles < kGrid ? tiles : kGrid;
+  hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU>), dim3(static_cast<unsigned>(grid)),
+                     dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy);
   return launch_status();
 }
 
-template <int K>
+template <int K, bool RELU>
 static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t n_rows,
                               const float* w, float* y, int64_t ldy, hipStream_t s) {
-  if (fout == 64) return launch_transform<K, 1>(x, ldx, n_rows, w, y, ldy, s);
-  if constexpr (K <= 128)
-    if (fout == 128) return launch_transform<K, 2>(x, ldx, n_rows, w, y, ldy, s);
+  if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, s);
+  if (fout == 128) {
+    if constexpr (K <= 128)
+      return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, s);
+    else
+      return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, s);
+  }
   if constexpr (K <= 64)
-    if (fout == 256) return launch_transform<K, 4>(x, ldx, n_rows, w, y, ldy, s);
+    if (fout == 256) return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, s);
   return GNN_E_UNSUPPORTED;
+}
+
+template <bool RELU>
+static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                           const float* w, int64_t fout, float* y, int64_t ldy,
+                           void* stream) {
+  if (n_rows < 0 || ldx < k || ldy < fout) return GNN_E_ARG;
+  if (!gnn_gcn_transform_supported(k, fout)) return GNN_E_UNSUPPORTED;
+  if (n_rows == 0) return GNN_OK;
+  if (!x || !w || !y) return GNN_E_ARG;
+  if (ldx % 4 || ldy % 4 || !aligned_to(x, 16) || !aligned_to(y, 16) || !aligned_to(w, 16))
+    return GNN_E_ALIGN;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (k) {
+    case 16: return dispatch_transform<16, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
+    case 32: return dispatch_transform<32, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
+    case 64: return dispatch_transform<64, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
+    case 128: return dispatch_transform<128, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
+    default: return dispatch_transform<256, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
+  }
 }
 
 }  // namespace gnn
@@ -144,8 +203,7 @@ using namespace gnn;
 extern "C" int gnn_gcn_transform_supported(int64_t k, int64_t fout) {
   const bool kk = k == 16 || k == 32 || k == 64 || k == 128 || k == 256;
   if (!kk) return 0;
-  if (fout == 64) return 1;
-  if (fout == 128) return k <= 128;
+  if (fout == 64 || fout == 128) return 1;
   if (fout == 256) return k <= 64;
   return 0;
 }
@@ -153,18 +211,11 @@ extern "C" int gnn_gcn_transform_supported(int64_t k, int64_t fout) {
 extern "C" int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
                                      const float* w, int64_t fout, float* y, int64_t ldy,
                                      void* stream) {
-  if (n_rows < 0 || ldx < k || ldy < fout) return GNN_E_ARG;
-  if (!gnn_gcn_transform_supported(k, fout)) return GNN_E_UNSUPPORTED;
-  if (n_rows == 0) return GNN_OK;
-  if (!x || !w || !y) return GNN_E_ARG;
-  if (ldx % 4 || ldy % 4 || !aligned_to(x, 16) || !aligned_to(y, 16) || !aligned_to(w, 16))
-    return GNN_E_ALIGN;
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  switch (k) {
-    case 16: return dispatch_transform<16>(fout, x, ldx, n_rows, w, y, ldy, s);
-    case 32: return dispatch_transform<32>(fout, x, ldx, n_rows, w, y, ldy, s);
-    case 64: return dispatch_transform<64>(fout, x, ldx, n_rows, w, y, ldy, s);
-    case 128: return dispatch_transform<128>(fout, x, ldx, n_rows, w, y, ldy, s);
-    default: return dispatch_transform<256>(fout, x, ldx, n_rows, w, y, ldy, s);
-  }
+  return transform_entry<false>(x, ldx, n_rows, k, w, fout, y, ldy, stream);
+}
+
+extern "C" int gnn_linear_relu_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                                   const float* w, int64_t fout, float* y, int64_t ldy,
+                                   void* stream) {
+  return transform_entry<true>(x, ldx, n_rows, k, w, fout, y, ldy, stream);
 }

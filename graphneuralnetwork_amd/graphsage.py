@@ -24,7 +24,22 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import from_coo
-from .ops import gather_rows, sage_aggregate, sage_gather_aggregate, sage_layer, spmm_forward
+from .ops import (gather_rows, gcn_transform, sage_aggregate, sage_gather_aggregate, sage_layer,
+                  spmm_forward)
+
+# the inference SageLayer GEMM relu([self | agg] @ W^T) runs on the hand-written fp32-MFMA
+# kernel (gnn_linear_relu_f32) up to SAGE_MFMA_MAX_SMALL rows and from SAGE_MFMA_MIN_LARGE
+# rows up, on hipBLASLt in between. Alone (K=256, N=128, tools/sage_gemm_ab.py,
+# profiles/r02zk_sage_gemm_ab.log): 8192 rows 16.6 vs 21.5-32.3 us, 62479 rows 46.7 vs
+# 40.4 us, 200000 rows 127 vs 136 us; but inside the cfg4 forward the 8192-row layer is
+# faster on hipBLASLt (145 vs 149 us per forward, tools/sage_gemm_forward_ab.py,
+# profiles/r02zk_sage_gemm_forward_ab.log), so the small-M range is off.
+SAGE_MFMA_MAX_SMALL = 0
+SAGE_MFMA_MIN_LARGE = 131072
+
+
+def _sage_gemm_on_mfma(rows: int) -> bool:
+    return rows <= SAGE_MFMA_MAX_SMALL or rows >= SAGE_MFMA_MIN_LARGE
 
 
 class Gathered(NamedTuple):
@@ -197,6 +212,10 @@ def _fused_sage_layer(block, center, neigh: Gathered):
     sage_gather_aggregate(neigh.table, neigh.index, "MEAN", check=not neigh.trusted,
                           out=buf[:, n:])
     W = block.weight.weight
+    if _sage_gemm_on_mfma(M):  # relu(buf @ W^T) on the hand-written fp32-MFMA kernel
+        y = gcn_transform(buf, W, relu=True)
+        if y is not None:
+            return y
     zero = torch.zeros(W.shape[0], dtype=W.dtype, device=W.device)
     return torch._addmm_activation(zero, buf, W.t())
 

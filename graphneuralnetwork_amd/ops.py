@@ -271,10 +271,13 @@ def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: to
     return wh, el, er
 
 
-def gcn_transform(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None:
+def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
+                  out: torch.Tensor | None = None) -> torch.Tensor | None:
     """support = x @ weight^T on fp32 MFMA (gnn_gcn_transform_f32), the dense half of
-    Graph_conv_layer.forward (GCN/GCN.py:42); inference only (no autograd). None when the
-    shape is not covered (the caller then uses nn.Linear / hipBLASLt)."""
+    Graph_conv_layer.forward (GCN/GCN.py:42); ``relu=True``: max(x @ weight^T, 0)
+    (gnn_linear_relu_f32, the SageLayer at GraphSAGE/GraphSAGE.py:18-20). Inference only
+    (no autograd). None when the shape is not covered (the caller then uses nn.Linear /
+    hipBLASLt)."""
     _require_device(x, weight)
     if (x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 2
             or weight.dim() != 2 or x.shape[1] != weight.shape[1]):
@@ -286,11 +289,16 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor | None:
     if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
         x = x.contiguous()
     w = weight.contiguous()
-    y = torch.empty((x.shape[0], fout), dtype=torch.float32, device=x.device)
-    _lib.check(lib.gnn_gcn_transform_f32(x.data_ptr(), x.stride(0), x.shape[0], k, w.data_ptr(),
-                                         fout, y.data_ptr(), fout, _lib.stream_handle(x.device)),
-               "gnn_gcn_transform_f32")
-    return y
+    if out is None:
+        out = torch.empty((x.shape[0], fout), dtype=torch.float32, device=x.device)
+    elif (out.shape != (x.shape[0], fout) or out.dtype != torch.float32 or out.stride(1) != 1
+          or out.stride(0) % 4 or out.data_ptr() % 16):
+        raise ValueError("out must be float32 [rows, fout], 16-B aligned rows")
+    fn, name = ((lib.gnn_linear_relu_f32, "gnn_linear_relu_f32") if relu else
+                (lib.gnn_gcn_transform_f32, "gnn_gcn_transform_f32"))
+    _lib.check(fn(x.data_ptr(), x.stride(0), x.shape[0], k, w.data_ptr(), fout, out.data_ptr(),
+                  out.stride(0), _lib.stream_handle(x.device)), name)
+    return out
 
 
 def col_mean(x: torch.Tensor) -> torch.Tensor:

@@ -151,13 +151,22 @@ int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t hea
  * nn.Linear weight [fout, k] (row-major), fp32 in / fp32 accumulate
  * (v_mfma_f32_16x16x4_f32). Replaces `support = self.dense(X_input)` at GCN/GCN.py:42
  * (inference path). Shapes covered: gnn_gcn_transform_supported(k, fout) != 0
- * (k in {16, 32, 64, 128, 256}; fout 64, or 128 with k <= 128, or 256 with k <= 64);
+ * (k in {16, 32, 64, 128, 256}; fout 64 or 128, or 256 with k <= 64);
  * other shapes return GNN_E_UNSUPPORTED (the caller uses a library GEMM). x, w, y
  * 16-B aligned, ldx and ldy multiples of 4 (else GNN_E_ALIGN).
  */
 int gnn_gcn_transform_supported(int64_t k, int64_t fout);
 int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,
                           int64_t fout, float* y, int64_t ldy, void* stream);
+
+/*
+ * The same product with a ReLU epilogue: y = max(x @ w^T, 0). Replaces the SageLayer's
+ * F.relu(self.weight(torch.cat([self_feats, aggregate_feats], dim=1))) at
+ * GraphSAGE/GraphSAGE.py:18-20 (inference; x = the [M, 2F] cat buffer). Same shapes,
+ * alignment and return codes as gnn_gcn_transform_f32.
+ */
+int gnn_linear_relu_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,
+                        int64_t fout, float* y, int64_t ldy, void* stream);
 
 /*
  * GAT feature transform on the matrix cores with the attention logits fused:

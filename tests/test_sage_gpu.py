@@ -202,3 +202,32 @@ def test_graphsage_forward_fused_matches_unfused(dev, monkeypatch):
         emb0, logits0 = net(*batch.forward_args(table), None, None, None, None, None)
     np.testing.assert_allclose(emb.cpu().numpy(), emb0.cpu().numpy(), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(logits.cpu().numpy(), logits0.cpu().numpy(), rtol=1e-4, atol=1e-5)
+
+
+def test_graphsage_forward_mfma_gemm_matches_library(dev, monkeypatch):
+    """The inference SageLayer GEMM relu([self | agg] @ W^T) on the hand-written fp32-MFMA
+    kernel (gnn_linear_relu_f32, forced for every layer here) gives the embeddings and logits
+    of the hipBLASLt GEMM within fp32 tolerance."""
+    from graphneuralnetwork_amd import graphsage as GS
+    from graphneuralnetwork_amd.graph import from_coo
+    from graphneuralnetwork_amd.sampler import sample_batch
+    rng = np.random.default_rng(11)
+    n, F = 5000, 128
+    s, d = rng.integers(0, n, 60000), rng.integers(0, n, 60000)
+    adj = from_coo(torch.from_numpy(np.concatenate([s, d])).to(dev),
+                   torch.from_numpy(np.concatenate([d, s])).to(dev),
+                   torch.ones(120000, device=dev), n, n)
+    table = torch.randn(n, F, device=dev)
+    deg = adj.rowptr[1:] - adj.rowptr[:-1]
+    seeds = torch.nonzero(deg > 0).view(-1)[:700]
+    batch = sample_batch(adj, seeds, (25, 10), seed=5)
+    net = GS.GraphSAGE(2, F, F, False, agg_func="MEAN", Unsupervised=False,
+                       class_size=3).to(dev).eval()
+    with torch.no_grad():
+        monkeypatch.setattr(GS, "_sage_gemm_on_mfma", lambda rows: True)
+        emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+        monkeypatch.setattr(GS, "_sage_gemm_on_mfma", lambda rows: False)
+        emb0, logits0 = net(*batch.forward_args(table), None, None, None, None, None)
+    assert (emb >= 0).all()
+    np.testing.assert_allclose(emb.cpu().numpy(), emb0.cpu().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(logits.cpu().numpy(), logits0.cpu().numpy(), rtol=1e-4, atol=1e-5)

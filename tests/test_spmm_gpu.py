@@ -381,10 +381,11 @@ def test_hub_plan_structure(dev):
 
 
 @pytest.mark.parametrize("k,fout", [(16, 64), (32, 128), (64, 64), (64, 256), (128, 128),
-                                    (256, 64)])
+                                    (256, 64), (256, 128)])
 @pytest.mark.parametrize("n", [1, 63, 1000, 4097])
 def test_gcn_transform_mfma(dev, k, fout, n):
-    """gnn_gcn_transform_f32 (fp32 MFMA, W [fout, k] as nn.Linear) vs a float64 matmul."""
+    """gnn_gcn_transform_f32 (fp32 MFMA, W [fout, k] as nn.Linear) vs a float64 matmul;
+    gnn_linear_relu_f32 = the same with max(., 0) (the SageLayer, GraphSAGE.py:18-20)."""
     from graphneuralnetwork_amd.ops import gcn_transform
     rng = np.random.default_rng(k * 7 + fout + n)
     X = rng.standard_normal((n, k + 4)).astype(np.float32)
@@ -395,6 +396,8 @@ def test_gcn_transform_mfma(dev, k, fout, n):
         y = gcn_transform(x, torch.from_numpy(W).to(dev))
         assert y is not None and y.shape == (n, fout)
         close(y.cpu().numpy(), ref)
+        yr = gcn_transform(x, torch.from_numpy(W).to(dev), relu=True)
+        assert torch.equal(yr, torch.clamp_min(y, 0.0))
 
 
 def test_gcn_transform_fallback_and_training(dev):
@@ -404,6 +407,8 @@ def test_gcn_transform_fallback_and_training(dev):
     x = torch.randn(100, 7, device=dev)
     assert gcn_transform(x, torch.randn(5, 7, device=dev)) is None
     assert gcn_transform(torch.randn(100, 256, device=dev), torch.randn(256, 256, device=dev)) is None
+    assert gcn_transform(torch.randn(100, 128, device=dev), torch.randn(256, 128, device=dev),
+                         relu=True) is None
     n = 300
     rowptr, col, val = _rand_graph(n, 3000, 8)
     g = _graph(rowptr, col, val, n, dev)
