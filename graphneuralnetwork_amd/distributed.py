@@ -623,9 +623,9 @@ class EdgeCutGat:
         p = self.part
         F = self.heads * self.fh
         el, er = self._logits(wh_own, self.heads, self.fh, a_src, a_dst)
-        packed = torch.cat([wh_own, er], dim=1)
-        if p.send_idx.numel():
-            self._gather(packed, p.send_idx, self.send_buf)
+        if p.send_idx.numel():  # [Wh | er] rows for the peers, gathered into their columns
+            self._gather(wh_own, p.send_idx, self.send_buf[:, :F])
+            self._gather(er.contiguous(), p.send_idx, self.send_buf[:, F:])
         _all_to_all_v(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts, self.group)
         wh_ext = torch.cat([wh_own, self.recv_buf[:, :F]], dim=0)
         er_ext = torch.cat([er, self.recv_buf[:, F:]], dim=0)
