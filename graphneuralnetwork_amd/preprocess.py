@@ -106,3 +106,29 @@ def gcn_normalized_csr(src, dst, n: int, device=None) -> CsrGraph:
     rowptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     torch.cumsum(torch.bincount(c, minlength=n), 0, out=rowptr[1:])
     return CsrGraph(rowptr, r[order].to(torch.int32).contiguous(), val[order].contiguous(), n, n)
+
+
+def normalize_features(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Row-normalised features as the reference loader produces them: normalize_features
+    (GCN/data_utils.py:39-51) on sp.csr_matrix(x, float32), then
+    torch.Tensor(features.toarray()) (:81-83) -- bit for bit (gnn_normalize_features_f32,
+    features.hip: numpy's float32 pairwise row sum over the nonzeros, a float64 reciprocal
+    with inf -> 0, float64 products rounded to fp32). ``x``: device float32 [N, F]
+    (F <= 16384); ``out`` must not overlap it."""
+    if not x.is_cuda:
+        raise RuntimeError("normalize_features runs on the GPU (HIP); got a CPU tensor")
+    if x.dtype != torch.float32 or x.dim() != 2:
+        raise ValueError("x must be a float32 [N, F] tensor")
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    elif out.shape != x.shape or out.dtype != torch.float32 or out.stride(1) != 1:
+        raise ValueError("out must be float32 with x's shape and unit column stride")
+    lib = _lib.load()
+    _lib.check(lib.gnn_normalize_features_f32(x.data_ptr(), x.stride(0), x.shape[0], x.shape[1],
+                                              out.data_ptr(), out.stride(0),
+                                              _lib.stream_handle(x.device)),
+               "gnn_normalize_features_f32")
+    return out
+

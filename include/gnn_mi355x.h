@@ -160,6 +160,17 @@ int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k
                           int64_t fout, float* y, int64_t ldy, void* stream);
 
 /*
+ * Feature row normalisation, bit-exact with the reference loader: normalize_features
+ * (GCN/data_utils.py:39-51) then torch.Tensor(features.toarray()) (:81-83). rowsum = the
+ * first nonzero of the row plus numpy's float32 pairwise sum of the others (scipy's csr
+ * sum = np.add.reduceat); r = rowsum ** -1 in float64, inf -> 0; y = fp32(r * x) in
+ * float64, +0.0 where x == 0 or r == 0. x [n_rows, ldx], y [n_rows, ldy] must not
+ * overlap; n_cols <= 16384 (else GNN_E_UNSUPPORTED).
+ */
+int gnn_normalize_features_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t n_cols,
+                               float* y, int64_t ldy, void* stream);
+
+/*
  * The same product with a ReLU epilogue: y = max(x @ w^T, 0). Replaces the SageLayer's
  * F.relu(self.weight(torch.cat([self_feats, aggregate_feats], dim=1))) at
  * GraphSAGE/GraphSAGE.py:18-20 (inference; x = the [M, 2F] cat buffer). Same shapes,

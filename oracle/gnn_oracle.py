@@ -22,6 +22,58 @@ import numpy as np
 # ----------------------------------------------------------------- graph prep
 
 
+def _np_pairwise_f32(a: np.ndarray) -> np.float32:
+    """numpy's float32 pairwise summation (the add-reduce inner loop, numpy 2.2
+    ``FLOAT_pairwise_sum``): fewer than 8 values left to right from -0.0; up to 128 values
+    in 8 strided accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail
+    left to right; longer runs split at n/2 rounded down to a multiple of 8."""
+    f = np.float32
+    n = a.size
+    if n < 8:
+        res = f(-0.0)
+        for v in a:
+            res = f(res + v)
+        return res
+    if n <= 128:
+        r = [f(v) for v in a[:8]]
+        i = 8
+        while i < n - (n % 8):
+            for j in range(8):
+                r[j] = f(r[j] + a[i + j])
+            i += 8
+        res = f(f(f(r[0] + r[1]) + f(r[2] + r[3])) + f(f(r[4] + r[5]) + f(r[6] + r[7])))
+        for v in a[i:]:
+            res = f(res + v)
+        return res
+    n2 = n // 2
+    n2 -= n2 % 8
+    return f(_np_pairwise_f32(a[:n2]) + _np_pairwise_f32(a[n2:]))
+
+
+def normalize_features(x: np.ndarray) -> np.ndarray:
+    """GCN/data_utils.py:39-51 applied to sp.csr_matrix(x, dtype=float32), then
+    torch.Tensor(.toarray()) as load_cora does (:83): the row sum is scipy's
+    ``np.add.reduceat`` over the row's stored (nonzero) values in column order -- the first
+    value plus numpy's float32 pairwise sum of the rest (``_np_pairwise_f32``); r_inv =
+    rowsum ** -1 in float64 with inf -> 0; each value r_inv * x in float64, cast to fp32.
+    A zero r_inv zeroes the row to +0.0: scipy's sparse product drops the exact-zero
+    products (0 x negative = -0.0 included), so toarray() reads +0.0 there."""
+    x = np.asarray(x, dtype=np.float32)
+    out = np.zeros_like(x)
+    for i in range(x.shape[0]):
+        nz = np.flatnonzero(x[i])
+        if nz.size == 0:
+            continue
+        v = x[i, nz]
+        s = np.float32(v[0] + _np_pairwise_f32(v[1:])) if v.size > 1 else v[0]
+        with np.errstate(divide="ignore"):
+            r = np.power(np.float64(s), -1.0)
+        if np.isinf(r):
+            continue          # r_inv = 0: every product is an exact zero, dropped -> +0.0
+        out[i, nz] = (r * v.astype(np.float64)).astype(np.float32)
+    return out
+
+
 def coalesce_counts(src: np.ndarray, dst: np.ndarray, n: int):
     """COO edge list -> unique (row, col, count) sorted row-major.
 

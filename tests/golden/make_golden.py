@@ -450,7 +450,45 @@ def part_pysampler():
     np.savez_compressed(HERE / "pysampler.npz", **out)
 
 
-PARTS = {"gcn": part_gcn, "gat": part_gat, "sage": part_sage, "han": part_han,
+def part_features():
+    """GCN/data_utils.py normalize_features (row normalisation of the feature matrix) on
+    real-valued float32 matrices, through the reference's own function and load_cora's
+    torch.Tensor(features.toarray()) (GCN/data_utils.py:81-83)."""
+    sys.path.insert(0, str(REF / "GCN"))
+    import torch
+    import data_utils as du  # reference GCN/data_utils.py
+    import scipy.sparse as sp
+
+    rng = np.random.default_rng(5)
+    mats = {}
+    # 1: Cora-like shape, ~2 % density, varied magnitudes; 2: long rows (pairwise splits
+    # past 128 and 256 stored values), zero rows, rows whose sum is exactly 0 or negative
+    n, f = 600, 1433
+    x = np.where(rng.random((n, f)) < 0.02,
+                 rng.standard_normal((n, f)) * rng.choice([1e-3, 1.0, 1e3], size=(n, 1)), 0)
+    x[::50] = 0
+    mats["a"] = x.astype(np.float32)
+    n, f = 64, 1100
+    y = np.zeros((n, f), np.float32)
+    for i in range(n):
+        k = int(rng.integers(0, f))
+        cols = rng.choice(f, size=k, replace=False)
+        y[i, cols] = rng.standard_normal(k).astype(np.float32) * 10
+    y[3] = 0
+    y[4] = 0
+    y[4, :3] = (1.5, -1.5, 0.0)   # sum exactly 0 -> inf -> 0 (and 0 x -1.5)
+    y[5] = -np.abs(y[5])          # negative sum
+    mats["b"] = y
+    out = {}
+    for k, m in mats.items():
+        norm = du.normalize_features(sp.csr_matrix(m, dtype=np.float32))
+        out[f"x_{k}"] = m
+        out[f"y_{k}"] = torch.Tensor(norm.toarray()).numpy()
+    np.savez_compressed(HERE / "gcn_features.npz", **out)
+    print("gcn_features.npz", {k: v.shape for k, v in out.items()})
+
+
+PARTS = {"gcn": part_gcn, "features": part_features, "gat": part_gat, "sage": part_sage, "han": part_han,
          "sagepy": part_sagepy, "pysampler": part_pysampler}
 
 if __name__ == "__main__":

@@ -57,3 +57,44 @@ def test_builder_rejects_bad_endpoints(dev):
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     with pytest.raises(IndexError):
         gcn_adjacency(torch.tensor([0, 5], device=dev), torch.tensor([1, 2], device=dev), 5)
+
+
+def test_normalize_features_bit_exact(golden, dev):
+    """gnn_normalize_features_f32 (C5, GCN/data_utils.py:39-51 + :81-83) equals the
+    reference's output bit for bit on the golden matrices and the Cora fixture, and the
+    oracle on wider random rows (pairwise trees several levels deep, NaN-free)."""
+    from graphneuralnetwork_amd.preprocess import normalize_features
+    g = golden("gcn_features")
+    for k in "ab":
+        x = torch.from_numpy(g["x_" + k]).to(dev)
+        y = normalize_features(x).cpu().numpy()
+        np.testing.assert_array_equal(y.view(np.uint32), g["y_" + k].view(np.uint32))
+        xs = torch.zeros(x.shape[0], x.shape[1] + 3, device=dev)[:, 1:x.shape[1] + 1]
+        xs.copy_(x)                                            # strided rows
+        assert torch.equal(normalize_features(xs).view(torch.int32),
+                           torch.from_numpy(g["y_" + k]).to(dev).view(torch.int32))
+    c = golden("gcn_cora")
+    raw = torch.zeros(int(c["n"]), int(c["n_feat"]), device=dev)
+    raw[torch.from_numpy(c["feat_row"]).long(), torch.from_numpy(c["feat_col"]).long()] = 1.0
+    y = normalize_features(raw).cpu().numpy()
+    np.testing.assert_array_equal(y[c["feat_row"], c["feat_col"]], c["feat_val"])
+    rng = np.random.default_rng(3)
+    x = np.where(rng.random((40, 3000)) < rng.random((40, 1)), rng.standard_normal((40, 3000)),
+                 0).astype(np.float32)
+    x[7] = 0
+    x[8, :] = -0.0
+    y = normalize_features(torch.from_numpy(x).to(dev)).cpu().numpy()
+    np.testing.assert_array_equal(y.view(np.uint32), O.normalize_features(x).view(np.uint32))
+
+
+def test_normalize_features_rejects(dev):
+    from graphneuralnetwork_amd.preprocess import normalize_features
+    x = torch.randn(10, 8, device=dev)
+    with pytest.raises(RuntimeError):
+        normalize_features(x, out=x)                           # overlapping x / out
+    with pytest.raises(RuntimeError):
+        normalize_features(torch.randn(2, 16385, device=dev))  # wider than the LDS row
+    with pytest.raises(RuntimeError):
+        normalize_features(x.cpu())                            # no CPU path
+    assert normalize_features(torch.empty(0, 8, device=dev)).shape == (0, 8)
+

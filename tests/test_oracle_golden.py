@@ -38,6 +38,35 @@ def test_gcn_adjacency_pipeline_matches_reference(golden):
     np.testing.assert_array_equal(val[key_o], rv[key_r])
 
 
+def test_normalize_features_matches_reference(golden):
+    """C5 normalize_features (GCN/data_utils.py:39-51, then torch.Tensor(.toarray()) at
+    :81-83): bit-exact on real-valued matrices (pairwise row sums past 128 and 256 values,
+    zero rows, an exactly-zero and a negative row sum) and on the Cora fixture's binary
+    features."""
+    g = golden("gcn_features")
+    for k in "ab":
+        y = O.normalize_features(g["x_" + k])
+        np.testing.assert_array_equal(y.view(np.uint32), g["y_" + k].view(np.uint32))
+    c = golden("gcn_cora")
+    raw = np.zeros((int(c["n"]), int(c["n_feat"])), np.float32)
+    raw[c["feat_row"], c["feat_col"]] = 1.0
+    y = O.normalize_features(raw)
+    np.testing.assert_array_equal(y[c["feat_row"], c["feat_col"]], c["feat_val"])
+    assert np.count_nonzero(y) == c["feat_val"].size
+
+
+def test_numpy_pairwise_restatement():
+    """The oracle's float32 pairwise sum is numpy's add-reduce (what scipy's csr row sum
+    runs): bit-exact on random lengths 1..700 and magnitudes."""
+    rng = np.random.default_rng(0)
+    for _ in range(400):
+        n = int(rng.integers(1, 700))
+        v = (rng.standard_normal(n) * rng.choice([1e-3, 1.0, 1e3])).astype(np.float32)
+        ref = np.add.reduceat(v, np.array([0]))[0]
+        mine = np.float32(v[0] + O._np_pairwise_f32(v[1:])) if n > 1 else v[0]
+        assert ref.tobytes() == np.float32(mine).tobytes(), n
+
+
 def test_gcn_spmm_adjacencies_match_reference(golden):
     g = golden("gcn_spmm")
     for name in g["cases"]:
