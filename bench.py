@@ -388,8 +388,11 @@ def run_gat(args, dev):
     return res
 
 
-def run_sage(args, dev):
-    """cfg4: GraphSAGE 2-layer MEAN forward on a device-sampled [25, 10] batch of 8192 seeds."""
+def run_sage(args, dev, rank: int = 0, world: int = 1):
+    """cfg4: GraphSAGE 2-layer MEAN forward on a device-sampled [25, 10] batch of 8192 seeds.
+    With N ranks (replicated table, no collective on the forward path) the global
+    batch is 8192 x N seeds and rank r runs its shard (distributed.shard_seeds, its own
+    sampler stream): weak scaling, value = all ranks' sampled edges / the slowest rank."""
     from graphneuralnetwork_amd.graphsage import GraphSAGE
     from graphneuralnetwork_amd.ops import sage_gather_aggregate
     from graphneuralnetwork_amd.rmat import rmat_edges
@@ -406,16 +409,33 @@ def run_sage(args, dev):
     table = torch.randn(n, F, device=dev, generator=gen)
     deg = adj.rowptr[1:] - adj.rowptr[:-1]
     cand = torch.nonzero(deg > 0).view(-1)
-    seeds = cand[torch.randperm(cand.numel(), device=dev, generator=gen)[:8192]]
+    seeds = cand[torch.randperm(cand.numel(), device=dev, generator=gen)[:8192 * world]]
+    sample_seed = 0
+    if world > 1:
+        from graphneuralnetwork_amd.distributed import rank_sample_seed, shard_seeds
+        seeds = shard_seeds(seeds, rank, world)
+        sample_seed = rank_sample_seed(0, rank)
     tb = time.perf_counter()
-    batch = sample_batch(adj, seeds, (25, 10), seed=0)
+    batch = sample_batch(adj, seeds, (25, 10), seed=sample_seed)
     torch.cuda.synchronize(dev)
     t_sample = time.perf_counter() - tb
     net = GraphSAGE(2, F, H, False, agg_func="MEAN", Unsupervised=False, class_size=3).to(dev).eval()
     fargs = batch.forward_args(table)
     with torch.no_grad():
+        if world > 1:
+            dist.barrier()
         fwd_ms, wall = time_steps(lambda: net(*fargs, None, None, None, None, None), args.steps,
                                   args.warmup, dev)
+        edges_all = batch.sampled_edges
+        if world > 1:
+            dist.barrier()
+            rdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+            red = torch.tensor([wall, float(batch.sampled_edges)], dtype=torch.float64,
+                               device=rdev)
+            mx = red[:1].clone()
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(red[1:], op=dist.ReduceOp.SUM)
+            wall, edges_all = float(mx.item()), int(red[1].item())
         agg_ms, _ = time_steps(lambda: sage_gather_aggregate(table, batch.frontier_nbrs, "MEAN",
                                                              check=False),
                                args.steps, args.warmup, dev)
@@ -442,7 +462,8 @@ def run_sage(args, dev):
                                                           dev)[0]]
         except Exception as e:
             log(f"[bench] graph capture of the aggregation failed: {e!r}")
-        smp_ms, _ = time_steps(lambda: sample_batch(adj, seeds, (25, 10), seed=0), 3, 1, dev)
+        smp_ms, _ = time_steps(lambda: sample_batch(adj, seeds, (25, 10), seed=sample_seed), 3,
+                               1, dev)
         # the same forward replayed from a HIP graph (fixed-shape serving): GPU time without
         # the Python launch overhead of the eager call
         graph_ms = None
@@ -468,7 +489,8 @@ def run_sage(args, dev):
     achieved = bytes_l0 / (k_ms / 1e3) / 1e9
     traffic, tsrc = load_traffic(f"cfg4_F{F}")
     res = {"metric": "GraphSAGE sampled-neighbour aggregated edges/sec (2-layer forward)",
-           "value": edges * args.steps / wall, "unit": "edges/s", "n_gpus": 1, "steps": args.steps,
+           "value": edges_all * args.steps / wall, "unit": "edges/s", "n_gpus": world,
+           "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic R-MAT",
            "config": {"workload": wl["name"], "nodes": n, "adj_nnz": adj.nnz, "seeds": B,
@@ -489,7 +511,10 @@ def run_sage(args, dev):
                                      ", eager per-launch HIP events"),
                         "eager_launch_ms": statistics.mean(agg_ms),
                         "algorithmic_bytes_per_launch": bytes_l0, "avg_launch_ms": k_ms}}
-    if not args.no_cpu_baseline:
+    if world > 1:
+        res["config"]["global_seeds"] = 8192 * world
+        res["config"]["parallelism"] = f"seed-sharded{world} (replicated table, no collective)"
+    if not args.no_cpu_baseline and world == 1:
         from oracle import gnn_oracle as O
         tn = table.cpu().numpy()
         idx = batch.frontier_nbrs[:50000].cpu().numpy()
@@ -555,10 +580,13 @@ def main():
     from graphneuralnetwork_amd.ops import spmm_forward
     _lib.load()
     if args.workload in ("cfg3", "cfg4"):
-        if world != 1:
-            raise SystemExit(f"--workload {args.workload} is a single-GPU measurement")
-        res = run_gat(args, dev) if args.workload == "cfg3" else run_sage(args, dev)
-        print(json.dumps(res), flush=True)
+        if world != 1 and args.workload == "cfg3":
+            raise SystemExit("--workload cfg3 is a single-GPU measurement")
+        res = run_gat(args, dev) if args.workload == "cfg3" else run_sage(args, dev, rank, world)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
         return
 
     wl = WORKLOADS[args.workload]

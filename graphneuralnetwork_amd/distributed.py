@@ -30,6 +30,9 @@ remotely computed partial row sums (a greedy vertex cover of the block's
 bipartite edge set), which ships 2-3x fewer rows on an RMAT cut; the two kinds
 travel in two all-to-all-v's that pipeline with the partial-sum, interior and
 halo SpMMs.
+
+GraphSAGE (``sage_forward_sharded``) needs no exchange on its forward path: seed batches
+shard across ranks and the feature table is replicated (5.1 GB at 10M x 128 fits 288 GB).
 """
 from __future__ import annotations
 
@@ -631,3 +634,55 @@ class EdgeCutGat:
         er_ext = torch.cat([er, self.recv_buf[:, F:]], dim=0)
         return self._aggregate(self.ext, wh_ext, el, er_ext, self.heads, self.fh,
                                negative_slope, mode, activation)
+
+
+# ------------------------------------------------------------------------------ GraphSAGE
+def shard_seeds(seeds: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    """Rank ``rank``'s contiguous block of a seed batch (sizes differ by at most one, order
+    kept): GraphSAGE data parallelism -- each rank samples and runs its own
+    seeds against a replicated feature table, with no collective on the forward path."""
+    n = seeds.numel()
+    lo = (n * rank) // world
+    hi = (n * (rank + 1)) // world
+    return seeds[lo:hi]
+
+
+def rank_sample_seed(seed: int, rank: int) -> int:
+    """The sampler seed of one rank's shard: independent device RNG streams per rank (the
+    reference draws every batch from one sequential generator)."""
+    return (int(seed) * 0x9E3779B97F4A7C15 + int(rank) + 1) & 0xFFFFFFFFFFFFFFFF
+
+
+def all_gather_rows(local: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """Every rank's [n_r, ...] rows concatenated in rank order (an all-gather-v built from a
+    count all-gather and one all-to-all-v of the rows each rank sends to every peer)."""
+    dev = local.device
+    counts = _all_gather_floats([float(local.shape[0])], world, dev, group)[:, 0]
+    counts = [int(c) for c in counts.tolist()]
+    width = 1
+    for d in local.shape[1:]:
+        width *= int(d)
+    flat = local.reshape(local.shape[0], width).contiguous()
+    out = torch.empty((sum(counts), width), dtype=local.dtype, device=dev)
+    inp = flat.repeat(world, 1) if world > 1 else flat
+    _all_to_all_v(out.view(-1), inp.view(-1), [c * width for c in counts],
+                  [local.shape[0] * width] * world, group)
+    return out.view(sum(counts), *local.shape[1:])
+
+
+def sage_forward_sharded(net, adj, table: torch.Tensor, seeds: torch.Tensor, rank: int,
+                         world: int, fanouts=(25, 10), seed: int = 0, group=None,
+                         gather: bool = False):
+    """Data-parallel GraphSAGE inference over one seed batch: rank ``rank`` samples its
+    shard (``shard_seeds``; sampler stream ``rank_sample_seed(seed, rank)``) from the
+    replicated adjacency and runs ``net`` (the drop-in GraphSAGE.forward, supervised
+    branch) against the replicated table. Returns (embeddings, logits) of the shard, or of
+    the whole batch in seed order with ``gather=True`` (``all_gather_rows``)."""
+    from .sampler import sample_batch
+    mine = shard_seeds(seeds, rank, world)
+    batch = sample_batch(adj, mine, fanouts, seed=rank_sample_seed(seed, rank))
+    emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+    if gather:
+        emb = all_gather_rows(emb, world, group)
+        logits = all_gather_rows(logits, world, group) if logits is not None else None
+    return emb, logits

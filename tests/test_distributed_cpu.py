@@ -263,3 +263,48 @@ def test_gat_edge_cut_matches_single_device():
     ref = np.where(ref > 0, ref, np.expm1(np.minimum(ref, 0)))
     for rank, r0, r1, y in res:
         np.testing.assert_allclose(y, ref[r0:r1], rtol=1e-5, atol=1e-5)
+
+
+def _sage_shard_worker(rank, world, port, n_seeds, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GLOO_SOCKET_IFNAME="lo")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from graphneuralnetwork_amd.distributed import all_gather_rows, shard_seeds
+        seeds = torch.arange(1000, 1000 + n_seeds, dtype=torch.int64)
+        mine = shard_seeds(seeds, rank, world)
+        # a stand-in per-seed "embedding" [len, 3] and logits [len, 2] of the shard
+        emb = torch.stack([mine.float(), mine.float() * 2, torch.full_like(mine, rank).float()], 1)
+        got = all_gather_rows(emb, world)
+        got1 = all_gather_rows(mine[:, None] * 10, world)
+        q.put((rank, mine.numpy(), got.numpy(), got1.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_seeds", [(2, 7), (3, 8), (3, 2)])
+def test_sage_seed_shards_and_gather(world, n_seeds):
+    """GraphSAGE data parallelism: shard_seeds splits a batch into contiguous,
+    disjoint, order-preserving blocks (empty ones too), and all_gather_rows hands every rank
+    the rows of all shards in seed order (gloo, world 2-3)."""
+    from graphneuralnetwork_amd.distributed import rank_sample_seed
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sage_shard_worker, args=(r, world, port, n_seeds, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(_collect(procs, q, world, 300), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    seeds = np.arange(1000, 1000 + n_seeds)
+    np.testing.assert_array_equal(np.concatenate([r[1] for r in res]), seeds)
+    sizes = [r[1].size for r in res]
+    assert max(sizes) - min(sizes) <= 1
+    owner = np.concatenate([np.full(r[1].size, r[0]) for r in res])
+    for _, _, got, got1 in res:
+        np.testing.assert_array_equal(got[:, 0], seeds)
+        np.testing.assert_array_equal(got[:, 2], owner)
+        np.testing.assert_array_equal(got1[:, 0], seeds * 10)
+    assert len({rank_sample_seed(0, r) for r in range(8)}) == 8
