@@ -1,5 +1,4 @@
 mkdir -p gpurun_out
-export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT"
-timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_sq_gat -o run -- python bench.py --workload cfg3 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_sq_gat.log 2>&1 && \
-timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_sq_spmm -o run -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-layer > gpurun_out/pmc_sq_spmm.log 2>&1
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest tests/test_distributed_gpu.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -k sage > gpurun_out/t_sage_dist.log 2>&1 && \
+GNN_BENCH_DEVICE=0 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 2 --backend gloo --workload cfg4 --steps 5 --warmup 2 > gpurun_out/rehearse2_cfg4.log 2>&1
