@@ -680,8 +680,14 @@ def sage_forward_sharded(net, adj, table: torch.Tensor, seeds: torch.Tensor, ran
     the whole batch in seed order with ``gather=True`` (``all_gather_rows``)."""
     from .sampler import sample_batch
     mine = shard_seeds(seeds, rank, world)
-    batch = sample_batch(adj, mine, fanouts, seed=rank_sample_seed(seed, rank))
-    emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+    if mine.numel():
+        batch = sample_batch(adj, mine, fanouts, seed=rank_sample_seed(seed, rank))
+        emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+    else:  # fewer seeds than ranks: an empty shard still joins the gather
+        last = list(net.sage_blocks)[-1]
+        emb = torch.empty((0, last.output_size), dtype=torch.float32, device=table.device)
+        logits = (torch.empty((0, net.dense.out_features), dtype=torch.float32,
+                              device=table.device) if not net.Unsupervised else None)
     if gather:
         emb = all_gather_rows(emb, world, group)
         logits = all_gather_rows(logits, world, group) if logits is not None else None
