@@ -24,6 +24,10 @@ namespace gnn {
 
 constexpr int kProjWaves = 4;
 constexpr int kProjBlock = kProjWaves * kWave;
+#ifndef GNN_PROJ_G
+#define GNN_PROJ_G 1  // 16-row blocks per wave per iteration (independent MFMA chains x G)
+#endif
+constexpr int kProjG = GNN_PROJ_G;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 // w2[k][c] = W[k, head c] . a_src[head c] (c < heads), W[k, head c-heads] . a_dst[head
@@ -54,7 +58,8 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
   constexpr int S = K / 4;   // MFMA k-steps
   constexpr int FO = 16 * NT;
   constexpr int LDA = K + 4;  // padded LDS row (floats) against bank conflicts
-  __shared__ float atile[kProjWaves][16 * LDA];
+  constexpr int G = kProjG;
+  __shared__ float atile[kProjWaves][16 * G * LDA];
   const int lane = threadIdx.x & (kWave - 1);
   const int q = lane >> 4, r = lane & 15;
   const bool vec_logits = heads % 4 == 0 && lde % 4 == 0 &&
@@ -84,12 +89,12 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
   // A tiles are staged through LDS: a coalesced 16-B-per-lane copy of the wave's 16 rows,
   // then each lane reads its row's quarter (row l & 15, k in [q*S, q*S + S)) as float4s
   float* at = atile[threadIdx.x >> 6];
-  const int64_t n_groups = (n_rows + 16 * kProjWaves - 1) / (16 * kProjWaves);
-  constexpr int V4 = 16 * K / 4;                  // float4s in the wave's tile
+  const int64_t n_groups = (n_rows + 16 * G * kProjWaves - 1) / (16 * G * kProjWaves);
+  constexpr int V4 = 16 * G * K / 4;              // float4s in the wave's tile
   constexpr int NV = (V4 + kWave - 1) / kWave;    // per lane
   float4 pre[NV];                                  // the next tile, in flight during the MFMAs
   auto fetch = [&](int64_t g) {
-    const int64_t r0 = (g * kProjWaves + (threadIdx.x >> 6)) * 16;
+    const int64_t r0 = (g * kProjWaves + (threadIdx.x >> 6)) * 16 * G;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = v * kWave + lane;
@@ -101,7 +106,7 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
   };
   fetch(blockIdx.x);
   for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {  // uniform over the block
-    const int64_t row0 = (g * kProjWaves + (threadIdx.x >> 6)) * 16;
+    const int64_t row0 = (g * kProjWaves + (threadIdx.x >> 6)) * 16 * G;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = v * kWave + lane;
@@ -112,63 +117,81 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
     }
     __syncthreads();
     fetch(g + gridDim.x);
-    float a[S];
+    float a[G][S];
 #pragma unroll
-    for (int v = 0; v < S / 4; ++v) {
-      const float4 t4 = *reinterpret_cast<const float4*>(at + r * LDA + q * S + 4 * v);
-      a[4 * v] = t4.x;
-      a[4 * v + 1] = t4.y;
-      a[4 * v + 2] = t4.z;
-      a[4 * v + 3] = t4.w;
+    for (int j = 0; j < G; ++j)
+#pragma unroll
+      for (int v = 0; v < S / 4; ++v) {
+        const float4 t4 =
+            *reinterpret_cast<const float4*>(at + (j * 16 + r) * LDA + q * S + 4 * v);
+        a[j][4 * v] = t4.x;
+        a[j][4 * v + 1] = t4.y;
+        a[j][4 * v + 2] = t4.z;
+        a[j][4 * v + 3] = t4.w;
+      }
+    f32x4 acc[G][NT], acc2[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    f32x4 acc[NT], acc2 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #ifdef GNN_PROJ_NO_MFMA
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x4{a[t], a[t + 1], a[t + 2], a[t + 3]};
-    acc2 = f32x4{a[4], a[5], a[6], a[7]};
+    for (int j = 0; j < G; ++j) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[j][t] = f32x4{a[j][t], a[j][t + 1], a[j][t + 2], a[j][t + 3]};
+      acc2[j] = f32x4{a[j][4], a[j][5], a[j][6], a[j][7]};
+    }
 #else
 #pragma unroll
     for (int s = 0; s < S; ++s) {
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
 #ifdef GNN_PROJ_B_LDS
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ws[(q * S + s) * FO + 16 * t + r], a[s],
-                                                     acc[t], 0, 0, 0);
-      acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(w2s[(q * S + s) * 16 + r], a[s], acc2, 0, 0, 0);
+        for (int t = 0; t < NT; ++t)
+          acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ws[(q * S + s) * FO + 16 * t + r],
+                                                           a[j][s], acc[j][t], 0, 0, 0);
+        acc2[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2s[(q * S + s) * 16 + r], a[j][s],
+                                                       acc2[j], 0, 0, 0);
 #else
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[t][s], a[s], acc[t], 0, 0, 0);
-      acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(b2[s], a[s], acc2, 0, 0, 0);
+        for (int t = 0; t < NT; ++t)
+          acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[t][s], a[j][s], acc[j][t], 0, 0, 0);
+        acc2[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b2[s], a[j][s], acc2[j], 0, 0, 0);
 #endif
+      }
     }
 #endif
-    // Operands are swapped (D = W^T X^T), so acc[t][i] is Wh[row0 + r][16t + 4q + i]:
-    // one 16-B store per tile, 4 lanes = 64 contiguous bytes of a row; acc2[i] is column
-    // 4q + i of [el | er] for row r
-    const int64_t orow = row0 + r;
-    if (orow < n_rows) {
+    // Operands are swapped (D = W^T X^T), so acc[j][t][i] is Wh[row0 + 16j + r][16t + 4q + i]:
+    // one 16-B store per tile, 4 lanes = 64 contiguous bytes of a row; acc2[j][i] is column
+    // 4q + i of [el | er] for row 16j + r
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      const int64_t orow = row0 + 16 * j + r;
+      if (orow < n_rows) {
 #ifndef GNN_PROJ_NO_WH
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-        *reinterpret_cast<float4*>(wh + orow * ldwh + 16 * t + 4 * q) =
-            make_float4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+        for (int t = 0; t < NT; ++t)
+          *reinterpret_cast<float4*>(wh + orow * ldwh + 16 * t + 4 * q) =
+              make_float4(acc[j][t][0], acc[j][t][1], acc[j][t][2], acc[j][t][3]);
 #endif
-      if (vec_logits) {  // heads % 4 == 0: quarter q holds 4 whole logits of el or er
-        const int c = 4 * q;
-        if (c < 2 * heads)
-          *reinterpret_cast<float4*>(c < heads ? el + orow * lde + c : er + orow * lde + c - heads) =
-              make_float4(acc2[0], acc2[1], acc2[2], acc2[3]);
-      } else {
+        if (vec_logits) {  // heads % 4 == 0: quarter q holds 4 whole logits of el or er
+          const int c = 4 * q;
+          if (c < 2 * heads)
+            *reinterpret_cast<float4*>(c < heads ? el + orow * lde + c
+                                                 : er + orow * lde + c - heads) =
+                make_float4(acc2[j][0], acc2[j][1], acc2[j][2], acc2[j][3]);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int c = 4 * q + i;
-          if (c < heads)
-            el[orow * lde + c] = acc2[i];
-          else if (c < 2 * heads)
-            er[orow * lde + c - heads] = acc2[i];
+          for (int i = 0; i < 4; ++i) {
+            const int c = 4 * q + i;
+            if (c < heads)
+              el[orow * lde + c] = acc2[j][i];
+            else if (c < 2 * heads)
+              er[orow * lde + c - heads] = acc2[j][i];
+          }
         }
       }
     }
@@ -180,9 +203,12 @@ template <int K, int NT>
 static int launch_project(const float* x, int64_t ldx, int64_t n_rows, const float* w,
                           const float* w2, int heads, float* wh, int64_t ldwh, float* el,
                           float* er, int64_t lde, hipStream_t s) {
-  const int64_t groups = (n_rows + 16 * kProjWaves - 1) / (16 * kProjWaves);
+  const int64_t groups = (n_rows + 16 * kProjG * kProjWaves - 1) / (16 * kProjG * kProjWaves);
 #ifndef GNN_PROJ_GRID
-#define GNN_PROJ_GRID 1024  // A/B at cfg3: 1024 < 512 < 256 < 2048 < 4096 (ms)
+// 512 = the resident workgroups at 2 waves/SIMD (144 VGPRs): A/B at cfg3 with isolated
+// variant libraries (tools/project_ab.py, profiles/r02zl_project_ab.log) 0.135 ms vs 0.139-0.147
+// at 1024; G = 2 row blocks per wave (10 MFMA chains) 0.152-0.157, W from LDS 0.153-0.156
+#define GNN_PROJ_GRID 512
 #endif
   const int64_t grid = groups < GNN_PROJ_GRID ? groups : GNN_PROJ_GRID;  // W resident across groups
   hipLaunchKernelGGL((gat_project_kernel<K, NT>), dim3(static_cast<unsigned>(grid)),
