@@ -47,6 +47,12 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* 
   static_assert(V4 % kTfBlock == 0, "tile must split evenly over the workgroup");
   static_assert(S % XC == 0 && XC % 4 == 0, "X chunks of whole float4s");
   __shared__ float xt[kTfRows * LDA];
+#ifdef GNN_TF_STAGE_OUT
+  // the tile's Y rows staged in LDS, then stored as whole contiguous rows (each wave
+  // instruction writes 1 KiB of consecutive bytes instead of 16 rows x 64 B)
+  constexpr int LDO = FO + 4;
+  __shared__ float ot[kTfRows * LDO];
+#endif
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = threadIdx.x >> 6;
   const int q = lane >> 4, r = lane & 15;
@@ -127,7 +133,11 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* 
       for (int j = 0; j < RB; ++j) {
         // acc[j][cb][i] = Y[row0 + 16 (rb0 + j) + r][(wv*CB + cb)*16 + 4q + i]
         const int64_t orow = row0 + (rb0 + j) * 16 + r;
+#ifndef GNN_TF_STAGE_OUT
         if (orow < n_rows) {
+#else
+        (void)orow;
+#endif
 #pragma unroll
           for (int cb = 0; cb < CB; ++cb) {
             float4 o = make_float4(acc[j][cb][0], acc[j][cb][1], acc[j][cb][2], acc[j][cb][3]);
@@ -137,12 +147,30 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* 
               o.z = fmaxf(o.z, 0.f);
               o.w = fmaxf(o.w, 0.f);
             }
+#ifdef GNN_TF_STAGE_OUT
+            *reinterpret_cast<float4*>(ot + ((rb0 + j) * 16 + r) * LDO + (wv * CB + cb) * 16 +
+                                       4 * q) = o;
+#else
             *reinterpret_cast<float4*>(y + orow * ldy + (wv * CB + cb) * 16 + 4 * q) = o;
+#endif
           }
+#ifndef GNN_TF_STAGE_OUT
         }
+#endif
       }
     }
-    __syncthreads();  // the next tile overwrites xt
+#ifdef GNN_TF_STAGE_OUT
+    __syncthreads();  // the whole Y tile is in LDS
+    constexpr int O4 = kTfRows * FO / 4;
+#pragma unroll
+    for (int e = static_cast<int>(threadIdx.x); e < O4; e += kTfBlock) {
+      const int rr = e / (FO / 4), c4 = e - rr * (FO / 4);
+      if (row0 + rr < n_rows)
+        *reinterpret_cast<float4*>(y + (row0 + rr) * ldy + 4 * c4) =
+            *reinterpret_cast<const float4*>(ot + rr * LDO + 4 * c4);
+    }
+#endif
+    __syncthreads();  // the next tile overwrites xt (and ot)
   }
   (void)FO;
 }

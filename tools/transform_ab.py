@@ -43,6 +43,10 @@ def main():
                 finally:
                     _lib.use_variant(None)
             fns[v] = fv
+            if ref is not None:  # every variant must compute the same product
+                yv = fv()
+                errv = float((yv - ref).abs().max() / ref.abs().max())
+                assert errv < 1e-5, (v, errv)
         t = {k_: [] for k_ in fns}
         for _ in range(5):
             for name, f in fns.items():
