@@ -609,6 +609,7 @@ class EdgeCutGat:
         self.heads, self.fh = heads, fh
         self.group = group
         self.device = torch.device(device)
+        hip_aggregate = aggregate is None
         if logits is None or aggregate is None or gather is None:
             from .ops import gat_aggregate, gat_logits, gather_rows
             logits = logits or gat_logits
@@ -620,6 +621,16 @@ class EdgeCutGat:
                                     device=self.device)
         self.recv_buf = torch.empty((part.n_halo, w), dtype=torch.float32, device=self.device)
         self.ext = extended_graph(part)
+        # the HIP path reads the received [Wh | er] rows in place: the extended graph with
+        # halo slot s as column -1-s of the staged tables (gat_aggregate_staged)
+        self._staged = None
+        if hip_aggregate and self.device.type == "cuda" and part.n_halo and \
+                not self.ext.has_empty_rows():
+            from .graph import CsrGraph
+            col = self.ext.col.to(torch.int64)
+            col = torch.where(col < part.n_own, col, part.n_own - 1 - col).to(torch.int32)
+            self._staged = CsrGraph(self.ext.rowptr, col.contiguous(), self.ext.val,
+                                    part.n_own, part.n_own)
 
     def __call__(self, wh_own: torch.Tensor, a_src: torch.Tensor, a_dst: torch.Tensor,
                  negative_slope: float, mode: int, activation: str | None = None):
@@ -630,6 +641,11 @@ class EdgeCutGat:
             self._gather(wh_own, p.send_idx, self.send_buf[:, :F])
             self._gather(er.contiguous(), p.send_idx, self.send_buf[:, F:])
         _all_to_all_v(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts, self.group)
+        if self._staged is not None and wh_own.stride(1) == 1:
+            from .ops import gat_aggregate_staged
+            return gat_aggregate_staged(self._staged, wh_own, el, er, self.recv_buf[:, :F],
+                                        self.recv_buf[:, F:], self.heads, self.fh,
+                                        negative_slope, mode, activation)
         wh_ext = torch.cat([wh_own, self.recv_buf[:, :F]], dim=0)
         er_ext = torch.cat([er, self.recv_buf[:, F:]], dim=0)
         return self._aggregate(self.ext, wh_ext, el, er_ext, self.heads, self.fh,

@@ -180,20 +180,28 @@ class XcdHubPlan:
         gather resolves negative ids through the staged buffer."""
         cache = self.__dict__.setdefault("_rest_plans", {})
         if seg_len not in cache:
-            p = self.rest.plan(seg_len)
-            rp = self.rest.rowptr
-            if p.n_small:
-                r = p.small_row.to(torch.int64)
-                staged = (p.small_col < 0) & ((rp[r + 1] - rp[r]) == 1)
-                if bool(staged.any()):
-                    keep = ~staged
-                    p = RowSplitPlan(p.seg_len, p.seg_row, p.seg_begin, p.long_row,
-                                     p.long_seg_ptr, p.small_row[keep].contiguous(),
-                                     p.small_col[keep].contiguous(),
-                                     p.small_val[keep].contiguous(),
-                                     torch.cat([p.mid_row, p.small_row[staged]]).contiguous())
-            cache[seg_len] = p
+            cache[seg_len] = staged_plan(self.rest, seg_len)
         return cache[seg_len]
+
+
+def staged_plan(g: "CsrGraph", seg_len: int) -> RowSplitPlan:
+    """The row-class plan of a graph whose negative column ids name rows of a staged table
+    (the hub kernels' convention): one-edge rows whose edge is staged leave the packed
+    small-row class (it reads its pre-resolved column from X and a negative id as "no
+    edge") for the mid-row class, whose gather resolves negative ids."""
+    p = g.plan(seg_len)
+    rp = g.rowptr
+    if p.n_small:
+        r = p.small_row.to(torch.int64)
+        staged = (p.small_col < 0) & ((rp[r + 1] - rp[r]) == 1)
+        if bool(staged.any()):
+            keep = ~staged
+            p = RowSplitPlan(p.seg_len, p.seg_row, p.seg_begin, p.long_row,
+                             p.long_seg_ptr, p.small_row[keep].contiguous(),
+                             p.small_col[keep].contiguous(),
+                             p.small_val[keep].contiguous(),
+                             torch.cat([p.mid_row, p.small_row[staged]]).contiguous())
+    return p
 
 
 def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, k: int,

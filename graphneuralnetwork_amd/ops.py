@@ -379,6 +379,50 @@ def _gat_xcd(lib, g: CsrGraph, xp, wh, el, er, heads, fh, slope, mode, fill, out
               stream, whb, erb, "gnn_gat_csr_hub_f32 (xcd rest)")
 
 
+def gat_aggregate_staged(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tensor,
+                         whh: torch.Tensor, erh: torch.Tensor, heads: int, fh: int,
+                         negative_slope: float, mode: int, activation: str | None = None,
+                         out: torch.Tensor | None = None) -> torch.Tensor:
+    """``gat_aggregate`` (inference: no dropout, no stats) over a graph whose column c >= 0
+    reads Wh / er row c and c < 0 reads row -1-c of the staged tables ``whh`` / ``erh``
+    (strided views allowed: e.g. the [Wh | er] rows an edge-cut rank received, used in
+    place instead of concatenated). gnn_gat_csr_hub_f32; rows without edges are rejected
+    (their dense-mode fill is a mean over every column, own and staged)."""
+    _require_device(g.rowptr, wh, el, er, whh, erh, out)
+    feat = heads * fh
+    if wh.shape != (g.n_cols, feat) or wh.stride(1) != 1:
+        raise ValueError("Wh must be [n_cols, heads * fh] with unit column stride")
+    if whh.shape[1] != feat or erh.shape != (whh.shape[0], heads) or whh.stride(1) != 1 \
+            or erh.stride(1) != 1:
+        raise ValueError("whh [K, heads * fh] and erh [K, heads] with unit column stride")
+    if el.shape != (g.n_rows, heads) or er.shape != (g.n_cols, heads):
+        raise ValueError("el must be [n_rows, heads] and er [n_cols, heads]")
+    el, er = el.contiguous(), er.contiguous()
+    if el.stride(0) != er.stride(0):
+        raise ValueError("el / er must share a row stride")
+    if g.has_empty_rows():
+        raise ValueError("gat_aggregate_staged: the graph has rows without edges")
+    if out is None:
+        out = torch.empty((g.n_rows, feat), dtype=torch.float32, device=wh.device)
+    if g.n_rows == 0:
+        return out
+    from .graph import staged_plan
+    seg = seg_len_for(feat, GAT_SEG_BYTES)
+    plan = g.__dict__.setdefault("_staged_plans", {}).get(seg)
+    if plan is None:
+        plan = g.__dict__["_staged_plans"][seg] = staged_plan(g, seg)
+    mid, short = plan.gat_split(g.rowptr, GAT_SHORT_MAX_DEG)
+    partial = None
+    if plan.n_seg:
+        partial = torch.empty((plan.n_seg, feat + 2 * heads), dtype=torch.float32,
+                              device=wh.device)
+    _gat_call(_lib.load(), g.rowptr, g.col, g.n_rows, wh, el, er, el.stride(0), heads, fh,
+              negative_slope, mode, None, out, out.stride(0), seg, plan, mid, short, partial,
+              None, _ACT_FLAGS[activation], _lib.stream_handle(wh.device), whh, erh,
+              "gnn_gat_csr_hub_f32 (staged)")
+    return out
+
+
 def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tensor, heads: int,
                   fh: int, negative_slope: float, mode: int, activation: str | None = None,
                   dropout_p: float = 0.0, seed: int = 0, seg_len: int | None = None,

@@ -116,6 +116,7 @@ def _gat_worker(rank, world, port, n, q):
         a_d = (torch.randn(64, generator=gen) * 0.3).to(dev)
         r0, r1 = part.bounds[rank], part.bounds[rank + 1]
         layer = EdgeCutGat(part, 8, 8, dev)
+        assert layer._staged is not None  # received rows read in place (gat_aggregate_staged)
         y = layer(Wh[r0:r1].contiguous(), a_s, a_d, 0.2, 0, "elu")
         torch.cuda.synchronize()
         q.put((rank, r0, r1, y.cpu().numpy()))
