@@ -5,6 +5,9 @@
 //     MEAN -> torch.mean(neigh_feat, dim=1)         (fp32 [M, F])
 //     MAX  -> torch.argmax(neigh_feat, dim=1)       (int64 [M, F]: FIRST maximal position,
 //                                                    a NaN counts as the maximum)
+//   value max-pool (north_star "mean/max-pool")     torch.max(neigh, dim=1).values, the
+//     value NeighborAggregator 'max' reaches for      (GraphSAGE_Pytorch/models/Aggregator.py:23-24):
+//                                                    fp32 [M, F], a NaN in the slice propagates
 //   torch.embedding(feats_data, index_map)          GraphSAGE/GraphSAGE.py:47-49,
 //                                                    GraphSAGE/data_utils.py:161-162
 // Two input forms:
@@ -33,7 +36,17 @@ constexpr int kSageBlock = 256;
 #endif
 constexpr int kSageWaves = kSageBlock / kWave;
 
-enum SageMode : int32_t { kMean = 0, kArgmax = 1, kSum = 2 };
+enum SageMode : int32_t { kMean = 0, kArgmax = 1, kSum = 2, kMaxPool = 3 };
+
+// torch.max's value rule: a NaN on either side wins, else the larger value
+__device__ __forceinline__ float nanmax(float a, float b) { return (a > b || a != a) ? a : b; }
+
+template <int VW>
+__device__ __forceinline__ typename Vec<VW>::T vnanmax(typename Vec<VW>::T a, typename Vec<VW>::T b) {
+#pragma unroll
+  for (int i = 0; i < VW; ++i) vset(a, i, nanmax(vget(a, i), vget(b, i)));
+  return a;
+}
 
 // (val, idx) "a beats b" under torch.argmax's rule.
 __device__ __forceinline__ bool beats(float va, int32_t ia, float vb, int32_t ib) {
@@ -58,7 +71,7 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
   int32_t arg[NCH][VW];
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
-    acc[ch] = MODE != kArgmax ? vzero<VW>() : typename Vec<VW>::T(-INFINITY);
+    acc[ch] = (MODE == kMean || MODE == kSum) ? vzero<VW>() : typename Vec<VW>::T(-INFINITY);
 #pragma unroll
     for (int i = 0; i < VW; ++i) arg[ch][i] = 0x7fffffff;
   }
@@ -90,15 +103,18 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
       for (int ch = 0; ch < NCH; ++ch) {
         const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
         xv[u][ch] = (ok && f < feat) ? vload<VW>(row + f)
-                                     : (MODE != kArgmax ? vzero<VW>() : typename Vec<VW>::T(-INFINITY));
+                                     : ((MODE == kMean || MODE == kSum) ? vzero<VW>()
+                                                                        : typename Vec<VW>::T(-INFINITY));
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
-        if (MODE != kArgmax) {
+        if (MODE == kMean || MODE == kSum) {
           acc[ch] += xv[u][ch];
+        } else if (MODE == kMaxPool) {
+          acc[ch] = vnanmax<VW>(acc[ch], xv[u][ch]);
         } else if (kk[u] != 0x7fffffff) {
 #pragma unroll
           for (int i = 0; i < VW; ++i) {
@@ -117,8 +133,10 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
   for (int mm = LPR; mm < kWave; mm <<= 1) {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
-      if (MODE != kArgmax) {
+      if (MODE == kMean || MODE == kSum) {
         acc[ch] += shfl_xor_f(acc[ch], mm);
+      } else if (MODE == kMaxPool) {
+        acc[ch] = vnanmax<VW>(acc[ch], shfl_xor_f(acc[ch], mm));
       } else {
 #pragma unroll
         for (int i = 0; i < VW; ++i) {
@@ -138,7 +156,7 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
     const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
     if (f >= feat) continue;
     if (MODE != kArgmax) {
-      // torch.mean: sum / k;  torch.sum: the sum
+      // torch.mean: sum / k;  torch.sum: the sum;  torch.max(...).values: the max
       typename Vec<VW>::T r = MODE == kMean ? acc[ch] / static_cast<float>(k) : acc[ch];
       vstore<VW>(static_cast<float*>(out) + m * ldo + f, r);
     } else {
@@ -229,6 +247,8 @@ static int run_sage(SageArgs a, int32_t mode, bool vec4) {
       rc = vec4 ? dispatch_sage<4, kMean, GATHER>(a) : dispatch_sage<1, kMean, GATHER>(a);
     else if (mode == kSum)
       rc = vec4 ? dispatch_sage<4, kSum, GATHER>(a) : dispatch_sage<1, kSum, GATHER>(a);
+    else if (mode == kMaxPool)
+      rc = vec4 ? dispatch_sage<4, kMaxPool, GATHER>(a) : dispatch_sage<1, kMaxPool, GATHER>(a);
     else
       rc = vec4 ? dispatch_sage<4, kArgmax, GATHER>(a) : dispatch_sage<1, kArgmax, GATHER>(a);
     if (rc != GNN_OK) return rc;
@@ -243,7 +263,7 @@ using namespace gnn;
 extern "C" int gnn_sage_aggregate_f32(const float* neigh, int64_t ld_k, int64_t ld_m, int64_t M,
                                       int64_t k, int64_t feat, int32_t mode, void* out,
                                       int64_t ldo, void* stream) {
-  if (M < 0 || k < 0 || feat < 0 || (mode != kMean && mode != kArgmax && mode != kSum)) return GNN_E_ARG;
+  if (M < 0 || k < 0 || feat < 0 || (mode < kMean || mode > kMaxPool)) return GNN_E_ARG;
   if (M == 0 || feat == 0) return GNN_OK;
   if (!neigh || !out || ld_k < feat || ldo < feat) return GNN_E_ARG;
   if (k == 0) return GNN_E_UNSUPPORTED;  // torch: mean of nothing is NaN, argmax raises
@@ -258,7 +278,7 @@ extern "C" int gnn_sage_gather_aggregate_f32(const float* table, int64_t ldt, in
                                              const int64_t* idx, int64_t ldi, int64_t M, int64_t k,
                                              int64_t feat, int32_t mode, void* out, int64_t ldo,
                                              int32_t* err_flag, void* stream) {
-  if (M < 0 || k < 0 || feat < 0 || n_table < 0 || (mode != kMean && mode != kArgmax && mode != kSum))
+  if (M < 0 || k < 0 || feat < 0 || n_table < 0 || (mode < kMean || mode > kMaxPool))
     return GNN_E_ARG;
   if (M == 0 || feat == 0) return GNN_OK;
   if (!table || !idx || !out || !err_flag || ldt < feat || ldo < feat || ldi < k) return GNN_E_ARG;

@@ -7,7 +7,7 @@ Same names, constructor arguments, 9-argument ``forward`` and state_dict keys
 Hot path on gfx950:
 
 * ``Aggregator`` (graph_utils.py:4-11) -> one HIP launch (mean, or torch.argmax's
-  int64 first-max indices, bit-exact);
+  int64 first-max indices, bit-exact; plus 'MAXPOOL', the value max-pool of the north star);
 * the re-gathers of GraphSAGE.py:47-49 (``torch.embedding(feats, map)`` followed
   by the next layer's ``Aggregator``) -> ONE fused gather-aggregate launch that
   never materialises the [M, k, H] neighbour tensor, plus one row-gather
@@ -114,6 +114,45 @@ class _GatherMeanAgg(torch.autograd.Function):
         return _scatter_rows(g, idx, ctx.n, scale), None, None, None
 
 
+class _MaxPoolAgg(torch.autograd.Function):
+    """Value max-pool over a pre-gathered [M, k, F] tensor with autograd: the gradient goes
+    to the first maximal neighbour of every (row, feature) -- the argmax kernel's index."""
+
+    @staticmethod
+    def forward(ctx, neigh):
+        arg = sage_aggregate(neigh, "MAX")
+        ctx.save_for_backward(arg)
+        ctx.k = neigh.shape[1]
+        return sage_aggregate(neigh, "MAXPOOL")
+
+    @staticmethod
+    def backward(ctx, g):
+        (arg,) = ctx.saved_tensors
+        M, F = g.shape
+        out = torch.zeros((M, ctx.k, F), dtype=g.dtype, device=g.device)
+        return out.scatter_(1, arg.unsqueeze(1), g.unsqueeze(1))
+
+
+class _GatherMaxPoolAgg(torch.autograd.Function):
+    """Fused gather + value max-pool with autograd w.r.t. the table (the gradient of each
+    (row, feature) lands on the table row of its first maximal neighbour)."""
+
+    @staticmethod
+    def forward(ctx, table, idx, check=True):
+        arg = sage_gather_aggregate(table, idx, "MAX", check=check)
+        ctx.save_for_backward(idx, arg)
+        ctx.n = table.shape[0]
+        return sage_gather_aggregate(table, idx, "MAXPOOL", check=False)
+
+    @staticmethod
+    def backward(ctx, g):
+        idx, arg = ctx.saved_tensors
+        rows = idx.to(torch.int64).gather(1, arg)                     # [M, F] table rows
+        cols = torch.arange(g.shape[1], device=g.device).expand_as(rows)
+        out = torch.zeros((ctx.n, g.shape[1]), dtype=g.dtype, device=g.device)
+        return out.index_put_((rows, cols), g, accumulate=True), None, None
+
+
 class _GatherRows(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, idx, check=True):
@@ -128,8 +167,12 @@ class _GatherRows(torch.autograd.Function):
 
 
 def Aggregator(neigh_feat, agg_func='MEAN'):
-    """GraphSAGE/graph_utils.py:4-11 on the device ('MEAN' -> fp32, 'MAX' -> int64 argmax)."""
-    if agg_func not in ('MEAN', 'MAX'):
+    """GraphSAGE/graph_utils.py:4-11 on the device ('MEAN' -> fp32, 'MAX' -> int64 argmax).
+
+    Extension beyond the reference: 'MAXPOOL' -> the fp32 value max-pool the north star
+    names (torch.max(neigh_feat, dim=1).values); the reference's own names keep their
+    meaning, and any other name prints and raises as the reference does."""
+    if agg_func not in ('MEAN', 'MAX', 'MAXPOOL'):
         print('请选择合适的聚合函数')  # the reference prints this, then a bare raise
         raise RuntimeError("No active exception to reraise")
     return reduce_neighbors(neigh_feat, agg_func)
@@ -138,16 +181,20 @@ def Aggregator(neigh_feat, agg_func='MEAN'):
 def _gather_aggregate(table, idx, agg_func, trusted=False):
     if agg_func in ('MEAN', 'SUM') and torch.is_grad_enabled() and table.requires_grad:
         return _GatherMeanAgg.apply(table, idx, agg_func, not trusted)
+    if agg_func == 'MAXPOOL' and torch.is_grad_enabled() and table.requires_grad:
+        return _GatherMaxPoolAgg.apply(table, idx, not trusted)
     return sage_gather_aggregate(table, idx, agg_func, check=not trusted)
 
 
 def reduce_neighbors(neigh_feat, kind='MEAN'):
-    """MEAN / SUM / MAX(argmax) over dim 1 of a pre-gathered [M, k, F] tensor or a
-    ``Gathered`` (table, [M, k] index), with autograd for MEAN / SUM."""
+    """MEAN / SUM / MAX(argmax) / MAXPOOL over dim 1 of a pre-gathered [M, k, F] tensor or a
+    ``Gathered`` (table, [M, k] index), with autograd for MEAN / SUM / MAXPOOL."""
     if isinstance(neigh_feat, Gathered):
         return _gather_aggregate(neigh_feat.table, neigh_feat.index, kind, neigh_feat.trusted)
     if kind in ('MEAN', 'SUM') and torch.is_grad_enabled() and neigh_feat.requires_grad:
         return _MeanAgg.apply(neigh_feat, kind)
+    if kind == 'MAXPOOL' and torch.is_grad_enabled() and neigh_feat.requires_grad:
+        return _MaxPoolAgg.apply(neigh_feat)
     return sage_aggregate(neigh_feat, kind)
 
 

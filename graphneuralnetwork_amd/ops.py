@@ -509,7 +509,9 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
 
 # ---------------------------------------------------------------- GraphSAGE
 SAGE_MODES = {"MEAN": 0, "MAX": 1}   # GraphSAGE/graph_utils.py Aggregator
-SAGE_KINDS = {"MEAN": 0, "MAX": 1, "SUM": 2}   # + NeighborAggregator 'sum' (GraphSAGE_Pytorch)
+# + NeighborAggregator 'sum' (GraphSAGE_Pytorch) and the value max-pool the north star names
+# ("mean/max-pool"; torch.max(dim=1).values, GraphSAGE_Pytorch/models/Aggregator.py:23-24)
+SAGE_KINDS = {"MEAN": 0, "MAX": 1, "SUM": 2, "MAXPOOL": 3}
 
 
 _EMPTY_FILL = {0: float("nan"), 2: 0.0}  # k == 0: torch.mean -> NaN, torch.sum -> 0
@@ -518,6 +520,8 @@ _EMPTY_FILL = {0: float("nan"), 2: 0.0}  # k == 0: torch.mean -> NaN, torch.sum 
 def _empty_reduction(mode: int) -> None:
     if mode == 1:  # torch.argmax over an empty dim raises
         raise IndexError("argmax(): Expected reduction dim 1 to have non-zero size.")
+    if mode == 3:  # so does torch.max(dim=1)
+        raise IndexError("max(): Expected reduction dim 1 to have non-zero size.")
 
 
 def _sage_out(M, F, mode, dev):

@@ -5,15 +5,14 @@ The reference's ``collate_fn`` samples on the host with Python sets and
 ``torch.tensor``) and materialises every neighbour feature row with
 ``torch.embedding``.  Here the frontier of a batch is built on the device:
 
-    nb0  = sample(adj, seeds, fanouts[0])             # [B, k0]   (gnn_sample_neighbors)
-    S1   = unique(seeds ++ nb0)                        # layer-0 centre nodes (sorted ids)
-    nb1  = sample(adj, S1, fanouts[1])                 # [|S1|, k1] global ids
-    maps = positions of seeds / nb0 inside S1          # the reference's -1-free index maps
+    nb_i    = sample(adj, S_i, fanouts[i])         # [|S_i|, k_i]  (gnn_sample_neighbors)
+    S_{i+1} = unique(S_i ++ nb_i)                   # sorted ids, S_0 = the seeds
+    maps_i  = positions of S_i / nb_i inside S_{i+1}  # the reference's -1-free index maps
 
 and the batch is handed to ``GraphSAGE.forward`` as ``Gathered`` (table, index)
 pairs, so no [M, k, F] neighbour tensor is ever written: the layer-0
 aggregation gathers straight from the feature table (gnn_sage_gather_aggregate_f32).
-Per-hop fanouts ([25, 10]) are supported.  The reference's set iteration order
+Per-hop fanouts ([25, 10], or any number of layers) are supported.  The reference's set iteration order
 and Mersenne-Twister draws are not reproduced (it is unseeded); the sampled
 distribution is (tests/test_sampler_gpu.py).
 """
@@ -82,6 +81,7 @@ def sample_neighbors(adj: CsrGraph, nodes: torch.Tensor, k: int, seed: int = 0,
 
 
 _FRONTIER_WS: dict = {}
+_FRONTIER_GEN = [0]  # bumped by every build_frontier: a rank() of an older build refuses to run
 
 
 def _frontier_ws(n_nodes: int, dev) -> torch.Tensor:
@@ -100,11 +100,17 @@ def build_frontier(ids_a: torch.Tensor, ids_b: torch.Tensor, n_nodes: int, err: 
     reference's set union + index remap (GraphSAGE/data_utils.py:100-116), as
     torch.unique(cat[a, b]) + torch.searchsorted would give, with a node bitmap instead of
     a sort (gnn_frontier_*). One host synchronisation: the frontier size, read together
-    with the pending sampler error bits ``err`` (raised first) and the marks' own."""
+    with the pending sampler error bits ``err`` (raised first) and the marks' own.
+
+    The bitmap and prefix workspace is shared per (device, n_nodes): ``rank`` must run on
+    the current stream before the next ``build_frontier`` (it raises once the workspace has
+    been rebuilt)."""
     dev = ids_a.device
     lib = _lib.load()
     stream = _lib.stream_handle(dev)
     ws = _frontier_ws(n_nodes, dev)
+    _FRONTIER_GEN[0] += 1
+    gen = _FRONTIER_GEN[0]
     a = ids_a.to(torch.int64).contiguous().view(-1)
     b = ids_b.to(torch.int64).contiguous().view(-1)
     stat = torch.zeros(3, dtype=torch.int64, device=dev)
@@ -122,6 +128,9 @@ def build_frontier(ids_a: torch.Tensor, ids_b: torch.Tensor, n_nodes: int, err: 
                "gnn_frontier_emit")
 
     def rank(ids: torch.Tensor) -> torch.Tensor:
+        if _FRONTIER_GEN[0] != gen or _FRONTIER_WS.get((dev, n_nodes)) is not ws:
+            raise RuntimeError("build_frontier: rank() called after the frontier workspace was "
+                               "rebuilt by a later build_frontier / sample_batch")
         ids = ids.to(torch.int64).contiguous()
         pos = torch.empty_like(ids)
         _lib.check(lib.gnn_frontier_rank(ids.data_ptr(), ids.numel(), n_nodes, ws.data_ptr(),
@@ -133,39 +142,71 @@ def build_frontier(ids_a: torch.Tensor, ids_b: torch.Tensor, n_nodes: int, err: 
 
 @dataclass
 class SampledBatch:
-    seeds: torch.Tensor        # [B] global ids
-    frontier: torch.Tensor     # S1 [M] global ids (sorted), layer-0 centres
-    frontier_nbrs: torch.Tensor  # [M, k1] global ids (index the feature table)
-    center_map: torch.Tensor   # [B] positions of the seeds in S1
-    neigh_map: torch.Tensor    # [B, k0] positions of the seeds' neighbours in S1
+    """The device form of collate_fn's output (GraphSAGE/data_utils.py:104-162) for L layers.
+
+    Sampling layer i draws ``fanouts[i]`` neighbours for S_i (S_0 = the seeds) and
+    S_{i+1} = sorted unique(S_i ++ those neighbours). The forward runs the other way round:
+    its layer 0 aggregates S_{L-1}'s neighbours, so the maps are kept in forward order --
+    ``center_maps[i]`` = positions of S_{L-2-i} in S_{L-1-i}, ``neigh_maps[i]`` = positions
+    of S_{L-2-i}'s sampled neighbours in S_{L-1-i}, exactly the reference's
+    nodes_map[1:] / neigh_nodes_map[1:] (without its -1 padding)."""
+    seeds: torch.Tensor        # [B] global ids (S_0)
+    frontier: torch.Tensor     # S_{L-1} global ids (sorted; the seeds when L = 1), layer-0 centres
+    frontier_nbrs: torch.Tensor  # [|S_{L-1}|, k_{L-1}] global ids (index the feature table)
+    center_maps: list          # L-1 tensors, forward order (see above)
+    neigh_maps: list           # L-1 tensors [|S_{L-2-i}|, k_{L-2-i}], forward order
+    layers: tuple = ()         # S_0 (the seeds), ..., S_{L-1} (= frontier)
+
+    @property
+    def layer_sizes(self) -> tuple:
+        return tuple(int(t.numel()) for t in self.layers)
+
+    @property
+    def center_map(self) -> torch.Tensor:
+        """Positions of the seeds in S_1 (the last forward layer's centre map)."""
+        return self.center_maps[-1]
+
+    @property
+    def neigh_map(self) -> torch.Tensor:
+        """Positions of the seeds' sampled neighbours in S_1 ([B, k_0])."""
+        return self.neigh_maps[-1]
 
     @property
     def sampled_edges(self) -> int:
-        return int(self.frontier_nbrs.numel() + self.neigh_map.numel())
+        return int(self.frontier_nbrs.numel() + sum(m.numel() for m in self.neigh_maps))
 
     def forward_args(self, table: torch.Tensor):
         """The 4 leading arguments of GraphSAGE.forward (supervised branch)."""
-        return (Gathered(table, self.frontier, True), [trust_map(self.center_map)],
-                Gathered(table, self.frontier_nbrs, True), [trust_map(self.neigh_map)])
+        return (Gathered(table, self.frontier, True), [trust_map(m) for m in self.center_maps],
+                Gathered(table, self.frontier_nbrs, True), [trust_map(m) for m in self.neigh_maps])
 
 
 def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int = 0,
                  gcn: bool = False) -> SampledBatch:
-    """Two-layer frontier for ``seeds`` (fanouts[0] for the seeds, fanouts[1] for S1)."""
-    if len(fanouts) != 2:
-        raise NotImplementedError("two-layer sampling (the reference's num_layers=2 runs)")
+    """L = len(fanouts) layer frontier for ``seeds`` (get_layer_adj_nodes,
+    GraphSAGE/data_utils.py:82-103, with a fanout per layer like GraphSAGE_Pytorch's
+    multihop_sampling): fanouts[i] neighbours for every node of S_i, chained per hop."""
+    fanouts = tuple(int(k) for k in fanouts)
+    if not fanouts or min(fanouts) < 1:
+        raise ValueError("fanouts must hold at least one positive neighbour count")
     seeds = seeds.to(device=adj.device, dtype=torch.int64).contiguous()
     err = torch.zeros(1, dtype=torch.int32, device=adj.device)
-    nb0 = _sample_into(adj, seeds, fanouts[0], seed, 0, err)
-    if gcn:  # the reference appends the node itself (data_utils.py:95-96)
-        nb0 = torch.cat([nb0, seeds[:, None]], dim=1)
-    # S1 = sorted unique(seeds ++ nb0) and the maps into it (bitmap frontier, no sort); the
-    # sampler's error bits are read with the frontier size (one host synchronisation)
-    s1, rank = build_frontier(seeds, nb0, adj.n_rows, err)
-    nb1 = _sample_into(adj, s1, fanouts[1], seed, 1, err)
-    if gcn:
-        nb1 = torch.cat([nb1, s1[:, None]], dim=1)
-    batch = SampledBatch(seeds, s1, nb1, rank(seeds), rank(nb0))
+    layers = [seeds]
+    cmaps, nmaps = [], []
+    nb = None
+    for i, k in enumerate(fanouts):
+        nb = _sample_into(adj, layers[i], k, seed, i, err)
+        if gcn:  # the reference appends the node itself (data_utils.py:95-96)
+            nb = torch.cat([nb, layers[i][:, None]], dim=1)
+        if i == len(fanouts) - 1:
+            break
+        # S_{i+1} = sorted unique(S_i ++ nb) and the maps into it (bitmap frontier, no sort);
+        # the sampler's error bits are read with the frontier size (one host synchronisation)
+        nxt, rank = build_frontier(layers[i], nb, adj.n_rows, err)
+        cmaps.append(rank(layers[i]))
+        nmaps.append(rank(nb))
+        layers.append(nxt)
+    batch = SampledBatch(seeds, layers[-1], nb, cmaps[::-1], nmaps[::-1], tuple(layers))
     _raise_sample_error(int(err.item()))
     return batch
 

@@ -304,6 +304,11 @@ int gnn_gat_backward_nodes_f32(const int64_t* rowptr_t, const int32_t* src_t,
                              NaN counts as the maximum                   -> int64 out */
 #define GNN_SAGE_SUM 2    /* neighbor_feature.sum(dim=1)                  -> fp32 out
                              (GraphSAGE_Pytorch/models/Aggregator.py:21-22)          */
+#define GNN_SAGE_MAXPOOL 3 /* value max-pool, torch.max(neigh, dim=1).values -> fp32 out:
+                             north_star "mean/max-pool"; the value that
+                             GraphSAGE_Pytorch/models/Aggregator.py:23-24 reaches for
+                             (there it gets the namedtuple and fails). A NaN in the
+                             slice propagates.                                       */
 
 /*
  * GraphSAGE Aggregator over a pre-gathered neighbour tensor

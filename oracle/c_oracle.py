@@ -1,6 +1,7 @@
 """ctypes loader for oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
 
-The C restatement of the reference SpMM (oracle/spmm_oracle.c), built by
+The C restatement of the reference SpMM, both GAT layers and the GraphSAGE
+gather-reduce (oracle/spmm_oracle.c), built by
 ``make -C oracle``.  Used as the fast checker at large sizes and as bench.py's
 cpu_baseline ("port") leg.
 """
@@ -33,6 +34,11 @@ def load():
         lib.oracle_spmm_csr.restype = None
         lib.oracle_num_threads.restype = ctypes.c_int
         lib.oracle_set_threads.argtypes = [ctypes.c_int]
+        lib.oracle_gat_csr.argtypes = [vp, vp, i64, i64, vp, i64, vp, vp, i64, i64, i64,
+                                       ctypes.c_double, ctypes.c_int, vp, i64]
+        lib.oracle_gat_csr.restype = None
+        lib.oracle_sage_gather.argtypes = [vp, i64, vp, i64, i64, i64, i64, ctypes.c_int, vp, i64]
+        lib.oracle_sage_gather.restype = None
         _lib = lib
     return _lib
 
@@ -61,3 +67,43 @@ def spmm_csr(rowptr, col, val, x, bias=None, row0: int = 0, row1: int | None = N
                         x.ctypes.data, feat, feat, None if b is None else b.ctypes.data,
                         y.ctypes.data, feat)
     return y
+
+
+def gat_csr(rowptr, col, wh, el, er, heads: int, fh: int, slope: float, sparse: bool,
+            row0: int = 0, row1: int | None = None):
+    """fp32 [row1 - row0, heads * fh] GAT aggregation (float64 inside) over CSR rows
+    [row0, row1): the dense (layers.py:25-32) or sparse (layers.py:105-122) layer, no
+    activation; an edgeless row is NaN. ``el`` has rows of the CSR (indexed by the global
+    row id), ``er`` rows of the columns."""
+    lib = load()
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    wh = np.ascontiguousarray(wh, dtype=np.float32)
+    el = np.ascontiguousarray(el, dtype=np.float32)
+    er = np.ascontiguousarray(er, dtype=np.float32)
+    if el.shape[1] != heads or er.shape[1] != heads or wh.shape[1] != heads * fh:
+        raise ValueError("el / er must be [*, heads], wh [*, heads * fh]")
+    row1 = rowptr.size - 1 if row1 is None else row1
+    y = np.empty((row1 - row0, heads * fh), dtype=np.float32)
+    # one row stride for el and er: the wider of the two is not needed (both are [*, heads])
+    lib.oracle_gat_csr(rowptr.ctypes.data, col.ctypes.data, row0, row1, wh.ctypes.data,
+                       wh.shape[1], el.ctypes.data, er.ctypes.data, heads, heads, fh,
+                       float(slope), int(bool(sparse)), y.ctypes.data, heads * fh)
+    return y
+
+
+_SAGE_MODES = {"MEAN": 0, "SUM": 2, "MAXPOOL": 3}
+
+
+def sage_gather(table, idx, mode: str = "MEAN"):
+    """fp32 [M, F] reduce over k of table[idx[m, j]] (float64 inside): MEAN, SUM or
+    MAXPOOL (torch.max(dim=1).values, NaN-propagating)."""
+    lib = load()
+    table = np.ascontiguousarray(table, dtype=np.float32)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    M, k = idx.shape
+    F = table.shape[1]
+    out = np.empty((M, F), dtype=np.float32)
+    lib.oracle_sage_gather(table.ctypes.data, F, idx.ctypes.data, k, M, k, F, _SAGE_MODES[mode],
+                           out.ctypes.data, F)
+    return out

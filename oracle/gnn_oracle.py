@@ -269,6 +269,11 @@ def aggregator(neigh_feat, agg_func="MEAN"):
         has_nan = nan.any(axis=1)
         first_nan = np.argmax(nan, axis=1)
         return np.where(has_nan, first_nan, arg).astype(np.int64)
+    if agg_func == "MAXPOOL":
+        # value max-pool, BASELINE north_star "mean/max-pool": the .values of
+        # neighbor_feature.max(dim=1) (GraphSAGE_Pytorch/models/Aggregator.py:23-24); a NaN
+        # anywhere in the slice propagates (torch.max rule)
+        return x.astype(np.float64).max(axis=1)
     raise RuntimeError("unknown agg_func")
 
 

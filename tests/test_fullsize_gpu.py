@@ -105,3 +105,50 @@ def test_gat_cfg3_full_size():
         ones = torch.ones_like(wh)
         o1 = gat_aggregate(gg, ones, el, er, H, fh, 0.2, mode)
         assert float((o1 - 1).abs().max()) < 1e-5
+
+
+@pytest.mark.parametrize("agg", ["MEAN"])
+def test_graphsage_cfg4_full_size(agg):
+    """BASELINE configs[3]: the device-sampled [25, 10] batch of 8192 seeds (degree >= 1) on
+    the 10M / 100M R-MAT adjacency, the drop-in GraphSAGE(2, 128, 128, MEAN) forward on a
+    10M x 128 table (5.1 GB: row offsets pass 2^32 bytes), against the numpy oracle
+    (GraphSAGE/GraphSAGE.py:38-53, graph_utils.py:6) on the SAME maps: every seed's embedding
+    and logits within 1e-4, plus a layer-0 gather-mean sample over the table's last rows."""
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    from graphneuralnetwork_amd.ops import sage_gather_aggregate
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    from graphneuralnetwork_amd.sampler import sample_batch, symmetric_adjacency
+    dev = torch.device("cuda:0")
+    n, F = 10_000_000, 128
+    s, d = rmat_edges(n, 100_000_000, 0)
+    adj = symmetric_adjacency(s, d, n, device=dev)
+    del s, d
+    gen = torch.Generator(device=dev).manual_seed(0)
+    table = torch.randn(n, F, device=dev, generator=gen)
+    deg = adj.rowptr[1:] - adj.rowptr[:-1]
+    cand = torch.nonzero(deg > 0).view(-1)
+    seeds = cand[torch.randperm(cand.numel(), device=dev, generator=gen)[:8192]]
+    batch = sample_batch(adj, seeds, (25, 10), seed=0)
+    assert batch.neigh_map.shape == (8192, 25) and batch.frontier_nbrs.shape[1] == 10
+    torch.manual_seed(0)
+    net = GraphSAGE(2, F, F, False, agg_func=agg, Unsupervised=False, class_size=3).to(dev).eval()
+    with torch.no_grad():
+        emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+    tn = table.cpu().numpy()
+    ws = [blk.weight.weight.detach().cpu().numpy() for blk in net.sage_blocks]
+    dense = (net.dense.weight.detach().cpu().numpy(), net.dense.bias.detach().cpu().numpy())
+    ref_emb, ref_logits = O.graphsage_forward(
+        tn[batch.frontier.cpu().numpy()], [m.cpu().numpy() for m in batch.center_maps],
+        tn[batch.frontier_nbrs.cpu().numpy()], [m.cpu().numpy() for m in batch.neigh_maps],
+        ws, agg, False, dense)
+    close(emb.cpu().numpy(), ref_emb)
+    close(logits.cpu().numpy(), ref_logits)
+    # layer-0 gather-mean over index rows that include the table's last rows (byte offsets
+    # above 2^32: row 8,388,608 onward at F = 128)
+    rng = np.random.default_rng(5)
+    idx = rng.integers(0, n, (4096, 10))
+    idx[:64] = n - 1 - np.arange(640).reshape(64, 10)
+    idx[64:96] = (1 << 32) // (4 * F) + np.arange(320).reshape(32, 10)
+    got = sage_gather_aggregate(table, torch.from_numpy(idx).to(dev), agg).cpu().numpy()
+    close(got, c_oracle.sage_gather(tn, idx, agg))
+    assert int(batch.frontier.max()) >= (1 << 32) // (4 * F)  # sampled rows past 2^32 bytes too

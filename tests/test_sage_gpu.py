@@ -231,3 +231,85 @@ def test_graphsage_forward_mfma_gemm_matches_library(dev, monkeypatch):
     assert (emb >= 0).all()
     np.testing.assert_allclose(emb.cpu().numpy(), emb0.cpu().numpy(), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(logits.cpu().numpy(), logits0.cpu().numpy(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("F", [1, 7, 128, 600])
+@pytest.mark.parametrize("k", [1, 10, 25])
+def test_maxpool_pregathered_and_gathered(dev, F, k):
+    """GNN_SAGE_MAXPOOL (the north star's value max-pool): torch.max(dim=1).values, a NaN in
+    the slice propagating -- vs the oracle and torch, pre-gathered and fused-gather forms."""
+    from graphneuralnetwork_amd.ops import sage_aggregate, sage_gather_aggregate
+    rng = np.random.default_rng(F * 31 + k)
+    n, M = 4000, 257
+    table = rng.standard_normal((n, F)).astype(np.float32)
+    table[5, 0] = np.nan
+    table[9, :] = -np.inf
+    idx = rng.integers(0, n, (M, k))
+    idx[0, 0] = 5
+    idx[1, :] = 9
+    pre = table[idx]
+    ref = O.aggregator(pre, "MAXPOOL")
+    tref = torch.from_numpy(pre).max(dim=1).values.numpy()
+    got_p = sage_aggregate(torch.from_numpy(pre).to(dev), "MAXPOOL").cpu().numpy()
+    got_g = sage_gather_aggregate(torch.from_numpy(table).to(dev), torch.from_numpy(idx).to(dev),
+                                  "MAXPOOL").cpu().numpy()
+    for got in (got_p, got_g):
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+        np.testing.assert_array_equal(got, tref)        # a max selects a value: bit-exact
+    with pytest.raises(IndexError):
+        sage_aggregate(torch.zeros(3, 0, F, device=dev), "MAXPOOL")
+
+
+def test_maxpool_backward(dev):
+    """d neigh / d table of the value max-pool vs torch autograd of .max(dim=1).values."""
+    from graphneuralnetwork_amd.graphsage import Aggregator, Gathered
+    gen = torch.Generator().manual_seed(4)
+    n, M, k, F = 300, 200, 7, 24
+    table = torch.randn(n, F, generator=gen)
+    idx = torch.randint(0, n, (M, k), generator=gen)
+    gy = torch.randn(M, F, generator=gen)
+    t = table.to(dev).requires_grad_(True)
+    (Aggregator(Gathered(t, idx.to(dev)), "MAXPOOL") * gy.to(dev)).sum().backward()
+    t64 = table.double().requires_grad_(True)
+    (t64[idx].max(1).values * gy.double()).sum().backward()
+    np.testing.assert_allclose(t.grad.cpu().numpy(), t64.grad.numpy(), rtol=1e-5, atol=1e-6)
+    x = table[idx].to(dev).requires_grad_(True)
+    (Aggregator(x, "MAXPOOL") * gy.to(dev)).sum().backward()
+    x64 = table[idx].double().requires_grad_(True)
+    (x64.max(1).values * gy.double()).sum().backward()
+    np.testing.assert_allclose(x.grad.cpu().numpy(), x64.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def _sage_net_oracle(net, table, batch, agg):
+    """oracle.graphsage_forward (GraphSAGE/GraphSAGE.py:42-53) on the batch's device maps."""
+    tn = table.cpu().numpy()
+    ws = [blk.weight.weight.detach().cpu().numpy() for blk in net.sage_blocks]
+    dense = (net.dense.weight.detach().cpu().numpy(), net.dense.bias.detach().cpu().numpy())
+    return O.graphsage_forward(tn[batch.frontier.cpu().numpy()],
+                               [m.cpu().numpy() for m in batch.center_maps],
+                               tn[batch.frontier_nbrs.cpu().numpy()],
+                               [m.cpu().numpy() for m in batch.neigh_maps], ws, agg, False, dense)
+
+
+@pytest.mark.parametrize("agg", ["MEAN", "MAXPOOL"])
+def test_graphsage_sampled_forward_vs_oracle(dev, agg):
+    """The [25, 10] forward on device-sampled maps (fused gather-mean, hipBLASLt / MFMA
+    SageLayer GEMMs) against the numpy oracle on the same maps -- the oracle check of the
+    cfg4 path at a small size (GraphSAGE/GraphSAGE.py:38-53, graph_utils.py:6)."""
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    from graphneuralnetwork_amd.sampler import sample_batch, symmetric_adjacency
+    n, F, H = 20000, 128, 128
+    s, d = rmat_edges(n, 200000, 9)
+    adj = symmetric_adjacency(s, d, n, device=dev)
+    deg = (adj.rowptr[1:] - adj.rowptr[:-1]).cpu().numpy()
+    seeds = torch.from_numpy(np.flatnonzero(deg > 0)[:1024]).to(dev)
+    batch = sample_batch(adj, seeds, (25, 10), seed=2)
+    table = torch.randn(n, F, device=dev, generator=torch.Generator(dev).manual_seed(3))
+    torch.manual_seed(0)
+    net = GraphSAGE(2, F, H, False, agg_func=agg, Unsupervised=False, class_size=3).to(dev).eval()
+    with torch.no_grad():
+        emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+    ref_emb, ref_logits = _sage_net_oracle(net, table, batch, agg)
+    close(emb.cpu().numpy(), ref_emb)
+    close(logits.cpu().numpy(), ref_logits)

@@ -132,3 +132,73 @@ def test_batch_errors_and_frontier_out_of_range(dev):
     assert torch.equal(b.frontier[b.center_map], torch.tensor([0, 1], device=dev))
     nb = b.frontier[b.neigh_map].cpu().numpy()   # every sampled id is a true neighbour
     assert set(nb[0]) <= {0, 1} and set(nb[1]) == {0}
+
+
+@pytest.mark.parametrize("fanouts", [(5,), (25, 10), (10, 5, 3), (4, 3, 2, 2)])
+@pytest.mark.parametrize("gcn", [False, True])
+def test_multi_hop_batch(dev, fanouts, gcn):
+    """L-hop frontier chain (get_layer_adj_nodes, GraphSAGE/data_utils.py:82-117, with a
+    fanout per hop): S_{i+1} = sorted unique(S_i ++ sampled), the maps are positions in the
+    next layer, every sampled id is a true neighbour; the L-layer forward on the maps equals
+    the numpy oracle."""
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    from graphneuralnetwork_amd.sampler import sample_batch
+    from oracle import gnn_oracle as O
+    adj = _adj(dev)
+    rowptr, col = adj.rowptr.cpu().numpy(), adj.col.cpu().numpy()
+    deg = np.diff(rowptr)
+    seeds = torch.from_numpy(np.nonzero(deg > 0)[0][:50]).to(dev)
+    b = sample_batch(adj, seeds, fanouts, seed=4, gcn=gcn)
+    L = len(fanouts)
+    assert len(b.center_maps) == len(b.neigh_maps) == L - 1 and len(b.layer_sizes) == L
+    layers = list(b.layers)
+    assert torch.equal(layers[0], seeds) and torch.equal(layers[-1], b.frontier)
+    for i in range(L - 1):  # forward order is reversed: layer i's maps are [L - 2 - i]
+        cm, nm, nxt = b.center_maps[L - 2 - i], b.neigh_maps[L - 2 - i], layers[i + 1]
+        assert torch.equal(nxt[cm], layers[i])
+        k = fanouts[i] + (1 if gcn else 0)
+        assert nm.shape == (layers[i].numel(), k)
+        ids = nxt[nm].cpu().numpy()
+        for r, v in enumerate(layers[i].cpu().numpy()):
+            nbs = set(col[rowptr[v]:rowptr[v + 1]].tolist()) | ({int(v)} if gcn else set())
+            assert set(ids[r].tolist()) <= nbs
+        if gcn:
+            assert (ids[:, -1] == layers[i].cpu().numpy()).all()
+        assert torch.equal(nxt, torch.unique(torch.cat([layers[i], nxt[nm].view(-1)])))
+    assert b.frontier_nbrs.shape == (b.frontier.numel(), fanouts[-1] + (1 if gcn else 0))
+    assert b.sampled_edges == sum(layers[i].numel() * (fanouts[i] + gcn) for i in range(L))
+    F, H = 16, 8
+    table = torch.randn(adj.n_rows, F, device=dev)
+    torch.manual_seed(1)
+    net = GraphSAGE(L, F, H, False, agg_func="MEAN", Unsupervised=False, class_size=3).to(dev).eval()
+    with torch.no_grad():
+        emb, logits = net(*b.forward_args(table), None, None, None, None, None)
+    tn = table.cpu().numpy()
+    ref_emb, ref_logits = O.graphsage_forward(
+        tn[b.frontier.cpu().numpy()], [m.cpu().numpy() for m in b.center_maps],
+        tn[b.frontier_nbrs.cpu().numpy()], [m.cpu().numpy() for m in b.neigh_maps],
+        [blk.weight.weight.detach().cpu().numpy() for blk in net.sage_blocks], "MEAN", False,
+        (net.dense.weight.detach().cpu().numpy(), net.dense.bias.detach().cpu().numpy()))
+    assert emb.shape == (seeds.numel(), H)
+    np.testing.assert_allclose(emb.cpu().numpy(), ref_emb, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(logits.cpu().numpy(), ref_logits, rtol=1e-4, atol=1e-5)
+
+
+def test_rank_after_rebuild_raises(dev):
+    """a rank() of an older build_frontier must not read a newer workspace."""
+    from graphneuralnetwork_amd.sampler import build_frontier
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    a = torch.tensor([3, 1, 4], device=dev)
+    _, rank1 = build_frontier(a, a, 10, err)
+    build_frontier(torch.tensor([2], device=dev), a, 10, err)
+    with pytest.raises(RuntimeError, match="rebuilt"):
+        rank1(a)
+
+
+def test_fanout_validation(dev):
+    from graphneuralnetwork_amd.sampler import sample_batch
+    adj = _adj(dev)
+    with pytest.raises(ValueError):
+        sample_batch(adj, torch.tensor([0], device=dev), ())
+    with pytest.raises(ValueError):
+        sample_batch(adj, torch.tensor([0], device=dev), (3, 0))
