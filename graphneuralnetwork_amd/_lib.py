@@ -46,6 +46,14 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _vp, _vp, _i64,            # small_row, small_col, small_val, n_small
         _vp, _i64, _vp,                 # mid_row, n_mid, partial
         _u32, _vp]),                    # flags, stream
+    "gnn_spmm_csr_tasks_f32": (ctypes.c_int, [
+        _vp, _vp, _vp, _i64,            # rowptr, col, val, n_rows
+        _vp, _i64, _vp, _i64, _i64,     # x, ldx, xh (nullable), ldh, feat
+        _vp, _vp, _i64,                 # bias, y, ldy
+        _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
+        _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
+        _vp, _i64, _vp, _i64,           # mid_row, n_mid, task_row, n_task
+        _vp, _u32, _vp]),               # partial, flags, stream
     "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
     "gnn_hub_plan_workspace_bytes": (_i64, [_i64]),
     "gnn_hub_plan_build": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
@@ -140,6 +148,10 @@ SIGNATURES: dict[str, tuple] = {
 EPI_RELU = 1
 EPI_ELU = 2
 EPI_ACCUMULATE = 4
+EPI_SKIP_EMPTY = 8
+E_ARG = -1
+E_ALIGN = -2
+E_UNSUPPORTED = -3
 
 
 def library_path() -> Path:

@@ -47,6 +47,9 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 #ifndef GNN_SPMM_SMALL_SPLIT
 #define GNN_SPMM_SMALL_SPLIT 0
 #endif
+#ifndef GNN_SPMM_TASK_U
+#define GNN_SPMM_TASK_U 0  // neighbour rows in flight per slot in packed tasks (0: as GNN_SPMM_U)
+#endif
 #ifndef GNN_SPMM_SMALL_SPLIT_UNROLL
 #define GNN_SPMM_SMALL_SPLIT_UNROLL 16
 #endif
@@ -89,10 +92,17 @@ struct SpmmParams {
   // hub staging (HUB kernels): col < 0 names row -1-col of the staged hub table xh
   const float* xh;
   int64_t ldh;
+  // packed row tasks (gnn_spmm_csr_tasks_f32): task t = rows [task_row[2t], task_row[2t+1]),
+  // at most kTaskRows rows, every row of degree <= the plan's packing threshold
+  const int32_t* task_row;
+  int64_t n_task;
   // launch geometry (wave index boundaries)
   int64_t seg_waves;
   int64_t mid_waves;
 };
+
+// rows per packed task: the task's rowptr values (rows + 1) live in one VGPR (lane = row)
+constexpr int kTaskRows = kWave - 1;
 
 // acc[ch] += sum_{e in [beg, end)} val[e] * x[col[e]][(ch*LPR + sub)*VW .. +VW)
 //
@@ -258,7 +268,116 @@ __device__ __forceinline__ void small_rows(const SpmmParams& P, int64_t swave, i
   }
 }
 
-template <int VW, int LPR, int NCH, int U, bool NT, bool STAGE = false, bool HUB = false>
+// Packed row task: rows [rb, re) of consecutive ids (at most kTaskRows, each of low degree),
+// their edges contiguous in col[] / val[]. The rows are split between the EPI edge slots of
+// the wave by cost (edges + rows, balanced); each slot streams ITS rows' edges in CSR order,
+// U neighbour rows in flight, and writes a row as soon as the stream passes its end. The
+// rowptr -> col -> X dependency chain is paid once per task instead of once per row, and the
+// gathers of a row overlap the bookkeeping of the next one. Each row's sum runs in edge order
+// in one slot: deterministic, no shuffle reduction.
+template <int VW, int LPR, int NCH, int U, bool NT, bool HUB>
+__device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int lane) {
+  constexpr int EPI = kWave / LPR;
+  static_assert(LPR % U == 0, "a batch of U edges never straddles a chunk of LPR edges");
+  const int sub = lane & (LPR - 1);
+  const int grp = lane / LPR;
+  const int32_t rb = P.task_row[2 * t];
+  const int nr = P.task_row[2 * t + 1] - rb;  // 1 .. kTaskRows
+  const int64_t e0 = P.rowptr[rb];
+  // lane l < nr: start of row rb + l relative to e0; lanes >= nr: the task's end
+  const int rp = static_cast<int>(P.rowptr[rb + min(lane, nr)] - e0);
+  const int E = __shfl(rp, nr, kWave);
+  // slot g takes rows [sb, se): the first row whose (edges + rows) prefix reaches g/EPI of
+  // the task's, found by a ballot over the row lanes
+  int sb = 0, se = nr;
+  if (EPI > 1) {
+    const int64_t total = static_cast<int64_t>(E) + nr;
+#pragma unroll
+    for (int b = 1; b < EPI; ++b) {
+      const int64_t target = total * b / EPI;
+      const uint64_t m = __ballot(lane <= nr && static_cast<int64_t>(rp) + lane >= target);
+      const int row_b = m ? (__ffsll(static_cast<unsigned long long>(m)) - 1) : nr;
+      if (grp == b) sb = row_b;
+      if (grp == b - 1) se = row_b;
+    }
+  }
+  int cur = sb;                                   // the row being accumulated
+  int cur_end = __shfl(rp, min(cur + 1, nr), kWave);  // its end (slot-uniform)
+  const int es = __shfl(rp, sb, kWave);          // the slot's edge range [es, ee)
+  const int ee = __shfl(rp, se, kWave);
+  const bool skip_empty = (P.flags & GNN_EPI_SKIP_EMPTY) != 0;
+  const uint32_t epi = P.flags & (GNN_EPI_RELU | GNN_EPI_ELU | GNN_EPI_ACCUMULATE);
+  typename Vec<VW>::T acc[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) acc[ch] = vzero<VW>();
+
+  // write every row of the slot that ends at or before edge position `pos` (several when
+  // rows without edges follow each other); the shuffles run with the whole slot active
+  auto flush_upto = [&](int pos) {
+    bool need = cur < se && pos >= cur_end;
+    while (__ballot(need)) {
+      if (need) {
+        const bool empty = __shfl(rp, cur, kWave) == cur_end;
+        if (!(empty && skip_empty))
+          store_slot_row<VW, LPR, NCH, NT>(P.y + static_cast<int64_t>(rb + cur) * P.ldy, P.bias,
+                                           P.feat, epi, sub, acc);
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) acc[ch] = vzero<VW>();
+      }
+      cur += need ? 1 : 0;
+      const int nxt = __shfl(rp, min(cur + 1, nr), kWave);
+      cur_end = need ? nxt : cur_end;
+      need = cur < se && pos >= cur_end;
+    }
+  };
+
+  // every loop below is wave-uniform (the slots' streams differ in length, so the shorter
+  // ones idle with their loads masked): the shuffles read rp / c / v from any lane, and a
+  // ds_bpermute from a lane outside EXEC would not return its value
+  int len = ee - es;
+#pragma unroll
+  for (int m = 1; m < kWave; m <<= 1) len = max(len, __shfl_xor(len, m, kWave));
+  flush_upto(es);  // leading rows without edges
+  for (int off = 0; off < len; off += LPR) {
+    const int cb = es + off;  // this slot's chunk: lane `sub` holds edge cb + sub
+    int c = 0;
+    float v = 0.f;
+    if (cb + sub < ee) {
+      c = __builtin_nontemporal_load(P.col + e0 + cb + sub);
+      v = __builtin_nontemporal_load(P.val + e0 + cb + sub);
+    }
+    const int n = min(LPR, len - off);  // wave-uniform
+    for (int k = 0; k < n; k += U) {
+      typename Vec<VW>::T xv[U][NCH];
+      float w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int src = grp * LPR + ((k + u) & (LPR - 1));
+        const int ce = __shfl(c, src, kWave);
+        const float we = __shfl(v, src, kWave);
+        const bool ok = cb + k + u < ee;
+        w[u] = ok ? we : 0.f;
+        const float* xr = (HUB && ce < 0) ? P.xh + static_cast<int64_t>(-1 - ce) * P.ldh
+                                          : P.x + static_cast<int64_t>(ce) * P.ldx;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+          xv[u][ch] = (ok && f < P.feat) ? vload<VW>(xr + f) : vzero<VW>();
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        flush_upto(cb + k + u);  // rows that end before this edge (all of them past ee)
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) acc[ch] += w[u] * xv[u][ch];
+      }
+    }
+  }
+  flush_upto(0x7fffffff);  // the last row and trailing rows without edges
+}
+
+template <int VW, int LPR, int NCH, int U, bool NT, bool STAGE = false, bool HUB = false,
+          bool TASKS = false>
 __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
   constexpr int EPI = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
@@ -301,9 +420,13 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
                                                      sub, acc);
     return;
   }
-  // ---- packed small rows (unless they have their own launch, spmm_small_kernel)
-  if constexpr (!kSmallSplit)
+  if constexpr (TASKS) {  // ---- packed row tasks
+    const int64_t t = wave - P.seg_waves - P.mid_waves;
+    if (t < P.n_task) packed_rows<VW, LPR, NCH, U, NT, HUB>(P, t, lane);
+  } else if constexpr (!kSmallSplit) {
+    // ---- packed small rows (unless they have their own launch, spmm_small_kernel)
     small_rows<VW, LPR, NCH, NT, small_unroll<NCH>()>(P, wave - P.seg_waves - P.mid_waves, lane);
+  }
 }
 
 // Packed small rows as their own launch: their unrolled loads then do not set the
@@ -391,6 +514,25 @@ static int launch_spmm_t(const SpmmLaunch& L) {
   SpmmParams p = L.p;
   const int64_t seg_blocks = (p.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
   const int64_t mid_blocks = (p.n_mid + kWavesPerBlock - 1) / kWavesPerBlock;
+  if constexpr (VW == 4 && LPR >= 16 && !STAGE) {
+    if (p.task_row != nullptr) {  // packed row tasks in place of the small-row class
+      constexpr int UT = (GNN_SPMM_TASK_U > 0 && NCH == 1) ? GNN_SPMM_TASK_U : (U > 1 ? U : 2);
+      const int64_t task_blocks = (p.n_task + kWavesPerBlock - 1) / kWavesPerBlock;
+      p.seg_waves = seg_blocks * kWavesPerBlock;
+      p.mid_waves = mid_blocks * kWavesPerBlock;
+      const int64_t blocks = seg_blocks + mid_blocks + task_blocks;
+      if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
+      if (blocks > 0)
+        hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, UT, NT, false, HUB, true>),
+                           dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, L.stream, p);
+      if (L.n_long > 0)
+        hipLaunchKernelGGL((spmm_fixup_kernel<VW, LPR, NCH, NT>), dim3(static_cast<unsigned>(L.n_long)),
+                           dim3(kBlock), 0, L.stream, L.long_row, L.long_seg_ptr, L.n_long, p.partial,
+                           p.ldp, p.feat, p.bias, p.y, p.ldy, p.flags & ~GNN_EPI_SKIP_EMPTY);
+      return launch_status();
+    }
+  }
+  if (p.task_row != nullptr) return GNN_E_UNSUPPORTED;
   constexpr int SU = kSmallSplit ? kSmallSplitUnroll : small_unroll<NCH>();
   const int64_t small_waves = (p.n_small + EPI * SU - 1) / (EPI * SU);
   const int64_t small_blocks = (small_waves + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -459,7 +601,8 @@ static int check_spmm_args(const int64_t* rowptr, int64_t n_rows, const float* x
   if (n_small > 0 && (small_row == nullptr || small_col == nullptr || small_val == nullptr))
     return GNN_E_ARG;
   if (mid_row != nullptr && (n_mid < 0 || n_mid + n_small + n_long > n_rows)) return GNN_E_ARG;
-  if (flags & ~(GNN_EPI_RELU | GNN_EPI_ELU | GNN_EPI_ACCUMULATE)) return GNN_E_ARG;
+  if (flags & ~(GNN_EPI_RELU | GNN_EPI_ELU | GNN_EPI_ACCUMULATE | GNN_EPI_SKIP_EMPTY))
+    return GNN_E_ARG;
   return GNN_OK;
 }
 
@@ -510,7 +653,8 @@ static int spmm_entry(const int64_t* rowptr, const int32_t* col, const float* va
                       const int32_t* long_seg_ptr, int64_t n_long, const int32_t* small_row,
                       const int32_t* small_col, const float* small_val, int64_t n_small,
                       const int32_t* mid_row, int64_t n_mid, float* partial, uint32_t flags,
-                      void* stream, int variant, const float* xh = nullptr, int64_t ldh = 0) {
+                      void* stream, int variant, const float* xh = nullptr, int64_t ldh = 0,
+                      const int32_t* task_row = nullptr, int64_t n_task = 0) {
   int rc = check_spmm_args(rowptr, n_rows, x, ldx, feat, y, ldy, seg_len, n_seg, n_long, n_small,
                            n_mid, seg_row, seg_begin, long_row, long_seg_ptr, small_row, small_col,
                            small_val, mid_row, partial, flags);
@@ -539,6 +683,8 @@ static int spmm_entry(const int64_t* rowptr, const int32_t* col, const float* va
   L.p.flags = flags;
   L.p.xh = xh;
   L.p.ldh = ldh;
+  L.p.task_row = task_row;
+  L.p.n_task = n_task;
   L.long_row = long_row;
   L.long_seg_ptr = long_seg_ptr;
   L.n_long = plan ? n_long : 0;
@@ -594,4 +740,22 @@ extern "C" int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* co
   return spmm_entry(rowptr, col, val, n_rows, x, ldx, feat, bias, y, ldy, seg_len, seg_row,
                     seg_begin, n_seg, long_row, long_seg_ptr, n_long, small_row, small_col,
                     small_val, n_small, mid_row, n_mid, partial, 0u, stream, variant);
+}
+
+// ---- packed row tasks (GCN/GCN.py:43-45, same aggregation): see packed_rows ----
+extern "C" int gnn_spmm_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, const float* val,
+                                      int64_t n_rows, const float* x, int64_t ldx, const float* xh,
+                                      int64_t ldh, int64_t feat, const float* bias, float* y,
+                                      int64_t ldy, int64_t seg_len, const int32_t* seg_row,
+                                      const int64_t* seg_begin, int64_t n_seg,
+                                      const int32_t* long_row, const int32_t* long_seg_ptr,
+                                      int64_t n_long, const int32_t* mid_row, int64_t n_mid,
+                                      const int32_t* task_row, int64_t n_task, float* partial,
+                                      uint32_t flags, void* stream) {
+  if (n_task < 0 || (n_task > 0 && task_row == nullptr) || mid_row == nullptr) return GNN_E_ARG;
+  if (xh == nullptr) ldh = 0;
+  return spmm_entry(rowptr, col, val, n_rows, x, ldx, feat, bias, y, ldy, seg_len, seg_row,
+                    seg_begin, n_seg, long_row, long_seg_ptr, n_long, nullptr, nullptr, nullptr, 0,
+                    mid_row, n_mid, partial, flags, stream, -1, xh, ldh,
+                    task_row != nullptr ? task_row : mid_row, n_task);
 }

@@ -117,6 +117,74 @@ class RowSplitPlan:
                 self.n_mid)
 
 
+# Packed row tasks (gnn_spmm_csr_tasks_f32): runs of consecutive rows of degree <= TASK_MAX_DEG
+# cut into tasks of at most TASK_ROWS rows and about TASK_COST (edges + rows) each; one
+# wavefront streams a task's edges (its EPI edge slots take balanced sub-ranges of rows).
+TASK_ROWS = 63  # spmm.hip kTaskRows: a task's rowptr values fit one VGPR
+
+
+@dataclass
+class TaskPlan:
+    """Row classes for gnn_spmm_csr_tasks_f32: segments of long rows (as RowSplitPlan), mid
+    rows (max_deg < degree <= seg_len, one wave each) and packed tasks (the other rows)."""
+
+    seg_len: int
+    base: RowSplitPlan         # seg_row / seg_begin / long_row / long_seg_ptr are used
+    mid_row: torch.Tensor      # int32 [n_mid]
+    task_row: torch.Tensor     # int32 [2 * n_task]: [begin, end) row ranges
+    max_deg: int
+    cost: int
+
+    @property
+    def n_task(self) -> int:
+        return int(self.task_row.numel()) // 2
+
+    @property
+    def n_mid(self) -> int:
+        return int(self.mid_row.numel())
+
+    def args(self):
+        """The plan arguments of gnn_spmm_csr_tasks_f32 after seg_len."""
+        from ._lib import ptr
+        b = self.base
+        return (ptr(b.seg_row), ptr(b.seg_begin), b.n_seg, ptr(b.long_row),
+                b.long_seg_ptr.data_ptr(), b.n_long,
+                self.mid_row.data_ptr() if self.n_mid else b.long_seg_ptr.data_ptr(), self.n_mid,
+                self.task_row.data_ptr() if self.n_task else None, self.n_task)
+
+
+def task_ranges(rowptr: torch.Tensor, max_deg: int, cost: int, rows: int = TASK_ROWS):
+    """[2 * n_task] int32 [begin, end) row ranges: maximal runs of consecutive rows of degree
+    <= max_deg, cut where the (edges + rows) prefix inside the run crosses a multiple of
+    ``cost`` and every ``rows`` rows (torch ops on any device)."""
+    dev = rowptr.device
+    n = rowptr.numel() - 1
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int32, device=dev)
+    deg = rowptr[1:] - rowptr[:-1]
+    pack = deg <= max_deg
+    if not bool(pack.any()):
+        return torch.zeros(0, dtype=torch.int32, device=dev)
+    prev = torch.cat([torch.zeros(1, dtype=torch.bool, device=dev), pack[:-1]])
+    run_start = pack & ~prev
+    run_id = torch.cumsum(run_start.to(torch.int64), 0) - 1
+    c = torch.where(pack, deg + 1, torch.zeros_like(deg))
+    excl = torch.cumsum(c, 0) - c
+    idx = torch.arange(n, device=dev, dtype=torch.int64)
+    first = idx[run_start]
+    rid = run_id.clamp_(min=0)
+    excl_in = excl - excl[first][rid]
+    pos_in = idx - first[rid]
+    bucket = excl_in // cost
+    prev_bucket = torch.cat([bucket[:1] - 1, bucket[:-1]])
+    start = pack & (run_start | (bucket != prev_bucket) | (pos_in % rows == 0))
+    bounds = torch.nonzero(start | ~pack).view(-1)
+    bounds = torch.cat([bounds, torch.full((1,), n, dtype=torch.int64, device=dev)])
+    tb = torch.nonzero(start).view(-1)
+    te = bounds[torch.searchsorted(bounds, tb, right=True)]
+    return torch.stack([tb, te], 1).reshape(-1).to(torch.int32).contiguous()
+
+
 @dataclass
 class HubPlan:
     """Hub staging of a graph's columns (gnn_spmm_csr_hub_f32): the k highest-degree
@@ -330,6 +398,20 @@ class CsrGraph:
         if p is None:
             p = _build_plan(self, seg_len)
             self._plans[seg_len] = p
+        return p
+
+    def task_plan(self, seg_len: int, max_deg: int, cost: int) -> TaskPlan:
+        """Packed-task plan (built once per (seg_len, max_deg, cost), cached)."""
+        key = ("_tasks", seg_len, max_deg, cost)
+        p = self._plans.get(key)
+        if p is None:
+            base = self.plan(seg_len)
+            deg = self.rowptr[1:] - self.rowptr[:-1]
+            mid = torch.nonzero((deg > max_deg) & (deg <= base.seg_len)).view(-1)
+            p = TaskPlan(base.seg_len, base, mid.to(torch.int32).contiguous(),
+                         task_ranges(self.rowptr, min(max_deg, base.seg_len), cost), max_deg,
+                         cost)
+            self._plans[key] = p
         return p
 
     def hub_plan(self, k: int) -> HubPlan:

@@ -75,6 +75,31 @@ def xcd_hub_rows_for(n_cols: int, feat: int) -> int:
     return min(n_cols, XCD_HUB_ROWS, max(64, XCD_HUB_BYTES // (4 * feat)))
 
 
+# Packed row tasks (gnn_spmm_csr_tasks_f32, spmm.hip packed_rows): rows of degree <=
+# TASK_MAX_DEG are streamed a task (<= 63 consecutive rows, ~TASK_COST edges + rows) per wave
+# instead of one wave per row, so the rowptr -> col -> X chain of short rows is paid once per
+# task. Needs the 16-B vector path and feat > 32 (two or fewer edge slots per 16 lanes).
+SPMM_TASKS = True
+TASK_MAX_DEG = 128
+TASK_COST = 256
+
+
+def _tasks_ok(feat: int, *ts) -> bool:
+    # every column block of the launch (<= 2048 wide) must be a vector block wider than 32
+    if not SPMM_TASKS or feat % 4 or feat <= 32 or 0 < feat % 2048 <= 32:
+        return False
+    return all(t is None or (t.data_ptr() % 16 == 0 and (t.dim() == 1 or t.stride(0) % 4 == 0))
+               for t in ts)
+
+
+def _spmm_tasks_call(lib, g: CsrGraph, col: torch.Tensor, tp, x, xh, feat, bias, y, ldy,
+                     partial, flags, stream, what):
+    _lib.check(lib.gnn_spmm_csr_tasks_f32(
+        g.rowptr.data_ptr(), col.data_ptr(), g.val.data_ptr(), g.n_rows, x.data_ptr(),
+        x.stride(0), _lib.ptr(xh), xh.stride(0) if xh is not None else 0, feat, _lib.ptr(bias),
+        y.data_ptr(), ldy, tp.seg_len, *tp.args(), _lib.ptr(partial), flags, stream), what)
+
+
 def _spmm_hub_call(lib, g: CsrGraph, col: torch.Tensor, plan, pargs, x, xh, feat, bias, y, ldy,
                    partial, flags, stream, what):
     _lib.check(lib.gnn_spmm_csr_hub_f32(
@@ -144,17 +169,31 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
         partial = torch.empty((plan.n_seg, feat), dtype=torch.float32, device=x.device)
     pargs = plan.args(skip_empty=skip_empty)
     k = hub_rows_for(g.n_cols, feat) if hubs is None else min(int(hubs), g.n_cols)
+    tasks = _tasks_ok(feat, x, out, bias, partial)
     if k > 0 and g.nnz:
         hp = g.hub_plan(k)
         xh = torch.empty((hp.k, feat), dtype=torch.float32, device=x.device)
         _lib.check(lib.gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0],
                                            hp.hub_ids.data_ptr(), hp.k, feat, xh.data_ptr(), feat,
                                            hp.err.data_ptr(), stream), "gnn_gather_rows_f32")
+        if tasks:
+            gh = CsrGraph(g.rowptr, hp.col_hub, g.val, g.n_rows, g.n_cols)
+            _spmm_tasks_call(lib, gh, hp.col_hub, g.task_plan(seg, TASK_MAX_DEG, TASK_COST), x,
+                             xh, feat, bias, out, out.stride(0), partial,
+                             flags | (_lib.EPI_SKIP_EMPTY if skip_empty else 0), stream,
+                             "gnn_spmm_csr_tasks_f32 (hub)")
+            return out
         rc = lib.gnn_spmm_csr_hub_f32(
             g.rowptr.data_ptr(), hp.col_hub.data_ptr(), g.val.data_ptr(), g.n_rows,
             x.data_ptr(), x.stride(0), xh.data_ptr(), feat, feat, _lib.ptr(bias),
             out.data_ptr(), out.stride(0), plan.seg_len, *pargs, _lib.ptr(partial), flags, stream)
         _lib.check(rc, "gnn_spmm_csr_hub_f32")
+        return out
+    if tasks and g.nnz:
+        _spmm_tasks_call(lib, g, g.col, g.task_plan(seg, TASK_MAX_DEG, TASK_COST), x, None, feat,
+                         bias, out, out.stride(0), partial,
+                         flags | (_lib.EPI_SKIP_EMPTY if skip_empty else 0), stream,
+                         "gnn_spmm_csr_tasks_f32")
         return out
     rc = lib.gnn_spmm_csr_f32(
         g.rowptr.data_ptr(), g.col.data_ptr(), g.val.data_ptr(), g.n_rows,
@@ -179,6 +218,15 @@ def _spmm_xcd(lib, g: CsrGraph, xp, x, feat, bias, out, seg, skip_empty, flags, 
         raise RuntimeError("XCD hub plan: item rows outside the mid-row class")
     _spmm_hub_call(lib, xp.items, xp.items.col, p1, p1.args(), x, buf, feat, None, buf[k:], feat,
                    None, 0, stream, "gnn_spmm_csr_hub_f32 (xcd items)")
+    if _tasks_ok(feat, x, out, bias, buf):
+        tp = xp.rest.task_plan(seg, TASK_MAX_DEG, TASK_COST)
+        partial = None
+        if tp.base.n_seg:
+            partial = torch.empty((tp.base.n_seg, feat), dtype=torch.float32, device=x.device)
+        _spmm_tasks_call(lib, xp.rest, xp.rest.col, tp, x, buf, feat, bias, out, out.stride(0),
+                         partial, flags | (_lib.EPI_SKIP_EMPTY if skip_empty else 0), stream,
+                         "gnn_spmm_csr_tasks_f32 (xcd rest)")
+        return
     p2 = xp.rest_plan(seg)
     partial = None
     if p2.n_seg:

@@ -45,6 +45,9 @@ extern "C" {
 #define GNN_EPI_ELU 2u  /* y = y > 0 ? y : expm1(y)   (F.elu, alpha = 1)             */
 #define GNN_EPI_ACCUMULATE 4u /* SpMM only: y = y_old + A.X (+ bias) (act) -- second pass
                                  of a split (interior + halo) aggregation             */
+#define GNN_EPI_SKIP_EMPTY 8u /* gnn_spmm_csr_tasks_f32 only: rows of a task without edges
+                                 are left unwritten (an accumulate pass with no bias /
+                                 activation: their output is unchanged anyway)        */
 
 /* Library version, e.g. 100 for 0.1.0. */
 int gnn_version(void);
@@ -99,6 +102,28 @@ int gnn_spmm_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub, const fl
                          int64_t n_long, const int32_t* small_row, const int32_t* small_col,
                          const float* small_val, int64_t n_small, const int32_t* mid_row,
                          int64_t n_mid, float* partial, uint32_t flags, void* stream);
+
+/*
+ * The same aggregation with short rows in packed row tasks (replaces the same call site,
+ * GCN/GCN.py:43-45). task_row int32 [2 * n_task] holds [begin, end) ranges of
+ * consecutive rows (at most 63 rows each; every row of a task has degree <= seg_len and
+ * is in no other list); one wavefront streams a task's edges, its edge slots taking
+ * cost-balanced sub-ranges of the rows, so the rowptr -> col -> X chain is paid once per
+ * task instead of once per row. mid_row lists the other rows of degree <= seg_len (one
+ * wavefront each), seg_* / long_* the long rows as in gnn_spmm_csr_f32. xh / ldh: the
+ * optional hub table (col < 0 names row -1-col of xh, as gnn_spmm_csr_hub_f32; NULL: none).
+ * flags: GNN_EPI_* including GNN_EPI_SKIP_EMPTY. Needs feat % 4 == 0, 32 < feat,
+ * 16-B aligned x / xh / y / bias / partial and ldx, ldh, ldy multiples of 4
+ * (else GNN_E_UNSUPPORTED). Each row's sum runs in edge order: deterministic.
+ */
+int gnn_spmm_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, const float* val,
+                           int64_t n_rows, const float* x, int64_t ldx, const float* xh,
+                           int64_t ldh, int64_t feat, const float* bias, float* y, int64_t ldy,
+                           int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin,
+                           int64_t n_seg, const int32_t* long_row, const int32_t* long_seg_ptr,
+                           int64_t n_long, const int32_t* mid_row, int64_t n_mid,
+                           const int32_t* task_row, int64_t n_task, float* partial,
+                           uint32_t flags, void* stream);
 
 /*
  * Hub-staging plan for gnn_spmm_csr_hub_f32 / gnn_gat_csr_hub_f32 (built once per graph

@@ -420,3 +420,74 @@ def test_gcn_transform_fallback_and_training(dev):
     with torch.no_grad():
         y2 = layer(X, g)  # MFMA transform path
     close(y2.cpu().numpy(), y.detach().cpu().numpy())
+
+
+@pytest.mark.parametrize("F", [36, 64, 128, 256, 512, 2100])
+def test_packed_tasks_vs_oracle(dev, F, monkeypatch):
+    """gnn_spmm_csr_tasks_f32 (short rows streamed a task of <= 63 rows per wave): against
+    the C oracle for several task shapes, with runs of edgeless rows, long-row segments,
+    hub staging, bias / activation, and accumulate with edgeless rows left unwritten; and
+    against the one-wave-per-row kernel."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.graph import CsrGraph
+    rng = np.random.default_rng(F)
+    n = 3000 if F < 1000 else 800
+    deg = rng.integers(0, 12, n)
+    deg[rng.integers(0, n, 30)] = rng.integers(60, 700, 30)
+    deg[100:190] = 0                                   # a run longer than one task
+    deg[500:503] = 0
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    col = rng.integers(0, n, rowptr[-1]).astype(np.int32)
+    val = rng.standard_normal(rowptr[-1]).astype(np.float32)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.from_numpy(val).to(dev), n, n)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    b = rng.standard_normal(F).astype(np.float32)
+    Xd, bd = torch.from_numpy(X).to(dev), torch.from_numpy(b).to(dev)
+    ref = O.spmm_csr(rowptr, col, val, X, b)
+    monkeypatch.setattr(ops, "SPMM_TASKS", False)
+    per_row = ops.spmm_forward(g, Xd, bd, seg_len=256, hubs=0)
+    monkeypatch.setattr(ops, "SPMM_TASKS", True)
+    for max_deg, cost in ((1, 4), (8, 16), (64, 256), (128, 256), (700, 2048)):
+        monkeypatch.setattr(ops, "TASK_MAX_DEG", max_deg)
+        monkeypatch.setattr(ops, "TASK_COST", cost)
+        for hubs in (0, 50):
+            y = ops.spmm_forward(g, Xd, bd, seg_len=256, hubs=hubs)
+            assert any(k[0] == "_tasks" for k in g._plans if isinstance(k, tuple))
+            close(y.cpu().numpy(), ref)
+            close(y.cpu().numpy(), per_row.cpu().numpy(), rtol=1e-5)
+        y = ops.spmm_forward(g, Xd, bd, activation="elu", seg_len=256, hubs=0)
+        close(y.cpu().numpy(), np.where(ref > 0, ref, np.expm1(np.minimum(ref, 0))))
+        base = rng.standard_normal((n, F)).astype(np.float32)
+        out = torch.from_numpy(base).to(dev)
+        ops.spmm_forward(g, Xd, None, out=out, accumulate=True, seg_len=256, hubs=0)
+        got = out.cpu().numpy()
+        close(got, base + O.spmm_csr(rowptr, col, val, X))
+        np.testing.assert_array_equal(got[deg == 0], base[deg == 0])  # never rewritten
+    assert torch.equal(ops.spmm_forward(g, Xd, bd, seg_len=256),
+                       ops.spmm_forward(g, Xd, bd, seg_len=256))  # deterministic
+
+
+def test_packed_tasks_c_abi_contract(dev):
+    """gnn_spmm_csr_tasks_f32 rejects what it does not cover (feat <= 32, misaligned
+    vectors) with GNN_E_UNSUPPORTED and unknown flags with GNN_E_ARG."""
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd.graph import CsrGraph
+    lib = _lib.load()
+    n = 64
+    rowptr = torch.arange(n + 1, dtype=torch.int64, device=dev)
+    col = torch.arange(n, dtype=torch.int32, device=dev)
+    val = torch.ones(n, device=dev)
+    g = CsrGraph(rowptr, col, val, n, n)
+    tp = g.task_plan(256, 64, 128)
+    s = torch.cuda.current_stream().cuda_stream
+    for F, off, flags, want in ((32, 0, 0, _lib.E_UNSUPPORTED), (64, 1, 0, _lib.E_UNSUPPORTED),
+                                (64, 0, 64, _lib.E_ARG), (64, 0, 0, 0)):
+        X = torch.randn(n, F + 4, device=dev)[:, off:off + F]
+        y = torch.empty(n, F, device=dev)
+        rc = lib.gnn_spmm_csr_tasks_f32(rowptr.data_ptr(), col.data_ptr(), val.data_ptr(), n,
+                                        X.data_ptr(), X.stride(0), None, 0, F, None, y.data_ptr(),
+                                        F, tp.seg_len, *tp.args(), None, flags, s)
+        assert rc == want, (F, off, flags, rc)
+        if rc == 0:
+            torch.testing.assert_close(y, X)

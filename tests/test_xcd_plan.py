@@ -117,3 +117,30 @@ def test_xcd_plan_none_without_items():
     with pytest.raises(ValueError):  # fewer hub rows than slices
         xcd_hub_coo(torch.from_numpy(rowptr), torch.from_numpy(ch.astype(np.int32)),
                     torch.from_numpy(val), 16, 2, 8, phases=4)
+
+
+@pytest.mark.parametrize("max_deg,cost", [(1, 4), (8, 16), (64, 256), (128, 256)])
+def test_task_ranges_invariants(max_deg, cost):
+    """graph.task_ranges (CPU torch ops): tasks cover exactly the rows of degree <= max_deg,
+    in order, without overlap; each holds <= 63 consecutive rows of one run and at most
+    cost + max_deg + 1 (edges + rows)."""
+    import numpy as np
+    import torch
+    from graphneuralnetwork_amd.graph import TASK_ROWS, task_ranges
+    rng = np.random.default_rng(max_deg + cost)
+    deg = rng.zipf(1.7, 20000).clip(0, 5000) - 1
+    deg[rng.random(deg.size) < 0.15] = 0
+    deg[5000:5200] = 0
+    rowptr = torch.from_numpy(np.concatenate([[0], np.cumsum(deg)]).astype(np.int64))
+    t = task_ranges(rowptr, max_deg, cost).numpy().reshape(-1, 2)
+    covered = np.zeros(deg.size, bool)
+    prev_end = 0
+    for b, e in t:
+        assert prev_end <= b < e <= deg.size and e - b <= TASK_ROWS
+        assert not covered[b:e].any()
+        covered[b:e] = True
+        assert (deg[b:e] <= max_deg).all()
+        assert int((deg[b:e] + 1).sum()) <= cost + max_deg + 1
+        prev_end = e
+    np.testing.assert_array_equal(covered, deg <= max_deg)
+    assert task_ranges(torch.zeros(1, dtype=torch.int64), max_deg, cost).numel() == 0

@@ -29,6 +29,9 @@ sys.path.insert(0, str(ROOT))
 # 512 workgroups 0.300 ms at 1M x 128 x 128, 256: 0.333, 768: 0.316, 1024: 0.30x.
 VARIANTS = {
     "base": [],
+    "tu2": ["GNN_SPMM_TASK_U=2"],
+    "tu8": ["GNN_SPMM_TASK_U=8"],
+    "tu16": ["GNN_SPMM_TASK_U=16"],
     "tf256": ["GNN_TF_GRID=256"],
     "tf768": ["GNN_TF_GRID=768"],
     "tf1024": ["GNN_TF_GRID=1024"],
