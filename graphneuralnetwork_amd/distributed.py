@@ -108,11 +108,66 @@ class EdgeCutPartition:
         return self.interior.nnz + self.halo.nnz
 
 
+class LocalGroup:
+    """``world`` ranks as threads of ONE process (one device): this module's collectives
+    (all-to-all-v, the count all-reduce, the float all-gather) become copies between the
+    ranks' tensors. It runs the whole N-rank path -- partition builders, handshakes and
+    exchanges -- at full size on one GPU without N processes time-slicing it (tests,
+    tools/rank_sim.py). Each thread calls ``bind(rank)`` first; every collective is entered
+    by all ranks, in the same order, as with torch.distributed."""
+
+    def __init__(self, world: int):
+        import threading
+        self.world = world
+        self._bar = threading.Barrier(world)
+        self._box: list = [None] * world
+        self._tls = threading.local()
+
+    def bind(self, rank: int) -> None:
+        self._tls.rank = rank
+
+    @property
+    def rank(self) -> int:
+        return self._tls.rank
+
+    @staticmethod
+    def _drain(t: torch.Tensor) -> None:
+        if t.is_cuda:  # this rank's queued work on the tensor is done (the exchange stream's)
+            torch.cuda.current_stream(t.device).synchronize()
+
+    def all_to_all_v(self, out, inp, out_splits, in_splits) -> None:
+        r = self.rank
+        self._drain(inp)
+        offs = [0]
+        for v in in_splits:
+            offs.append(offs[-1] + int(v))
+        self._box[r] = [inp[offs[k]:offs[k + 1]] for k in range(self.world)]
+        self._bar.wait()
+        parts = [self._box[k][r] for k in range(self.world)]
+        if sum(int(v) for v in out_splits) != sum(int(p.shape[0]) for p in parts):
+            raise RuntimeError("LocalGroup.all_to_all_v: split sizes do not match the peers'")
+        if out.numel():
+            torch.cat([p.to(out.device) for p in parts], out=out)
+        self._drain(out)  # the copies are done before any sender reuses its buffer
+        self._bar.wait()
+
+    def all_gather(self, v: list) -> list:
+        r = self.rank
+        self._box[r] = list(v)
+        self._bar.wait()
+        res = [list(self._box[k]) for k in range(self.world)]
+        self._bar.wait()
+        return res
+
+
 def _all_to_all_v(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None):
     """All-to-all-v (RCCL ncclAllToAllv under the nccl backend).
 
     Device tensors under a gloo group (multi-rank rehearsal on one GPU) are
     staged through host memory; the RCCL path never is."""
+    if isinstance(group, LocalGroup):
+        group.all_to_all_v(out, inp, out_splits, in_splits)
+        return
     if inp.is_cuda and dist.get_backend(group) == "gloo":
         o = out.cpu()
         dist.all_to_all_single(o, inp.cpu(), output_split_sizes=list(out_splits),
@@ -233,6 +288,8 @@ def _exclusive_cumsum(t: torch.Tensor) -> torch.Tensor:
 
 
 def _global_sum(v: int, device, group=None) -> int:
+    if isinstance(group, LocalGroup):
+        return int(sum(x[0] for x in group.all_gather([int(v)])))
     on_dev = torch.device(device).type == "cuda" and dist.get_backend(group) != "gloo"
     t = torch.tensor([v], dtype=torch.int64, device=device if on_dev else "cpu")
     dist.all_reduce(t, group=group)
@@ -334,6 +391,8 @@ def build_cover_exchange(g: CsrGraph, rank: int, world: int, group=None,
 
 def _all_gather_floats(v: list, world: int, device, group=None) -> torch.Tensor:
     """[world, len(v)] float64: every rank's ``v`` (an all-to-all-v of the same row)."""
+    if isinstance(group, LocalGroup):
+        return torch.tensor(group.all_gather([float(x) for x in v]), dtype=torch.float64)
     on_dev = torch.device(device).type == "cuda" and dist.get_backend(group) != "gloo"
     dev = device if on_dev else "cpu"
     inp = torch.tensor(v, dtype=torch.float64, device=dev).repeat(world)

@@ -308,3 +308,43 @@ def test_sage_seed_shards_and_gather(world, n_seeds):
         np.testing.assert_array_equal(got[:, 2], owner)
         np.testing.assert_array_equal(got1[:, 0], seeds * 10)
     assert len({rank_sample_seed(0, r) for r in range(8)}) == 8
+
+
+@pytest.mark.parametrize("world,kind", [(3, "cover"), (4, "balanced"), (2, "gather")])
+def test_local_group_matches_single_device(world, kind):
+    """distributed.LocalGroup (the N ranks as threads of one process, collectives as
+    in-memory copies) runs the same builders and EdgeCutSpmm exchange as gloo: the row
+    blocks concatenate to the single-device A X + b."""
+    import threading
+    from graphneuralnetwork_amd import distributed as D
+    n, F = 2500, 8
+    g = _graph(n, 5)
+    comm = D.LocalGroup(world)
+    X = torch.from_numpy(np.random.default_rng(1).standard_normal((n, F)).astype(np.float32))
+    b = torch.arange(F, dtype=torch.float32) / F
+    outs, errs = [None] * world, []
+
+    def rank_main(r):
+        try:
+            comm.bind(r)
+            if kind == "cover":
+                part = D.build_cover_exchange(g, r, world, group=comm)
+            elif kind == "balanced":
+                part, _ = D.build_cover_exchange_balanced(g, r, world, group=comm)
+            else:
+                part = D.build_partition(g, r, world, group=comm)
+            r0, r1 = part.bounds[r], part.bounds[r + 1]
+            run = D.EdgeCutSpmm(part, F, "cpu", group=comm, spmm=_cpu_spmm, gather=_cpu_gather)
+            outs[r] = (r0, run(X[r0:r1].contiguous(), b).clone())
+        except Exception as e:  # noqa: BLE001 -- re-raised in the main thread
+            errs.append(e)
+            comm._bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    if errs:
+        raise errs[0]
+    y = torch.cat([o[1] for o in sorted(outs, key=lambda o: o[0])]).numpy()
+    ref = O.spmm_csr(g.rowptr.numpy(), g.col.numpy(), g.val.numpy(), X.numpy(), b.numpy())
+    np.testing.assert_allclose(y, ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())

@@ -212,3 +212,119 @@ def test_sage_sharded_forward_matches_per_shard_runs(dev):
     for _, emb, logits in res:
         np.testing.assert_array_equal(emb, emb_ref)
         np.testing.assert_array_equal(logits, log_ref)
+
+
+def _run_ranks(world, fn):
+    """fn(rank) on `world` threads of this process (distributed.LocalGroup ranks)."""
+    import threading
+    errs = []
+
+    def main(r):
+        try:
+            fn(r)
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            errs.append(e)
+            _run_ranks.comm._bar.abort()
+
+    th = [threading.Thread(target=main, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    if errs:
+        raise errs[0]
+
+
+@pytest.mark.timeout(900)
+def test_cfg5_eight_ranks_full_size():
+    """BASELINE configs[4] rehearsed on one GPU: the 8 cover-exchange partitions of the full
+    10M / 207M-entry graph (build_cover_exchange_balanced, three builds with the cost re-cut,
+    what bench.py --gpus 8 --workload cfg5 runs on every rank), each rank's EdgeCutSpmm at
+    F = 256 with the RCCL all-to-all-v replaced by device copies between the ranks' buffers
+    (distributed.LocalGroup: the 8 ranks are threads of this process). The concatenated
+    output must equal the single-GPU aggregation: row samples (every hub row included)
+    against the single-GPU kernel and the C oracle, plus the all-row checksum
+    1^T (A X + 1 b^T) v = (1^T A)(X v) + n (b . v). Per-rank setup times are printed."""
+    import time
+    from graphneuralnetwork_amd import distributed as D
+    from graphneuralnetwork_amd.ops import spmm_forward
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    from oracle import c_oracle
+    dev = torch.device("cuda:0")
+    W, F, n = 8, 256, 10_000_000
+    t0 = time.perf_counter()
+    s, d = rmat_edges(n, 100_000_000, 0)
+    t_edges = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n)
+    torch.cuda.synchronize()
+    t_adj = time.perf_counter() - t0
+    del s, d
+    assert g.nnz == 206_948_698
+    comm = D.LocalGroup(W)
+    _run_ranks.comm = comm
+    parts, setup = [None] * W, [dict() for _ in range(W)]
+
+    def build(r):
+        comm.bind(r)
+        t = time.perf_counter()
+        parts[r], hist = D.build_cover_exchange_balanced(
+            g, r, W, group=comm,
+            progress=lambda it, mx, mean, sec: setup[r].__setitem__(f"build{it}_s", round(sec, 2)))
+        torch.cuda.synchronize()
+        setup[r]["cover_total_s"] = round(time.perf_counter() - t, 2)
+        setup[r]["max_mean_cost"] = [round(a / b, 3) for a, b in hist]
+        print(f"  rank {r} partition built in {setup[r]['cover_total_s']}s", flush=True)
+
+    t0 = time.perf_counter()
+    _run_ranks(W, build)
+    t_parts = time.perf_counter() - t0
+    bounds = parts[0].bounds
+    assert all(p.bounds == bounds for p in parts) and bounds[0] == 0 and bounds[-1] == n
+    gen = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(n, F, device=dev, generator=gen)
+    b = torch.randn(F, device=dev, generator=gen)
+    Y = torch.empty(n, F, device=dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(W)]
+
+    def step(r):
+        comm.bind(r)
+        r0, r1 = bounds[r], bounds[r + 1]
+        with torch.cuda.stream(streams[r]):
+            run = D.EdgeCutSpmm(parts[r], F, dev, group=comm)
+            x = X[r0:r1].contiguous()
+            t = time.perf_counter()
+            run(x, b)                     # the first call also builds every sub-SpMM's plans
+            torch.cuda.synchronize()
+            setup[r]["first_step_s"] = round(time.perf_counter() - t, 2)
+            Y[r0:r1].copy_(run(x, b))
+            torch.cuda.synchronize()
+
+    _run_ranks(W, step)
+    print(f"\ncfg5 8-rank rehearsal: rmat edges {t_edges:.1f}s, gcn_adjacency {t_adj:.2f}s, "
+          f"8 x build_cover_exchange_balanced (concurrent threads) {t_parts:.1f}s")
+    for r in range(W):
+        p = parts[r]
+        print(f"  rank {r}: rows {p.n_own} interior {p.interior.nnz} send_p {p.send_p.nnz} "
+              f"halo_x {p.halo_x.nnz} halo_p {p.halo_p.nnz} send {sum(p.send_counts)} recv "
+              f"{p.n_halo} rows; setup {setup[r]}")
+    ref = spmm_forward(g, X, b)
+    rowptr = g.rowptr.cpu().numpy()
+    deg = np.diff(rowptr)
+    rng = np.random.default_rng(4)
+    rows = np.unique(np.concatenate([rng.choice(n, 1500, replace=False), np.argsort(-deg)[:32],
+                                     np.array(bounds[1:-1]) - 1, np.array(bounds[:-1])]))
+    ri = torch.from_numpy(rows).to(dev)
+    got, want = Y[ri].cpu().numpy(), ref[ri].cpu().numpy()
+    scale = float(np.abs(want).max())
+    np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5 * scale)
+    col, val = g.col.cpu().numpy(), g.val.cpu().numpy()
+    Xn = X.cpu().numpy()
+    oracle = np.concatenate([c_oracle.spmm_csr(rowptr, col, val, Xn, b.cpu().numpy(), r, r + 1)
+                             for r in rows[:400]])
+    np.testing.assert_allclose(got[:400], oracle, rtol=1e-4, atol=1e-5 * scale)
+    v = np.random.default_rng(2).standard_normal(F)
+    lhs = float((Y.double() @ torch.from_numpy(v).to(dev)).sum())
+    colsum = np.bincount(col, weights=val.astype(np.float64), minlength=n)
+    xv = Xn.astype(np.float64) @ v
+    rhs = float(colsum @ xv) + n * float(b.cpu().double().numpy() @ v)
+    assert abs(lhs - rhs) <= 1e-4 * float(np.abs(colsum) @ np.abs(xv)), (lhs, rhs)
