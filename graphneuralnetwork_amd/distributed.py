@@ -656,14 +656,26 @@ def extended_graph(part: EdgeCutPartition) -> CsrGraph:
 class EdgeCutGat:
     """One GAT attention layer (all heads) on one rank of the edge-cut.
 
-    The halo rows of Wh AND of the column logits er are packed into one buffer
-    and exchanged with a single all-to-all-v; the fused edge-softmax aggregation
-    then runs over the rank's extended graph [own | halo] (the softmax of a row
-    needs all its edges, so the interior and halo edges are reduced together).
+    The halo rows of Wh AND of the column logits er are packed into one buffer and
+    exchanged with a single all-to-all-v (RCCL on a communication stream). The softmax of
+    a row needs all its edges, so on the HIP path (``overlap``) the row is reduced in two
+    passes whose partial softmaxes merge exactly:
+
+      1. while the exchange is in flight, the interior pass aggregates each row over its
+         OWNED columns (gat_aggregate with per-row log-sum-exp stats L_int, no activation);
+      2. after it, the halo pass aggregates each row over its halo columns (read in place
+         from the received [Wh | er] rows, halo slot s = staged row -1-s) plus ONE
+         pseudo-edge: the row's interior result, whose logit is made to equal L_int
+         (er_pseudo = LeakyReLU^-1(+-L_int) - el_i), so the online softmax weighs it by
+         exp(L_int) = sum of the interior edges' weights -- the log-sum-exp merge that
+         gat_fixup_kernel applies to segments -- and the activation is applied there.
+
+    Otherwise (CPU checkers, rows with no edge at all) the fused aggregation runs once
+    over the rank's extended graph [own | halo] after a blocking exchange.
     """
 
     def __init__(self, part: EdgeCutPartition, heads: int, fh: int, device, group=None,
-                 logits=None, aggregate=None, gather=None):
+                 logits=None, aggregate=None, gather=None, overlap: bool = True):
         self.part = part
         self.heads, self.fh = heads, fh
         self.group = group
@@ -680,25 +692,74 @@ class EdgeCutGat:
                                     device=self.device)
         self.recv_buf = torch.empty((part.n_halo, w), dtype=torch.float32, device=self.device)
         self.ext = extended_graph(part)
-        # the HIP path reads the received [Wh | er] rows in place: the extended graph with
-        # halo slot s as column -1-s of the staged tables (gat_aggregate_staged)
+        self.cuda = self.device.type == "cuda"
+        self.comm_stream = torch.cuda.Stream(self.device) if self.cuda else None
+        from .graph import CsrGraph
+        # the HIP path reads the received [Wh | er] rows in place: halo slot s is column -1-s
+        # of the staged tables (gat_aggregate_staged)
         self._staged = None
-        if hip_aggregate and self.device.type == "cuda" and part.n_halo and \
-                not self.ext.has_empty_rows():
-            from .graph import CsrGraph
+        self._halo_pass = None
+        if hip_aggregate and self.cuda and part.n_halo and not self.ext.has_empty_rows():
             col = self.ext.col.to(torch.int64)
             col = torch.where(col < part.n_own, col, part.n_own - 1 - col).to(torch.int32)
             self._staged = CsrGraph(self.ext.rowptr, col.contiguous(), self.ext.val,
                                     part.n_own, part.n_own)
+            if overlap:
+                self._halo_pass = self._build_halo_pass()
+        if self._halo_pass is not None:
+            F = heads * fh
+            f32 = dict(dtype=torch.float32, device=self.device)
+            self.out_int = torch.empty((part.n_own, F), **f32)
+            self.lse = torch.empty((part.n_own, heads), **f32)
+            self.er_pseudo = torch.empty((part.n_own, heads), **f32)
+
+    def _build_halo_pass(self):
+        """Rows = owned rows; per row a pseudo-edge to column i (the row's interior result,
+        only for rows with interior edges) followed by its halo edges as columns -1-slot."""
+        p = self.part
+        dev = self.device
+        i64 = torch.int64
+        deg_i = p.interior.rowptr[1:] - p.interior.rowptr[:-1]
+        has_int = torch.nonzero(deg_i > 0).view(-1)
+        hrows = torch.repeat_interleave(torch.arange(p.n_own, device=dev, dtype=i64),
+                                        p.halo.rowptr[1:] - p.halo.rowptr[:-1])
+        rows = torch.cat([has_int, hrows])
+        cols = torch.cat([has_int, -1 - p.halo.col.to(i64)])
+        vals = torch.ones(rows.numel(), dtype=torch.float32, device=dev)
+        g = from_coo(rows, cols, vals, p.n_own, p.n_own, check=False)  # stable: pseudo first
+        return None if g.has_empty_rows() else g
 
     def __call__(self, wh_own: torch.Tensor, a_src: torch.Tensor, a_dst: torch.Tensor,
-                 negative_slope: float, mode: int, activation: str | None = None):
+                 negative_slope: float, mode: int, activation: str | None = None,
+                 el: torch.Tensor | None = None, er: torch.Tensor | None = None):
+        """``el`` / ``er``: this rank's logits when already computed (gat_project fuses them
+        into the projection); otherwise they are computed here from ``wh_own``."""
         p = self.part
         F = self.heads * self.fh
-        el, er = self._logits(wh_own, self.heads, self.fh, a_src, a_dst)
+        if el is None or er is None:
+            el, er = self._logits(wh_own, self.heads, self.fh, a_src, a_dst)
         if p.send_idx.numel():  # [Wh | er] rows for the peers, gathered into their columns
             self._gather(wh_own, p.send_idx, self.send_buf[:, :F])
             self._gather(er.contiguous(), p.send_idx, self.send_buf[:, F:])
+        if self._halo_pass is not None and wh_own.stride(1) == 1 and negative_slope > 0:
+            from .ops import GAT_DENSE, gat_aggregate, gat_aggregate_staged
+            cur = torch.cuda.current_stream(self.device)
+            self.comm_stream.wait_stream(cur)
+            with torch.cuda.stream(self.comm_stream):
+                _all_to_all_v(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts,
+                              self.group)
+                ev = torch.cuda.Event()
+                ev.record(self.comm_stream)
+            # interior pass over the owned columns, overlapping the exchange
+            el_c, er_c = el.contiguous(), er.contiguous()
+            gat_aggregate(p.interior, wh_own, el_c, er_c, self.heads, self.fh, negative_slope,
+                          mode, None, out=self.out_int, stats=self.lse)
+            y = self.lse if mode == GAT_DENSE else -self.lse
+            torch.sub(torch.where(y >= 0, y, y / negative_slope), el_c, out=self.er_pseudo)
+            cur.wait_event(ev)
+            return gat_aggregate_staged(self._halo_pass, self.out_int, el_c, self.er_pseudo,
+                                        self.recv_buf[:, :F], self.recv_buf[:, F:], self.heads,
+                                        self.fh, negative_slope, mode, activation)
         _all_to_all_v(self.recv_buf, self.send_buf, p.recv_counts, p.send_counts, self.group)
         if self._staged is not None and wh_own.stride(1) == 1:
             from .ops import gat_aggregate_staged

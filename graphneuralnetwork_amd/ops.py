@@ -437,7 +437,19 @@ def gat_aggregate_staged(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: to
     place instead of concatenated). gnn_gat_csr_hub_f32; rows without edges are rejected
     (their dense-mode fill is a mean over every column, own and staged)."""
     _require_device(g.rowptr, wh, el, er, whh, erh, out)
+    for t, name in ((wh, "Wh"), (el, "el"), (er, "er"), (whh, "whh"), (erh, "erh")):
+        if t.dtype != torch.float32:
+            raise TypeError(f"{name} must be float32 (got {t.dtype})")
     feat = heads * fh
+    # column range, checked once per graph (one host sync, cached): -1-c must name a row of
+    # the staged tables, c a row of Wh -- the hub kernel does not bound-check its reads
+    rng_ = g._plans.get("_col_range")
+    if rng_ is None and g.nnz:
+        rng_ = g._plans["_col_range"] = tuple(int(v) for v in
+                                              torch.stack([g.col.min(), g.col.max()]).tolist())
+    if rng_ is not None and (rng_[0] < -whh.shape[0] or rng_[1] >= g.n_cols):
+        raise IndexError(f"gat_aggregate_staged: column ids span [{rng_[0]}, {rng_[1]}], the "
+                         f"tables hold {whh.shape[0]} staged rows and {g.n_cols} rows")
     if wh.shape != (g.n_cols, feat) or wh.stride(1) != 1:
         raise ValueError("Wh must be [n_cols, heads * fh] with unit column stride")
     if whh.shape[1] != feat or erh.shape != (whh.shape[0], heads) or whh.stride(1) != 1 \

@@ -328,3 +328,108 @@ def test_cfg5_eight_ranks_full_size():
     xv = Xn.astype(np.float64) @ v
     rhs = float(colsum @ xv) + n * float(b.cpu().double().numpy() @ v)
     assert abs(lhs - rhs) <= 1e-4 * float(np.abs(colsum) @ np.abs(xv)), (lhs, rhs)
+
+
+def _gat_graph(n, dev, self_loops):
+    """R-MAT graph with unit values, with or without self-loops (without: rows whose every
+    edge is remote, one-edge rows pointing at a halo slot, long hub rows)."""
+    from graphneuralnetwork_amd.graph import from_coo
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    s, d = rmat_edges(n, 12 * n, 11)
+    s, d = torch.from_numpy(s), torch.from_numpy(d)
+    keep = s != d
+    s, d = s[keep], d[keep]
+    key = torch.unique(torch.cat([s * n + d, d * n + s]))
+    r, c = key // n, key % n
+    if self_loops:
+        r = torch.cat([r, torch.arange(n)])
+        c = torch.cat([c, torch.arange(n)])
+    else:  # every row needs an edge: isolated rows get one to node 0 (a remote hub)
+        deg = torch.bincount(r, minlength=n)
+        iso = torch.nonzero(deg == 0).view(-1)
+        r = torch.cat([r, iso])
+        c = torch.cat([c, torch.zeros_like(iso)])
+    return from_coo(r.to(dev), c.to(dev), torch.ones(r.numel(), device=dev), n, n)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("self_loops,heads,fh", [(True, 8, 8), (False, 8, 8), (False, 1, 64)])
+def test_gat_edge_cut_overlapped_two_pass(dev, world, mode, self_loops, heads, fh):
+    """EdgeCutGat on the HIP path (ranks as LocalGroup threads): the interior pass during the
+    exchange + the halo pass with the interior result as a log-sum-exp pseudo-edge equals
+    the single-GPU layer (dense and sparse semantics, ELU), with and without self-loops
+    (rows without interior edges), and heads=1 x 64 (row stride 65 of the [Wh | er]
+    buffer); and equals the blocking one-pass path."""
+    from graphneuralnetwork_amd import distributed as D
+    from graphneuralnetwork_amd.ops import gat_aggregate, gat_logits
+    n = 6000
+    g = _gat_graph(n, dev, self_loops)
+    gen = torch.Generator().manual_seed(world + mode)
+    F = heads * fh
+    Wh = (torch.randn(n, F, generator=gen) * 0.5).to(dev)
+    a_s = (torch.randn(F, generator=gen) * 0.3).to(dev)
+    a_d = (torch.randn(F, generator=gen) * 0.3).to(dev)
+    el, er = gat_logits(Wh, heads, fh, a_s, a_d)
+    ref = gat_aggregate(g, Wh, el, er, heads, fh, 0.2, mode, "elu").cpu().numpy()
+    comm = D.LocalGroup(world)
+    _run_ranks.comm = comm
+    outs = {}
+
+    def rank_main(r):
+        comm.bind(r)
+        part = D.build_partition(g, r, world, group=comm)
+        r0, r1 = part.bounds[r], part.bounds[r + 1]
+        s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            for overlap in (True, False):
+                layer = D.EdgeCutGat(part, heads, fh, dev, group=comm, overlap=overlap)
+                assert (layer._halo_pass is not None) == overlap
+                y = layer(Wh[r0:r1].contiguous(), a_s, a_d, 0.2, mode, "elu")
+                y2 = layer(Wh[r0:r1].contiguous(), a_s, a_d, 0.2, mode, "elu",
+                           el=el[r0:r1], er=er[r0:r1])
+                torch.cuda.synchronize()
+                outs[(r, overlap)] = (r0, r1, y.cpu().numpy(), y2.cpu().numpy())
+
+    _run_ranks(world, rank_main)
+    for (r, overlap), (r0, r1, y, y2) in outs.items():
+        np.testing.assert_allclose(y, ref[r0:r1], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(y2, y, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("heads,fh", [(8, 8), (1, 64), (2, 5)])
+def test_gat_aggregate_staged_matches_concatenated(dev, mode, heads, fh):
+    """gat_aggregate_staged over [own | staged-view] tables == gat_aggregate over
+    the concatenated tables -- one-edge rows whose only edge is staged, long rows cut into
+    segments, both modes, a (F + heads) % 4 != 0 row stride."""
+    from graphneuralnetwork_amd.graph import CsrGraph, from_coo
+    from graphneuralnetwork_amd.ops import gat_aggregate, gat_aggregate_staged
+    rng = np.random.default_rng(heads * 10 + fh + mode)
+    n, k = 3000, 700
+    F = heads * fh
+    rows = np.concatenate([rng.integers(0, n, 20000), np.arange(200), np.full(2500, 7)])
+    cols = np.concatenate([rng.integers(0, n + k, 20000), n + rng.integers(0, k, 200),
+                           rng.integers(0, n + k, 2500)])
+    present = np.zeros(n, bool)
+    present[rows] = True
+    rows = np.concatenate([rows, np.flatnonzero(~present)])
+    cols = np.concatenate([cols, np.full((~present).sum(), n)])
+    gcat = from_coo(torch.from_numpy(rows).to(dev), torch.from_numpy(cols).to(dev),
+                    torch.ones(rows.size, device=dev), n, n + k)
+    buf = torch.randn(k, F + heads + 1, device=dev)[:, 1:]   # a strided [Wh | er] view
+    wh = torch.randn(n, F, device=dev)
+    er = torch.randn(n, heads, device=dev)
+    el = torch.randn(n, heads, device=dev)
+    whh, erh = buf[:, :F], buf[:, F:]
+    ref = gat_aggregate(gcat, torch.cat([wh, whh]), el, torch.cat([er, erh]), heads, fh, 0.2,
+                        mode, "elu")
+    c = gcat.col.to(torch.int64)
+    gst = CsrGraph(gcat.rowptr, torch.where(c < n, c, n - 1 - c).to(torch.int32).contiguous(),
+                   gcat.val, n, n)
+    got = gat_aggregate_staged(gst, wh, el, er, whh, erh, heads, fh, 0.2, mode, "elu")
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+    with pytest.raises(TypeError):
+        gat_aggregate_staged(gst, wh, el, er, whh.double(), erh, heads, fh, 0.2, mode)
+    with pytest.raises(IndexError):
+        gat_aggregate_staged(gst, wh, el, er, whh[:k - 5], erh[:k - 5], heads, fh, 0.2, mode)
