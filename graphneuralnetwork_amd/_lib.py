@@ -54,6 +54,8 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
         _vp, _i64, _vp, _i64,           # mid_row, n_mid, task_row, n_task
         _vp, _u32, _vp]),               # partial, flags, stream
+    "gnn_sage_gather_concat_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _i64, _i64, _i64,
+                                                   _i64, _i32, _vp, _i64, _vp, _i64, _vp, _vp]),
     "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
     "gnn_hub_plan_workspace_bytes": (_i64, [_i64]),
     "gnn_hub_plan_build": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),

@@ -55,11 +55,16 @@ __device__ __forceinline__ bool beats(float va, int32_t ia, float vb, int32_t ib
   return va > vb || (va == vb && ia < ib);
 }
 
-template <int VW, int LPR, int NCH, int MODE, bool GATHER, int U>
+// SELF (gather form only): the wave also copies table[self_idx[m]] into self_out[m] -- the
+// centre half of the SageLayer's cat[self, agg] (GraphSAGE/GraphSAGE.py:17, 47-48) written by
+// the same launch as the aggregate half, its load in flight with the neighbour loads.
+template <int VW, int LPR, int NCH, int MODE, bool GATHER, int U, bool SELF = false>
 __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
     const float* __restrict__ src, int64_t ld_row, int64_t ld_m, int64_t n_table,
     const int64_t* __restrict__ idx, int64_t ldi, int64_t M, int64_t k, int64_t feat,
-    void* __restrict__ out, int64_t ldo, int32_t* __restrict__ err) {
+    void* __restrict__ out, int64_t ldo, int32_t* __restrict__ err,
+    const int64_t* __restrict__ self_idx = nullptr, float* __restrict__ self_out = nullptr,
+    int64_t ld_self = 0) {
   constexpr int EPI = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t m = static_cast<int64_t>(blockIdx.x) * kSageWaves + (threadIdx.x >> 6);
@@ -69,6 +74,17 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
 
   typename Vec<VW>::T acc[NCH];
   int32_t arg[NCH][VW];
+  typename Vec<VW>::T self_v[NCH];
+  if constexpr (SELF) {  // issued first, stored last: overlaps the neighbour gathers
+    const int64_t rs = self_idx[m];
+    const bool ok = rs >= 0 && rs < n_table;
+    if (!ok && lane == 0) atomicOr(err, 1);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+      self_v[ch] = (ok && grp == 0 && f < feat) ? vload<VW>(src + rs * ld_row + f) : vzero<VW>();
+    }
+  }
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     acc[ch] = (MODE == kMean || MODE == kSum) ? vzero<VW>() : typename Vec<VW>::T(-INFINITY);
@@ -151,6 +167,13 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
     }
   }
   if (lane >= LPR) return;
+  if constexpr (SELF) {
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+      if (f < feat) vstore<VW>(self_out + m * ld_self + f, self_v[ch]);
+    }
+  }
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
     const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
@@ -197,6 +220,9 @@ struct SageArgs {
   int64_t ldo;
   int32_t* err;
   hipStream_t s;
+  const int64_t* self_idx = nullptr;  // gather form: also copy table[self_idx[m]] ...
+  float* self_out = nullptr;          // ... into self_out[m] (one launch for cat[self, agg])
+  int64_t ld_self = 0;
 };
 
 template <int VW, int LPR, int NCH, int MODE, bool GATHER>
@@ -204,9 +230,16 @@ static int launch_sage(const SageArgs& a) {
   constexpr int U = NCH >= 2 ? 2 : GNN_SAGE_U;
   const int64_t blocks = (a.M + kSageWaves - 1) / kSageWaves;
   if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
-  hipLaunchKernelGGL((sage_aggregate_kernel<VW, LPR, NCH, MODE, GATHER, U>),
-                     dim3(static_cast<unsigned>(blocks)), dim3(kSageBlock), GNN_SAGE_LDS_PAD, a.s, a.src, a.ld_row,
-                     a.ld_m, a.n_table, a.idx, a.ldi, a.M, a.k, a.feat, a.out, a.ldo, a.err);
+  if (GATHER && a.self_idx != nullptr)
+    hipLaunchKernelGGL((sage_aggregate_kernel<VW, LPR, NCH, MODE, GATHER, U, GATHER>),
+                       dim3(static_cast<unsigned>(blocks)), dim3(kSageBlock), GNN_SAGE_LDS_PAD, a.s,
+                       a.src, a.ld_row, a.ld_m, a.n_table, a.idx, a.ldi, a.M, a.k, a.feat, a.out,
+                       a.ldo, a.err, a.self_idx, a.self_out, a.ld_self);
+  else
+    hipLaunchKernelGGL((sage_aggregate_kernel<VW, LPR, NCH, MODE, GATHER, U>),
+                       dim3(static_cast<unsigned>(blocks)), dim3(kSageBlock), GNN_SAGE_LDS_PAD, a.s,
+                       a.src, a.ld_row, a.ld_m, a.n_table, a.idx, a.ldi, a.M, a.k, a.feat, a.out,
+                       a.ldo, a.err, nullptr, nullptr, 0);
   return launch_status();
 }
 
@@ -237,9 +270,11 @@ static int run_sage(SageArgs a, int32_t mode, bool vec4) {
   const int64_t feat = a.feat;
   const float* src0 = a.src;
   void* out0 = a.out;
+  float* self0 = a.self_out;
   for (int64_t c0 = 0; c0 < feat; c0 += blk) {
     a.feat = feat - c0 < blk ? feat - c0 : blk;
     a.src = src0 + c0;
+    if (self0 != nullptr) a.self_out = self0 + c0;
     a.out = mode != kArgmax ? static_cast<void*>(static_cast<float*>(out0) + c0)
                             : static_cast<void*>(static_cast<int64_t*>(out0) + c0);
     int rc;
@@ -308,4 +343,23 @@ extern "C" int gnn_gather_rows_f32(const float* x, int64_t ldx, int64_t n_x, con
     hipLaunchKernelGGL(gather_rows_kernel<1>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
                        x, ldx, n_x, idx, n, feat, out, ldo, err_flag);
   return launch_status();
+}
+
+extern "C" int gnn_sage_gather_concat_f32(const float* table, int64_t ldt, int64_t n_table,
+                                          const int64_t* self_idx, const int64_t* idx, int64_t ldi,
+                                          int64_t M, int64_t k, int64_t feat, int32_t mode,
+                                          float* self_out, int64_t ld_self, float* out, int64_t ldo,
+                                          int32_t* err_flag, void* stream) {
+  if (M < 0 || k < 0 || feat < 0 || n_table < 0 || !(mode == kMean || mode == kSum || mode == kMaxPool))
+    return GNN_E_ARG;
+  if (M == 0 || feat == 0) return GNN_OK;
+  if (!table || !self_idx || !idx || !self_out || !out || !err_flag || ldt < feat ||
+      ldo < feat || ld_self < feat || ldi < k)
+    return GNN_E_ARG;
+  if (k == 0) return GNN_E_UNSUPPORTED;
+  const bool vec4 = feat % 4 == 0 && ldt % 4 == 0 && ldo % 4 == 0 && ld_self % 4 == 0 &&
+                    aligned_to(table, 16) && aligned_to(out, 16) && aligned_to(self_out, 16);
+  SageArgs a{table, ldt, 0, n_table, idx, ldi, M, k, feat, out, ldo, err_flag,
+             static_cast<hipStream_t>(stream), self_idx, self_out, ld_self};
+  return run_sage<true>(a, mode, vec4);
 }

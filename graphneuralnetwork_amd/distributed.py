@@ -510,6 +510,8 @@ class EdgeCutSpmm:
         # (stacked layers of one width) is never the buffer that call writes
         self._outs = [torch.empty((part.n_own, feat), **f32) for _ in range(2)]
         self._turn = 0
+        self._last = None        # the tensor the most recent call wrote
+        self._prof_out = None    # profile()'s own output (it must not use up a turn)
         self.cuda = self.device.type == "cuda"
         self.comm_stream = torch.cuda.Stream(self.device) if self.cuda else None
         self._marks = None  # [(name, event)] while profile() runs
@@ -544,9 +546,13 @@ class EdgeCutSpmm:
             raise RuntimeError("profile() needs the GPU path")
         self._marks = []
         cur = torch.cuda.current_stream(self.device)
+        if self._prof_out is None:
+            self._prof_out = torch.empty_like(self._outs[0])
+        last = self._last
         try:
             self._mark("start", cur)
-            self(x, bias, activation)
+            self(x, bias, activation, out=self._prof_out)
+            self._last = last
             self._mark("end", cur)
             torch.cuda.synchronize(self.device)
         finally:
@@ -569,9 +575,10 @@ class EdgeCutSpmm:
             cur.wait_event(ev)
 
     @property
-    def out(self) -> torch.Tensor:
-        """The buffer the most recent call wrote."""
-        return self._outs[self._turn ^ 1]
+    def out(self) -> torch.Tensor | None:
+        """The tensor the most recent call wrote (an internal buffer or the caller's ``out``;
+        ``profile()`` calls are not counted)."""
+        return self._last
 
     def __call__(self, x: torch.Tensor, bias: torch.Tensor | None = None,
                  activation: str | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -588,6 +595,7 @@ class EdgeCutSpmm:
         if x.numel() and out.numel() and _overlaps(x, out):
             raise ValueError("x and the output buffer overlap: the interior SpMM would read "
                              "rows it is writing")
+        self._last = out
         cur = torch.cuda.current_stream(self.device) if self.cuda else None
         if self.cover:
             ev_x = ev_p = None

@@ -24,8 +24,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import from_coo
-from .ops import (gather_rows, gcn_transform, sage_aggregate, sage_gather_aggregate, sage_layer,
-                  spmm_forward)
+from .ops import (gather_rows, gcn_transform, sage_aggregate, sage_gather_aggregate,
+                  sage_gather_concat, sage_layer, spmm_forward)
 
 # the inference SageLayer GEMM relu([self | agg] @ W^T) runs on the hand-written fp32-MFMA
 # kernel (gnn_linear_relu_f32) up to SAGE_MFMA_MAX_SMALL rows and from SAGE_MFMA_MIN_LARGE
@@ -240,7 +240,9 @@ def _fused_sage_layer(block, center, neigh: Gathered):
     Otherwise the centre rows and the fused gather-mean write the two halves of ONE
     [M, 2F] buffer (the reference's torch.cat, never copied), then a single K=2F GEMM with
     the ReLU in the hipBLASLt epilogue: GraphSAGE.py:18-20 + the gathers of :47-49 as 3
-    launches instead of 7."""
+    launches instead of 7; with the centre rows and the neighbours drawn from the same table
+    (the sampler's Gathered maps) the two halves come from ONE launch
+    (``ops.sage_gather_concat``), then the GEMM: 2 launches."""
     if isinstance(center, Gathered):
         self_src, self_idx, trusted = center.table, center.index, center.trusted
     else:
@@ -252,12 +254,17 @@ def _fused_sage_layer(block, center, neigh: Gathered):
     M, n = neigh.index.shape[0], block.input_size
     dev = neigh.table.device
     buf = torch.empty((M, 2 * n), dtype=torch.float32, device=dev)
-    if isinstance(center, Gathered):
-        gather_rows(center.table, center.index, out=buf[:, :n], check=not center.trusted)
+    if isinstance(center, Gathered) and center.table is neigh.table:
+        # both halves of cat[self, agg] in one launch (gnn_sage_gather_concat_f32)
+        sage_gather_concat(neigh.table, center.index, neigh.index, "MEAN",
+                           check=not (center.trusted and neigh.trusted), out=buf)
     else:
-        buf[:, :n].copy_(center)
-    sage_gather_aggregate(neigh.table, neigh.index, "MEAN", check=not neigh.trusted,
-                          out=buf[:, n:])
+        if isinstance(center, Gathered):
+            gather_rows(center.table, center.index, out=buf[:, :n], check=not center.trusted)
+        else:
+            buf[:, :n].copy_(center)
+        sage_gather_aggregate(neigh.table, neigh.index, "MEAN", check=not neigh.trusted,
+                              out=buf[:, n:])
     W = block.weight.weight
     if _sage_gemm_on_mfma(M):  # relu(buf @ W^T) on the hand-written fp32-MFMA kernel
         y = gcn_transform(buf, W, relu=True)

@@ -672,6 +672,49 @@ def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str 
     return out
 
 
+def sage_gather_concat(table: torch.Tensor, self_idx: torch.Tensor, idx: torch.Tensor,
+                       agg_func: str = "MEAN", check: bool = True,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """[M, 2F] = cat[table[self_idx], Aggregator(table[idx])] in one launch
+    (gnn_sage_gather_concat_f32): the SageLayer input of GraphSAGE/GraphSAGE.py:17 with the
+    gathers of :47-49. ``out`` may be any [M, 2F] float32 view with unit column stride."""
+    if agg_func not in ("MEAN", "SUM", "MAXPOOL"):
+        raise RuntimeError(f"agg_func {agg_func!r} has no concat form")
+    _require_device(table, self_idx, idx, out)
+    table = _rows_f32(table, "table")
+    if idx.dim() != 2:
+        raise ValueError("idx must be [M, k]")
+    idx = idx.to(torch.int64)
+    if idx.stride(1) != 1:
+        idx = idx.contiguous()
+    self_idx = self_idx.to(torch.int64).contiguous().view(-1)
+    M, k = idx.shape
+    F = table.shape[1]
+    if self_idx.numel() != M:
+        raise ValueError("self_idx must hold one index per output row")
+    if out is None:
+        out = torch.empty((M, 2 * F), dtype=torch.float32, device=table.device)
+    elif out.shape != (M, 2 * F) or out.dtype != torch.float32 or out.stride(1) != 1:
+        raise ValueError(f"out must be a float32 [{M}, {2 * F}] view with unit column stride")
+    if M == 0:
+        return out
+    if k == 0:
+        _empty_reduction(SAGE_KINDS[agg_func])
+        out[:, :F].copy_(gather_rows(table, self_idx, check=check))
+        out[:, F:].fill_(_EMPTY_FILL[SAGE_KINDS[agg_func]])
+        return out
+    err = _err_flag(table.device, check)
+    lib = _lib.load()
+    _lib.check(lib.gnn_sage_gather_concat_f32(
+        table.data_ptr(), table.stride(0), table.shape[0], self_idx.data_ptr(), idx.data_ptr(),
+        idx.stride(0), M, k, F, SAGE_KINDS[agg_func], out.data_ptr(), out.stride(0),
+        out[:, F:].data_ptr(), out.stride(0), err.data_ptr(), _lib.stream_handle(table.device)),
+        "gnn_sage_gather_concat_f32")
+    if check:
+        _check_err(err, "sage_gather_concat")
+    return out
+
+
 # The fused layer is opt-in (set SAGE_FUSED_MIN_ROWS to the smallest frontier to fuse): at
 # cfg4 it gains 2-3 % on layer 0 (62,479 rows: 110 vs 112 us) and loses on the 8,192-row
 # layer 1 (33 vs 25 us) -- its gathers and MFMAs do not overlap, so it costs about their

@@ -358,6 +358,20 @@ int gnn_sage_gather_aggregate_f32(const float* table, int64_t ldt, int64_t n_tab
                                   int32_t* err_flag, void* stream);
 
 /*
+ * Both halves of the SageLayer input cat[self, agg] in ONE launch (GraphSAGE/GraphSAGE.py:17
+ * with the torch.embedding gathers of :47-49 and Aggregator, graph_utils.py:6):
+ *   self_out[m, :] = table[self_idx[m], :]
+ *   out[m, :]      = reduce_j table[idx[m * ldi + j], :]   (mode GNN_SAGE_MEAN / SUM / MAXPOOL)
+ * self_out and out may be the two column halves of one [M, 2F] buffer. An index outside
+ * [0, n_table) sets *err_flag |= 1 and reads nothing. k == 0 -> GNN_E_UNSUPPORTED.
+ */
+int gnn_sage_gather_concat_f32(const float* table, int64_t ldt, int64_t n_table,
+                               const int64_t* self_idx, const int64_t* idx, int64_t ldi,
+                               int64_t M, int64_t k, int64_t feat, int32_t mode, float* self_out,
+                               int64_t ld_self, float* out, int64_t ldo, int32_t* err_flag,
+                               void* stream);
+
+/*
  * One fused GraphSAGE inference layer (MEAN, not gcn):
  *   out[m] = relu(W . cat[self[m], mean_j table[nbr_idx[m, j]]])
  * Replaces SageLayer.forward(self, Aggregator(neigh, 'MEAN')) -- GraphSAGE/GraphSAGE.py:15-20,

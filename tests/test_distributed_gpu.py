@@ -433,3 +433,67 @@ def test_gat_aggregate_staged_matches_concatenated(dev, mode, heads, fh):
         gat_aggregate_staged(gst, wh, el, er, whh.double(), erh, heads, fh, 0.2, mode)
     with pytest.raises(IndexError):
         gat_aggregate_staged(gst, wh, el, er, whh[:k - 5], erh[:k - 5], heads, fh, 0.2, mode)
+
+
+@pytest.mark.parametrize("unsup", [False, True])
+def test_sage_sharded_empty_shard(dev, unsup):
+    """fewer seeds than ranks -- the empty shard still joins the gather with
+    placeholders of the right widths (supervised and unsupervised nets), and the gathered
+    result equals the single-process forward of the one non-empty shard (LocalGroup ranks)."""
+    from graphneuralnetwork_amd import distributed as D
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    net, adj, table, seeds = _sage_setup(dev)
+    if unsup:
+        torch.manual_seed(4)
+        net = GraphSAGE(2, table.shape[1], table.shape[1], False, agg_func="MEAN",
+                        Unsupervised=True).to(dev).eval()
+    one = seeds[:1]
+    world = 2
+    comm = D.LocalGroup(world)
+    _run_ranks.comm = comm
+    res = {}
+
+    def rank_main(r):
+        comm.bind(r)
+        with torch.no_grad():
+            res[r] = D.sage_forward_sharded(net, adj, table, one, r, world, seed=7, group=comm,
+                                            gather=True)
+
+    _run_ranks(world, rank_main)
+    owner = [r for r in range(world) if D.shard_seeds(one, r, world).numel()][0]
+    from graphneuralnetwork_amd.sampler import sample_batch
+    with torch.no_grad():
+        b = sample_batch(adj, one, (25, 10), seed=D.rank_sample_seed(7, owner))
+        emb, logits = net(*b.forward_args(table), None, None, None, None, None)
+    for r in range(world):
+        e, lg = res[r]
+        assert e.shape == (1, emb.shape[1])
+        torch.testing.assert_close(e, emb)
+        if unsup:
+            assert lg is None
+        else:
+            assert lg.shape == (1, net.dense.out_features)
+            torch.testing.assert_close(lg, logits)
+
+
+def test_edge_cut_out_property_and_profile(dev):
+    """EdgeCutSpmm.out is the tensor the last call wrote (also a caller's ``out``),
+    and profile() neither changes it nor uses up a turn of the internal double buffer."""
+    from graphneuralnetwork_amd import distributed as D
+    n, F = 3000, 32
+    g = _graph(n, dev)
+    comm = D.LocalGroup(1)
+    comm.bind(0)
+    part = D.build_cover_exchange(g, 0, 1, group=comm)
+    run = D.EdgeCutSpmm(part, F, dev, group=comm)
+    x = torch.randn(n, F, device=dev)
+    y1 = run(x)
+    assert run.out is y1
+    mine = torch.empty(n, F, device=dev)
+    y2 = run(x, out=mine)
+    assert y2 is mine and run.out is mine
+    run.profile(x)
+    assert run.out is mine
+    y3 = run(x)
+    assert y3 is not y1 and y3.data_ptr() != y1.data_ptr()  # the other internal buffer
+    torch.testing.assert_close(y3, y1)
