@@ -22,15 +22,22 @@ extern "C" int gnn_gcn_transform_supported(int64_t k, int64_t fout);
 namespace gnn {
 
 constexpr int kTfWaves = 4;
-constexpr int kTfRows = 64;  // rows per tile (4 MFMA row blocks)
 using tf32x4 = __attribute__((ext_vector_type(4))) float;
 
-// NW waves per workgroup, each owning CB 16-column blocks of W (FO = NW * CB * 16).
+#ifndef GNN_TF_SINGLE_BUFFER
+#define GNN_TF_SINGLE_BUFFER 0  // A/B: the round-2 one-buffer tile loop (two barriers per tile)
+#endif
+
+// NW waves per workgroup, each owning CB 16-column blocks of W (FO = NW * CB * 16); a tile is
+// TR rows of X (TR = 16, 32 or 64: small launches use short tiles so that every CU gets work).
 // K = 256 (the SageLayer's cat[self, agg]) runs 8 waves x 1 block: its 64 W values per lane
-// stay resident, the X fragment is read from LDS in chunks of XC k-steps, and the four
-// 16-row blocks of a tile run as four independent MFMA chains (one chain of 64 dependent
-// MFMAs per wave would leave the matrix core waiting on its own results).
-template <int K, int CB, int NW, bool RELU>
+// stay resident, the X fragment is read from LDS in chunks of XC k-steps, and the tile's
+// 16-row blocks run as independent MFMA chains (one chain of 64 dependent MFMAs per wave
+// would leave the matrix core waiting on its own results).
+// Tiles are double-buffered in LDS (TileLds layout: no bank conflicts on the fragment
+// reads): tile g+1 is loaded into registers during tile g's MFMAs and written to the other
+// buffer before tile g's epilogue, so one barrier per tile separates the two.
+template <int K, int CB, int NW, bool RELU, int TR>
 __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* __restrict__ x,
                                                                    int64_t ldx, int64_t n_rows,
                                                                    const float* __restrict__ w,
@@ -39,20 +46,14 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* 
   constexpr int kTfBlock = NW * kWave;
   constexpr int S = K / 4;           // MFMA k-steps
   constexpr int XC = S <= 32 ? S : 16;  // k-steps of X held in registers at a time
-  constexpr int RB = CB == 1 && S > 32 ? 4 : 1;  // 16-row blocks computed together
-  constexpr int FO = NW * CB * 16;
-  constexpr int LDA = K + 4;         // padded LDS row (floats)
-  constexpr int V4 = kTfRows * K / 4;  // float4s per tile
-  constexpr int NV = V4 / kTfBlock;    // per thread
-  static_assert(V4 % kTfBlock == 0, "tile must split evenly over the workgroup");
+  constexpr int RB0 = CB == 1 && S > 32 ? 4 : 1;
+  constexpr int RB = RB0 < TR / 16 ? RB0 : TR / 16;  // 16-row blocks computed together
+  constexpr int LDA = 4 * TileLds<K>::L4;  // LDS row pitch (floats)
+  constexpr int V4 = TR * K / 4;       // float4s per tile
+  constexpr int NV = (V4 + kTfBlock - 1) / kTfBlock;  // per thread
+  constexpr int NBUF = GNN_TF_SINGLE_BUFFER ? 1 : 2;
   static_assert(S % XC == 0 && XC % 4 == 0, "X chunks of whole float4s");
-  __shared__ float xt[kTfRows * LDA];
-#ifdef GNN_TF_STAGE_OUT
-  // the tile's Y rows staged in LDS, then stored as whole contiguous rows (each wave
-  // instruction writes 1 KiB of consecutive bytes instead of 16 rows x 64 B)
-  constexpr int LDO = FO + 4;
-  __shared__ float ot[kTfRows * LDO];
-#endif
+  __shared__ float xt[NBUF][TR * LDA];
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = threadIdx.x >> 6;
   const int q = lane >> 4, r = lane & 15;
@@ -72,47 +73,62 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* 
     }
   }
 
-  const int64_t n_tiles = (n_rows + kTfRows - 1) / kTfRows;
+  const int64_t n_tiles = (n_rows + TR - 1) / TR;
   float4 pre[NV];
   auto fetch = [&](int64_t g) {
-    const int64_t r0 = g * kTfRows;
+    const int64_t r0 = g * TR;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = v * kTfBlock + static_cast<int>(threadIdx.x);
       const int rr = e / (K / 4), c4 = e - rr * (K / 4);
-      pre[v] = (g < n_tiles && r0 + rr < n_rows)
+      pre[v] = (e < V4 && g < n_tiles && r0 + rr < n_rows)
                    ? *reinterpret_cast<const float4*>(x + (r0 + rr) * ldx + 4 * c4)
                    : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  fetch(blockIdx.x);
-  for (int64_t g = blockIdx.x; g < n_tiles; g += gridDim.x) {  // uniform over the block
+  auto stage = [&](float* buf) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = v * kTfBlock + static_cast<int>(threadIdx.x);
-      const int rr = e / (K / 4), c4 = e - rr * (K / 4);
-      *reinterpret_cast<float4*>(xt + rr * LDA + 4 * c4) = pre[v];
+      if (e < V4) {
+        const int rr = e / (K / 4), c4 = e - rr * (K / 4);
+        *reinterpret_cast<float4*>(buf + rr * LDA + 4 * (c4 ^ TileLds<K>::swz(rr))) = pre[v];
+      }
     }
+  };
+  fetch(blockIdx.x);
+  if (NBUF == 2) {
+    stage(xt[0]);
     __syncthreads();
-    fetch(g + gridDim.x);
-    const int64_t row0 = g * kTfRows;
+  }
+  int it = 0;
+  for (int64_t g = blockIdx.x; g < n_tiles; g += gridDim.x, ++it) {  // uniform over the block
+    const float* cur = xt[NBUF == 2 ? (it & 1) : 0];
+    if (NBUF == 1) {
+      stage(xt[0]);
+      __syncthreads();
+    }
+    fetch(g + gridDim.x);  // the next tile, in flight during this tile's MFMAs
+    const int64_t row0 = g * TR;
+    tf32x4 acc[TR / 16][CB];
 #pragma unroll
-    for (int rb0 = 0; rb0 < kTfRows / 16; rb0 += RB) {
-      // RB row blocks at once: RB * CB independent accumulation chains per wave
-      tf32x4 acc[RB][CB];
+    for (int rb0 = 0; rb0 < TR / 16; rb0 += RB) {
 #pragma unroll
       for (int j = 0; j < RB; ++j)
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb) acc[j][cb] = tf32x4{0.f, 0.f, 0.f, 0.f};
+        for (int cb = 0; cb < CB; ++cb) acc[rb0 + j][cb] = tf32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int c0 = 0; c0 < S; c0 += XC) {
         float xb[RB][XC];
 #pragma unroll
         for (int j = 0; j < RB; ++j) {
-          const float* xr = xt + ((rb0 + j) * 16 + r) * LDA + q * S + c0;
+          const int rr = (rb0 + j) * 16 + r;
+          const float* xr = cur + rr * LDA;
 #pragma unroll
           for (int v = 0; v < XC / 4; ++v) {
-            const float4 t = *reinterpret_cast<const float4*>(xr + 4 * v);
+            const int c4 = (q * S + c0) / 4 + v;
+            const float4 t =
+                *reinterpret_cast<const float4*>(xr + 4 * (c4 ^ TileLds<K>::swz(rr)));
             xb[j][4 * v] = t.x;
             xb[j][4 * v + 1] = t.y;
             xb[j][4 * v + 2] = t.z;
@@ -125,68 +141,64 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* 
           for (int j = 0; j < RB; ++j)
 #pragma unroll
             for (int cb = 0; cb < CB; ++cb)
-              acc[j][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[cb][c0 + s], xb[j][s],
-                                                                acc[j][cb], 0, 0, 0);
+              acc[rb0 + j][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[cb][c0 + s], xb[j][s],
+                                                                      acc[rb0 + j][cb], 0, 0, 0);
         }
       }
+    }
+    // the next tile goes to the other buffer while the last MFMAs drain (nobody reads it:
+    // the barrier that ended the previous tile saw every wave's reads of it complete)
+    if (NBUF == 2) stage(xt[(it + 1) & 1]);
 #pragma unroll
-      for (int j = 0; j < RB; ++j) {
-        // acc[j][cb][i] = Y[row0 + 16 (rb0 + j) + r][(wv*CB + cb)*16 + 4q + i]
-        const int64_t orow = row0 + (rb0 + j) * 16 + r;
-#ifndef GNN_TF_STAGE_OUT
-        if (orow < n_rows) {
-#else
-        (void)orow;
-#endif
+    for (int j = 0; j < TR / 16; ++j) {
+      // acc[j][cb][i] = Y[row0 + 16 j + r][(wv*CB + cb)*16 + 4q + i]
+      const int64_t orow = row0 + j * 16 + r;
+      if (orow < n_rows) {
 #pragma unroll
-          for (int cb = 0; cb < CB; ++cb) {
-            float4 o = make_float4(acc[j][cb][0], acc[j][cb][1], acc[j][cb][2], acc[j][cb][3]);
-            if constexpr (RELU) {
-              o.x = fmaxf(o.x, 0.f);
-              o.y = fmaxf(o.y, 0.f);
-              o.z = fmaxf(o.z, 0.f);
-              o.w = fmaxf(o.w, 0.f);
-            }
-#ifdef GNN_TF_STAGE_OUT
-            *reinterpret_cast<float4*>(ot + ((rb0 + j) * 16 + r) * LDO + (wv * CB + cb) * 16 +
-                                       4 * q) = o;
-#else
-            *reinterpret_cast<float4*>(y + orow * ldy + (wv * CB + cb) * 16 + 4 * q) = o;
-#endif
+        for (int cb = 0; cb < CB; ++cb) {
+          float4 o = make_float4(acc[j][cb][0], acc[j][cb][1], acc[j][cb][2], acc[j][cb][3]);
+          if constexpr (RELU) {
+            o.x = fmaxf(o.x, 0.f);
+            o.y = fmaxf(o.y, 0.f);
+            o.z = fmaxf(o.z, 0.f);
+            o.w = fmaxf(o.w, 0.f);
           }
-#ifndef GNN_TF_STAGE_OUT
+          *reinterpret_cast<float4*>(y + orow * ldy + (wv * CB + cb) * 16 + 4 * q) = o;
         }
-#endif
       }
     }
-#ifdef GNN_TF_STAGE_OUT
-    __syncthreads();  // the whole Y tile is in LDS
-    constexpr int O4 = kTfRows * FO / 4;
-#pragma unroll
-    for (int e = static_cast<int>(threadIdx.x); e < O4; e += kTfBlock) {
-      const int rr = e / (FO / 4), c4 = e - rr * (FO / 4);
-      if (row0 + rr < n_rows)
-        *reinterpret_cast<float4*>(y + (row0 + rr) * ldy + 4 * c4) =
-            *reinterpret_cast<const float4*>(ot + rr * LDO + 4 * c4);
-    }
-#endif
-    __syncthreads();  // the next tile overwrites xt (and ot)
+    __syncthreads();  // one barrier per tile: the staged next tile is complete, this one free
   }
-  (void)FO;
 }
 
-template <int K, int CB, int NW, bool RELU>
-static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const float* w,
-                            float* y, int64_t ldy, hipStream_t s) {
-  const int64_t tiles = (n_rows + kTfRows - 1) / kTfRows;
+template <int K, int CB, int NW, bool RELU, int TR>
+static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, const float* w,
+                               float* y, int64_t ldy, hipStream_t s) {
+  const int64_t tiles = (n_rows + TR - 1) / TR;
 #ifndef GNN_TF_GRID
 #define GNN_TF_GRID 512  // persistent grid: 2 workgroups per CU
 #endif
   constexpr int64_t kGrid = GNN_TF_GRID * kTfWaves / NW;  // 8-wave workgroups: 1 per CU
   const int64_t grid = tiles < kGrid ? tiles : kGrid;
-  hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU>), dim3(static_cast<unsigned>(grid)),
+  hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR>), dim3(static_cast<unsigned>(grid)),
                      dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy);
   return launch_status();
+}
+
+#ifndef GNN_TF_MIN_TR
+#define GNN_TF_MIN_TR 16  // A/B: 64 = always the round-2 64-row tiles
+#endif
+// Tile rows: 64 unless that leaves CUs without a tile (< 2 tiles per resident workgroup
+// slot), then 32 or 16 -- the fixed cost of a small launch is its first tile.
+template <int K, int CB, int NW, bool RELU>
+static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const float* w,
+                            float* y, int64_t ldy, hipStream_t s) {
+  constexpr int64_t slots = GNN_TF_GRID * kTfWaves / NW;
+  if (GNN_TF_MIN_TR <= 16 && n_rows < 32 * 2 * slots)
+    return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, s);
+  if (GNN_TF_MIN_TR <= 32 && n_rows < 64 * 2 * slots)
+    return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, s);
+  return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, s);
 }
 
 template <int K, bool RELU>
@@ -199,8 +211,17 @@ static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t
     else
       return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, s);
   }
-  if constexpr (K <= 64)
-    if (fout == 256) return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, s);
+  if (fout == 256) {
+    if constexpr (K <= 64) {
+      return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, s);
+    } else {
+      // two launches of the 128-column kernel, one per half of W's rows (output columns);
+      // X is read twice, but the launch is MFMA-bound at these K (cfg5's 256 -> 256 layer)
+      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, s);
+      if (rc != GNN_OK) return rc;
+      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, s);
+    }
+  }
   return GNN_E_UNSUPPORTED;
 }
 
@@ -231,9 +252,7 @@ using namespace gnn;
 extern "C" int gnn_gcn_transform_supported(int64_t k, int64_t fout) {
   const bool kk = k == 16 || k == 32 || k == 64 || k == 128 || k == 256;
   if (!kk) return 0;
-  if (fout == 64 || fout == 128) return 1;
-  if (fout == 256) return k <= 64;
-  return 0;
+  return fout == 64 || fout == 128 || fout == 256;
 }
 
 extern "C" int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,

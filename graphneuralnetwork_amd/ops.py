@@ -319,6 +319,12 @@ def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: to
     return wh, el, er
 
 
+# fout = 256 at k > 64 runs as two 128-column launches (X read twice); hipBLASLt is faster there
+# (10M x 256 -> 256: 10.4 vs 11.5 ms, tools/sage_gemm_ab.py --big, profiles/r03f_gemm_ab.log),
+# so those shapes stay on nn.Linear unless this is set
+TRANSFORM_WIDE_MFMA = False
+
+
 def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
                   out: torch.Tensor | None = None) -> torch.Tensor | None:
     """support = x @ weight^T on fp32 MFMA (gnn_gcn_transform_f32), the dense half of
@@ -333,6 +339,8 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
     lib = _lib.load()
     fout, k = weight.shape
     if not lib.gnn_gcn_transform_supported(k, fout):
+        return None
+    if fout == 256 and k > 64 and not TRANSFORM_WIDE_MFMA:
         return None
     if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
         x = x.contiguous()

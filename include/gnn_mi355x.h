@@ -176,7 +176,7 @@ int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t hea
  * nn.Linear weight [fout, k] (row-major), fp32 in / fp32 accumulate
  * (v_mfma_f32_16x16x4_f32). Replaces `support = self.dense(X_input)` at GCN/GCN.py:42
  * (inference path). Shapes covered: gnn_gcn_transform_supported(k, fout) != 0
- * (k in {16, 32, 64, 128, 256}; fout 64 or 128, or 256 with k <= 64);
+ * (k in {16, 32, 64, 128, 256}; fout 64, 128 or 256 -- 256 with k > 64 as two launches);
  * other shapes return GNN_E_UNSUPPORTED (the caller uses a library GEMM). x, w, y
  * 16-B aligned, ldx and ldy multiples of 4 (else GNN_E_ALIGN).
  */

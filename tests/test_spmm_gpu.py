@@ -491,3 +491,20 @@ def test_packed_tasks_c_abi_contract(dev):
         assert rc == want, (F, off, flags, rc)
         if rc == 0:
             torch.testing.assert_close(y, X)
+
+
+@pytest.mark.parametrize("k", [128, 256])
+def test_gcn_transform_wide_output_c_abi(dev, k):
+    """gnn_gcn_transform_f32 at fout = 256 with k > 64 (two 128-column launches; the Python
+    policy keeps nn.Linear there, TRANSFORM_WIDE_MFMA): against a float64 product."""
+    from graphneuralnetwork_amd import _lib
+    n = 3000
+    x = torch.randn(n, k, device=dev)
+    w = torch.randn(256, k, device=dev) / k ** 0.5
+    y = torch.empty(n, 256, device=dev)
+    lib = _lib.load()
+    assert lib.gnn_gcn_transform_supported(k, 256)
+    assert lib.gnn_gcn_transform_f32(x.data_ptr(), k, n, k, w.data_ptr(), 256, y.data_ptr(), 256,
+                                     torch.cuda.current_stream().cuda_stream) == 0
+    ref = (x.double() @ w.double().T).float()
+    close(y.cpu().numpy(), ref.cpu().numpy())

@@ -12,8 +12,8 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 VARIANTS = {"base": [], "d1": ["GNN_PROJ_DEPTH=1"], "d3": ["GNN_PROJ_DEPTH=3"],
             "d4": ["GNN_PROJ_DEPTH=4"], "d2g1024": ["GNN_PROJ_GRID=1024"],
-            "d3g1024": ["GNN_PROJ_DEPTH=3", "GNN_PROJ_GRID=1024"], "oldlds": ["GNN_PROJ_OLD_LDS", "GNN_PROJ_BLOCK_SYNC=1"],
-            "blocksync": ["GNN_PROJ_BLOCK_SYNC=1"], "oldlds_wave": ["GNN_PROJ_OLD_LDS"], "blds": ["GNN_PROJ_B_LDS"], "nowh": ["GNN_PROJ_NO_WH"],
+            "d3g1024": ["GNN_PROJ_DEPTH=3", "GNN_PROJ_GRID=1024"], "oldlds": ["GNN_TILE_OLD_LDS", "GNN_PROJ_BLOCK_SYNC=1"],
+            "blocksync": ["GNN_PROJ_BLOCK_SYNC=1"], "oldlds_wave": ["GNN_TILE_OLD_LDS"], "blds": ["GNN_PROJ_B_LDS"], "nowh": ["GNN_PROJ_NO_WH"],
             "g256": ["GNN_PROJ_GRID=256"], "g512": ["GNN_PROJ_GRID=512"],
             "g1024": ["GNN_PROJ_GRID=1024"], "g4096": ["GNN_PROJ_GRID=4096"],
             "g8192": ["GNN_PROJ_GRID=8192"], "blds_g4096": ["GNN_PROJ_B_LDS", "GNN_PROJ_GRID=4096"],

@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", default="8192,32768,62479,200000")
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--big", action="store_true", help="also 10M x 128 -> 128 and 10M x 256 -> 256")
     args = ap.parse_args()
     from graphneuralnetwork_amd import _lib
     from graphneuralnetwork_amd.ops import gcn_transform
@@ -27,6 +28,8 @@ def main():
     dev = torch.device("cuda:0")
     shapes = [(m, 256, 128, True) for m in (int(v) for v in args.rows.split(","))]
     shapes += [(1_000_000, 128, 128, False), (1_000_000, 256, 128, False)]
+    if args.big:
+        shapes += [(10_000_000, 128, 128, False), (10_000_000, 256, 256, False)]
     for M, K, N, relu in shapes:
         x = torch.randn(M, K, device=dev)
         W = torch.randn(N, K, device=dev) / K ** 0.5

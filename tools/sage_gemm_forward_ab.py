@@ -38,6 +38,7 @@ def main():
     fargs = batch.forward_args(table)
     default = GS._sage_gemm_on_mfma
     policies = {"hipblaslt": lambda rows: False, "mfma all": lambda rows: True,
+                "mfma small": lambda rows: rows <= 16384 or rows >= 131072,
                 "default": default}
     outs, graphs = {}, {}
     with torch.no_grad():
