@@ -56,6 +56,8 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _u32, _vp]),               # partial, flags, stream
     "gnn_sage_gather_concat_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _i64, _i64, _i64,
                                                    _i64, _i32, _vp, _i64, _vp, _i64, _vp, _vp]),
+    "gnn_halo_alltoallv_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp]),
+    "gnn_halo_rccl_path": (ctypes.c_int, [ctypes.c_char_p, _i64]),
     "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
     "gnn_hub_plan_workspace_bytes": (_i64, [_i64]),
     "gnn_hub_plan_build": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),

@@ -63,7 +63,7 @@ EXPORT_MAP = CSRC_DIR / "exports.map"
 
 def _link_cmd(hipcc: str, out: Path, objs) -> list[str]:
     return [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread",
-            f"-Wl,--version-script={EXPORT_MAP}", "-o", str(out), *map(str, objs)]
+            f"-Wl,--version-script={EXPORT_MAP}", "-o", str(out), *map(str, objs), "-ldl"]
 
 
 def _stale(target: Path, deps: list[Path]) -> bool:

@@ -219,6 +219,7 @@ extern "C" const char* gnn_error_string(int code) {
     case GNN_E_EMPTY: return "Cannot choose from an empty sequence";
     case GNN_E_RAGGED: return "gnn: index maps of unequal length (ragged nested sequence)";
     case GNN_E_NOMEM: return "gnn: host allocation failed";
+    case GNN_E_COMM: return "gnn: RCCL not found in the process, or its call failed";
     default: break;
   }
   if (code > 0) return hipGetErrorString(static_cast<hipError_t>(code));

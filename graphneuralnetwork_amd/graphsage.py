@@ -30,11 +30,11 @@ from .ops import (gather_rows, gcn_transform, sage_aggregate, sage_gather_aggreg
 # the inference SageLayer GEMM relu([self | agg] @ W^T) runs on the hand-written fp32-MFMA
 # kernel (gnn_linear_relu_f32) up to SAGE_MFMA_MAX_SMALL rows and from SAGE_MFMA_MIN_LARGE
 # rows up, on hipBLASLt in between. Alone (K=256, N=128, tools/sage_gemm_ab.py,
-# profiles/r02zk_sage_gemm_ab.log): 8192 rows 16.6 vs 21.5-32.3 us, 62479 rows 46.7 vs
-# 40.4 us, 200000 rows 127 vs 136 us; but inside the cfg4 forward the 8192-row layer is
-# faster on hipBLASLt (145 vs 149 us per forward, tools/sage_gemm_forward_ab.py,
-# profiles/r02zk_sage_gemm_forward_ab.log), so the small-M range is off.
-SAGE_MFMA_MAX_SMALL = 0
+# profiles/r03f_gemm_ab.log, 16-row tiles for small launches): 8192 rows 11.9 vs 21.9 us,
+# 62479 rows 46.8 vs 41.0 us, 200000 rows 131 vs 144 us; inside the cfg4 forward
+# (tools/sage_gemm_forward_ab.py, profiles/r03f_sage_fwd_ab.log) MFMA for the 8192-row layer
+# only: 138.5 us vs 139.1 (hipBLASLt both) vs 140.5 (MFMA both).
+SAGE_MFMA_MAX_SMALL = 16384
 SAGE_MFMA_MIN_LARGE = 131072
 
 

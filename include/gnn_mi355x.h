@@ -39,6 +39,7 @@ extern "C" {
 #define GNN_E_RAGGED (-5)     /* index maps of unequal length (the reference's torch.tensor
                                  ValueError)                                           */
 #define GNN_E_NOMEM (-6)      /* host allocation failed                                 */
+#define GNN_E_COMM (-7)       /* RCCL not found in the process, or its call failed      */
 
 /* ---- epilogue flags ---- */
 #define GNN_EPI_RELU 1u /* y = max(y, 0) after the bias add                          */
@@ -502,6 +503,23 @@ int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* col, const fl
                              const int32_t* small_row, const int32_t* small_col,
                              const float* small_val, int64_t n_small, const int32_t* mid_row,
                              int64_t n_mid, float* partial, int32_t variant, void* stream);
+
+/*
+ * Edge-cut halo exchange (SURVEY 8(b) gnn_halo_alltoallv; the all-to-all-v that
+ * distributed.EdgeCutSpmm / EdgeCutGat run through torch.distributed on the nccl = RCCL
+ * backend). Rank p sends send_rows[q] rows of row_floats floats to every rank q (blocks
+ * in peer order, contiguous in `send`) and receives recv_rows[q] rows from each into `recv`,
+ * with ncclAllToAllv on the caller's communicator `comm` (an ncclComm_t) and HIP stream.
+ * send_rows / recv_rows are host arrays [world]. The library does not link RCCL:
+ * ncclAllToAllv is resolved from the process at the first call (the global scope, then an
+ * already-loaded librccl.so / librccl.so.1, then librccl.so.1), so it is the same RCCL
+ * that made `comm`; gnn_halo_rccl_path writes that library's path. No host sync.
+ * Returns GNN_E_COMM when RCCL is not found or its call fails.
+ */
+int gnn_halo_alltoallv_f32(const float* send, const int64_t* send_rows, float* recv,
+                           const int64_t* recv_rows, int64_t row_floats, int64_t world,
+                           void* comm, void* stream);
+int gnn_halo_rccl_path(char* buf, int64_t len);
 
 #ifdef __cplusplus
 }

@@ -65,3 +65,16 @@ def test_ops_refuse_cpu_tensors():
                  torch.zeros(0), 2, 2)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         spmm_forward(g, torch.zeros(2, 4))
+
+
+def test_halo_exchange_entry_without_gpu(lib):
+    """gnn_halo_alltoallv_f32: argument checks before any RCCL call, and the
+    RCCL the entry would call is resolved from the process (torch's own librccl)."""
+    import ctypes
+    import torch  # noqa: F401  (loads the RCCL that torch.distributed's nccl backend uses)
+    counts = (ctypes.c_int64 * 2)(1, 1)
+    assert lib.gnn_halo_alltoallv_f32(None, counts, None, counts, 4, 2, None, None) == -1
+    assert lib.gnn_halo_alltoallv_f32(None, counts, None, counts, 4, 0, 1, None) == -1
+    buf = ctypes.create_string_buffer(4096)
+    assert lib.gnn_halo_rccl_path(buf, 4096) == 0, "ncclAllToAllv not resolvable"
+    assert "rccl" in buf.value.decode()

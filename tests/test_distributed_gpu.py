@@ -497,3 +497,31 @@ def test_edge_cut_out_property_and_profile(dev):
     y3 = run(x)
     assert y3 is not y1 and y3.data_ptr() != y1.data_ptr()  # the other internal buffer
     torch.testing.assert_close(y3, y1)
+
+
+def test_halo_alltoallv_c_abi_single_rank(dev):
+    """gnn_halo_alltoallv_f32 on a one-rank RCCL communicator made with the same librccl the
+    entry resolves (ncclCommInitAll over device 0): the all-to-all-v of one rank is a copy."""
+    import ctypes
+    from graphneuralnetwork_amd import _lib
+    lib = _lib.load()
+    path = ctypes.create_string_buffer(4096)
+    assert lib.gnn_halo_rccl_path(path, 4096) == 0
+    rccl = ctypes.CDLL(path.value.decode())
+    comm = (ctypes.c_void_p * 1)()
+    devs = (ctypes.c_int * 1)(dev.index or 0)
+    assert rccl.ncclCommInitAll(comm, 1, devs) == 0
+    try:
+        F, n = 24, 1000
+        send = torch.randn(n, F, device=dev)
+        recv = torch.empty(n, F, device=dev)
+        cnt = (ctypes.c_int64 * 1)(n)
+        s = torch.cuda.current_stream(dev)
+        rc = lib.gnn_halo_alltoallv_f32(send.data_ptr(), cnt, recv.data_ptr(), cnt, F, 1,
+                                        comm[0], s.cuda_stream)
+        assert rc == 0, _lib.error_string(rc)
+        torch.cuda.synchronize(dev)
+        assert torch.equal(recv, send)
+    finally:
+        rccl.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+        rccl.ncclCommDestroy(comm[0])
