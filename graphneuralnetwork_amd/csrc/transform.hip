@@ -22,6 +22,12 @@ extern "C" int gnn_gcn_transform_supported(int64_t k, int64_t fout);
 namespace gnn {
 
 constexpr int kTfWaves = 4;
+
+struct RowIdx {  // the optional output-row scatter (gcn_transform_kernel y_row)
+  const int64_t* row;
+  int64_t n_y;
+  int32_t* err;
+};
 using tf32x4 = __attribute__((ext_vector_type(4))) float;
 
 #ifndef GNN_TF_SINGLE_BUFFER
@@ -37,12 +43,15 @@ using tf32x4 = __attribute__((ext_vector_type(4))) float;
 // Tiles are double-buffered in LDS (TileLds layout: no bank conflicts on the fragment
 // reads): tile g+1 is loaded into registers during tile g's MFMAs and written to the other
 // buffer before tile g's epilogue, so one barrier per tile separates the two.
+// y_row (optional): X row i goes to output row y_row[i] -- the support written in another
+// row order (a degree-ordered graph's, graph.degree_order) while X is read in order; ids
+// outside [0, n_y) are not stored and raise *err. The stores are scattered 64-B row pieces
+// (fire and forget); a gather on the X side would put the index load in front of every tile.
 template <int K, int CB, int NW, bool RELU, int TR>
-__global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* __restrict__ x,
-                                                                   int64_t ldx, int64_t n_rows,
-                                                                   const float* __restrict__ w,
-                                                                   float* __restrict__ y,
-                                                                   int64_t ldy) {
+__global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
+    const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
+    float* __restrict__ y, int64_t ldy, const int64_t* __restrict__ y_row, int64_t n_y,
+    int32_t* __restrict__ err) {
   constexpr int kTfBlock = NW * kWave;
   constexpr int S = K / 4;           // MFMA k-steps
   constexpr int XC = S <= 32 ? S : 16;  // k-steps of X held in registers at a time
@@ -110,6 +119,13 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* 
     }
     fetch(g + gridDim.x);  // the next tile, in flight during this tile's MFMAs
     const int64_t row0 = g * TR;
+    int64_t dst[TR / 16];  // output rows of this lane's rows (loaded before the MFMAs)
+#pragma unroll
+    for (int j = 0; j < TR / 16; ++j) {
+      const int64_t orow = row0 + j * 16 + r;
+      dst[j] = orow;
+      if (y_row != nullptr && orow < n_rows) dst[j] = y_row[orow];
+    }
     tf32x4 acc[TR / 16][CB];
 #pragma unroll
     for (int rb0 = 0; rb0 < TR / 16; rb0 += RB) {
@@ -152,8 +168,11 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* 
 #pragma unroll
     for (int j = 0; j < TR / 16; ++j) {
       // acc[j][cb][i] = Y[row0 + 16 j + r][(wv*CB + cb)*16 + 4q + i]
-      const int64_t orow = row0 + j * 16 + r;
-      if (orow < n_rows) {
+      const int64_t orow = dst[j];
+      const bool ok = y_row == nullptr || (orow >= 0 && orow < n_y);
+      if (y_row != nullptr && !ok && row0 + j * 16 + r < n_rows && q == 0 && wv == 0)
+        atomicOr(err, 1);
+      if (row0 + j * 16 + r < n_rows && ok) {
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
           float4 o = make_float4(acc[j][cb][0], acc[j][cb][1], acc[j][cb][2], acc[j][cb][3]);
@@ -173,7 +192,7 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(const float* 
 
 template <int K, int CB, int NW, bool RELU, int TR>
 static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, const float* w,
-                               float* y, int64_t ldy, hipStream_t s) {
+                               float* y, int64_t ldy, const RowIdx& ri, hipStream_t s) {
   const int64_t tiles = (n_rows + TR - 1) / TR;
 #ifndef GNN_TF_GRID
 #define GNN_TF_GRID 512  // persistent grid: 2 workgroups per CU
@@ -181,7 +200,7 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
   constexpr int64_t kGrid = GNN_TF_GRID * kTfWaves / NW;  // 8-wave workgroups: 1 per CU
   const int64_t grid = tiles < kGrid ? tiles : kGrid;
   hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR>), dim3(static_cast<unsigned>(grid)),
-                     dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy);
+                     dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err);
   return launch_status();
 }
 
@@ -192,34 +211,35 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
 // slot), then 32 or 16 -- the fixed cost of a small launch is its first tile.
 template <int K, int CB, int NW, bool RELU>
 static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const float* w,
-                            float* y, int64_t ldy, hipStream_t s) {
+                            float* y, int64_t ldy, const RowIdx& ri, hipStream_t s) {
   constexpr int64_t slots = GNN_TF_GRID * kTfWaves / NW;
   if (GNN_TF_MIN_TR <= 16 && n_rows < 32 * 2 * slots)
-    return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, s);
+    return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, s);
   if (GNN_TF_MIN_TR <= 32 && n_rows < 64 * 2 * slots)
-    return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, s);
-  return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, s);
+    return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, s);
+  return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, ri, s);
 }
 
 template <int K, bool RELU>
 static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t n_rows,
-                              const float* w, float* y, int64_t ldy, hipStream_t s) {
-  if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, s);
+                              const float* w, float* y, int64_t ldy, const RowIdx& ri,
+                              hipStream_t s) {
+  if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
   if (fout == 128) {
     if constexpr (K <= 128)
-      return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, s);
+      return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
     else
-      return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, s);
+      return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
   }
   if (fout == 256) {
     if constexpr (K <= 64) {
-      return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, s);
+      return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
     } else {
       // two launches of the 128-column kernel, one per half of W's rows (output columns);
       // X is read twice, but the launch is MFMA-bound at these K (cfg5's 256 -> 256 layer)
-      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, s);
+      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, s);
       if (rc != GNN_OK) return rc;
-      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, s);
+      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, s);
     }
   }
   return GNN_E_UNSUPPORTED;
@@ -228,8 +248,9 @@ static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t
 template <bool RELU>
 static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
                            const float* w, int64_t fout, float* y, int64_t ldy,
-                           void* stream) {
+                           void* stream, const RowIdx& ri = RowIdx{nullptr, 0, nullptr}) {
   if (n_rows < 0 || ldx < k || ldy < fout) return GNN_E_ARG;
+  if (ri.row != nullptr && (ri.err == nullptr || ri.n_y < 0)) return GNN_E_ARG;
   if (!gnn_gcn_transform_supported(k, fout)) return GNN_E_UNSUPPORTED;
   if (n_rows == 0) return GNN_OK;
   if (!x || !w || !y) return GNN_E_ARG;
@@ -237,11 +258,11 @@ static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t 
     return GNN_E_ALIGN;
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (k) {
-    case 16: return dispatch_transform<16, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
-    case 32: return dispatch_transform<32, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
-    case 64: return dispatch_transform<64, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
-    case 128: return dispatch_transform<128, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
-    default: return dispatch_transform<256, RELU>(fout, x, ldx, n_rows, w, y, ldy, s);
+    case 16: return dispatch_transform<16, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
+    case 32: return dispatch_transform<32, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
+    case 64: return dispatch_transform<64, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
+    case 128: return dispatch_transform<128, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
+    default: return dispatch_transform<256, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
   }
 }
 
@@ -259,6 +280,16 @@ extern "C" int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows
                                      const float* w, int64_t fout, float* y, int64_t ldy,
                                      void* stream) {
   return transform_entry<false>(x, ldx, n_rows, k, w, fout, y, ldy, stream);
+}
+
+extern "C" int gnn_gcn_transform_rows_f32(const float* x, int64_t ldx, int64_t n_rows,
+                                          int64_t k, const float* w, int64_t fout, float* y,
+                                          int64_t ldy, const int64_t* y_row, int64_t n_y,
+                                          int32_t* err_flag, void* stream) {
+  if (n_rows > 0 && !y_row) return GNN_E_ARG;
+  if (n_rows > 0 && n_y == 0) return GNN_E_ARG;  // every id would be out of range
+  return transform_entry<false>(x, ldx, n_rows, k, w, fout, y, ldy, stream,
+                                RowIdx{y_row, n_y, err_flag});
 }
 
 extern "C" int gnn_linear_relu_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,

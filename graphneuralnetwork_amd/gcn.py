@@ -14,6 +14,10 @@ the feature transform ``support = dense(X)`` is an fp32 MFMA GEMM: the hand-writ
 otherwise (training, other shapes) nn.Linear on hipBLASLt.  ``adj`` may be the reference's sparse COO tensor, a sparse CSR
 tensor, a dense tensor or a prebuilt ``CsrGraph``; the CSR form is cached on
 the adjacency tensor.
+
+On graphs large enough for the XCD-sliced hub staging, the inference layer runs over the
+column-degree-ordered graph A P^T (``ops.column_order``): the transform writes the support
+rows in that order and the SpMM reads the hub rows in place, with no per-call staging copy.
 """
 from __future__ import annotations
 
@@ -21,7 +25,7 @@ import torch
 from torch import nn
 
 from .graph import as_csr
-from .ops import gcn_transform, spmm
+from .ops import column_order, gcn_transform, spmm
 
 
 class GCN_Model(nn.Module):
@@ -65,13 +69,22 @@ class Graph_conv_layer(nn.Module):
             self.register_parameter('bias', None)
 
     def forward(self, X_input, adj):
+        g = as_csr(adj)
         support = None
         if X_input.is_cuda and not (torch.is_grad_enabled() and
                                     (X_input.requires_grad or self.dense.weight.requires_grad)):
+            order = column_order(g, self.out_features)
+            if order is not None and X_input.shape[0] == g.n_cols:
+                # support rows in the column-degree order of A P^T: the SpMM then reads its hub
+                # rows in place; A P^T (P X W^T) = A X W^T, rows in the original order
+                support = gcn_transform(X_input, self.dense.weight, out_rows=order.inv,
+                                        check_rows=False)
+                if support is not None:
+                    return spmm(order.graph, support, self.bias)
             support = gcn_transform(X_input, self.dense.weight)  # MFMA kernel (inference)
         if support is None:
             support = self.dense(X_input)
-        return spmm(as_csr(adj), support, self.bias)
+        return spmm(g, support, self.bias)
 
     def __repr__(self):
         return self.__class__.__name__ + ' (' \

@@ -239,6 +239,35 @@ class XcdHubPlan:
     def n_pos(self) -> int:
         return self.items.n_rows
 
+    @property
+    def prefix(self) -> bool:
+        """True when the hub rows are X's first k rows in rank order (a graph relabelled by
+        ``degree_order``): the staged table is then X itself and needs no copy."""
+        v = self.__dict__.get("_prefix")
+        if v is None:
+            ids = self.hub.hub_ids
+            v = bool(torch.equal(ids, torch.arange(ids.numel(), device=ids.device,
+                                                   dtype=ids.dtype)))
+            self.__dict__["_prefix"] = v
+        return v
+
+    def direct(self) -> tuple["CsrGraph", "CsrGraph"]:
+        """(items, rest) of a prefix plan with the hub references turned back into X row ids
+        (-1-rank -> rank) and the partial refs renumbered -1-(k + pos) -> -1-pos: pass 1 reads
+        X with the plain kernel, pass 2 reads X and a separate partial-row buffer (cached)."""
+        d = self.__dict__.get("_direct")
+        if d is None:
+            k = self.k
+            ic = (-1 - self.items.col.to(torch.int64)).to(torch.int32)
+            items = CsrGraph(self.items.rowptr, ic.contiguous(), self.items.val,
+                             self.items.n_rows, k)
+            c = self.rest.col
+            rc = torch.where(c >= 0, c, torch.where(c >= -k, -1 - c, c + k))
+            rest = CsrGraph(self.rest.rowptr, rc.to(torch.int32).contiguous(), self.rest.val,
+                            self.rest.n_rows, self.rest.n_cols)
+            d = self.__dict__["_direct"] = (items, rest)
+        return d
+
     def rest_plan(self, seg_len: int) -> RowSplitPlan:
         """The row-class plan of ``rest`` for the hub kernels (cached per seg_len).
 
@@ -275,7 +304,7 @@ def staged_plan(g: "CsrGraph", seg_len: int) -> RowSplitPlan:
 def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, k: int,
                 min_deg: int, chunk: int, xcds: int = XCDS,
                 waves_per_wg: int = SPMM_WAVES_PER_WG, phases: int = 1,
-                item_k: int | None = None):
+                item_k: int | None = None, small_item: int | None = None):
     """The two COO edge lists of ``XcdHubPlan`` (torch ops on any device; the CPU tests
     check them against the oracle SpMM).
 
@@ -290,7 +319,11 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     launch order, so each XCD's L2 holds 1 / (xcds * phases) of the table at a time.
 
     ``item_k`` < k limits the items to the item_k hottest hub rows (a smaller set per XCD
-    slice); the edges to the other hub rows stay in ``rest`` and read the whole table."""
+    slice); the edges to the other hub rows stay in ``rest`` and read the whole table.
+
+    ``small_item`` (>= 2): rows below ``min_deg`` also get items, for the slices where they
+    have at least ``small_item`` hub edges (a partial row pays off only when it replaces
+    enough shared-table gathers)."""
     S = xcds * phases
     if chunk < 4 or k < S or phases < 1:  # balanced chunks of a >= 2-edge item hold >= 2 edges
         raise ValueError("xcd hub staging needs chunk >= 4 and k >= xcds * phases")
@@ -303,13 +336,21 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     ik = k if item_k is None else min(int(item_k), k)
     if ik < S:
         raise ValueError("xcd hub staging needs item_k >= xcds * phases")
-    eid = torch.nonzero((c < 0) & (c >= -ik) & (deg[rows_e] >= min_deg)).view(-1)
+    if small_item is not None and small_item < 2:
+        raise ValueError("small_item must be >= 2")
+    if small_item is None:
+        eid = torch.nonzero((c < 0) & (c >= -ik) & (deg[rows_e] >= min_deg)).view(-1)
+    else:
+        eid = torch.nonzero((c < 0) & (c >= -ik) & (deg[rows_e] >= 2)).view(-1)
     s_e = (-1 - c[eid]) % S
     key = rows_e[eid] * S + s_e
     order = torch.argsort(key, stable=True)                  # by (row, slice), CSR order kept
     eid, key, s_e = eid[order], key[order], s_e[order]
     _, inv, m = torch.unique_consecutive(key, return_inverse=True, return_counts=True)
     moved = m >= 2                                           # a 1-edge item saves nothing
+    if small_item is not None:
+        first = torch.cumsum(m, 0) - m                       # first edge of each group
+        moved &= (deg[rows_e[eid[first]]] >= min_deg) | (m >= small_item)
     if not bool(moved.any()):
         return None
     em = moved[inv]
@@ -424,12 +465,14 @@ class CsrGraph:
         return p
 
     def xcd_hub_plan(self, k: int, min_deg: int, chunk: int, phases: int = 1,
-                     item_k: int | None = None) -> "XcdHubPlan | None":
-        """XCD-sliced hub staging plan (built once per (k, min_deg, chunk, phases, item_k),
-        cached); None when no row has two hub edges in one slice."""
-        key = ("_xcd", k, min_deg, chunk, phases, item_k)
+                     item_k: int | None = None,
+                     small_item: int | None = None) -> "XcdHubPlan | None":
+        """XCD-sliced hub staging plan (built once per (k, min_deg, chunk, phases, item_k,
+        small_item), cached); None when no row has two hub edges in one slice."""
+        key = ("_xcd", k, min_deg, chunk, phases, item_k, small_item)
         if key not in self._plans:
-            self._plans[key] = _build_xcd_hub_plan(self, k, min_deg, chunk, phases, item_k)
+            self._plans[key] = _build_xcd_hub_plan(self, k, min_deg, chunk, phases, item_k,
+                                                   small_item)
         return self._plans[key]
 
     def transpose(self) -> "CsrGraph":
@@ -516,14 +559,15 @@ def _build_hub_plan(g: CsrGraph, k: int) -> HubPlan:
 
 
 def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int, phases: int = 1,
-                        item_k: int | None = None) -> "XcdHubPlan | None":
+                        item_k: int | None = None,
+                        small_item: int | None = None) -> "XcdHubPlan | None":
     hub = g.hub_plan(k)
     if hub.k < XCDS * phases or g.nnz == 0:
         return None
     if item_k is not None and min(int(item_k), hub.k) < XCDS * phases:
         return None
     coo = xcd_hub_coo(g.rowptr, hub.col_hub, g.val, hub.k, min_deg, chunk, phases=phases,
-                      item_k=item_k)
+                      item_k=item_k, small_item=small_item)
     if coo is None:
         return None
     (ir, ic, iv, n_pos, n_items), (rr, rc, rv), pos_row = coo
@@ -532,6 +576,60 @@ def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int, phases: i
     items = from_coo(ir, ic, iv, n_pos, hub.k, check=False)
     rest = from_coo(rr, rc, rv, g.n_rows, g.n_cols, check=False)
     return XcdHubPlan(hub, items, rest, n_items, min_deg, chunk, pos_row)
+
+
+@dataclass
+class DegreeOrder:
+    """A relabelling of a square graph's nodes by in-degree (descending, ties by ascending
+    id): new id i is old node ``perm[i]``; ``inv[old]`` is its new id. Under it the hub rows
+    that the staging would copy (the same ranking as hub.hip) are the first rows of X, so
+    the SpMM reads them in place (``XcdHubPlan.direct``)."""
+
+    perm: torch.Tensor  # int64 [n]: new -> old
+    inv: torch.Tensor   # int64 [n]: old -> new
+    graph: "CsrGraph"   # P A P^T, or A P^T (degree_order(rows=False))
+
+    def permute_rows(self, x: torch.Tensor) -> torch.Tensor:
+        """X' = P X (rows in the new order)."""
+        return x.index_select(0, self.perm)
+
+    def unpermute_rows(self, y: torch.Tensor) -> torch.Tensor:
+        """Y = P^T Y' (rows back in the original order)."""
+        return y.index_select(0, self.inv)
+
+
+def degree_order(g: "CsrGraph", rows: bool = True) -> DegreeOrder:
+    """Relabel a CSR graph by column in-degree (torch ops on its device). The edges of each
+    row keep their CSR order (renamed), so every row sum runs in the same order: the result
+    is bit-identical to the original graph's, permuted.
+
+    ``rows=True`` (square graphs): both sides, A' = P A P^T, for Y' = A' X' = P Y.
+    ``rows=False``: the columns only, A' = A P^T, for Y = A' (P X) -- the output rows stay
+    in the original order."""
+    n = g.n_cols
+    dev = g.device
+    indeg = torch.bincount(g.col.to(torch.int64), minlength=n)
+    idx = torch.arange(n, device=dev, dtype=torch.int64)
+    # descending in-degree, ascending id on ties: one stable sort of -indeg
+    perm = torch.sort(-indeg, stable=True).indices
+    inv = torch.empty_like(perm)
+    inv[perm] = idx
+    if not rows:
+        col = inv[g.col.to(torch.int64)].to(torch.int32).contiguous()
+        return DegreeOrder(perm, inv, CsrGraph(g.rowptr, col, g.val, g.n_rows, n))
+    if g.n_rows != g.n_cols:
+        raise ValueError("degree_order(rows=True) needs a square adjacency")
+    deg = g.rowptr[1:] - g.rowptr[:-1]
+    new_deg = deg[perm]
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(new_deg, 0, out=rowptr[1:])
+    # edge e of new row i is edge (rowptr_old[perm[i]] + j) of the old graph
+    rows_new = torch.repeat_interleave(idx, new_deg)
+    src = g.rowptr[perm][rows_new] + (torch.arange(rows_new.numel(), device=dev,
+                                                   dtype=torch.int64) - rowptr[rows_new])
+    col = inv[g.col.to(torch.int64)[src]].to(torch.int32).contiguous()
+    val = g.val[src].contiguous()
+    return DegreeOrder(perm, inv, CsrGraph(rowptr, col, val, n, n))
 
 
 # ---------------------------------------------------------------- builders

@@ -8,7 +8,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
-from .graph import GAT_SEG_BYTES, CsrGraph, seg_len_for
+from .graph import GAT_SEG_BYTES, CsrGraph, seg_len_for, staged_plan
 
 _ACT_FLAGS = {None: 0, "relu": _lib.EPI_RELU, "elu": _lib.EPI_ELU}
 
@@ -66,6 +66,12 @@ XCD_MIN_DEG = 128
 XCD_CHUNK = 128
 XCD_PHASES = 1  # slices per XCD, run one after another (graph.xcd_hub_coo ``phases``)
 XCD_ITEM_ROWS = None  # items read only the hottest XCD_ITEM_ROWS hub rows (None: all K)
+# rows below XCD_MIN_DEG get items too, for each slice holding >= XCD_SMALL_ITEM of their hub
+# edges (None: off; graph.xcd_hub_coo ``small_item``)
+XCD_SMALL_ITEM = None
+# on a degree-ordered graph (graph.degree_order) the hub rows are X's first rows: read them
+# in place instead of copying them into a staged table (XcdHubPlan.prefix / direct)
+XCD_DIRECT = True
 
 
 def xcd_hub_rows_for(n_cols: int, feat: int) -> int:
@@ -158,7 +164,7 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
     if xcd and g.nnz:
         kx = xcd_hub_rows_for(g.n_cols, feat) if hubs is None else min(int(hubs), g.n_cols)
         chunk = min(XCD_CHUNK, seg)
-        xp = (g.xcd_hub_plan(kx, XCD_MIN_DEG, chunk, XCD_PHASES, XCD_ITEM_ROWS)
+        xp = (g.xcd_hub_plan(kx, XCD_MIN_DEG, chunk, XCD_PHASES, XCD_ITEM_ROWS, XCD_SMALL_ITEM)
               if kx >= 8 * XCD_PHASES and chunk >= 4 else None)
         if xp is not None:
             _spmm_xcd(lib, g, xp, x, feat, bias, out, seg, skip_empty, flags, stream)
@@ -208,6 +214,9 @@ def _spmm_xcd(lib, g: CsrGraph, xp, x, feat, bias, out, seg, skip_empty, flags, 
     the same buffer, workgroup w on XCD w % 8 holds only slice w % 8), pass 2 (remaining
     edges + partial refs, with the epilogue). Three launches on one stream."""
     k, n_pos = xp.k, xp.n_pos
+    if XCD_DIRECT and xp.prefix:
+        _spmm_xcd_direct(lib, xp, x, feat, bias, out, seg, skip_empty, flags, stream)
+        return
     buf = torch.empty((k + n_pos, feat), dtype=torch.float32, device=x.device)
     hp = xp.hub
     _lib.check(lib.gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0],
@@ -234,6 +243,62 @@ def _spmm_xcd(lib, g: CsrGraph, xp, x, feat, bias, out, seg, skip_empty, flags, 
     _spmm_hub_call(lib, xp.rest, xp.rest.col, p2, p2.args(skip_empty=skip_empty), x, buf, feat,
                    bias, out, out.stride(0), partial, flags, stream,
                    "gnn_spmm_csr_hub_f32 (xcd rest)")
+
+
+# Graph_conv_layer runs its aggregation over the column-degree-ordered graph A P^T
+# (graph.degree_order(rows=False)) whenever the SpMM would take the XCD-sliced path: the
+# transform writes the support rows in that order (gcn_transform rows=perm) and the SpMM reads
+# the hub rows in place (no staging copy). Output rows stay in the original order.
+DEGREE_ORDER = True
+
+
+def column_order(g: CsrGraph, feat: int):
+    """The cached ``DegreeOrder(rows=False)`` of ``g`` when a feat-wide SpMM over it would
+    take the XCD-sliced hub path (else None)."""
+    if not (DEGREE_ORDER and XCD_DIRECT) or g.nnz < XCD_MIN_NNZ:
+        return None
+    if xcd_hub_rows_for(g.n_cols, feat) < 8 * XCD_PHASES:
+        return None
+    key = ("_colorder",)
+    o = g._plans.get(key)
+    if o is None:
+        from .graph import degree_order
+        o = g._plans[key] = degree_order(g, rows=False)
+    return o
+
+
+def _spmm_xcd_direct(lib, xp, x, feat, bias, out, seg, skip_empty, flags, stream):
+    """The XCD-sliced SpMM of a degree-ordered graph (graph.degree_order): the hub rows are
+    X's first k rows, so there is no staging copy. Pass 1 (plain kernel) reads the items'
+    hub rows from X into a partial-row buffer; pass 2 reads X and that buffer (c < 0 ->
+    partial row -1-c)."""
+    items, rest = xp.direct()
+    part = torch.empty((xp.n_pos, feat), dtype=torch.float32, device=x.device)
+    p1 = items.plan(seg)
+    if p1.n_seg or p1.n_small:
+        raise RuntimeError("XCD hub plan: item rows outside the mid-row class")
+    _lib.check(lib.gnn_spmm_csr_f32(
+        items.rowptr.data_ptr(), items.col.data_ptr(), items.val.data_ptr(), items.n_rows,
+        x.data_ptr(), x.stride(0), feat, None, part.data_ptr(), feat, p1.seg_len, *p1.args(),
+        None, 0, stream), "gnn_spmm_csr_f32 (xcd direct items)")
+    if _tasks_ok(feat, x, out, bias, part):
+        tp = rest.task_plan(seg, TASK_MAX_DEG, TASK_COST)
+        partial = None
+        if tp.base.n_seg:
+            partial = torch.empty((tp.base.n_seg, feat), dtype=torch.float32, device=x.device)
+        _spmm_tasks_call(lib, rest, rest.col, tp, x, part, feat, bias, out, out.stride(0),
+                         partial, flags | (_lib.EPI_SKIP_EMPTY if skip_empty else 0), stream,
+                         "gnn_spmm_csr_tasks_f32 (xcd direct rest)")
+        return
+    p2 = staged_plan(rest, seg)
+    partial = None
+    if p2.n_seg:
+        partial = torch.empty((p2.n_seg, feat), dtype=torch.float32, device=x.device)
+    _lib.check(lib.gnn_spmm_csr_hub_f32(
+        rest.rowptr.data_ptr(), rest.col.data_ptr(), rest.val.data_ptr(), rest.n_rows,
+        x.data_ptr(), x.stride(0), part.data_ptr(), feat, feat, _lib.ptr(bias), out.data_ptr(),
+        out.stride(0), p2.seg_len, *p2.args(skip_empty=skip_empty), _lib.ptr(partial), flags,
+        stream), "gnn_spmm_csr_hub_f32 (xcd direct rest)")
 
 
 class _SpmmFn(torch.autograd.Function):
@@ -326,12 +391,19 @@ TRANSFORM_WIDE_MFMA = False
 
 
 def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
-                  out: torch.Tensor | None = None) -> torch.Tensor | None:
+                  out: torch.Tensor | None = None, out_rows: torch.Tensor | None = None,
+                  check_rows: bool = True) -> torch.Tensor | None:
     """support = x @ weight^T on fp32 MFMA (gnn_gcn_transform_f32), the dense half of
     Graph_conv_layer.forward (GCN/GCN.py:42); ``relu=True``: max(x @ weight^T, 0)
     (gnn_linear_relu_f32, the SageLayer at GraphSAGE/GraphSAGE.py:18-20). Inference only
     (no autograd). None when the shape is not covered (the caller then uses nn.Linear /
-    hipBLASLt)."""
+    hipBLASLt).
+
+    ``out_rows`` (int64 [rows of x]): x row i goes to support row out_rows[i]
+    (gnn_gcn_transform_rows_f32), e.g. a degree order's ``inv`` so that the support is in the
+    degree-ordered graph's column order; ``out`` (or a new [rows of x, fout] tensor) receives
+    it. ``check_rows=False`` skips the host read of the range-check flag (trusted ids, e.g. a
+    ``DegreeOrder``'s; the kernel still skips the store of a bad id)."""
     _require_device(x, weight)
     if (x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 2
             or weight.dim() != 2 or x.shape[1] != weight.shape[1]):
@@ -342,14 +414,33 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
         return None
     if fout == 256 and k > 64 and not TRANSFORM_WIDE_MFMA:
         return None
+    if out_rows is not None and relu:
+        raise ValueError("out_rows= is supported without the ReLU epilogue only")
     if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
         x = x.contiguous()
     w = weight.contiguous()
+    m = x.shape[0]
     if out is None:
-        out = torch.empty((x.shape[0], fout), dtype=torch.float32, device=x.device)
-    elif (out.shape != (x.shape[0], fout) or out.dtype != torch.float32 or out.stride(1) != 1
+        out = torch.empty((m, fout), dtype=torch.float32, device=x.device)
+    elif (out.dim() != 2 or out.shape[1] != fout or (out_rows is None and out.shape[0] != m)
+          or out.dtype != torch.float32 or out.stride(1) != 1
           or out.stride(0) % 4 or out.data_ptr() % 16):
         raise ValueError("out must be float32 [rows, fout], 16-B aligned rows")
+    if out_rows is not None:
+        _require_device(out_rows)
+        if out_rows.dtype != torch.int64 or out_rows.dim() != 1 or out_rows.numel() != m:
+            raise TypeError("out_rows must be a 1-D int64 tensor with one id per row of x")
+        out_rows = out_rows.contiguous()
+        if m == 0:
+            return out
+        err = torch.zeros(1, dtype=torch.int32, device=x.device)
+        _lib.check(lib.gnn_gcn_transform_rows_f32(
+            x.data_ptr(), x.stride(0), m, k, w.data_ptr(), fout, out.data_ptr(), out.stride(0),
+            out_rows.data_ptr(), out.shape[0], err.data_ptr(), _lib.stream_handle(x.device)),
+            "gnn_gcn_transform_rows_f32")
+        if check_rows and int(err.item()):
+            raise IndexError("gcn_transform: an output row id is out of range")
+        return out
     fn, name = ((lib.gnn_linear_relu_f32, "gnn_linear_relu_f32") if relu else
                 (lib.gnn_gcn_transform_f32, "gnn_gcn_transform_f32"))
     _lib.check(fn(x.data_ptr(), x.stride(0), x.shape[0], k, w.data_ptr(), fout, out.data_ptr(),

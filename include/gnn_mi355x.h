@@ -186,6 +186,21 @@ int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k
                           int64_t fout, float* y, int64_t ldy, void* stream);
 
 /*
+ * The same product with the output rows scattered: y[y_row[i], :fout] = x[i, :k] @ w^T for
+ * i < n_rows (y has n_y rows; x is read in order). With y_row = a degree order's inv (old ->
+ * new id) it writes the support of GCN/GCN.py:42 directly in the row order the
+ * column-degree-ordered graph A P^T reads it (A P^T . P (X W^T) = A . X W^T:
+ * Graph_conv_layer's output rows stay in the original order), so the SpMM gathers its hub
+ * rows from the first rows of y with no staging copy. Rows whose id is outside [0, n_y) are
+ * not stored and set *err_flag = 1. Same shapes, alignment and return codes as
+ * gnn_gcn_transform_f32.
+ */
+int gnn_gcn_transform_rows_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                               const float* w, int64_t fout, float* y, int64_t ldy,
+                               const int64_t* y_row, int64_t n_y, int32_t* err_flag,
+                               void* stream);
+
+/*
  * Feature row normalisation, bit-exact with the reference loader: normalize_features
  * (GCN/data_utils.py:39-51) then torch.Tensor(features.toarray()) (:81-83). rowsum = the
  * first nonzero of the row plus numpy's float32 pairwise sum of the others (scipy's csr

@@ -322,7 +322,7 @@ def test_xcd_hub_staging(dev, F, monkeypatch):
                 monkeypatch.setattr(ops, "XCD_PHASES", ph)  # slices per XCD, in launch order
                 monkeypatch.setattr(ops, "XCD_ITEM_ROWS", ik)  # items from the ik hottest rows
                 y = spmm_forward(g, X, b, activation="elu", seg_len=seg_len, hubs=k, xcd=True)
-                key = ("_xcd", k, 4, min(8, seg_len or 10 ** 9), ph, ik)
+                key = ("_xcd", k, 4, min(8, seg_len or 10 ** 9), ph, ik, None)
                 assert g._plans.get(key) is not None, key
                 close(y.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5)
                 assert torch.equal(y, spmm_forward(g, X, b, activation="elu", seg_len=seg_len,
@@ -508,3 +508,114 @@ def test_gcn_transform_wide_output_c_abi(dev, k):
                                      torch.cuda.current_stream().cuda_stream) == 0
     ref = (x.double() @ w.double().T).float()
     close(y.cpu().numpy(), ref.cpu().numpy())
+
+
+@pytest.mark.parametrize("rows", [True, False])
+@pytest.mark.parametrize("F", [64, 128, 600])
+def test_xcd_direct_degree_order(dev, F, rows, monkeypatch):
+    """On a degree-ordered graph (graph.degree_order) the XCD-sliced SpMM reads the hub rows
+    in place (XcdHubPlan.prefix / direct: no staging copy). Its output is bit-identical to
+    the staged copy's and to the natural-order graph's XCD result (the same items, slices
+    and edge order), permuted; epilogues, accumulate, long-row segments."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.graph import degree_order
+    from graphneuralnetwork_amd.ops import spmm_forward
+    monkeypatch.setattr(ops, "XCD_MIN_DEG", 4)
+    monkeypatch.setattr(ops, "XCD_CHUNK", 8)
+    n = 1500
+    rowptr, col, val = _xcd_graph(n, 90 + F)
+    g = _graph(rowptr, col, val, n, dev)
+    o = degree_order(g, rows=rows)
+    perm = o.perm
+    X = torch.randn(n, F, device=dev)
+    Xp = o.permute_rows(X)
+    b = torch.randn(F, device=dev)
+    base = torch.randn(n, F, device=dev)
+    for seg_len in (None, 16):
+        for k in (200, n):
+            nat = spmm_forward(g, X, b, activation="relu", seg_len=seg_len, hubs=k, xcd=True)
+            monkeypatch.setattr(ops, "XCD_DIRECT", True)
+            y = spmm_forward(o.graph, Xp, b, activation="relu", seg_len=seg_len, hubs=k,
+                             xcd=True)
+            key = ("_xcd", k, 4, min(8, seg_len or 10 ** 9), 1, None, None)
+            assert o.graph._plans[key].prefix
+            monkeypatch.setattr(ops, "XCD_DIRECT", False)
+            y_staged = spmm_forward(o.graph, Xp, b, activation="relu", seg_len=seg_len, hubs=k,
+                                    xcd=True)
+            assert torch.equal(y, y_staged)
+            assert torch.equal(y, nat[perm] if rows else nat)
+            monkeypatch.setattr(ops, "XCD_DIRECT", True)
+            acc = spmm_forward(o.graph, Xp, None, out=(base[perm] if rows else base).clone(),
+                               accumulate=True, seg_len=seg_len, hubs=k, xcd=True)
+            acc_nat = spmm_forward(g, X, None, out=base.clone(), accumulate=True,
+                                   seg_len=seg_len, hubs=k, xcd=True)
+            assert torch.equal(acc, acc_nat[perm] if rows else acc_nat)
+    y = spmm_forward(o.graph, Xp, b, hubs=n, xcd=True).cpu().numpy()
+    want = O.spmm_csr(rowptr, col, val, X.cpu().numpy(), b.cpu().numpy())
+    close(y, want[perm.cpu().numpy()] if rows else want)
+
+
+@pytest.mark.parametrize("k,fout", [(64, 64), (128, 128), (256, 128), (64, 256)])
+def test_transform_out_rows(dev, k, fout):
+    """gnn_gcn_transform_rows_f32: y[out_rows[i]] = x[i] W^T, bit-identical to the in-order
+    transform scattered (each row's MFMA chain does not depend on the others); a permutation,
+    a scatter into a larger output (rows not named stay untouched), every tile size; an id out
+    of range is not stored and raises."""
+    from graphneuralnetwork_amd.ops import gcn_transform
+    for n in (5000, 37, 1 << 17):
+        x = torch.randn(n, k, device=dev)
+        w = torch.randn(fout, k, device=dev) / k ** 0.5
+        ref = gcn_transform(x, w)
+        close(ref.cpu().numpy(), (x.double() @ w.double().T).cpu().numpy(), rtol=1e-5)
+        perm = torch.randperm(n, device=dev)
+        y = gcn_transform(x, w, out_rows=perm)
+        want = torch.empty_like(ref)
+        want[perm] = ref
+        assert torch.equal(y, want)
+        big = torch.full((2 * n + 3, fout), 7.0, device=dev)
+        ids = torch.randperm(2 * n + 3, device=dev)[:n]
+        gcn_transform(x, w, out=big, out_rows=ids)
+        assert torch.equal(big[ids], ref)
+        rest = torch.ones(2 * n + 3, dtype=torch.bool, device=dev)
+        rest[ids] = False
+        assert bool((big[rest] == 7.0).all())
+    x = torch.randn(3, k, device=dev)
+    w = torch.randn(fout, k, device=dev)
+    bad = torch.tensor([0, 3, 1], device=dev)
+    with pytest.raises(IndexError):
+        gcn_transform(x, w, out_rows=bad)
+    out = torch.zeros(3, fout, device=dev)
+    gcn_transform(x, w, out=out, out_rows=bad, check_rows=False)
+    assert torch.equal(out[2], torch.zeros(fout, device=dev))
+    with pytest.raises(TypeError):
+        gcn_transform(x, w, out_rows=bad.to(torch.int32))
+
+
+def test_gcn_layer_column_order(dev, monkeypatch):
+    """Graph_conv_layer on a graph that takes the XCD path: the inference forward runs over
+    the column-degree-ordered graph (transform rows = perm, hub rows read in place) and
+    returns the rows in the original order, bit-identical to the natural-order layer."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.gcn import Graph_conv_layer
+    monkeypatch.setattr(ops, "HUB_MIN_X_BYTES", 0)
+    monkeypatch.setattr(ops, "XCD_MIN_NNZ", 1)
+    monkeypatch.setattr(ops, "XCD_MIN_DEG", 4)
+    n, F = 2000, 128
+    rowptr, col, val = _rand_graph(n, 30 * n, 5, hub_deg=6000)
+    g = _graph(rowptr, col, val, n, dev)
+    layer = Graph_conv_layer(64, F).to(dev)
+    with torch.no_grad():
+        layer.bias.normal_()
+    X = torch.randn(n, 64, device=dev)
+    with torch.no_grad():
+        y = layer(X, g)
+        assert ("_colorder",) in g._plans
+        xp = next(p for key, p in g._plans[("_colorder",)].graph._plans.items()
+                  if isinstance(key, tuple) and key[0] == "_xcd")
+        assert xp is not None and xp.prefix
+        monkeypatch.setattr(ops, "DEGREE_ORDER", False)
+        y_nat = layer(X, _graph(rowptr, col, val, n, dev))
+    assert torch.equal(y, y_nat)
+    support = (X.double() @ layer.dense.weight.detach().double().T).cpu().numpy()
+    close(y.cpu().numpy(), O.spmm_csr(rowptr, col, val, support, layer.bias.detach().cpu().numpy()),
+          rtol=1e-4)

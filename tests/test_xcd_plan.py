@@ -42,17 +42,19 @@ def _csr_spmm(rows, cols, vals, n_rows, src):
     return out
 
 
-@pytest.mark.parametrize("k,min_deg,chunk,phases,item_k", [
-    (64, 16, 8, 1, None), (200, 2, 4, 1, None), (500, 64, 128, 1, None),
-    (3000, 1, 4, 1, None), (3000, 1, 5, 1, None), (500, 16, 8, 2, None),
-    (3000, 2, 4, 4, None), (3000, 2, 8, 1, 100), (500, 16, 8, 2, 64)])
-def test_xcd_plan_algebra_and_layout(k, min_deg, chunk, phases, item_k):
+@pytest.mark.parametrize("k,min_deg,chunk,phases,item_k,small_item", [
+    (64, 16, 8, 1, None, None), (200, 2, 4, 1, None, None), (500, 64, 128, 1, None, None),
+    (3000, 1, 4, 1, None, None), (3000, 1, 5, 1, None, None), (500, 16, 8, 2, None, None),
+    (3000, 2, 4, 4, None, None), (3000, 2, 8, 1, 100, None), (500, 16, 8, 2, 64, None),
+    (500, 64, 128, 1, None, 3), (3000, 32, 8, 1, None, 4), (500, 10 ** 9, 16, 1, None, 2)])
+def test_xcd_plan_algebra_and_layout(k, min_deg, chunk, phases, item_k, small_item):
     from graphneuralnetwork_amd.graph import xcd_hub_coo
     rowptr, col, val = _graph()
     n = rowptr.size - 1
     hub, ch = _hub_rename(col, n, k)
     res = xcd_hub_coo(torch.from_numpy(rowptr), torch.from_numpy(ch.astype(np.int32)),
-                      torch.from_numpy(val), k, min_deg, chunk, phases=phases, item_k=item_k)
+                      torch.from_numpy(val), k, min_deg, chunk, phases=phases, item_k=item_k,
+                      small_item=small_item)
     assert res is not None
     (ir, ic, iv, n_pos, n_items), (rr, rc, rv), pos_row = res
     ir, ic, iv, rr, rc, rv = (t.numpy() for t in (ir, ic, iv, rr, rc, rv))
@@ -84,6 +86,15 @@ def test_xcd_plan_algebra_and_layout(k, min_deg, chunk, phases, item_k):
     orig = np.stack([rows_e, ch])
     np.testing.assert_array_equal(np.lexsort(both[::-1]).size, orig.shape[1])
     np.testing.assert_array_equal(both[:, np.lexsort(both[::-1])], orig[:, np.lexsort(orig[::-1])])
+    # items of rows below min_deg only for (row, slice) groups of >= small_item hub edges
+    deg_item = deg[moved_rows]
+    grp = moved_rows * (XCDS * phases) + (-1 - ic[~pads]) % (XCDS * phases)
+    _, inv, gsize = np.unique(grp, return_inverse=True, return_counts=True)
+    low = deg_item < min_deg
+    if small_item is None:
+        assert not low.any()
+    else:
+        assert (gsize[inv][low] >= small_item).all() and low.any()
     # rest rows: own edges in CSR order before the partial refs
     order = np.argsort(rr, kind="stable")
     rs, rcs = rr[order], rc[order]
@@ -144,3 +155,62 @@ def test_task_ranges_invariants(max_deg, cost):
         prev_end = e
     np.testing.assert_array_equal(covered, deg <= max_deg)
     assert task_ranges(torch.zeros(1, dtype=torch.int64), max_deg, cost).numel() == 0
+
+
+@pytest.mark.parametrize("rows", [True, False])
+def test_degree_order_bit_identical_and_hub_prefix(rows):
+    """graph.degree_order (CPU torch ops): A' = P A P^T (or A P^T) with each row's edges in
+    their CSR order, so A' X' equals the original product bit for bit (permuted); the
+    in-degree ranking of hub.hip (descending, ties by ascending id) is then the identity."""
+    from graphneuralnetwork_amd.graph import CsrGraph, degree_order
+    rowptr, col, val = _graph(4000, 50000, 3)
+    n = rowptr.size - 1
+    g = CsrGraph(torch.from_numpy(rowptr), torch.from_numpy(col.astype(np.int32)),
+                 torch.from_numpy(val), n, n)
+    o = degree_order(g, rows=rows)
+    perm, inv = o.perm.numpy(), o.inv.numpy()
+    np.testing.assert_array_equal(inv[perm], np.arange(n))
+    gp = o.graph
+    X = np.random.default_rng(5).standard_normal((n, 6))
+    Y = O.spmm_csr(rowptr, col, val, X)
+    Yp = O.spmm_csr(gp.rowptr.numpy(), gp.col.numpy(), gp.val.numpy(), X[perm])
+    np.testing.assert_array_equal(Yp, Y[perm] if rows else Y)
+    hub, _ = _hub_rename(gp.col.numpy(), n, 300)
+    np.testing.assert_array_equal(hub, np.arange(300))
+    if rows:
+        np.testing.assert_array_equal(o.unpermute_rows(torch.from_numpy(Yp)).numpy(), Y)
+
+
+def test_xcd_direct_plan_algebra():
+    """XcdHubPlan.direct on a degree-ordered graph: pass 1 gathers the items' hub rows
+    straight from X (hub rank = X row), pass 2 reads X and a separate partial-row buffer
+    (-1-pos); together they equal A' X' (float64)."""
+    from graphneuralnetwork_amd.graph import (CsrGraph, HubPlan, XcdHubPlan, degree_order,
+                                              from_coo, xcd_hub_coo)
+    rowptr, col, val = _graph(3000, 60000, 0)
+    n = rowptr.size - 1
+    g = CsrGraph(torch.from_numpy(rowptr), torch.from_numpy(col.astype(np.int32)),
+                 torch.from_numpy(val), n, n)
+    gp = degree_order(g).graph
+    k = 500
+    c = gp.col.to(torch.int64)
+    col_hub = torch.where(c < k, -1 - c, c).to(torch.int32)
+    (ir, ic, iv, n_pos, n_items), (rr, rc, rv), pos_row = xcd_hub_coo(
+        gp.rowptr, col_hub, gp.val, k, 16, 8)
+    hp = HubPlan(torch.arange(k), col_hub, torch.zeros(1, dtype=torch.int32))
+    xp = XcdHubPlan(hp, from_coo(ir, ic, iv, n_pos, k, check=False),
+                    from_coo(rr, rc, rv, n, n, check=False),
+                    n_items, 16, 8, pos_row)
+    assert xp.prefix
+    items, rest = xp.direct()
+    assert int(items.col.min()) >= 0 and int(items.col.max()) < k
+    assert int(rest.col.min()) >= -n_pos
+    X = np.random.default_rng(6).standard_normal((n, 4))
+    ipr = items.rowptr.numpy()
+    P = _csr_spmm(np.repeat(np.arange(n_pos), np.diff(ipr)), items.col.numpy(),
+                  items.val.numpy(), n_pos, X[items.col.numpy()])
+    rpr, rcol = rest.rowptr.numpy(), rest.col.numpy()
+    src = np.where(rcol[:, None] >= 0, X[np.maximum(rcol, 0)], P[np.maximum(-1 - rcol, 0)])
+    Y = _csr_spmm(np.repeat(np.arange(n), np.diff(rpr)), rcol, rest.val.numpy(), n, src)
+    want = O.spmm_csr(gp.rowptr.numpy(), gp.col.numpy(), gp.val.numpy(), X)
+    np.testing.assert_allclose(Y, want, rtol=1e-12, atol=1e-12)

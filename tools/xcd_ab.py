@@ -29,6 +29,9 @@ def main():
                     help="slices per XCD run one after another (ops.XCD_PHASES)")
     ap.add_argument("--item-rows", default="0",
                     help="items read only the hottest N hub rows (ops.XCD_ITEM_ROWS; 0 = all)")
+    ap.add_argument("--small-items", default="0",
+                    help="rows below the degree threshold get items for slices with >= N hub "
+                         "edges (ops.XCD_SMALL_ITEM; 0 = off)")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--op", default="spmm", choices=["spmm", "gat"],
                     help="gat: the cfg3 GAT aggregation (dense softmax + ELU, 8 heads x F/8)")
@@ -65,13 +68,16 @@ def main():
             for ch in (int(v) for v in args.chunks.split(",")):
                 for ph in (int(v) for v in args.phases.split(",")):
                     for ik in (int(v) or None for v in args.item_rows.split(",")):
-                        variants[f"xcd K={k} deg>={dg} chunk={ch} phases={ph} items<{ik}"] = \
-                            dict(hubs=k, xcd=True, deg=dg, chunk=ch, phases=ph, ik=ik)
+                        for si in (int(v) or None for v in args.small_items.split(",")):
+                            variants[f"xcd K={k} deg>={dg} chunk={ch} phases={ph} items<{ik} "
+                                     f"small>={si}"] = dict(hubs=k, xcd=True, deg=dg, chunk=ch,
+                                                            phases=ph, ik=ik, si=si)
 
     def call(v):
         if v.get("xcd"):
             ops.XCD_MIN_DEG, ops.XCD_CHUNK = v["deg"], v["chunk"]
             ops.XCD_PHASES, ops.XCD_ITEM_ROWS = v["phases"], v["ik"]
+            ops.XCD_SMALL_ITEM = v["si"]
         return spmm_forward(g, X, b, out=Y, hubs=v["hubs"], xcd=v["xcd"])
 
     scale = float(ref.abs().max())
@@ -83,7 +89,7 @@ def main():
         v["err"] = err
         if v.get("xcd") and args.op == "spmm":
             xp = g.xcd_hub_plan(min(v["hubs"], n), v["deg"], min(v["chunk"], ops.seg_len_for(F)),
-                                v["phases"], v["ik"])
+                                v["phases"], v["ik"], v["si"])
             v["items"] = xp.n_items if xp is not None else 0
     print(json.dumps({"op": args.op, "workload": args.workload, "feat": F, "nnz": g.nnz}),
           flush=True)
