@@ -75,6 +75,8 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_normalize_features_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     "gnn_gat_project_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _i64,
                                            _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
+    "gnn_gat_project_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64,
+                                                _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
     "gnn_gat_csr_f32": (ctypes.c_int, [
         _vp, _vp, _i64,                 # rowptr, col, n_rows
         _vp, _i64, _i64, _i64,          # wh, ldw, heads, fh

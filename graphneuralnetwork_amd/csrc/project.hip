@@ -73,11 +73,12 @@ __device__ __forceinline__ void proj_tile_sync() {
 #endif
 }
 
-template <int K, int NT>
+template <int K, int NT, bool COLROW>
 __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
     const float* __restrict__ w2, int heads, float* __restrict__ wh, int64_t ldwh,
-    float* __restrict__ el, float* __restrict__ er, int64_t lde) {
+    float* __restrict__ el, float* __restrict__ er, int64_t lde,
+    const int64_t* __restrict__ col_row) {
   constexpr int S = K / 4;   // MFMA k-steps
   constexpr int FO = 16 * NT;
   constexpr int LDA = 4 * ProjLds<K>::L4;  // LDS row (floats), see ProjLds
@@ -198,17 +199,29 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
     for (int j = 0; j < G; ++j) {
       const int64_t orow = row0 + 16 * j + r;
       if (orow < n_rows) {
+        // col_row: Wh and er are the column side of the aggregation -- rows in the
+        // column order of a degree-ordered graph; el (the row side) stays in place
+        // (a template flag: the index load and range check cost 10 % of the in-order
+        // launch when compiled in, profiles/r03i_proj_colrow_ab.log)
+        int64_t crow = orow;
+        bool cok = true;
+        if constexpr (COLROW) {
+          crow = col_row[orow];
+          cok = crow >= 0 && crow < n_rows;  // an id out of range is not stored
+          crow = cok ? crow : 0;
+        }
 #ifndef GNN_PROJ_NO_WH
 #pragma unroll
         for (int t = 0; t < NT; ++t)
-          *reinterpret_cast<float4*>(wh + orow * ldwh + 16 * t + 4 * q) =
-              make_float4(acc[j][t][0], acc[j][t][1], acc[j][t][2], acc[j][t][3]);
+          if (cok)
+            *reinterpret_cast<float4*>(wh + crow * ldwh + 16 * t + 4 * q) =
+                make_float4(acc[j][t][0], acc[j][t][1], acc[j][t][2], acc[j][t][3]);
 #endif
         if (vec_logits) {  // heads % 4 == 0: quarter q holds 4 whole logits of el or er
           const int c = 4 * q;
-          if (c < 2 * heads)
+          if (c < 2 * heads && (c < heads || cok))
             *reinterpret_cast<float4*>(c < heads ? el + orow * lde + c
-                                                 : er + orow * lde + c - heads) =
+                                                 : er + crow * lde + c - heads) =
                 make_float4(acc2[j][0], acc2[j][1], acc2[j][2], acc2[j][3]);
         } else {
 #pragma unroll
@@ -216,8 +229,8 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
             const int c = 4 * q + i;
             if (c < heads)
               el[orow * lde + c] = acc2[j][i];
-            else if (c < 2 * heads)
-              er[orow * lde + c - heads] = acc2[j][i];
+            else if (c < 2 * heads && cok)
+              er[crow * lde + c - heads] = acc2[j][i];
           }
         }
       }
@@ -238,7 +251,7 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
 template <int K, int NT>
 static int launch_project(const float* x, int64_t ldx, int64_t n_rows, const float* w,
                           const float* w2, int heads, float* wh, int64_t ldwh, float* el,
-                          float* er, int64_t lde, hipStream_t s) {
+                          float* er, int64_t lde, const int64_t* col_row, hipStream_t s) {
   const int64_t groups = (n_rows + 16 * kProjG * kProjWaves - 1) / (16 * kProjG * kProjWaves);
 #ifndef GNN_PROJ_GRID
 // 512 = the resident workgroups at 2 waves/SIMD (144 VGPRs): A/B at cfg3 with isolated
@@ -247,22 +260,28 @@ static int launch_project(const float* x, int64_t ldx, int64_t n_rows, const flo
 #define GNN_PROJ_GRID 512
 #endif
   const int64_t grid = groups < GNN_PROJ_GRID ? groups : GNN_PROJ_GRID;  // W resident across groups
-  hipLaunchKernelGGL((gat_project_kernel<K, NT>), dim3(static_cast<unsigned>(grid)),
-                     dim3(kProjBlock), 0, s, x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er,
-                     lde);
+  if (col_row != nullptr)
+    hipLaunchKernelGGL((gat_project_kernel<K, NT, true>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kProjBlock), 0, s, x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er,
+                       lde, col_row);
+  else
+    hipLaunchKernelGGL((gat_project_kernel<K, NT, false>), dim3(static_cast<unsigned>(grid)),
+                       dim3(kProjBlock), 0, s, x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er,
+                       lde, col_row);
   return launch_status();
 }
 
 template <int K>
 static int dispatch_project_nt(int64_t fout, const float* x, int64_t ldx, int64_t n_rows,
                                const float* w, const float* w2, int heads, float* wh,
-                               int64_t ldwh, float* el, float* er, int64_t lde, hipStream_t s) {
+                               int64_t ldwh, float* el, float* er, int64_t lde,
+                               const int64_t* col_row, hipStream_t s) {
   // B fragments live in registers: (K / 4) * NT <= 64
-  if (fout == 16) return launch_project<K, 1>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, s);
+  if (fout == 16) return launch_project<K, 1>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row, s);
   if constexpr (K <= 128)
-    if (fout == 32) return launch_project<K, 2>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, s);
+    if (fout == 32) return launch_project<K, 2>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row, s);
   if constexpr (K <= 64)
-    if (fout == 64) return launch_project<K, 4>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, s);
+    if (fout == 64) return launch_project<K, 4>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row, s);
   return GNN_E_UNSUPPORTED;
 }
 
@@ -279,11 +298,11 @@ extern "C" int gnn_gat_project_supported(int64_t k, int64_t fout, int64_t fh) {
   return 0;
 }
 
-extern "C" int gnn_gat_project_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
-                                   const float* w, int64_t fout, const float* a_src,
-                                   const float* a_dst, int64_t heads, int64_t fh, float* wh,
-                                   int64_t ldwh, float* el, float* er, int64_t lde,
-                                   float* w2_scratch, void* stream) {
+static int project_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                         const float* w, int64_t fout, const float* a_src, const float* a_dst,
+                         int64_t heads, int64_t fh, float* wh, int64_t ldwh, float* el,
+                         float* er, int64_t lde, const int64_t* col_row, float* w2_scratch,
+                         void* stream) {
   if (n_rows < 0 || heads < 1 || fh < 1 || heads * fh != fout || ldx < k || ldwh < fout ||
       lde < heads)
     return GNN_E_ARG;
@@ -298,10 +317,30 @@ extern "C" int gnn_gat_project_f32(const float* x, int64_t ldx, int64_t n_rows, 
                      a_dst, h, static_cast<int>(fh), w2_scratch);
   const float* w2 = w2_scratch;
   switch (k) {
-    case 16: return dispatch_project_nt<16>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
-    case 32: return dispatch_project_nt<32>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
-    case 64: return dispatch_project_nt<64>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
-    case 128: return dispatch_project_nt<128>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
-    default: return dispatch_project_nt<256>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, s);
+    case 16: return dispatch_project_nt<16>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
+    case 32: return dispatch_project_nt<32>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
+    case 64: return dispatch_project_nt<64>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
+    case 128: return dispatch_project_nt<128>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
+    default: return dispatch_project_nt<256>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
   }
+}
+
+extern "C" int gnn_gat_project_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                                   const float* w, int64_t fout, const float* a_src,
+                                   const float* a_dst, int64_t heads, int64_t fh, float* wh,
+                                   int64_t ldwh, float* el, float* er, int64_t lde,
+                                   float* w2_scratch, void* stream) {
+  return project_entry(x, ldx, n_rows, k, w, fout, a_src, a_dst, heads, fh, wh, ldwh, el, er,
+                       lde, nullptr, w2_scratch, stream);
+}
+
+extern "C" int gnn_gat_project_rows_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                                        const float* w, int64_t fout, const float* a_src,
+                                        const float* a_dst, int64_t heads, int64_t fh,
+                                        float* wh, int64_t ldwh, float* el, float* er,
+                                        int64_t lde, const int64_t* col_row,
+                                        float* w2_scratch, void* stream) {
+  if (n_rows > 0 && col_row == nullptr) return GNN_E_ARG;
+  return project_entry(x, ldx, n_rows, k, w, fout, a_src, a_dst, heads, fh, wh, ldwh, el, er,
+                       lde, col_row, w2_scratch, stream);
 }

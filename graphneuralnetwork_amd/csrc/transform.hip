@@ -47,7 +47,7 @@ using tf32x4 = __attribute__((ext_vector_type(4))) float;
 // row order (a degree-ordered graph's, graph.degree_order) while X is read in order; ids
 // outside [0, n_y) are not stored and raise *err. The stores are scattered 64-B row pieces
 // (fire and forget); a gather on the X side would put the index load in front of every tile.
-template <int K, int CB, int NW, bool RELU, int TR>
+template <int K, int CB, int NW, bool RELU, int TR, bool SCATTER>
 __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
     float* __restrict__ y, int64_t ldy, const int64_t* __restrict__ y_row, int64_t n_y,
@@ -124,7 +124,8 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
     for (int j = 0; j < TR / 16; ++j) {
       const int64_t orow = row0 + j * 16 + r;
       dst[j] = orow;
-      if (y_row != nullptr && orow < n_rows) dst[j] = y_row[orow];
+      if constexpr (SCATTER)
+        if (orow < n_rows) dst[j] = y_row[orow];
     }
     tf32x4 acc[TR / 16][CB];
 #pragma unroll
@@ -169,9 +170,8 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
     for (int j = 0; j < TR / 16; ++j) {
       // acc[j][cb][i] = Y[row0 + 16 j + r][(wv*CB + cb)*16 + 4q + i]
       const int64_t orow = dst[j];
-      const bool ok = y_row == nullptr || (orow >= 0 && orow < n_y);
-      if (y_row != nullptr && !ok && row0 + j * 16 + r < n_rows && q == 0 && wv == 0)
-        atomicOr(err, 1);
+      const bool ok = !SCATTER || (orow >= 0 && orow < n_y);
+      if (SCATTER && !ok && row0 + j * 16 + r < n_rows && q == 0 && wv == 0) atomicOr(err, 1);
       if (row0 + j * 16 + r < n_rows && ok) {
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
@@ -199,8 +199,14 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
 #endif
   constexpr int64_t kGrid = GNN_TF_GRID * kTfWaves / NW;  // 8-wave workgroups: 1 per CU
   const int64_t grid = tiles < kGrid ? tiles : kGrid;
-  hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR>), dim3(static_cast<unsigned>(grid)),
-                     dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err);
+  if (ri.row != nullptr)  // a template flag: no index loads in the in-order kernel
+    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, true>),
+                       dim3(static_cast<unsigned>(grid)), dim3(NW * kWave), 0, s, x, ldx, n_rows,
+                       w, y, ldy, ri.row, ri.n_y, ri.err);
+  else
+    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, false>),
+                       dim3(static_cast<unsigned>(grid)), dim3(NW * kWave), 0, s, x, ldx, n_rows,
+                       w, y, ldy, ri.row, ri.n_y, ri.err);
   return launch_status();
 }
 

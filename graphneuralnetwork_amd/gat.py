@@ -22,6 +22,10 @@ does not cover or when autograd needs the GEMM), and one HIP launch for the
 fused edge-softmax + aggregation (+ ELU) over the CSR adjacency.  ``adj`` may be the
 reference's dense tensor, a torch sparse tensor or a ``CsrGraph``.
 
+At inference on graphs whose Wh is hub-staged, the layer runs over the column-degree-ordered
+graph A P^T (``_AttentionBase._ordered``): the projection writes Wh / er in that column order
+and the aggregation reads their hub rows in place (no per-call staging copies).
+
 Training: the aggregation is an autograd Function whose backward is three
 more HIP passes (gat_bwd.hip: ELU/softmax backward, SDDMM edge gradients,
 transposed aggregation), with the forward's per-row log-sum-exp and dropout
@@ -34,7 +38,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
-from .ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_backward, gat_logits, gat_project
+from .ops import (GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_backward, gat_column_order,
+                  gat_logits, gat_project)
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
@@ -84,6 +89,11 @@ def _project(x, W, heads, fh, a_src, a_dst):
     return torch.mm(x, W), None
 
 
+def _inference(x, *params) -> bool:
+    return x.is_cuda and not (torch.is_grad_enabled() and
+                              (x.requires_grad or any(p.requires_grad for p in params)))
+
+
 def _dropout_seed() -> int:
     return int(torch.randint(0, 2 ** 62, (1,)).item())
 
@@ -113,10 +123,37 @@ class _AttentionBase(nn.Module):
             assert not torch.isnan(out).any()
         return out
 
+    def _ordered(self, x, W, heads, fh, a_src, a_dst, adj, activation):
+        """Inference over the column-degree-ordered graph A P^T (ops.gat_column_order): the
+        projection writes Wh / er in its column order (el in place) and the aggregation reads
+        the hub rows of Wh / er in place. Same values, output rows in the original order.
+        None when it does not apply (training, dropout, small graph, uncovered shape)."""
+        if self.training or not _inference(x, W, a_src, a_dst):
+            return None
+        g = as_csr(adj, self.PREDICATE)
+        if g.n_rows != x.shape[0] or g.n_cols != x.shape[0]:
+            return None
+        order = gat_column_order(g, heads, fh)
+        if order is None:
+            return None
+        r = gat_project(x, W, heads, fh, a_src, a_dst, col_rows=order.inv)
+        if r is None:
+            return None
+        Wh, el, er = r
+        if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
+            assert not torch.isnan(Wh).any()
+        out = gat_aggregate(order.graph, Wh, el, er, heads, fh, self.alpha, self.MODE, activation)
+        if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
+            assert not torch.isnan(out).any()
+        return out
+
     def forward(self, h, adj, activation: str | None = "__concat__"):
         if activation == "__concat__":
             activation = "elu" if self.concat else None
         a_src, a_dst = self._a_parts()
+        out = self._ordered(h, self.W, 1, self.out_features, a_src, a_dst, adj, activation)
+        if out is not None:
+            return out
         Wh, logits = _project(h, self.W, 1, self.out_features, a_src, a_dst)
         if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
             assert not torch.isnan(Wh).any()
@@ -195,6 +232,9 @@ class GATBase(nn.Module):
         parts = [m._a_parts() for m in heads]
         a_src = torch.cat([p[0] for p in parts])
         a_dst = torch.cat([p[1] for p in parts])
+        out = first._ordered(x, W, len(heads), fh, a_src, a_dst, adj, "elu")
+        if out is not None:
+            return out
         Wh, logits = _project(x, W, len(heads), fh, a_src, a_dst)  # one MFMA pass, all heads
         if first.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
             assert not torch.isnan(Wh).any()

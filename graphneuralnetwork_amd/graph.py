@@ -198,6 +198,18 @@ class HubPlan:
     def k(self) -> int:
         return int(self.hub_ids.numel())
 
+    @property
+    def prefix(self) -> bool:
+        """True when the hub rows are the first k rows in rank order (a graph relabelled by
+        ``degree_order``): the staged table is then the operand itself, no copy needed."""
+        v = self.__dict__.get("_prefix")
+        if v is None:
+            ids = self.hub_ids
+            v = bool(torch.equal(ids, torch.arange(ids.numel(), device=ids.device,
+                                                   dtype=ids.dtype)))
+            self.__dict__["_prefix"] = v
+        return v
+
 
 # gfx950: 8 XCDs with one 4 MiB L2 each; the workgroups of a launch are dealt to them
 # round-robin (workgroup w runs on XCD w % 8), and the SpMM kernel runs 4 waves per
@@ -243,13 +255,7 @@ class XcdHubPlan:
     def prefix(self) -> bool:
         """True when the hub rows are X's first k rows in rank order (a graph relabelled by
         ``degree_order``): the staged table is then X itself and needs no copy."""
-        v = self.__dict__.get("_prefix")
-        if v is None:
-            ids = self.hub.hub_ids
-            v = bool(torch.equal(ids, torch.arange(ids.numel(), device=ids.device,
-                                                   dtype=ids.dtype)))
-            self.__dict__["_prefix"] = v
-        return v
+        return self.hub.prefix
 
     def direct(self) -> tuple["CsrGraph", "CsrGraph"]:
         """(items, rest) of a prefix plan with the hub references turned back into X row ids

@@ -110,8 +110,8 @@ def _spmm_hub_call(lib, g: CsrGraph, col: torch.Tensor, plan, pargs, x, xh, feat
                    partial, flags, stream, what):
     _lib.check(lib.gnn_spmm_csr_hub_f32(
         g.rowptr.data_ptr(), col.data_ptr(), g.val.data_ptr(), g.n_rows, x.data_ptr(),
-        x.stride(0), xh.data_ptr(), feat, feat, _lib.ptr(bias), y.data_ptr(), ldy, plan.seg_len,
-        *pargs, _lib.ptr(partial), flags, stream), what)
+        x.stride(0), xh.data_ptr(), xh.stride(0), feat, _lib.ptr(bias), y.data_ptr(), ldy,
+        plan.seg_len, *pargs, _lib.ptr(partial), flags, stream), what)
 
 
 def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
@@ -178,10 +178,14 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
     tasks = _tasks_ok(feat, x, out, bias, partial)
     if k > 0 and g.nnz:
         hp = g.hub_plan(k)
-        xh = torch.empty((hp.k, feat), dtype=torch.float32, device=x.device)
-        _lib.check(lib.gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0],
-                                           hp.hub_ids.data_ptr(), hp.k, feat, xh.data_ptr(), feat,
-                                           hp.err.data_ptr(), stream), "gnn_gather_rows_f32")
+        if XCD_DIRECT and hp.prefix:  # degree-ordered columns: the hub rows are X's first rows
+            xh = x
+        else:
+            xh = torch.empty((hp.k, feat), dtype=torch.float32, device=x.device)
+            _lib.check(lib.gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0],
+                                               hp.hub_ids.data_ptr(), hp.k, feat, xh.data_ptr(),
+                                               feat, hp.err.data_ptr(), stream),
+                       "gnn_gather_rows_f32")
         if tasks:
             gh = CsrGraph(g.rowptr, hp.col_hub, g.val, g.n_rows, g.n_cols)
             _spmm_tasks_call(lib, gh, hp.col_hub, g.task_plan(seg, TASK_MAX_DEG, TASK_COST), x,
@@ -191,7 +195,7 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
             return out
         rc = lib.gnn_spmm_csr_hub_f32(
             g.rowptr.data_ptr(), hp.col_hub.data_ptr(), g.val.data_ptr(), g.n_rows,
-            x.data_ptr(), x.stride(0), xh.data_ptr(), feat, feat, _lib.ptr(bias),
+            x.data_ptr(), x.stride(0), xh.data_ptr(), xh.stride(0), feat, _lib.ptr(bias),
             out.data_ptr(), out.stride(0), plan.seg_len, *pargs, _lib.ptr(partial), flags, stream)
         _lib.check(rc, "gnn_spmm_csr_hub_f32")
         return out
@@ -252,6 +256,15 @@ def _spmm_xcd(lib, g: CsrGraph, xp, x, feat, bias, out, seg, skip_empty, flags, 
 DEGREE_ORDER = True
 
 
+def _cached_column_order(g: CsrGraph):
+    key = ("_colorder",)
+    o = g._plans.get(key)
+    if o is None:
+        from .graph import degree_order
+        o = g._plans[key] = degree_order(g, rows=False)
+    return o
+
+
 def column_order(g: CsrGraph, feat: int):
     """The cached ``DegreeOrder(rows=False)`` of ``g`` when a feat-wide SpMM over it would
     take the XCD-sliced hub path (else None)."""
@@ -259,12 +272,18 @@ def column_order(g: CsrGraph, feat: int):
         return None
     if xcd_hub_rows_for(g.n_cols, feat) < 8 * XCD_PHASES:
         return None
-    key = ("_colorder",)
-    o = g._plans.get(key)
-    if o is None:
-        from .graph import degree_order
-        o = g._plans[key] = degree_order(g, rows=False)
-    return o
+    return _cached_column_order(g)
+
+
+def gat_column_order(g: CsrGraph, heads: int, fh: int):
+    """The cached ``DegreeOrder(rows=False)`` of ``g`` when the GAT aggregation over it would
+    stage hub rows of Wh / er (``hub_rows_for``; else None): over A P^T those rows are the
+    first rows of the projection's column-ordered output, read in place."""
+    if not (DEGREE_ORDER and XCD_DIRECT) or g.nnz == 0:
+        return None
+    if hub_rows_for(g.n_cols, heads * fh + heads) == 0:
+        return None
+    return _cached_column_order(g)
 
 
 def _spmm_xcd_direct(lib, xp, x, feat, bias, out, seg, skip_empty, flags, stream):
@@ -350,13 +369,17 @@ def gat_logits(wh: torch.Tensor, heads: int, fh: int, a_src: torch.Tensor,
 
 
 def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: torch.Tensor,
-                a_dst: torch.Tensor, packed: bool = False):
+                a_dst: torch.Tensor, packed: bool = False, col_rows: torch.Tensor | None = None):
     """(Wh = x @ w, el, er) in one MFMA pass (inference; no autograd), or None when the
     shape is not covered by gnn_gat_project_f32 (the caller then uses torch.mm +
     gat_logits). ``packed``: the three are views of ONE [n, H*Fh + 2H] buffer, rows
     [Wh | er | el], so the aggregation's er gather lands next to the Wh row it also
     gathers. Same output bits; measured neutral at cfg3 on a slow box (1.297 vs 1.298 ms,
-    profiles/r01i_gat_pack_ab_slow.log), so it is not the default."""
+    profiles/r01i_gat_pack_ab_slow.log), so it is not the default.
+
+    ``col_rows`` (int64 [n], a permutation): Wh and er of node i go to row col_rows[i], el
+    stays at row i (gnn_gat_project_rows_f32) -- the operands of the aggregation over a
+    column-degree-ordered graph (``gat_column_order``; col_rows = its ``inv``)."""
     _require_device(x, w, a_src, a_dst)
     if (x.dtype != torch.float32 or w.dtype != torch.float32 or x.dim() != 2 or w.dim() != 2
             or x.shape[1] != w.shape[0] or w.shape[1] != heads * fh):
@@ -368,6 +391,13 @@ def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: to
     if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
         x = x.contiguous()
     n = x.shape[0]
+    if col_rows is not None:
+        _require_device(col_rows)
+        if packed:
+            raise ValueError("col_rows= needs separate el / er buffers (packed=False)")
+        if col_rows.dtype != torch.int64 or col_rows.shape != (n,):
+            raise TypeError("col_rows must be int64 [rows of x]")
+        col_rows = col_rows.contiguous()
     if packed:
         buf = torch.empty((n, fout + 2 * heads), dtype=torch.float32, device=x.device)
         wh, er, el = buf[:, :fout], buf[:, fout:fout + heads], buf[:, fout + heads:]
@@ -376,6 +406,14 @@ def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: to
         el = torch.empty((n, heads), dtype=torch.float32, device=x.device)
         er = torch.empty((n, heads), dtype=torch.float32, device=x.device)
     w2 = torch.empty((k, 16), dtype=torch.float32, device=x.device)
+    if col_rows is not None:
+        _lib.check(lib.gnn_gat_project_rows_f32(
+            x.data_ptr(), x.stride(0), n, k, w.contiguous().data_ptr(), fout,
+            a_src.contiguous().data_ptr(), a_dst.contiguous().data_ptr(), heads, fh,
+            wh.data_ptr(), wh.stride(0), el.data_ptr(), er.data_ptr(), el.stride(0),
+            col_rows.data_ptr(), w2.data_ptr(), _lib.stream_handle(x.device)),
+            "gnn_gat_project_rows_f32")
+        return wh, el, er
     _lib.check(lib.gnn_gat_project_f32(
         x.data_ptr(), x.stride(0), n, k, w.contiguous().data_ptr(), fout,
         a_src.contiguous().data_ptr(), a_dst.contiguous().data_ptr(), heads, fh, wh.data_ptr(),
@@ -651,14 +689,19 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
     k = hub_rows_for(g.n_cols, feat + heads) if hubs is None else min(int(hubs), g.n_cols)
     if k > 0 and g.nnz:
         hp = g.hub_plan(k)
-        whh = torch.empty((hp.k, feat), dtype=torch.float32, device=wh.device)
-        erh = torch.empty((hp.k, heads), dtype=torch.float32, device=wh.device)
-        for src, dst, w in ((wh, whh, feat), (er, erh, heads)):
-            _lib.check(lib.gnn_gather_rows_f32(src.data_ptr(), src.stride(0), src.shape[0],
-                                               hp.hub_ids.data_ptr(), hp.k, w, dst.data_ptr(), w,
-                                               hp.err.data_ptr(), stream), "gnn_gather_rows_f32")
+        if XCD_DIRECT and hp.prefix:  # degree-ordered columns: hub rows read in place
+            whh, ldwh, erh, lderh = wh, wh.stride(0), er, lde
+        else:
+            whh = torch.empty((hp.k, feat), dtype=torch.float32, device=wh.device)
+            erh = torch.empty((hp.k, heads), dtype=torch.float32, device=wh.device)
+            ldwh, lderh = feat, heads
+            for src, dst, w in ((wh, whh, feat), (er, erh, heads)):
+                _lib.check(lib.gnn_gather_rows_f32(src.data_ptr(), src.stride(0), src.shape[0],
+                                                   hp.hub_ids.data_ptr(), hp.k, w,
+                                                   dst.data_ptr(), w, hp.err.data_ptr(), stream),
+                           "gnn_gather_rows_f32")
         rc = lib.gnn_gat_csr_hub_f32(g.rowptr.data_ptr(), hp.col_hub.data_ptr(), *args,
-                                     whh.data_ptr(), feat, erh.data_ptr(), heads)
+                                     whh.data_ptr(), ldwh, erh.data_ptr(), lderh)
         _lib.check(rc, "gnn_gat_csr_hub_f32")
         return out
     rc = lib.gnn_gat_csr_f32(g.rowptr.data_ptr(), g.col.data_ptr(), *args)

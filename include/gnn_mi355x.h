@@ -240,6 +240,19 @@ int gnn_gat_project_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, 
                         float* w2_scratch, void* stream);
 
 /*
+ * The same with the column side scattered: wh and er of node n go to row col_row[n], el stays
+ * at row n -- the operands of the aggregation over a column-degree-ordered graph A P^T
+ * (col_row = the order's inv; GAT/models/layers.py:23-26 unchanged in value). el and er must
+ * be separate [n_rows, lde] buffers. Rows whose col_row id is outside [0, n_rows) are not
+ * stored.
+ */
+int gnn_gat_project_rows_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                             const float* w, int64_t fout, const float* a_src,
+                             const float* a_dst, int64_t heads, int64_t fh, float* wh,
+                             int64_t ldwh, float* el, float* er, int64_t lde,
+                             const int64_t* col_row, float* w2_scratch, void* stream);
+
+/*
  * GAT edge-softmax + neighbour aggregation over CSR, all heads in one pass:
  *   out[i, h*fh+f] = act( sum_{j in row i} p_ijh * Wh[j, h*fh+f] / sum_j p_ijh )
  * mode 0 (dense layer, GAT/models/layers.py:22-37):

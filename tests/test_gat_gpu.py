@@ -441,3 +441,57 @@ def test_gat_project_unsupported_shapes_fall_back(dev):
     w = torch.randn(64, 16, device=dev)
     wh, _, _ = gat_project(big[:, 1:], w, 2, 8, torch.randn(16, device=dev), torch.randn(16, device=dev))
     close(wh.cpu().numpy(), big[:, 1:].cpu().double().numpy() @ w.cpu().double().numpy())
+
+
+def test_gat_project_col_rows_bitexact(dev):
+    """gat_project(col_rows=inv): Wh / er of node i land in row inv[i], el stays in row i;
+    the values are the in-order projection's bits. An id out of range is not stored."""
+    from graphneuralnetwork_amd.ops import gat_project
+    n, H, fh, k = 3000, 8, 8, 64
+    x = torch.randn(n, k, device=dev)
+    w = torch.randn(k, H * fh, device=dev) * 0.2
+    a_s, a_d = torch.randn(H * fh, device=dev) * 0.3, torch.randn(H * fh, device=dev) * 0.3
+    wh0, el0, er0 = gat_project(x, w, H, fh, a_s, a_d)
+    inv = torch.randperm(n, device=dev)
+    wh, el, er = gat_project(x, w, H, fh, a_s, a_d, col_rows=inv)
+    assert torch.equal(wh[inv], wh0) and torch.equal(er[inv], er0) and torch.equal(el, el0)
+    bad = inv.clone()
+    bad[5] = n + 7
+    wh2, el2, er2 = gat_project(x, w, H, fh, a_s, a_d, col_rows=bad)
+    keep = torch.ones(n, dtype=torch.bool, device=dev)
+    keep[5] = False
+    assert torch.equal(wh2[bad[keep]], wh0[keep]) and torch.equal(el2, el0)
+    with pytest.raises(ValueError):
+        gat_project(x, w, H, fh, a_s, a_d, packed=True, col_rows=inv)
+
+
+@pytest.mark.parametrize("kind", ["GAT", "SpGAT"])
+def test_gat_model_column_order(dev, kind, monkeypatch):
+    """GAT / SpGAT inference on a graph whose Wh is hub-staged: every attention layer runs
+    over the column-degree-ordered graph (projection rows scattered, hub rows read in place)
+    and equals the natural-order path bit for bit (no edgeless rows) and the oracle."""
+    from graphneuralnetwork_amd import gat as gat_mod
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.graph import CsrGraph
+    monkeypatch.setattr(ops, "HUB_MIN_X_BYTES", 0)
+    n, nfeat = 2500, 64
+    rowptr, col = _rand_csr(n, 8 * n, 21, hub=1800)
+    assert (np.diff(rowptr) > 0).all()
+    torch.manual_seed(0)
+    model = getattr(gat_mod, kind)(nfeat, 8, 16, 0.1, 0.2, 8).to(dev).eval()
+    x = torch.randn(n, nfeat, device=dev)
+
+    def graph():
+        return CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                        torch.ones(col.size, device=dev), n, n)
+
+    g = graph()
+    with torch.no_grad():
+        y = model(x, g)
+        assert ("_colorder",) in g._plans
+        hp = next(p for key, p in g._plans[("_colorder",)].graph._plans.items()
+                  if isinstance(key, tuple) and key[0] == "_hub")
+        assert hp.prefix
+        monkeypatch.setattr(ops, "DEGREE_ORDER", False)
+        y_nat = model(x, graph())
+    assert torch.equal(y, y_nat)
