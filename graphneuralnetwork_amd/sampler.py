@@ -211,6 +211,26 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
     return batch
 
 
+def degree_ordered(adj: CsrGraph, table: torch.Tensor | None = None):
+    """The dataset relabelled once by degree (``graph.degree_order``, rows and columns): the
+    highest-degree nodes get the smallest ids, so the rows the sampled batches gather most
+    often sit together at the top of the feature table (fewer pages, more L2 / Infinity-Cache
+    hits: cfg4 layer-0 gather 51.9 -> 45.5 us, forward 135 -> 128 us,
+    profiles/r03j_sage_order_probe.log). Returns ``(adj', table', order)``: adj' keeps
+    ascending neighbours per row (``symmetric_adjacency``'s layout), table' = table[perm];
+    a seed v becomes ``order.inv[v]``, and every output row stays the row of its seed."""
+    from .graph import degree_order
+    o = degree_order(adj, rows=True)
+    g = o.graph
+    n = g.n_rows
+    rows = torch.repeat_interleave(torch.arange(n, device=g.device, dtype=torch.int64),
+                                   g.rowptr[1:] - g.rowptr[:-1])
+    key = torch.sort(rows * n + g.col.to(torch.int64)).values
+    del rows
+    g2 = CsrGraph(g.rowptr, (key % n).to(torch.int32).contiguous(), g.val, n, n)
+    return g2, (o.permute_rows(table) if table is not None else None), o
+
+
 def symmetric_adjacency(src, dst, n: int, device=None) -> CsrGraph:
     """Undirected neighbour lists without self-loops (the reference's ``adj_lists`` of sets,
     GraphSAGE/data_utils.py:30-38) as a CSR with ascending neighbours."""

@@ -214,3 +214,25 @@ def test_xcd_direct_plan_algebra():
     Y = _csr_spmm(np.repeat(np.arange(n), np.diff(rpr)), rcol, rest.val.numpy(), n, src)
     want = O.spmm_csr(gp.rowptr.numpy(), gp.col.numpy(), gp.val.numpy(), X)
     np.testing.assert_allclose(Y, want, rtol=1e-12, atol=1e-12)
+
+
+def test_sampler_degree_ordered_dataset():
+    """sampler.degree_ordered (CPU torch ops): node v of the relabelled dataset is node
+    perm[v]; every row keeps its neighbour set (renamed) in ascending order; the table rows
+    follow; degrees are non-increasing."""
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    from graphneuralnetwork_amd.sampler import degree_ordered, symmetric_adjacency
+    n = 3000
+    s, d = rmat_edges(n, 30000, 4)
+    adj = symmetric_adjacency(s, d, n)
+    table = torch.randn(n, 5)
+    g2, t2, o = degree_ordered(adj, table)
+    perm, inv = o.perm.numpy(), o.inv.numpy()
+    rp, c = adj.rowptr.numpy(), adj.col.numpy()
+    rp2, c2 = g2.rowptr.numpy(), g2.col.numpy()
+    assert (np.diff(np.diff(rp2)) <= 0).all()
+    for v in range(n):
+        got = c2[rp2[v]:rp2[v + 1]]
+        want = np.sort(inv[c[rp[perm[v]]:rp[perm[v] + 1]]])
+        np.testing.assert_array_equal(got, want)
+    assert torch.equal(t2, table[o.perm])
