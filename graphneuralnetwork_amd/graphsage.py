@@ -270,7 +270,14 @@ def _fused_sage_layer(block, center, neigh: Gathered):
         y = gcn_transform(buf, W, relu=True)
         if y is not None:
             return y
-    zero = torch.zeros(W.shape[0], dtype=W.dtype, device=W.device)
+    # the addmm's bias operand: a zero vector cached on the block (not a registered buffer,
+    # so state_dict keys stay the reference's); a fresh torch.zeros cost a 5 us fill launch
+    # per call (profiles/r03k_sage_trace_summary.txt)
+    zero = block.__dict__.get("_zero_bias")
+    if zero is None or zero.device != W.device or zero.dtype != W.dtype or \
+            zero.numel() != W.shape[0]:
+        zero = torch.zeros(W.shape[0], dtype=W.dtype, device=W.device)
+        block.__dict__["_zero_bias"] = zero
     return torch._addmm_activation(zero, buf, W.t())
 
 
