@@ -440,7 +440,8 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
     ``out_rows`` (int64 [rows of x]): x row i goes to support row out_rows[i]
     (gnn_gcn_transform_rows_f32), e.g. a degree order's ``inv`` so that the support is in the
     degree-ordered graph's column order; ``out`` (or a new [rows of x, fout] tensor) receives
-    it. ``check_rows=False`` skips the host read of the range-check flag (trusted ids, e.g. a
+    it; the ids must not repeat (two rows stored to one support row leave either).
+    ``check_rows=False`` skips the host read of the range-check flag (trusted ids, e.g. a
     ``DegreeOrder``'s; the kernel still skips the store of a bad id)."""
     _require_device(x, weight)
     if (x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 2

@@ -192,8 +192,9 @@ int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k
  * column-degree-ordered graph A P^T reads it (A P^T . P (X W^T) = A . X W^T:
  * Graph_conv_layer's output rows stay in the original order), so the SpMM gathers its hub
  * rows from the first rows of y with no staging copy. Rows whose id is outside [0, n_y) are
- * not stored and set *err_flag = 1. Same shapes, alignment and return codes as
- * gnn_gcn_transform_f32.
+ * not stored and set *err_flag = 1. y_row must not repeat an id (a permutation or another
+ * injective map): two rows stored to one output row leave either. Same shapes, alignment and
+ * return codes as gnn_gcn_transform_f32.
  */
 int gnn_gcn_transform_rows_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
                                const float* w, int64_t fout, float* y, int64_t ldy,
@@ -244,7 +245,7 @@ int gnn_gat_project_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, 
  * at row n -- the operands of the aggregation over a column-degree-ordered graph A P^T
  * (col_row = the order's inv; GAT/models/layers.py:23-26 unchanged in value). el and er must
  * be separate [n_rows, lde] buffers. Rows whose col_row id is outside [0, n_rows) are not
- * stored.
+ * stored; col_row must not repeat an id (a permutation).
  */
 int gnn_gat_project_rows_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
                              const float* w, int64_t fout, const float* a_src,
