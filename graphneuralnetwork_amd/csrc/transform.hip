@@ -213,17 +213,33 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
 #ifndef GNN_TF_MIN_TR
 #define GNN_TF_MIN_TR 16  // A/B: 64 = always the round-2 64-row tiles
 #endif
-// Tile rows: 64 unless that leaves CUs without a tile (< 2 tiles per resident workgroup
-// slot), then 32 or 16 -- the fixed cost of a small launch is its first tile.
+#ifndef GNN_TF_TR64_MAX_K
+#define GNN_TF_TR64_MAX_K 64  // K above this: at most 32-row tiles
+#endif
+// Tile rows: 16 or 32 when 64-row tiles would leave CUs without a tile (< 2 tiles per
+// resident workgroup slot): the fixed cost of a small launch is its first tile. K >= 128 runs
+// 32-row tiles at every size: in one process (tools/transform_tile_ab.py,
+// profiles/r03m_transform_tile_ab2.log) 32 vs 64 rows: K = 256 -> 128 at 62,479 / 200K / 1M
+// rows 40.7 / 111.8 / 524 vs 44.3 / 124.5 / 559 us, K = 128 -> 128 at 1M / 10M rows 299 /
+// 2891 vs 307 / 2932 us; K = 64 -> 64 keeps 64 rows (95 vs 113 us at 1M).
 template <int K, int CB, int NW, bool RELU>
 static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const float* w,
                             float* y, int64_t ldy, const RowIdx& ri, hipStream_t s) {
   constexpr int64_t slots = GNN_TF_GRID * kTfWaves / NW;
+#ifdef GNN_TF_TR32_ROWS  // A/B: 16-row tiles below GNN_TF_TR16_ROWS, 32-row below this
+#ifndef GNN_TF_TR16_ROWS
+#define GNN_TF_TR16_ROWS (32 * 2 * slots)
+#endif
+  if (n_rows < GNN_TF_TR16_ROWS) return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, s);
+  if (n_rows < GNN_TF_TR32_ROWS) return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, s);
+#endif
   if (GNN_TF_MIN_TR <= 16 && n_rows < 32 * 2 * slots)
     return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, s);
-  if (GNN_TF_MIN_TR <= 32 && n_rows < 64 * 2 * slots)
+  if (GNN_TF_MIN_TR <= 32 && (K > GNN_TF_TR64_MAX_K || n_rows < 64 * 2 * slots))
     return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, s);
-  return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, ri, s);
+  if constexpr (K <= GNN_TF_TR64_MAX_K || GNN_TF_MIN_TR > 32)
+    return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, ri, s);
+  return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, s);
 }
 
 template <int K, bool RELU>
