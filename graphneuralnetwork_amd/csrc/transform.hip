@@ -33,6 +33,12 @@ using tf32x4 = __attribute__((ext_vector_type(4))) float;
 #ifndef GNN_TF_SINGLE_BUFFER
 #define GNN_TF_SINGLE_BUFFER 0  // A/B: the round-2 one-buffer tile loop (two barriers per tile)
 #endif
+#ifndef GNN_TF_K256_CB2
+#define GNN_TF_K256_CB2 0  // A/B: K = 256 -> 128 as 4 waves x 2 column blocks
+#endif
+#ifndef GNN_TF_ONE256
+#define GNN_TF_ONE256 0  // A/B: 256 output columns at K >= 128 as one 8-wave x 2-block launch
+#endif
 
 // NW waves per workgroup, each owning CB 16-column blocks of W (FO = NW * CB * 16); a tile is
 // TR rows of X (TR = 16, 32 or 64: small launches use short tiles so that every CU gets work).
@@ -248,7 +254,7 @@ static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t
                               hipStream_t s) {
   if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
   if (fout == 128) {
-    if constexpr (K <= 128)
+    if constexpr (K <= 128 || GNN_TF_K256_CB2)
       return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
     else
       return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
@@ -256,6 +262,9 @@ static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t
   if (fout == 256) {
     if constexpr (K <= 64) {
       return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
+    } else if constexpr (GNN_TF_ONE256) {
+      // one launch, 8 waves x 2 column blocks: X read and staged once for all 256 columns
+      return launch_transform<K, 2, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
     } else {
       // two launches of the 128-column kernel, one per half of W's rows (output columns);
       // X is read twice, but the launch is MFMA-bound at these K (cfg5's 256 -> 256 layer)

@@ -15,7 +15,8 @@ sys.path.insert(0, str(ROOT))
 VARIANTS = {"base": [], "tr32_1m": ["GNN_TF_TR32_ROWS=1000000"],
             "tr32": ["GNN_TF_TR32_ROWS=(1LL<<40)"],
             "tr16": ["GNN_TF_TR32_ROWS=(1LL<<40)", "GNN_TF_TR16_ROWS=(1LL<<40)"],
-            "grid1024": ["GNN_TF_GRID=1024"]}
+            "grid1024": ["GNN_TF_GRID=1024"],
+            "one256": ["GNN_TF_ONE256=1"], "cb2": ["GNN_TF_K256_CB2=1"]}
 
 
 def main():
