@@ -37,7 +37,7 @@ using tf32x4 = __attribute__((ext_vector_type(4))) float;
 #define GNN_TF_K256_CB2 0  // A/B: K = 256 -> 128 as 4 waves x 2 column blocks
 #endif
 #ifndef GNN_TF_ONE256
-#define GNN_TF_ONE256 0  // A/B: 256 output columns at K >= 128 as one 8-wave x 2-block launch
+#define GNN_TF_ONE256 1  // 0 = A/B: 256 output columns at K >= 128 as two 128-column launches
 #endif
 
 // NW waves per workgroup, each owning CB 16-column blocks of W (FO = NW * CB * 16); a tile is
@@ -263,11 +263,13 @@ static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t
     if constexpr (K <= 64) {
       return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
     } else if constexpr (GNN_TF_ONE256) {
-      // one launch, 8 waves x 2 column blocks: X read and staged once for all 256 columns
+      // one launch, 8 waves x 2 column blocks (128 W values per lane resident, 200 VGPRs):
+      // X read and staged once for all 256 columns. In one process (tools/transform_tile_ab.py,
+      // profiles/r03o_transform_one256_ab.log): 10M x 256 -> 256 9.63 ms (136 TF/s) vs 10.57
+      // as two launches vs 9.95 hipBLASLt; 1M x 128 -> 256 0.545 vs 0.618 vs 0.628 ms
       return launch_transform<K, 2, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
     } else {
-      // two launches of the 128-column kernel, one per half of W's rows (output columns);
-      // X is read twice, but the launch is MFMA-bound at these K (cfg5's 256 -> 256 layer)
+      // A/B: two launches of the 128-column kernel, one per half of W's rows (X read twice)
       const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, s);
       if (rc != GNN_OK) return rc;
       return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, s);

@@ -422,10 +422,10 @@ def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: to
     return wh, el, er
 
 
-# fout = 256 at k > 64 runs as two 128-column launches (X read twice); hipBLASLt is faster there
-# (10M x 256 -> 256: 10.4 vs 11.5 ms, tools/sage_gemm_ab.py --big, profiles/r03f_gemm_ab.log),
-# so those shapes stay on nn.Linear unless this is set
-TRANSFORM_WIDE_MFMA = False
+# fout = 256 at k > 64 (cfg5's 256 -> 256 layer) runs as ONE 8-wave x 2-block launch, faster
+# than hipBLASLt (10M x 256 -> 256: 9.63 vs 9.95 ms, profiles/r03o_transform_one256_ab.log; the
+# round-3 two-launch form lost, 10.57 ms); False keeps those shapes on nn.Linear
+TRANSFORM_WIDE_MFMA = True
 
 
 def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,

@@ -381,7 +381,7 @@ def test_hub_plan_structure(dev):
 
 
 @pytest.mark.parametrize("k,fout", [(16, 64), (32, 128), (64, 64), (64, 256), (128, 128),
-                                    (256, 64), (256, 128)])
+                                    (256, 64), (256, 128), (128, 256), (256, 256)])
 @pytest.mark.parametrize("n", [1, 63, 1000, 4097])
 def test_gcn_transform_mfma(dev, k, fout, n):
     """gnn_gcn_transform_f32 (fp32 MFMA, W [fout, k] as nn.Linear) vs a float64 matmul;
@@ -406,8 +406,8 @@ def test_gcn_transform_fallback_and_training(dev):
     from graphneuralnetwork_amd.ops import gcn_transform
     x = torch.randn(100, 7, device=dev)
     assert gcn_transform(x, torch.randn(5, 7, device=dev)) is None
-    assert gcn_transform(torch.randn(100, 256, device=dev), torch.randn(256, 256, device=dev)) is None
-    assert gcn_transform(torch.randn(100, 128, device=dev), torch.randn(256, 128, device=dev),
+    assert gcn_transform(torch.randn(100, 100, device=dev), torch.randn(128, 100, device=dev)) is None
+    assert gcn_transform(torch.randn(100, 128, device=dev), torch.randn(96, 128, device=dev),
                          relu=True) is None
     n = 300
     rowptr, col, val = _rand_graph(n, 3000, 8)
@@ -495,8 +495,9 @@ def test_packed_tasks_c_abi_contract(dev):
 
 @pytest.mark.parametrize("k", [128, 256])
 def test_gcn_transform_wide_output_c_abi(dev, k):
-    """gnn_gcn_transform_f32 at fout = 256 with k > 64 (two 128-column launches; the Python
-    policy keeps nn.Linear there, TRANSFORM_WIDE_MFMA): against a float64 product."""
+    """gnn_gcn_transform_f32 at fout = 256 with k > 64 (one 8-wave x 2-block launch; the
+    Python policy TRANSFORM_WIDE_MFMA routes Graph_conv_layer there): against a float64
+    product."""
     from graphneuralnetwork_amd import _lib
     n = 3000
     x = torch.randn(n, k, device=dev)
@@ -555,7 +556,7 @@ def test_xcd_direct_degree_order(dev, F, rows, monkeypatch):
     close(y, want[perm.cpu().numpy()] if rows else want)
 
 
-@pytest.mark.parametrize("k,fout", [(64, 64), (128, 128), (256, 128), (64, 256)])
+@pytest.mark.parametrize("k,fout", [(64, 64), (128, 128), (256, 128), (64, 256), (256, 256)])
 def test_transform_out_rows(dev, k, fout):
     """gnn_gcn_transform_rows_f32: y[out_rows[i]] = x[i] W^T, bit-identical to the in-order
     transform scattered (each row's MFMA chain does not depend on the others); a permutation,
