@@ -1,7 +1,8 @@
 """Runs the cfg4 GraphSAGE forward (degree-ordered dataset, 8192 seeds, [25, 10]) REPS times
 after warm-up, for a rocprofv3 --kernel-trace of its kernels:
 
-    rocprofv3 --kernel-trace -d gpurun_out/sage_trace -o run -- python3 tools/sage_forward_trace.py
+    rocprofv3 --kernel-trace -d gpurun_out/sage_trace -o run --output-format csv -- python3 tools/sage_forward_trace.py
+    python3 tools/sage_forward_trace.py --summarize gpurun_out/sage_trace/.../run_kernel_trace.csv
 """
 import sys
 from pathlib import Path
@@ -28,16 +29,53 @@ def main():
     b = sample_batch(adj, seeds, (25, 10), seed=0)
     net = GraphSAGE(2, F, F, False, agg_func="MEAN", Unsupervised=False, class_size=3).to(dev).eval()
     fa = b.forward_args(table)
+    import time
     with torch.no_grad():
         for _ in range(10):
             net(*fa, None, None, None, None, None)
         torch.cuda.synchronize()
-        torch.cuda.nvtx.range_push("forwards") if hasattr(torch.cuda, "nvtx") else None
+        # host enqueue time per forward (no sync inside) vs the wall time until the GPU is done:
+        # equal = the eager forward is paced by the host, not by its kernels
+        t0 = time.perf_counter()
         for _ in range(50):
             net(*fa, None, None, None, None, None)
+        t1 = time.perf_counter()
         torch.cuda.synchronize()
-    print("done", b.frontier.numel())
+        t2 = time.perf_counter()
+    print(f"done frontier {b.frontier.numel()}: host enqueue {(t1 - t0) / 50 * 1e6:.1f} us per "
+          f"forward, wall {(t2 - t0) / 50 * 1e6:.1f} us per forward", flush=True)
+
+
+def summarize(csv_path: str, per: int = 0, last: int = 50) -> None:
+    """Median duration per kernel position of the last ``last`` forwards (``per`` kernels each,
+    default: inferred from the repeating kernel-name cycle) and the median gap before it."""
+    import csv
+    import statistics
+    rows = sorted(csv.DictReader(open(csv_path)), key=lambda r: int(r["Start_Timestamp"]))
+    names = [r["Kernel_Name"] for r in rows]
+    if not per:
+        for p in range(1, 20):
+            if names[-p:] == names[-2 * p:-p] and names[-p:] == names[-3 * p:-2 * p]:
+                per = p
+                break
+    tail = rows[-per * last:]
+    print(f"{per} kernels per forward, last {last} forwards")
+    tot = 0.0
+    for i in range(per):
+        ks = tail[i::per]
+        d = statistics.median((int(k["End_Timestamp"]) - int(k["Start_Timestamp"])) / 1e3 for k in ks)
+        prev = [tail[(i - 1) % per + per * j] if i else (tail[per * j - 1] if j else None)
+                for j in range(last)]
+        g = statistics.median((int(k["Start_Timestamp"]) - int(pv["End_Timestamp"])) / 1e3
+                              for k, pv in zip(ks, prev) if pv is not None)
+        tot += d
+        print(f"  {d:7.1f} us (gap {g:5.1f})  {ks[0]['Kernel_Name'][:110]}")
+    span = (int(tail[-1]["End_Timestamp"]) - int(tail[0]["Start_Timestamp"])) / 1e3 / last
+    print(f"sum of kernels {tot:.1f} us per forward; first start to last end {span:.1f} us per forward")
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[1] == "--summarize":
+        summarize(sys.argv[2])
+    else:
+        main()
