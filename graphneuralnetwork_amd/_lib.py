@@ -70,6 +70,8 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_gcn_transform_supported": (ctypes.c_int, [_i64, _i64]),
     "gnn_gcn_transform_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnn_linear_relu_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "gnn_linear_relu_cls_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64,
+                                               _vp, _vp, _i64, _vp, _i64, _vp]),
     "gnn_gcn_transform_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64,
                                                   _vp, _i64, _vp, _vp]),
     "gnn_normalize_features_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),

@@ -28,6 +28,17 @@ struct RowIdx {  // the optional output-row scatter (gcn_transform_kernel y_row)
   int64_t n_y;
   int32_t* err;
 };
+// the optional classifier epilogue (gnn_linear_relu_cls_f32): logits = y wd^T + bd
+constexpr int kMaxCls = 4;
+struct Classifier {
+  const float* wd;  // [n_cls, FO] (nn.Linear weight)
+  const float* bd;  // [n_cls] or null
+  float* logits;    // [n_rows, ldl]
+  int64_t ldl;
+  int n_cls;
+};
+// kernel epilogue modes
+constexpr int kTfPlain = 0, kTfScatter = 1, kTfClassify = 2;
 using tf32x4 = __attribute__((ext_vector_type(4))) float;
 
 #ifndef GNN_TF_SINGLE_BUFFER
@@ -53,11 +64,17 @@ using tf32x4 = __attribute__((ext_vector_type(4))) float;
 // row order (a degree-ordered graph's, graph.degree_order) while X is read in order; ids
 // outside [0, n_y) are not stored and raise *err. The stores are scattered 64-B row pieces
 // (fire and forget); a gather on the X side would put the index load in front of every tile.
-template <int K, int CB, int NW, bool RELU, int TR, bool SCATTER>
+// MODE kTfClassify (the GraphSAGE classifier fused into the last SageLayer's GEMM,
+// GraphSAGE.py:51-52): each lane dots its 4 * CB output columns of a row with the classifier
+// weights, the 4 lane quarters are summed by shuffles and the NW waves' partials through LDS
+// (fixed order, deterministic), + bias: logits[row, c] for c < n_cls <= 4.
+template <int K, int CB, int NW, bool RELU, int TR, int MODE>
 __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
     float* __restrict__ y, int64_t ldy, const int64_t* __restrict__ y_row, int64_t n_y,
-    int32_t* __restrict__ err) {
+    int32_t* __restrict__ err, Classifier cls) {
+  constexpr bool SCATTER = MODE == kTfScatter;
+  constexpr bool CLS = MODE == kTfClassify;
   constexpr int kTfBlock = NW * kWave;
   constexpr int S = K / 4;           // MFMA k-steps
   constexpr int XC = S <= 32 ? S : 16;  // k-steps of X held in registers at a time
@@ -69,9 +86,21 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
   constexpr int NBUF = GNN_TF_SINGLE_BUFFER ? 1 : 2;
   static_assert(S % XC == 0 && XC % 4 == 0, "X chunks of whole float4s");
   __shared__ float xt[NBUF][TR * LDA];
+  __shared__ float part[CLS ? 2 : 1][CLS ? NW * TR * kMaxCls : 1];  // per-wave logit partials
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = threadIdx.x >> 6;
   const int q = lane >> 4, r = lane & 15;
+  float wd[CLS ? CB : 1][4][kMaxCls];  // classifier weights of this lane's output columns
+  if constexpr (CLS) {
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < kMaxCls; ++c)
+          wd[cb][i][c] = c < cls.n_cls ? cls.wd[c * (NW * CB * 16) + (wv * CB + cb) * 16 + 4 * q + i]
+                                       : 0.f;
+  }
 
   // A fragments: W[c0 + r][q*S + s] for this wave's CB column blocks, resident
   float wa[CB][S];
@@ -191,14 +220,53 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
           *reinterpret_cast<float4*>(y + orow * ldy + (wv * CB + cb) * 16 + 4 * q) = o;
         }
       }
+      if constexpr (CLS) {  // every lane, rows past n_rows included (their sums go unused)
+        float pc[kMaxCls];
+#pragma unroll
+        for (int c = 0; c < kMaxCls; ++c) pc[c] = 0.f;
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float v = RELU ? fmaxf(acc[j][cb][i], 0.f) : acc[j][cb][i];
+#pragma unroll
+            for (int c = 0; c < kMaxCls; ++c) pc[c] = fmaf(v, wd[cb][i][c], pc[c]);
+          }
+#pragma unroll
+        for (int c = 0; c < kMaxCls; ++c) {
+          pc[c] += __shfl_xor(pc[c], 16, kWave);
+          pc[c] += __shfl_xor(pc[c], 32, kWave);
+        }
+        if (q == 0) {
+#pragma unroll
+          for (int c = 0; c < kMaxCls; ++c)
+            part[it & 1][(wv * TR + j * 16 + r) * kMaxCls + c] = pc[c];
+        }
+      }
     }
     __syncthreads();  // one barrier per tile: the staged next tile is complete, this one free
+    if constexpr (CLS) {
+      // the waves' partials of this tile, summed in wave order (the buffer of parity it & 1 is
+      // written again two tiles on, after the next tile's barrier)
+      const int t = static_cast<int>(threadIdx.x);
+      if (t < TR * kMaxCls) {
+        const int rr = t / kMaxCls, c = t - rr * kMaxCls;
+        if (c < cls.n_cls && row0 + rr < n_rows) {
+          float v = 0.f;
+#pragma unroll
+          for (int wq = 0; wq < NW; ++wq) v += part[it & 1][(wq * TR + rr) * kMaxCls + c];
+          if (cls.bd) v += cls.bd[c];
+          cls.logits[(row0 + rr) * cls.ldl + c] = v;
+        }
+      }
+    }
   }
 }
 
 template <int K, int CB, int NW, bool RELU, int TR>
 static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, const float* w,
-                               float* y, int64_t ldy, const RowIdx& ri, hipStream_t s) {
+                               float* y, int64_t ldy, const RowIdx& ri, const Classifier& cls,
+                               hipStream_t s) {
   const int64_t tiles = (n_rows + TR - 1) / TR;
 #ifndef GNN_TF_GRID
 #define GNN_TF_GRID 512  // persistent grid: 2 workgroups per CU
@@ -206,13 +274,17 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
   constexpr int64_t kGrid = GNN_TF_GRID * kTfWaves / NW;  // 8-wave workgroups: 1 per CU
   const int64_t grid = tiles < kGrid ? tiles : kGrid;
   if (ri.row != nullptr)  // a template flag: no index loads in the in-order kernel
-    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, true>),
+    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfScatter>),
                        dim3(static_cast<unsigned>(grid)), dim3(NW * kWave), 0, s, x, ldx, n_rows,
-                       w, y, ldy, ri.row, ri.n_y, ri.err);
+                       w, y, ldy, ri.row, ri.n_y, ri.err, cls);
+  else if (RELU && cls.logits != nullptr)  // the classifier epilogue: SageLayer GEMMs only
+    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, RELU ? kTfClassify : kTfPlain>),
+                       dim3(static_cast<unsigned>(grid)), dim3(NW * kWave), 0, s, x, ldx, n_rows,
+                       w, y, ldy, ri.row, ri.n_y, ri.err, cls);
   else
-    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, false>),
+    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfPlain>),
                        dim3(static_cast<unsigned>(grid)), dim3(NW * kWave), 0, s, x, ldx, n_rows,
-                       w, y, ldy, ri.row, ri.n_y, ri.err);
+                       w, y, ldy, ri.row, ri.n_y, ri.err, cls);
   return launch_status();
 }
 
@@ -230,49 +302,50 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
 // 2891 vs 307 / 2932 us; K = 64 -> 64 keeps 64 rows (95 vs 113 us at 1M).
 template <int K, int CB, int NW, bool RELU>
 static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const float* w,
-                            float* y, int64_t ldy, const RowIdx& ri, hipStream_t s) {
+                            float* y, int64_t ldy, const RowIdx& ri, const Classifier& cls, hipStream_t s) {
   constexpr int64_t slots = GNN_TF_GRID * kTfWaves / NW;
 #ifdef GNN_TF_TR32_ROWS  // A/B: 16-row tiles below GNN_TF_TR16_ROWS, 32-row below this
 #ifndef GNN_TF_TR16_ROWS
 #define GNN_TF_TR16_ROWS (32 * 2 * slots)
 #endif
-  if (n_rows < GNN_TF_TR16_ROWS) return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, s);
-  if (n_rows < GNN_TF_TR32_ROWS) return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, s);
+  if (n_rows < GNN_TF_TR16_ROWS) return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+  if (n_rows < GNN_TF_TR32_ROWS) return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
 #endif
   if (GNN_TF_MIN_TR <= 16 && n_rows < 32 * 2 * slots)
-    return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, s);
+    return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
   if (GNN_TF_MIN_TR <= 32 && (K > GNN_TF_TR64_MAX_K || n_rows < 64 * 2 * slots))
-    return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, s);
+    return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
   if constexpr (K <= GNN_TF_TR64_MAX_K || GNN_TF_MIN_TR > 32)
-    return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, ri, s);
-  return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, s);
+    return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+  return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
 }
 
 template <int K, bool RELU>
 static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t n_rows,
                               const float* w, float* y, int64_t ldy, const RowIdx& ri,
-                              hipStream_t s) {
-  if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
+                              const Classifier& cls, hipStream_t s) {
+  if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
   if (fout == 128) {
     if constexpr (K <= 128 || GNN_TF_K256_CB2)
-      return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
+      return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
     else
-      return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
+      return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
   }
   if (fout == 256) {
     if constexpr (K <= 64) {
-      return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
+      return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
     } else if constexpr (GNN_TF_ONE256) {
       // one launch, 8 waves x 2 column blocks (128 W values per lane resident, 200 VGPRs):
       // X read and staged once for all 256 columns. In one process (tools/transform_tile_ab.py,
       // profiles/r03o_transform_one256_ab.log): 10M x 256 -> 256 9.63 ms (136 TF/s) vs 10.57
       // as two launches vs 9.95 hipBLASLt; 1M x 128 -> 256 0.545 vs 0.618 vs 0.628 ms
-      return launch_transform<K, 2, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, s);
+      return launch_transform<K, 2, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
     } else {
       // A/B: two launches of the 128-column kernel, one per half of W's rows (X read twice)
-      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, s);
+      if (cls.logits != nullptr) return GNN_E_UNSUPPORTED;
+      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, s);
       if (rc != GNN_OK) return rc;
-      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, s);
+      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, cls, s);
     }
   }
   return GNN_E_UNSUPPORTED;
@@ -281,7 +354,8 @@ static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t
 template <bool RELU>
 static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
                            const float* w, int64_t fout, float* y, int64_t ldy,
-                           void* stream, const RowIdx& ri = RowIdx{nullptr, 0, nullptr}) {
+                           void* stream, const RowIdx& ri = RowIdx{nullptr, 0, nullptr},
+                           const Classifier& cls = Classifier{nullptr, nullptr, nullptr, 0, 0}) {
   if (n_rows < 0 || ldx < k || ldy < fout) return GNN_E_ARG;
   if (ri.row != nullptr && (ri.err == nullptr || ri.n_y < 0)) return GNN_E_ARG;
   if (!gnn_gcn_transform_supported(k, fout)) return GNN_E_UNSUPPORTED;
@@ -291,11 +365,11 @@ static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t 
     return GNN_E_ALIGN;
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (k) {
-    case 16: return dispatch_transform<16, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
-    case 32: return dispatch_transform<32, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
-    case 64: return dispatch_transform<64, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
-    case 128: return dispatch_transform<128, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
-    default: return dispatch_transform<256, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, s);
+    case 16: return dispatch_transform<16, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+    case 32: return dispatch_transform<32, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+    case 64: return dispatch_transform<64, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+    case 128: return dispatch_transform<128, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+    default: return dispatch_transform<256, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
   }
 }
 
@@ -329,4 +403,15 @@ extern "C" int gnn_linear_relu_f32(const float* x, int64_t ldx, int64_t n_rows, 
                                    const float* w, int64_t fout, float* y, int64_t ldy,
                                    void* stream) {
   return transform_entry<true>(x, ldx, n_rows, k, w, fout, y, ldy, stream);
+}
+
+extern "C" int gnn_linear_relu_cls_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                                       const float* w, int64_t fout, float* y, int64_t ldy,
+                                       const float* wd, const float* bd, int64_t n_cls,
+                                       float* logits, int64_t ldl, void* stream) {
+  if (n_cls < 1 || n_cls > kMaxCls || ldl < n_cls) return GNN_E_ARG;
+  if (n_rows > 0 && (!wd || !logits)) return GNN_E_ARG;
+  return transform_entry<true>(x, ldx, n_rows, k, w, fout, y, ldy, stream,
+                               RowIdx{nullptr, 0, nullptr},
+                               Classifier{wd, bd, logits, ldl, static_cast<int>(n_cls)});
 }

@@ -24,8 +24,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import from_coo
-from .ops import (gather_rows, gcn_transform, sage_aggregate, sage_gather_aggregate,
-                  sage_gather_concat, sage_layer, spmm_forward)
+from .ops import (gather_rows, gcn_transform, linear_relu_classify, sage_aggregate,
+                  sage_gather_aggregate, sage_gather_concat, sage_layer, spmm_forward)
 
 # the inference SageLayer GEMM relu([self | agg] @ W^T) runs on the hand-written fp32-MFMA
 # kernel (gnn_linear_relu_f32) up to SAGE_MFMA_MAX_SMALL rows and from SAGE_MFMA_MIN_LARGE
@@ -232,7 +232,7 @@ class SageLayer(nn.Module):
         return torch._addmm_activation(part, aggregate_feats, W[:, n:].t())
 
 
-def _fused_sage_layer(block, center, neigh: Gathered):
+def _fused_sage_layer(block, center, neigh: Gathered, dense: nn.Linear | None = None):
     """Inference SageLayer on a (table, index map) aggregate.
 
     Covered shapes (``ops.sage_layer``): ONE launch gathers the centre rows and the
@@ -242,7 +242,11 @@ def _fused_sage_layer(block, center, neigh: Gathered):
     the ReLU in the hipBLASLt epilogue: GraphSAGE.py:18-20 + the gathers of :47-49 as 3
     launches instead of 7; with the centre rows and the neighbours drawn from the same table
     (the sampler's Gathered maps) the two halves come from ONE launch
-    (``ops.sage_gather_concat``), then the GEMM: 2 launches."""
+    (``ops.sage_gather_concat``), then the GEMM: 2 launches.
+
+    ``dense`` (the last layer of a supervised net): the classifier of GraphSAGE.py:51-52 runs in
+    the GEMM's epilogue when the MFMA kernel takes the shape (``ops.linear_relu_classify``);
+    the return value is then ``(y, logits)``, else ``y`` alone."""
     if isinstance(center, Gathered):
         self_src, self_idx, trusted = center.table, center.index, center.trusted
     else:
@@ -266,6 +270,10 @@ def _fused_sage_layer(block, center, neigh: Gathered):
         sage_gather_aggregate(neigh.table, neigh.index, "MEAN", check=not neigh.trusted,
                               out=buf[:, n:])
     W = block.weight.weight
+    if dense is not None and _sage_gemm_on_mfma(M):
+        yl = linear_relu_classify(buf, W, dense.weight, dense.bias)
+        if yl is not None:
+            return yl
     if _sage_gemm_on_mfma(M):  # relu(buf @ W^T) on the hand-written fp32-MFMA kernel
         y = gcn_transform(buf, W, relu=True)
         if y is not None:
@@ -307,10 +315,14 @@ class GraphSAGE(nn.Module):
         if contexts_negatives_feats_data is None:
             center = center_feats_data         # tensor, or Gathered (table, [M] index)
             neigh = center_neigh_feats_data    # [M, k, F] tensor, or Gathered (table, [M, k] index)
-            feats_data = None
+            feats_data = classes = None
             for i, block in enumerate(self.sage_blocks):
                 if isinstance(neigh, Gathered) and self._fused_ok(block):
-                    feats_data = _fused_sage_layer(block, center, neigh)
+                    last = i == self.num_layers - 1 and not self.Unsupervised
+                    feats_data = _fused_sage_layer(block, center, neigh,
+                                                   self.dense if last else None)
+                    if isinstance(feats_data, tuple):  # the classifier ran in the epilogue
+                        feats_data, classes = feats_data
                 else:
                     if isinstance(center, Gathered):
                         center = _gather(center.table, center.index, center.trusted)
@@ -324,8 +336,7 @@ class GraphSAGE(nn.Module):
                     else:                              # GraphSAGE.py:56-57 (-1 padding dropped)
                         center = Gathered(feats_data, cm[cm != -1], False)
                         neigh = Gathered(feats_data, nm[nm[:, 0] != -1, :], False)
-            classes = None
-            if not self.Unsupervised:
+            if not self.Unsupervised and classes is None:
                 classes = self.dense(feats_data)
             return feats_data, classes
         center_feats_data, _ = self(center_feats_data, center_nodes_map, center_neigh_feats_data,

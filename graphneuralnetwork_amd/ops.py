@@ -487,6 +487,42 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
     return out
 
 
+def linear_relu_classify(x: torch.Tensor, weight: torch.Tensor, wd: torch.Tensor,
+                         bd: torch.Tensor | None = None, out: torch.Tensor | None = None):
+    """(y, logits) = (relu(x @ weight^T), y @ wd^T + bd) in ONE launch
+    (gnn_linear_relu_cls_f32): the last SageLayer (GraphSAGE/GraphSAGE.py:18-20) with the
+    classifier ``self.dense`` (GraphSAGE.py:51-52) in its epilogue. Inference only; None when
+    the shape is not covered (more than 4 classes, or a transform shape gcn_transform does not
+    take), and the caller then runs the two layers separately."""
+    _require_device(x, weight, wd)
+    fout, k = weight.shape
+    n_cls = wd.shape[0] if wd.dim() == 2 else 0
+    if (x.dtype != torch.float32 or weight.dtype != torch.float32 or wd.dtype != torch.float32
+            or x.dim() != 2 or x.shape[1] != k or wd.dim() != 2 or wd.shape[1] != fout
+            or not 1 <= n_cls <= 4 or (bd is not None and (bd.dtype != torch.float32
+                                                            or bd.numel() != n_cls))):
+        return None
+    lib = _lib.load()
+    if not lib.gnn_gcn_transform_supported(k, fout) or (fout == 256 and k > 64
+                                                         and not TRANSFORM_WIDE_MFMA):
+        return None
+    if bd is not None:
+        _require_device(bd)
+        bd = bd.contiguous()
+    if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
+        x = x.contiguous()
+    w, wdc = weight.contiguous(), wd.contiguous()
+    m = x.shape[0]
+    if out is None:
+        out = torch.empty((m, fout), dtype=torch.float32, device=x.device)
+    logits = torch.empty((m, n_cls), dtype=torch.float32, device=x.device)
+    _lib.check(lib.gnn_linear_relu_cls_f32(
+        x.data_ptr(), x.stride(0), m, k, w.data_ptr(), fout, out.data_ptr(), out.stride(0),
+        wdc.data_ptr(), _lib.ptr(bd), n_cls, logits.data_ptr(), logits.stride(0),
+        _lib.stream_handle(x.device)), "gnn_linear_relu_cls_f32")
+    return out, logits
+
+
 def col_mean(x: torch.Tensor) -> torch.Tensor:
     """Mean over rows (double accumulation) -- the dense GAT layer's edgeless-row output."""
     _require_device(x)

@@ -177,7 +177,7 @@ int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t hea
  * nn.Linear weight [fout, k] (row-major), fp32 in / fp32 accumulate
  * (v_mfma_f32_16x16x4_f32). Replaces `support = self.dense(X_input)` at GCN/GCN.py:42
  * (inference path). Shapes covered: gnn_gcn_transform_supported(k, fout) != 0
- * (k in {16, 32, 64, 128, 256}; fout 64, 128 or 256 -- 256 with k > 64 as two launches);
+ * (k in {16, 32, 64, 128, 256}; fout 64, 128 or 256);
  * other shapes return GNN_E_UNSUPPORTED (the caller uses a library GEMM). x, w, y
  * 16-B aligned, ldx and ldy multiples of 4 (else GNN_E_ALIGN).
  */
@@ -220,6 +220,19 @@ int gnn_normalize_features_f32(const float* x, int64_t ldx, int64_t n_rows, int6
  */
 int gnn_linear_relu_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,
                         int64_t fout, float* y, int64_t ldy, void* stream);
+
+/*
+ * The last SageLayer with the GraphSAGE classifier fused into its epilogue:
+ *   y = max(x @ w^T, 0)                      GraphSAGE/GraphSAGE.py:18-20 (the embedding)
+ *   logits[n, c] = y[n, :] . wd[c, :] + bd[c]  GraphSAGE.py:51-52 (self.dense, nn.Linear)
+ * for c < n_cls <= 4 (wd [n_cls, fout] row-major, bd nullable = no bias; logits row pitch
+ * ldl >= n_cls). The per-row sums run in a fixed order (deterministic). Shapes, alignment
+ * and return codes as gnn_gcn_transform_f32; GNN_E_ARG for n_cls outside [1, 4].
+ */
+int gnn_linear_relu_cls_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                            const float* w, int64_t fout, float* y, int64_t ldy, const float* wd,
+                            const float* bd, int64_t n_cls, float* logits, int64_t ldl,
+                            void* stream);
 
 /*
  * GAT feature transform on the matrix cores with the attention logits fused:

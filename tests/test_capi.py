@@ -55,6 +55,10 @@ def test_argument_rejection_without_launch(lib):
     assert lib.gnn_spmm_plan_count(None, 10, 4, None, None, None) == -1
     assert lib.gnn_spmm_plan_scratch_bytes(-5) < 0
     assert lib.gnn_spmm_plan_scratch_bytes(10_000_000) > 0
+    # the fused classifier: n_cls outside [1, 4] / missing operands, nothing launched
+    for n_cls, wd, lg in ((0, 1, 1), (5, 1, 1), (3, None, 1), (3, 1, None)):
+        assert lib.gnn_linear_relu_cls_f32(16, 256, 100, 256, 16, 128, 16, 128, wd, None, n_cls,
+                                           lg, 4, None) == -1
 
 
 def test_ops_refuse_cpu_tensors():

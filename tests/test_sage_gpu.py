@@ -234,6 +234,70 @@ def test_graphsage_forward_mfma_gemm_matches_library(dev, monkeypatch):
     np.testing.assert_allclose(logits.cpu().numpy(), logits0.cpu().numpy(), rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("k,fout", [(256, 128), (128, 128), (64, 64), (128, 256), (32, 128)])
+@pytest.mark.parametrize("n", [1, 100, 8192, 20001])
+@pytest.mark.parametrize("n_cls,bias", [(3, True), (1, False), (4, True)])
+def test_linear_relu_classify(dev, k, fout, n, n_cls, bias):
+    """gnn_linear_relu_cls_f32 (the last SageLayer with the classifier in its epilogue,
+    GraphSAGE.py:18-20 + :51-52): the embedding equals gnn_linear_relu_f32 bit for bit and the
+    logits equal a float64 (relu(x W^T)) wd^T + bd within fp32 tolerance; deterministic."""
+    from graphneuralnetwork_amd.ops import gcn_transform, linear_relu_classify
+    g = torch.Generator(device=dev).manual_seed(n * 7 + k + n_cls)
+    x = torch.randn(n, k, device=dev, generator=g)
+    w = torch.randn(fout, k, device=dev, generator=g) / k ** 0.5
+    wd = torch.randn(n_cls, fout, device=dev, generator=g) / fout ** 0.5
+    bd = torch.randn(n_cls, device=dev, generator=g) if bias else None
+    y, lg = linear_relu_classify(x, w, wd, bd)
+    assert torch.equal(y, gcn_transform(x, w, relu=True))
+    ref = y.double() @ wd.double().T + (bd.double() if bias else 0.0)
+    np.testing.assert_allclose(lg.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    y2, lg2 = linear_relu_classify(x, w, wd, bd)
+    assert torch.equal(lg, lg2) and torch.equal(y, y2)
+
+
+def test_linear_relu_classify_uncovered(dev):
+    """More than 4 classes or an uncovered transform shape: None (the caller runs nn.Linear)."""
+    from graphneuralnetwork_amd.ops import linear_relu_classify
+    x = torch.randn(50, 128, device=dev)
+    w = torch.randn(128, 128, device=dev)
+    assert linear_relu_classify(x, w, torch.randn(5, 128, device=dev)) is None
+    assert linear_relu_classify(torch.randn(50, 100, device=dev), torch.randn(128, 100, device=dev),
+                                torch.randn(3, 128, device=dev)) is None
+
+
+def test_graphsage_forward_classifier_epilogue(dev, monkeypatch):
+    """The supervised forward on device-sampler maps with the classifier fused into the last
+    SageLayer's GEMM gives the logits of the separate self.dense (nn.Linear) call."""
+    from graphneuralnetwork_amd import graphsage as GS
+    from graphneuralnetwork_amd.graph import from_coo
+    from graphneuralnetwork_amd.sampler import sample_batch
+    rng = np.random.default_rng(13)
+    n, F = 4000, 128
+    s, d = rng.integers(0, n, 50000), rng.integers(0, n, 50000)
+    adj = from_coo(torch.from_numpy(np.concatenate([s, d])).to(dev),
+                   torch.from_numpy(np.concatenate([d, s])).to(dev),
+                   torch.ones(100000, device=dev), n, n)
+    table = torch.randn(n, F, device=dev)
+    deg = adj.rowptr[1:] - adj.rowptr[:-1]
+    seeds = torch.nonzero(deg > 0).view(-1)[:600]
+    batch = sample_batch(adj, seeds, (25, 10), seed=9)
+    net = GS.GraphSAGE(2, F, F, False, agg_func="MEAN", Unsupervised=False,
+                       class_size=3).to(dev).eval()
+    calls = []
+    real = GS.linear_relu_classify
+    monkeypatch.setattr(GS, "linear_relu_classify",
+                        lambda *a, **kw: calls.append(1) or real(*a, **kw))
+    with torch.no_grad():
+        emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+        assert calls, "the classifier epilogue did not run"
+        ref = net.dense(emb)
+        monkeypatch.setattr(GS, "linear_relu_classify", lambda *a, **kw: None)
+        emb0, logits0 = net(*batch.forward_args(table), None, None, None, None, None)
+    assert torch.equal(emb, emb0)
+    np.testing.assert_allclose(logits.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(logits.cpu().numpy(), logits0.cpu().numpy(), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("F", [1, 7, 128, 600])
 @pytest.mark.parametrize("k", [1, 10, 25])
 def test_maxpool_pregathered_and_gathered(dev, F, k):

@@ -1,6 +1,7 @@
 """Interleaved A/B of the cfg4 GraphSAGE forward (8192 seeds, [25, 10], 10M / 100M R-MAT,
-F=H=128, eval) with the SageLayer GEMMs on hipBLASLt vs the hand-written fp32-MFMA kernel
-(graphsage._sage_gemm_on_mfma), eager and replayed from a HIP graph.
+F=H=128, eval; the degree-ordered dataset as bench.py) with the SageLayer GEMMs on hipBLASLt
+vs the hand-written fp32-MFMA kernel (graphsage._sage_gemm_on_mfma; the last layer's MFMA GEMM
+carries the classifier epilogue), eager and replayed from a HIP graph.
 
     python tools/sage_gemm_forward_ab.py [--rounds 8]
 """
@@ -21,11 +22,11 @@ def main():
     args = ap.parse_args()
     from graphneuralnetwork_amd import graphsage as GS
     from graphneuralnetwork_amd.rmat import rmat_edges
-    from graphneuralnetwork_amd.sampler import sample_batch, symmetric_adjacency
+    from graphneuralnetwork_amd.sampler import degree_ordered, sample_batch, symmetric_adjacency
     dev = torch.device("cuda:0")
     n, F = 10_000_000, 128
     s, d = rmat_edges(n, 100_000_000, 0)
-    adj = symmetric_adjacency(s, d, n, device=dev)
+    adj, _, _ = degree_ordered(symmetric_adjacency(s, d, n, device=dev))  # as bench.py
     del s, d
     gen = torch.Generator(device=dev).manual_seed(0)
     table = torch.randn(n, F, device=dev, generator=gen)
