@@ -655,6 +655,7 @@ def run_sage(args, dev, rank: int = 0, world: int = 1, edges_np=None):
                       "frontier": M, "fanout": [k0, k1], "sampled_edges": edges, "feat_dim": F,
                       "step": "GraphSAGE.forward (one [self | mean] gather launch + one K=2F "
                               "GEMM per SageLayer, classifier) on device-sampled index maps",
+                      "sage_layer_gemm": transform_note(),
                       "node_order": "dataset relabelled once by degree (sampler.degree_ordered, "
                                     "%.2f s, outside the timed region); seeds drawn in the new "
                                     "ids" % order_s},
@@ -707,6 +708,19 @@ def run_sage(args, dev, rank: int = 0, world: int = 1, edges_np=None):
     del table, adj, batch, fargs
     torch.cuda.empty_cache()
     return res
+
+
+def transform_note() -> str:
+    """The arithmetic of the MFMA feature transforms (the GEMM half of a layer, outside the
+    aggregation the headline times)."""
+    from graphneuralnetwork_amd.ops import transform_precision
+    if transform_precision() == "split-bf16":
+        return ("gnn_gcn_transform / gnn_linear_relu on v_mfma_f32_16x16x32_bf16 at K >= 128: fp32 "
+                "inputs split into three bf16 pieces, the six products down to order 2^-16 "
+                "accumulated in fp32 (error per product a few fp32 ulps, below the fp32-MFMA "
+                "path's in tests/test_spmm_gpu.py::test_transform_split_bf16_accuracy); fp32 "
+                "v_mfma_f32_16x16x4_f32 at K < 128")
+    return "gnn_gcn_transform / gnn_linear_relu on v_mfma_f32_16x16x4_f32 (fp32 fmaf chain)"
 
 
 def host_cpu_info(threads: int) -> dict:
@@ -949,7 +963,8 @@ def run_gcn(args, dev, rank: int, world: int, workload: str, edges_np=None, extr
             "achieved_GBps": roof["achieved"],
             "graph_build_s": BUILD_INFO.get("gcn_adjacency_build_s"),
             "first_step_s": BUILD_INFO.get("first_step_s"),
-            **({"gcn_layer_ms": layer_ms} if layer_ms is not None else {}),
+            **({"gcn_layer_ms": layer_ms, "gcn_layer_transform": transform_note()}
+               if layer_ms is not None else {}),
             **({"partition_build_s": BUILD_INFO.get("partition_build_s"),
                 "row_bounds": part.bounds,
                 "balance_max_mean_cost": BUILD_INFO.get("balance_max_mean_cost"),

@@ -68,6 +68,7 @@ SIGNATURES: dict[str, tuple] = {
                                           _vp]),
     "gnn_gat_project_supported": (ctypes.c_int, [_i64, _i64, _i64]),
     "gnn_gcn_transform_supported": (ctypes.c_int, [_i64, _i64]),
+    "gnn_transform_set_precision": (ctypes.c_int, [ctypes.c_int]),
     "gnn_gcn_transform_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnn_linear_relu_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnn_linear_relu_cls_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64,

@@ -40,9 +40,41 @@ struct Classifier {
 // kernel epilogue modes
 constexpr int kTfPlain = 0, kTfScatter = 1, kTfClassify = 2;
 using tf32x4 = __attribute__((ext_vector_type(4))) float;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------
+// fp32 products from bf16 MFMAs (X6 kernels). Every fp32 value is split into three bf16
+// pieces, v = v0 + v1 + v2 + e with |e| <= 2^-24 |v| (v0 = bf16(v), v1 = bf16(v - v0),
+// v2 = bf16(v - v0 - v1); the differences are exact in fp32), and a product x w is summed
+// from the six piece products down to order 2^-16: x0w0 + x0w1 + x1w0 + x0w2 + x1w1 + x2w0.
+// A bf16 x bf16 product is exact in fp32 and v_mfma_f32_16x16x32_bf16 accumulates in fp32,
+// so what is left out (x1w2, x2w1, x2w2 and the pieces' residues) is ~4 * 2^-24 |x w| per
+// product -- the size of fp32's own rounding -- while the six MFMAs take 6 x 16 cycles
+// against 8 x 32 for the same 32-long k-step on v_mfma_f32_16x16x4_f32.
+// Non-finite inputs: an inf becomes NaN (inf - inf in the split); the GCN / SAGE layers
+// never feed one.
+__device__ __forceinline__ void split3(float v, __bf16& a, __bf16& b, __bf16& c) {
+  a = static_cast<__bf16>(v);
+  const float r1 = v - static_cast<float>(a);
+  b = static_cast<__bf16>(r1);
+  c = static_cast<__bf16>(r1 - static_cast<float>(b));
+}
+// LDS image of an X6 tile: three bf16 planes (pieces 0, 1, 2), row pitch 2K + 32 bytes, the
+// 16-B chunk c of row rr stored at chunk c ^ swz6(rr): enumerated against the ds_read_b128
+// lane groups (4 x 16 lanes, bank (a/4) mod 64) for the fragment reads (lane (q, r): row r,
+// chunk q*K/32 + s) -- conflict-free -- and the staging ds_write_b64 (16 contiguous lanes =
+// one 128-B run of a row) stays conflict-free under the permutation.
+template <int K> __device__ __forceinline__ int swz6(int rr) {
+  return K >= 256 ? (rr >> 2) & 1 : K >= 128 ? (rr >> 1) & 1 : rr & 1;
+}
+template <int K> constexpr int x6_pitch() { return 2 * K + 32; }  // bytes per LDS row
 
 #ifndef GNN_TF_SINGLE_BUFFER
 #define GNN_TF_SINGLE_BUFFER 0  // A/B: the round-2 one-buffer tile loop (two barriers per tile)
+#endif
+#ifndef GNN_TF_X6_PIPE
+#define GNN_TF_X6_PIPE 0  // A/B: X6 fragments of k-step s + 1 read during step s's MFMAs
 #endif
 #ifndef GNN_TF_K256_CB2
 #define GNN_TF_K256_CB2 0  // A/B: K = 256 -> 128 as 4 waves x 2 column blocks
@@ -68,7 +100,7 @@ using tf32x4 = __attribute__((ext_vector_type(4))) float;
 // GraphSAGE.py:51-52): each lane dots its 4 * CB output columns of a row with the classifier
 // weights, the 4 lane quarters are summed by shuffles and the NW waves' partials through LDS
 // (fixed order, deterministic), + bias: logits[row, c] for c < n_cls <= 4.
-template <int K, int CB, int NW, bool RELU, int TR, int MODE>
+template <int K, int CB, int NW, bool RELU, int TR, int MODE, bool X6 = false>
 __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
     float* __restrict__ y, int64_t ldy, const int64_t* __restrict__ y_row, int64_t n_y,
@@ -85,7 +117,11 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
   constexpr int NV = (V4 + kTfBlock - 1) / kTfBlock;  // per thread
   constexpr int NBUF = GNN_TF_SINGLE_BUFFER ? 1 : 2;
   static_assert(S % XC == 0 && XC % 4 == 0, "X chunks of whole float4s");
-  __shared__ float xt[NBUF][TR * LDA];
+  constexpr int S32 = K / 32;  // X6: bf16 MFMA k-steps (32 k each, 8 per lane quarter)
+  constexpr int P6 = x6_pitch<K>();
+  constexpr int PLANE = TR * P6;  // bytes per bf16 plane
+  static_assert(!X6 || (K >= 64 && K % 64 == 0), "X6 tiles: K in {64, 128, 256}");
+  __shared__ float xt[NBUF][X6 ? 3 * PLANE / 4 : TR * LDA];
   __shared__ float part[CLS ? 2 : 1][CLS ? NW * TR * kMaxCls : 1];  // per-wave logit partials
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = threadIdx.x >> 6;
@@ -103,17 +139,31 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
   }
 
   // A fragments: W[c0 + r][q*S + s] for this wave's CB column blocks, resident
-  float wa[CB][S];
+  float wa[X6 ? 1 : CB][X6 ? 1 : S];
+  // X6: the bf16 pieces of W[c0 + r][q*K/4 + 8s + j] (j < 8) for k-step s, resident
+  bf16x8 wb[X6 ? CB : 1][X6 ? S32 : 1][3];
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) {
     const float* wr = w + static_cast<int64_t>((wv * CB + cb) * 16 + r) * K + q * S;
 #pragma unroll
     for (int v = 0; v < S / 4; ++v) {
       const float4 t = *reinterpret_cast<const float4*>(wr + 4 * v);
-      wa[cb][4 * v] = t.x;
-      wa[cb][4 * v + 1] = t.y;
-      wa[cb][4 * v + 2] = t.z;
-      wa[cb][4 * v + 3] = t.w;
+      if constexpr (X6) {
+        const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          __bf16 a, b, c;
+          split3(tv[i], a, b, c);
+          wb[cb][v / 2][0][(v & 1) * 4 + i] = a;
+          wb[cb][v / 2][1][(v & 1) * 4 + i] = b;
+          wb[cb][v / 2][2][(v & 1) * 4 + i] = c;
+        }
+      } else {
+        wa[cb][4 * v] = t.x;
+        wa[cb][4 * v + 1] = t.y;
+        wa[cb][4 * v + 2] = t.z;
+        wa[cb][4 * v + 3] = t.w;
+      }
     }
   }
 
@@ -136,7 +186,25 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
       const int e = v * kTfBlock + static_cast<int>(threadIdx.x);
       if (e < V4) {
         const int rr = e / (K / 4), c4 = e - rr * (K / 4);
-        *reinterpret_cast<float4*>(buf + rr * LDA + 4 * (c4 ^ TileLds<K>::swz(rr))) = pre[v];
+        if constexpr (X6) {  // 4 floats -> 4 bf16 of each plane (8 B), chunk c4 / 2 swizzled
+          const float tv[4] = {pre[v].x, pre[v].y, pre[v].z, pre[v].w};
+          bf16x4 p0, p1, p2;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            __bf16 a, b, c;
+            split3(tv[i], a, b, c);
+            p0[i] = a;
+            p1[i] = b;
+            p2[i] = c;
+          }
+          char* base = reinterpret_cast<char*>(buf) + rr * P6 +
+                       16 * ((c4 >> 1) ^ swz6<K>(rr)) + 8 * (c4 & 1);
+          *reinterpret_cast<bf16x4*>(base) = p0;
+          *reinterpret_cast<bf16x4*>(base + PLANE) = p1;
+          *reinterpret_cast<bf16x4*>(base + 2 * PLANE) = p2;
+        } else {
+          *reinterpret_cast<float4*>(buf + rr * LDA + 4 * (c4 ^ TileLds<K>::swz(rr))) = pre[v];
+        }
       }
     }
   };
@@ -163,6 +231,48 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
         if (orow < n_rows) dst[j] = y_row[orow];
     }
     tf32x4 acc[TR / 16][CB];
+    if constexpr (X6) {
+#pragma unroll
+      for (int j = 0; j < TR / 16; ++j) {
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) acc[j][cb] = tf32x4{0.f, 0.f, 0.f, 0.f};
+        const int rr = j * 16 + r;
+        const char* xr = reinterpret_cast<const char*>(cur) + rr * P6;
+#if GNN_TF_X6_PIPE
+        // the next k-step's three fragments are read while this step's MFMAs run
+        bf16x8 fr[2][3];
+        auto rd = [&](int s6, bf16x8 (&f)[3]) {
+          const char* xp = xr + 16 * ((q * S32 + s6) ^ swz6<K>(rr));
+          f[0] = *reinterpret_cast<const bf16x8*>(xp);
+          f[1] = *reinterpret_cast<const bf16x8*>(xp + PLANE);
+          f[2] = *reinterpret_cast<const bf16x8*>(xp + 2 * PLANE);
+        };
+        rd(0, fr[0]);
+#endif
+#pragma unroll
+        for (int s6 = 0; s6 < S32; ++s6) {
+#if GNN_TF_X6_PIPE
+          if (s6 + 1 < S32) rd(s6 + 1, fr[(s6 + 1) & 1]);
+          const bf16x8 x0 = fr[s6 & 1][0], x1 = fr[s6 & 1][1], x2 = fr[s6 & 1][2];
+#else
+          const char* xp = xr + 16 * ((q * S32 + s6) ^ swz6<K>(rr));
+          const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(xp);
+          const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(xp + PLANE);
+          const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(xp + 2 * PLANE);
+#endif
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) {  // smallest terms first
+            tf32x4 a = acc[j][cb];
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[cb][s6][0], x2, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[cb][s6][1], x1, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[cb][s6][2], x0, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[cb][s6][0], x1, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[cb][s6][1], x0, a, 0, 0, 0);
+            acc[j][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[cb][s6][0], x0, a, 0, 0, 0);
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int rb0 = 0; rb0 < TR / 16; rb0 += RB) {
 #pragma unroll
@@ -263,6 +373,29 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
   }
 }
 
+// transform precision (gnn_transform_set_precision): 1 = fp32 products from bf16 MFMAs (X6,
+// K >= 128), 0 = v_mfma_f32_16x16x4_f32 (a k-ordered fp32 fmaf chain)
+static int g_tf_x6 = 1;
+
+template <int K, int CB, int NW, bool RELU, int TR, bool X6>
+static void launch_transform_kernel(dim3 grid, const float* x, int64_t ldx, int64_t n_rows,
+                                    const float* w, float* y, int64_t ldy, const RowIdx& ri,
+                                    const Classifier& cls, hipStream_t s) {
+  if (ri.row != nullptr)  // a template flag: no index loads in the in-order kernel
+    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfScatter, X6>), grid,
+                       dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err,
+                       cls);
+  else if (RELU && cls.logits != nullptr)  // the classifier epilogue: SageLayer GEMMs only
+    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, RELU ? kTfClassify : kTfPlain,
+                                             X6>),
+                       grid, dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y,
+                       ri.err, cls);
+  else
+    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfPlain, X6>), grid,
+                       dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err,
+                       cls);
+}
+
 template <int K, int CB, int NW, bool RELU, int TR>
 static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, const float* w,
                                float* y, int64_t ldy, const RowIdx& ri, const Classifier& cls,
@@ -273,18 +406,15 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
 #endif
   constexpr int64_t kGrid = GNN_TF_GRID * kTfWaves / NW;  // 8-wave workgroups: 1 per CU
   const int64_t grid = tiles < kGrid ? tiles : kGrid;
-  if (ri.row != nullptr)  // a template flag: no index loads in the in-order kernel
-    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfScatter>),
-                       dim3(static_cast<unsigned>(grid)), dim3(NW * kWave), 0, s, x, ldx, n_rows,
-                       w, y, ldy, ri.row, ri.n_y, ri.err, cls);
-  else if (RELU && cls.logits != nullptr)  // the classifier epilogue: SageLayer GEMMs only
-    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, RELU ? kTfClassify : kTfPlain>),
-                       dim3(static_cast<unsigned>(grid)), dim3(NW * kWave), 0, s, x, ldx, n_rows,
-                       w, y, ldy, ri.row, ri.n_y, ri.err, cls);
-  else
-    hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfPlain>),
-                       dim3(static_cast<unsigned>(grid)), dim3(NW * kWave), 0, s, x, ldx, n_rows,
-                       w, y, ldy, ri.row, ri.n_y, ri.err, cls);
+  const dim3 g(static_cast<unsigned>(grid));
+  // X6 tiles: 3 bf16 planes, at most 32 rows; 2 blocks of K = 256 pieces (192 VGPRs) spill
+  if constexpr (K >= 128 && TR <= 32 && !(K == 256 && CB == 2)) {
+    if (g_tf_x6) {
+      launch_transform_kernel<K, CB, NW, RELU, TR, true>(g, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+      return launch_status();
+    }
+  }
+  launch_transform_kernel<K, CB, NW, RELU, TR, false>(g, x, ldx, n_rows, w, y, ldy, ri, cls, s);
   return launch_status();
 }
 
@@ -311,7 +441,11 @@ static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const f
   if (n_rows < GNN_TF_TR16_ROWS) return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
   if (n_rows < GNN_TF_TR32_ROWS) return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
 #endif
-  if (GNN_TF_MIN_TR <= 16 && n_rows < 32 * 2 * slots)
+  // X6 at K = 256: 16-row tiles at every size (in one process, tools/transform_x6_ab.py,
+  // profiles/r03x_transform_x6_ab.log: 62K / 200K x 256 -> 128 30.9 / 79.9 vs 32.9 / 89.7 us
+  // with 32-row tiles; K = 128 keeps 32: 1M x 128 -> 128 205 vs 211 us)
+  if ((GNN_TF_MIN_TR <= 16 && n_rows < 32 * 2 * slots) ||
+      (K == 256 && g_tf_x6 && !(CB == 2 && K == 256)))
     return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
   if (GNN_TF_MIN_TR <= 32 && (K > GNN_TF_TR64_MAX_K || n_rows < 64 * 2 * slots))
     return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
@@ -334,6 +468,12 @@ static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t
   if (fout == 256) {
     if constexpr (K <= 64) {
       return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+    } else if (K == 256 && g_tf_x6 && cls.logits == nullptr) {
+      // X6 at K = 256: the 2-block tile does not fit the registers, so two launches of the
+      // 1-block kernel, one per half of W's rows (X read twice; memory-bound either way)
+      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+      if (rc != GNN_OK) return rc;
+      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, cls, s);
     } else if constexpr (GNN_TF_ONE256) {
       // one launch, 8 waves x 2 column blocks (128 W values per lane resident, 200 VGPRs):
       // X read and staged once for all 256 columns. In one process (tools/transform_tile_ab.py,
@@ -376,6 +516,13 @@ static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t 
 }  // namespace gnn
 
 using namespace gnn;
+
+extern "C" int gnn_transform_set_precision(int mode) {
+  if (mode != 0 && mode != 1) return GNN_E_ARG;
+  const int prev = g_tf_x6;
+  g_tf_x6 = mode;
+  return prev;
+}
 
 extern "C" int gnn_gcn_transform_supported(int64_t k, int64_t fout) {
   const bool kk = k == 16 || k == 32 || k == 64 || k == 128 || k == 256;

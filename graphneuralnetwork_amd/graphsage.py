@@ -27,18 +27,21 @@ from .graph import from_coo
 from .ops import (gather_rows, gcn_transform, linear_relu_classify, sage_aggregate,
                   sage_gather_aggregate, sage_gather_concat, sage_layer, spmm_forward)
 
-# the inference SageLayer GEMM relu([self | agg] @ W^T) runs on the hand-written fp32-MFMA
-# kernel (gnn_linear_relu_f32) up to SAGE_MFMA_MAX_SMALL rows and from SAGE_MFMA_MIN_LARGE
-# rows up, on hipBLASLt in between. Alone (K=256, N=128, tools/sage_gemm_ab.py,
-# profiles/r03f_gemm_ab.log, 16-row tiles for small launches): 8192 rows 11.9 vs 21.9 us,
-# 62479 rows 46.8 vs 41.0 us, 200000 rows 131 vs 144 us; inside the cfg4 forward
-# (tools/sage_gemm_forward_ab.py, profiles/r03f_sage_fwd_ab.log) MFMA for the 8192-row layer
-# only: 138.5 us vs 139.1 (hipBLASLt both) vs 140.5 (MFMA both).
+# the inference SageLayer GEMM relu([self | agg] @ W^T) runs on the hand-written MFMA kernel
+# (gnn_linear_relu_f32). With the split-bf16 arithmetic (the default, ops.set_transform_precision)
+# it beats hipBLASLt at every size (K=256, N=128, tools/transform_prec_ab.py,
+# profiles/r03w_transform_prec_ab.log: 8192 rows 11.0 vs 19.9 us, 61771 rows 32.6 vs 40.1,
+# 200000 rows 90.2 vs 136.5); on the fp32-MFMA arithmetic it ran up to SAGE_MFMA_MAX_SMALL rows and
+# from SAGE_MFMA_MIN_LARGE rows up, hipBLASLt in between (62479 rows 46.8 vs 41.0 us,
+# profiles/r03f_gemm_ab.log).
 SAGE_MFMA_MAX_SMALL = 16384
 SAGE_MFMA_MIN_LARGE = 131072
 
 
 def _sage_gemm_on_mfma(rows: int) -> bool:
+    from .ops import transform_precision
+    if transform_precision() == "split-bf16":
+        return True
     return rows <= SAGE_MFMA_MAX_SMALL or rows >= SAGE_MFMA_MIN_LARGE
 
 

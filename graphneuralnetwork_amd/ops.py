@@ -428,6 +428,27 @@ def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: to
 TRANSFORM_WIDE_MFMA = True
 
 
+TRANSFORM_PRECISIONS = ("split-bf16", "fp32-mfma")
+_TRANSFORM_PRECISION = ["split-bf16"]  # the library's default (gnn_transform_set_precision)
+
+
+def transform_precision() -> str:
+    """The MFMA transforms' arithmetic at K >= 128 (see set_transform_precision)."""
+    return _TRANSFORM_PRECISION[0]
+
+
+def set_transform_precision(mode: str) -> str:
+    """Arithmetic of the MFMA transforms at K >= 128 (gnn_transform_set_precision), returns the
+    previous mode: 'split-bf16' (default: fp32 products from three-piece bf16 splits on
+    v_mfma_f32_16x16x32_bf16, a few fp32 ulps per product) or 'fp32-mfma'
+    (v_mfma_f32_16x16x4_f32, a k-ordered fp32 fmaf chain)."""
+    if mode not in TRANSFORM_PRECISIONS:
+        raise ValueError(f"transform precision must be one of {TRANSFORM_PRECISIONS}")
+    prev = _lib.load().gnn_transform_set_precision(0 if mode == "fp32-mfma" else 1)
+    _TRANSFORM_PRECISION[0] = mode
+    return TRANSFORM_PRECISIONS[0] if prev == 1 else TRANSFORM_PRECISIONS[1]
+
+
 def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
                   out: torch.Tensor | None = None, out_rows: torch.Tensor | None = None,
                   check_rows: bool = True) -> torch.Tensor | None:
@@ -499,6 +520,7 @@ def linear_relu_classify(x: torch.Tensor, weight: torch.Tensor, wd: torch.Tensor
     n_cls = wd.shape[0] if wd.dim() == 2 else 0
     if (x.dtype != torch.float32 or weight.dtype != torch.float32 or wd.dtype != torch.float32
             or x.dim() != 2 or x.shape[1] != k or wd.dim() != 2 or wd.shape[1] != fout
+            or fout > 128
             or not 1 <= n_cls <= 4 or (bd is not None and (bd.dtype != torch.float32
                                                             or bd.numel() != n_cls))):
         return None

@@ -182,6 +182,17 @@ int gnn_gat_logits_f32(const float* wh, int64_t ldw, int64_t n_rows, int64_t hea
  * 16-B aligned, ldx and ldy multiples of 4 (else GNN_E_ALIGN).
  */
 int gnn_gcn_transform_supported(int64_t k, int64_t fout);
+
+/*
+ * Arithmetic of the transform entries (gnn_gcn_transform_f32 / _rows_f32, gnn_linear_relu_f32
+ * / _cls_f32) at k >= 128, process-wide: mode 1 (the default) forms every fp32 product from
+ * bf16 MFMAs -- x and w split into three bf16 pieces each (v = v0 + v1 + v2 to 2^-24
+ * relative), the six piece products down to order 2^-16 accumulated in fp32 by
+ * v_mfma_f32_16x16x32_bf16 -- an error per product of a few fp32 ulps (tested against the
+ * fp32 path and a float64 product); mode 0: v_mfma_f32_16x16x4_f32 (a k-ordered fp32 fmaf
+ * chain). k < 128 always takes mode 0. Returns the previous mode, GNN_E_ARG for another value.
+ */
+int gnn_transform_set_precision(int mode);
 int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,
                           int64_t fout, float* y, int64_t ldy, void* stream);
 

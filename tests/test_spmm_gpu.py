@@ -400,6 +400,48 @@ def test_gcn_transform_mfma(dev, k, fout, n):
         assert torch.equal(yr, torch.clamp_min(y, 0.0))
 
 
+@pytest.mark.parametrize("k,fout", [(128, 64), (128, 128), (128, 256), (256, 64), (256, 128),
+                                    (256, 256)])
+@pytest.mark.parametrize("n", [37, 5000])
+@pytest.mark.parametrize("scale", [1.0, 1e-3])
+def test_transform_split_bf16_accuracy(dev, k, fout, n, scale):
+    """The split-bf16 transform (fp32 products from bf16 MFMAs, gnn_transform_set_precision(1),
+    the default at K >= 128) against a float64 product: its error, relative to sum_k |x w| of
+    each output (the scale of a dot product's rounding), stays below 1e-6 and within 4x of the
+    fp32-MFMA path's own error (mode 0, a k-ordered fp32 fmaf chain); every epilogue."""
+    from graphneuralnetwork_amd.ops import (gcn_transform, linear_relu_classify,
+                                            set_transform_precision)
+    g = torch.Generator(device=dev).manual_seed(k + fout + n)
+    x = torch.randn(n, k, device=dev, generator=g) * scale
+    w = torch.randn(fout, k, device=dev, generator=g) / k ** 0.5
+    xd, wd = x.double(), w.double()
+    ref = xd @ wd.T
+    mag = x.abs().double() @ w.abs().double().T
+    errs = {}
+    prev = set_transform_precision("split-bf16")
+    try:
+        for mode in ("fp32-mfma", "split-bf16"):
+            set_transform_precision(mode)
+            y = gcn_transform(x, w)
+            assert y is not None
+            errs[mode] = float(((y.double() - ref).abs() / mag.clamp_min(1e-300)).max())
+            yr = gcn_transform(x, w, relu=True)
+            assert torch.equal(yr, torch.clamp_min(y, 0.0))
+            perm = torch.randperm(n, device=dev, generator=g)
+            ys = gcn_transform(x, w, out=torch.empty_like(y), out_rows=perm)
+            assert torch.equal(ys[perm], y)
+            if fout <= 128:
+                wcls = torch.randn(3, fout, device=dev, generator=g)
+                y2, lg = linear_relu_classify(x, w, wcls, None)
+                assert torch.equal(y2, yr)
+                lref = yr.double() @ wcls.double().T
+                close(lg.cpu().numpy(), lref.cpu().numpy(), rtol=1e-5)
+    finally:
+        set_transform_precision(prev)
+    assert errs["split-bf16"] < 1e-6, errs
+    assert errs["split-bf16"] <= 4 * errs["fp32-mfma"] + 1e-7, errs
+
+
 def test_gcn_transform_fallback_and_training(dev):
     """Uncovered shapes return None (nn.Linear runs); with autograd the layer uses nn.Linear."""
     from graphneuralnetwork_amd.gcn import Graph_conv_layer

@@ -34,7 +34,9 @@ def main():
         return
     import torch
     from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.ops import gcn_transform
+    ops.TRANSFORM_WIDE_MFMA = True  # time the 256-column MFMA paths too (off by policy)
     dev = torch.device("cuda:0")
     res = {}
     for sh in a.shapes.split(","):
