@@ -109,4 +109,37 @@ template <> struct TileLds<256> {  // a 1-float4 row pad alone is conflict-free 
 };
 #endif
 
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------
+// fp32 products from bf16 MFMAs (X6 kernels). Every fp32 value is split into three bf16
+// pieces, v = v0 + v1 + v2 + e with |e| <= 2^-24 |v| (v0 = bf16(v), v1 = bf16(v - v0),
+// v2 = bf16(v - v0 - v1); the differences are exact in fp32), and a product x w is summed
+// from the six piece products down to order 2^-16: x0w0 + x0w1 + x1w0 + x0w2 + x1w1 + x2w0.
+// A bf16 x bf16 product is exact in fp32 and v_mfma_f32_16x16x32_bf16 accumulates in fp32,
+// so what is left out (x1w2, x2w1, x2w2 and the pieces' residues) is ~4 * 2^-24 |x w| per
+// product -- the size of fp32's own rounding -- while the six MFMAs take 6 x 16 cycles
+// against 8 x 32 for the same 32-long k-step on v_mfma_f32_16x16x4_f32.
+// Non-finite inputs: an inf becomes NaN (inf - inf in the split); the GCN / SAGE layers
+// never feed one.
+__device__ __forceinline__ void split3(float v, __bf16& a, __bf16& b, __bf16& c) {
+  a = static_cast<__bf16>(v);
+  const float r1 = v - static_cast<float>(a);
+  b = static_cast<__bf16>(r1);
+  c = static_cast<__bf16>(r1 - static_cast<float>(b));
+}
+// LDS image of an X6 tile: three bf16 planes (pieces 0, 1, 2), row pitch 2K + 32 bytes, the
+// 16-B chunk c of row rr stored at chunk c ^ swz6(rr): enumerated against the ds_read_b128
+// lane groups (4 x 16 lanes, bank (a/4) mod 64) for the fragment reads (lane (q, r): row r,
+// chunk q*K/32 + s) -- conflict-free -- and the staging ds_write_b64 (16 contiguous lanes =
+// one 128-B run of a row) stays conflict-free under the permutation.
+template <int K> __device__ __forceinline__ int swz6(int rr) {
+  return K >= 256 ? (rr >> 2) & 1 : K >= 128 ? (rr >> 1) & 1 : rr & 1;
+}
+template <int K> constexpr int x6_pitch() { return 2 * K + 32; }  // bytes per LDS row
+// the transforms' arithmetic at K >= 128 and the GAT projection's at K in {64, 128}
+// (gnn_transform_set_precision, defined in transform.hip): 1 = X6 split bf16, 0 = fp32 MFMA
+extern int g_tf_x6;
+
 }  // namespace gnn

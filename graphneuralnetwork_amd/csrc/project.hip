@@ -73,7 +73,10 @@ __device__ __forceinline__ void proj_tile_sync() {
 #endif
 }
 
-template <int K, int NT, bool COLROW>
+// X6 (K = 64; the kernel takes 64 and 128): the products from bf16 MFMAs with three-piece fp32 splits (common.hpp
+// split3): W and the logit tile split once into registers, each wave's X tile split while it
+// is staged into three bf16 LDS planes, six v_mfma_f32_16x16x32_bf16 per 32-long k-step.
+template <int K, int NT, bool COLROW, bool X6 = false>
 __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
     const float* __restrict__ w2, int heads, float* __restrict__ wh, int64_t ldwh,
@@ -83,7 +86,11 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
   constexpr int FO = 16 * NT;
   constexpr int LDA = 4 * ProjLds<K>::L4;  // LDS row (floats), see ProjLds
   constexpr int G = kProjG;
-  __shared__ float atile[kProjWaves][16 * G * LDA];
+  constexpr int S32 = K / 32;
+  constexpr int P6 = x6_pitch<K>();
+  constexpr int PLANE = 16 * G * P6;  // bytes per bf16 plane of a wave's tile
+  static_assert(!X6 || K == 64 || K == 128, "X6 projection: K in {64, 128}");
+  __shared__ float atile[kProjWaves][X6 ? 3 * PLANE / 4 : 16 * G * LDA];
   const int lane = threadIdx.x & (kWave - 1);
   const int q = lane >> 4, r = lane & 15;
   const bool vec_logits = heads % 4 == 0 && lde % 4 == 0 &&
@@ -99,15 +106,35 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
   for (int e = threadIdx.x; e < K * FO; e += kProjBlock) ws[e] = w[e];
   __syncthreads();
 #else
-  float b[NT][S];  // B fragments: W[q*S + s][16t + r], resident for the whole launch
+  float b[X6 ? 1 : NT][X6 ? 1 : S];  // B fragments: W[q*S + s][16t + r], resident
+  float b2[X6 ? 1 : S];
+  bf16x8 bx[X6 ? NT + 1 : 1][X6 ? S32 : 1][3];  // X6: pieces of W[q*S + 8 s6 + j][16t + r]
+  if constexpr (X6) {
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+    for (int t = 0; t <= NT; ++t)  // t == NT: the logit tile w2
 #pragma unroll
-    for (int s = 0; s < S; ++s) b[t][s] = w[(q * S + s) * FO + 16 * t + r];
+      for (int s6 = 0; s6 < S32; ++s6)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = q * S + 8 * s6 + j;
+          const float v = t < NT ? w[k * FO + 16 * t + r] : w2[k * 16 + r];
+          __bf16 p0, p1, p2;
+          split3(v, p0, p1, p2);
+          bx[t][s6][0][j] = p0;
+          bx[t][s6][1][j] = p1;
+          bx[t][s6][2][j] = p2;
+        }
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int s = 0; s < S; ++s) b[t][s] = w[(q * S + s) * FO + 16 * t + r];
+  }
   __syncthreads();
-  float b2[S];
+  if constexpr (!X6) {
 #pragma unroll
-  for (int s = 0; s < S; ++s) b2[s] = w2s[(q * S + s) * 16 + r];
+    for (int s = 0; s < S; ++s) b2[s] = w2s[(q * S + s) * 16 + r];
+  }
 #endif
 
   // A tiles are staged through LDS: a coalesced 16-B-per-lane copy of the wave's 16 rows,
@@ -139,12 +166,31 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
       const int e = v * kWave + lane;
       if (e < V4) {
         const int rr = e / (K / 4), c4 = e - rr * (K / 4);
-        *reinterpret_cast<float4*>(at + rr * LDA + 4 * (c4 ^ ProjLds<K>::swz(rr))) = src[v];
+        if constexpr (X6) {
+          const float tv[4] = {src[v].x, src[v].y, src[v].z, src[v].w};
+          bf16x4 p0, p1, p2;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            __bf16 u0, u1, u2;
+            split3(tv[i], u0, u1, u2);
+            p0[i] = u0;
+            p1[i] = u1;
+            p2[i] = u2;
+          }
+          char* base = reinterpret_cast<char*>(at) + rr * P6 + 16 * ((c4 >> 1) ^ swz6<K>(rr)) +
+                       8 * (c4 & 1);
+          *reinterpret_cast<bf16x4*>(base) = p0;
+          *reinterpret_cast<bf16x4*>(base + PLANE) = p1;
+          *reinterpret_cast<bf16x4*>(base + 2 * PLANE) = p2;
+        } else {
+          *reinterpret_cast<float4*>(at + rr * LDA + 4 * (c4 ^ ProjLds<K>::swz(rr))) = src[v];
+        }
       }
     }
     proj_tile_sync();
     fetch(src, g + DEPTH * static_cast<int64_t>(gridDim.x));  // refill this slot
-    float a[G][S];
+    float a[X6 ? 1 : G][X6 ? 1 : S];
+    if constexpr (!X6)
 #pragma unroll
     for (int j = 0; j < G; ++j)
 #pragma unroll
@@ -164,12 +210,42 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    if constexpr (X6) {
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        const int rr = j * 16 + r;
+#pragma unroll
+        for (int s6 = 0; s6 < S32; ++s6) {
+          const char* xp = reinterpret_cast<const char*>(at) + rr * P6 +
+                           16 * ((q * S32 + s6) ^ swz6<K>(rr));
+          const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(xp);
+          const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(xp + PLANE);
+          const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(xp + 2 * PLANE);
+#pragma unroll
+          for (int t = 0; t <= NT; ++t) {  // smallest terms first; t == NT: the logit tile
+            f32x4 c = t < NT ? acc[j][t] : acc2[j];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[t][s6][0], x2, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[t][s6][1], x1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[t][s6][2], x0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[t][s6][0], x1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[t][s6][1], x0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx[t][s6][0], x0, c, 0, 0, 0);
+            if (t < NT)
+              acc[j][t] = c;
+            else
+              acc2[j] = c;
+          }
+        }
+      }
+    } else
 #ifdef GNN_PROJ_NO_MFMA
+    {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[j][t] = f32x4{a[j][t], a[j][t + 1], a[j][t + 2], a[j][t + 3]};
       acc2[j] = f32x4{a[j][4], a[j][5], a[j][6], a[j][7]};
+    }
     }
 #else
 #pragma unroll
@@ -260,14 +336,27 @@ static int launch_project(const float* x, int64_t ldx, int64_t n_rows, const flo
 #define GNN_PROJ_GRID 512
 #endif
   const int64_t grid = groups < GNN_PROJ_GRID ? groups : GNN_PROJ_GRID;  // W resident across groups
+  const dim3 g(static_cast<unsigned>(grid));
+  // X6 at K = 64 only: in one process (tools/transform_prec_ab.py,
+  // profiles/r03z_transform_prec_ab.log) 1M x 64 -> 8 x 8 112.5 vs 130.4 us in order, 145.5 vs
+  // 142.0 with the rows scattered by a random permutation; 1M x 128 -> 4 x 8 138.6 vs 139.2
+  if constexpr (K == 64) {
+    if (g_tf_x6) {  // the transforms' arithmetic (gnn_transform_set_precision)
+      if (col_row != nullptr)
+        hipLaunchKernelGGL((gat_project_kernel<K, NT, true, true>), g, dim3(kProjBlock), 0, s, x,
+                           ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row);
+      else
+        hipLaunchKernelGGL((gat_project_kernel<K, NT, false, true>), g, dim3(kProjBlock), 0, s, x,
+                           ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row);
+      return launch_status();
+    }
+  }
   if (col_row != nullptr)
-    hipLaunchKernelGGL((gat_project_kernel<K, NT, true>), dim3(static_cast<unsigned>(grid)),
-                       dim3(kProjBlock), 0, s, x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er,
-                       lde, col_row);
+    hipLaunchKernelGGL((gat_project_kernel<K, NT, true>), g, dim3(kProjBlock), 0, s, x, ldx,
+                       n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row);
   else
-    hipLaunchKernelGGL((gat_project_kernel<K, NT, false>), dim3(static_cast<unsigned>(grid)),
-                       dim3(kProjBlock), 0, s, x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er,
-                       lde, col_row);
+    hipLaunchKernelGGL((gat_project_kernel<K, NT, false>), g, dim3(kProjBlock), 0, s, x, ldx,
+                       n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row);
   return launch_status();
 }
 

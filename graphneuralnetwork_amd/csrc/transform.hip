@@ -40,35 +40,7 @@ struct Classifier {
 // kernel epilogue modes
 constexpr int kTfPlain = 0, kTfScatter = 1, kTfClassify = 2;
 using tf32x4 = __attribute__((ext_vector_type(4))) float;
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-
-// ---------------------------------------------------------------------------------------
-// fp32 products from bf16 MFMAs (X6 kernels). Every fp32 value is split into three bf16
-// pieces, v = v0 + v1 + v2 + e with |e| <= 2^-24 |v| (v0 = bf16(v), v1 = bf16(v - v0),
-// v2 = bf16(v - v0 - v1); the differences are exact in fp32), and a product x w is summed
-// from the six piece products down to order 2^-16: x0w0 + x0w1 + x1w0 + x0w2 + x1w1 + x2w0.
-// A bf16 x bf16 product is exact in fp32 and v_mfma_f32_16x16x32_bf16 accumulates in fp32,
-// so what is left out (x1w2, x2w1, x2w2 and the pieces' residues) is ~4 * 2^-24 |x w| per
-// product -- the size of fp32's own rounding -- while the six MFMAs take 6 x 16 cycles
-// against 8 x 32 for the same 32-long k-step on v_mfma_f32_16x16x4_f32.
-// Non-finite inputs: an inf becomes NaN (inf - inf in the split); the GCN / SAGE layers
-// never feed one.
-__device__ __forceinline__ void split3(float v, __bf16& a, __bf16& b, __bf16& c) {
-  a = static_cast<__bf16>(v);
-  const float r1 = v - static_cast<float>(a);
-  b = static_cast<__bf16>(r1);
-  c = static_cast<__bf16>(r1 - static_cast<float>(b));
-}
-// LDS image of an X6 tile: three bf16 planes (pieces 0, 1, 2), row pitch 2K + 32 bytes, the
-// 16-B chunk c of row rr stored at chunk c ^ swz6(rr): enumerated against the ds_read_b128
-// lane groups (4 x 16 lanes, bank (a/4) mod 64) for the fragment reads (lane (q, r): row r,
-// chunk q*K/32 + s) -- conflict-free -- and the staging ds_write_b64 (16 contiguous lanes =
-// one 128-B run of a row) stays conflict-free under the permutation.
-template <int K> __device__ __forceinline__ int swz6(int rr) {
-  return K >= 256 ? (rr >> 2) & 1 : K >= 128 ? (rr >> 1) & 1 : rr & 1;
-}
-template <int K> constexpr int x6_pitch() { return 2 * K + 32; }  // bytes per LDS row
+// split3 / swz6 / x6_pitch (fp32 products from bf16 MFMAs): common.hpp
 
 #ifndef GNN_TF_SINGLE_BUFFER
 #define GNN_TF_SINGLE_BUFFER 0  // A/B: the round-2 one-buffer tile loop (two barriers per tile)
@@ -375,7 +347,7 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
 
 // transform precision (gnn_transform_set_precision): 1 = fp32 products from bf16 MFMAs (X6,
 // K >= 128), 0 = v_mfma_f32_16x16x4_f32 (a k-ordered fp32 fmaf chain)
-static int g_tf_x6 = 1;
+int g_tf_x6 = 1;
 
 template <int K, int CB, int NW, bool RELU, int TR, bool X6>
 static void launch_transform_kernel(dim3 grid, const float* x, int64_t ldx, int64_t n_rows,

@@ -35,7 +35,7 @@ def timed(fn, reps=20, rounds=5):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--shapes", default=SHAPES,
+    ap.add_argument("--shapes", default="8192:256:128:1,61771:256:128:1,1000000:128:128:0",
                     help="rows:k:fout:mode, mode 0 = plain, 1 = ReLU, 2 = scattered rows")
     a = ap.parse_args()
     from graphneuralnetwork_amd.ops import gcn_transform, set_transform_precision
@@ -75,6 +75,29 @@ def main():
         del x, out, perm
         torch.cuda.empty_cache()
     print(json.dumps({"us": res}), flush=True)
+    # the GAT projection (gnn_gat_project_f32 / _rows_f32): cfg3's 1M x 64 -> 8 heads x 8
+    from graphneuralnetwork_amd.ops import gat_project
+    for n, k, H, fh in ((1_000_000, 64, 8, 8), (1_000_000, 128, 4, 8)):
+        x = torch.randn(n, k, device=dev)
+        w = torch.randn(k, H * fh, device=dev) / k ** 0.5
+        a_s, a_d = torch.randn(H * fh, device=dev), torch.randn(H * fh, device=dev)
+        perm = torch.randperm(n, device=dev)
+        idx = torch.randint(0, n, (2048,), device=dev)
+        ref = x[idx].double() @ w.double()
+        mag = x[idx].abs().double() @ w.abs().double()
+        r = {}
+        for prec in ("fp32-mfma", "split-bf16"):
+            set_transform_precision(prec)
+            r[prec] = timed(lambda: gat_project(x, w, H, fh, a_s, a_d))
+            r[prec + "_rows"] = timed(lambda: gat_project(x, w, H, fh, a_s, a_d, col_rows=perm))
+            wh = gat_project(x, w, H, fh, a_s, a_d)[0]
+            r[prec + "_err"] = float(((wh[idx].double() - ref).abs() / mag).max())
+        set_transform_precision("split-bf16")
+        tag = f"project {n}x{k}->{H}x{fh}"
+        res[tag] = r
+        print(json.dumps({tag: r}), flush=True)
+        del x, perm
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
