@@ -604,20 +604,26 @@ class DegreeOrder:
         return y.index_select(0, self.inv)
 
 
-def degree_order(g: "CsrGraph", rows: bool = True) -> DegreeOrder:
+def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None) -> DegreeOrder:
     """Relabel a CSR graph by column in-degree (torch ops on its device). The edges of each
     row keep their CSR order (renamed), so every row sum runs in the same order: the result
     is bit-identical to the original graph's, permuted.
 
     ``rows=True`` (square graphs): both sides, A' = P A P^T, for Y' = A' X' = P Y.
     ``rows=False``: the columns only, A' = A P^T, for Y = A' (P X) -- the output rows stay
-    in the original order."""
+    in the original order.
+    ``prefix``: only the ``prefix`` highest-degree ids are ranked (first, by degree); the rest
+    follow in their original id order, so a producer that writes its rows in the new order
+    (a transform or projection with scattered output rows) stores all but the prefix rows in
+    ascending address order. The hub ranking of any K <= prefix is the full order's."""
     n = g.n_cols
     dev = g.device
     indeg = torch.bincount(g.col.to(torch.int64), minlength=n)
     idx = torch.arange(n, device=dev, dtype=torch.int64)
     # descending in-degree, ascending id on ties: one stable sort of -indeg
     perm = torch.sort(-indeg, stable=True).indices
+    if prefix is not None and prefix < n:
+        perm = torch.cat([perm[:prefix], torch.sort(perm[prefix:]).values])
     inv = torch.empty_like(perm)
     inv[perm] = idx
     if not rows:

@@ -256,12 +256,22 @@ def _spmm_xcd(lib, g: CsrGraph, xp, x, feat, bias, out, seg, skip_empty, flags, 
 DEGREE_ORDER = True
 
 
+# None: every column ranked by in-degree; an int: only that many hub columns ranked first, the
+# rest in id order (graph.degree_order ``prefix``), so the scattered-row producers (transform /
+# projection) store the non-hub rows in ascending order. Must be >= every hub count K taken
+# from the order (XCD_HUB_ROWS, HUB_ROWS).
+COLUMN_ORDER_PREFIX = None
+
+
 def _cached_column_order(g: CsrGraph):
-    key = ("_colorder",)
+    prefix = COLUMN_ORDER_PREFIX
+    if prefix is not None and prefix < max(XCD_HUB_ROWS, HUB_ROWS):
+        raise ValueError("COLUMN_ORDER_PREFIX must cover the hub rows (XCD_HUB_ROWS, HUB_ROWS)")
+    key = ("_colorder", prefix)
     o = g._plans.get(key)
     if o is None:
         from .graph import degree_order
-        o = g._plans[key] = degree_order(g, rows=False)
+        o = g._plans[key] = degree_order(g, rows=False, prefix=prefix)
     return o
 
 

@@ -190,7 +190,8 @@ int gnn_gcn_transform_supported(int64_t k, int64_t fout);
  * relative), the six piece products down to order 2^-16 accumulated in fp32 by
  * v_mfma_f32_16x16x32_bf16 -- an error per product of a few fp32 ulps (tested against the
  * fp32 path and a float64 product); mode 0: v_mfma_f32_16x16x4_f32 (a k-ordered fp32 fmaf
- * chain). k < 128 always takes mode 0. Returns the previous mode, GNN_E_ARG for another value.
+ * chain). k < 128 always takes mode 0; the GAT projection (gnn_gat_project_f32 / _rows_f32)
+ * follows the same mode at k = 64. Returns the previous mode, GNN_E_ARG for another value.
  */
 int gnn_transform_set_precision(int mode);
 int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,

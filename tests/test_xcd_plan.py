@@ -157,18 +157,24 @@ def test_task_ranges_invariants(max_deg, cost):
     assert task_ranges(torch.zeros(1, dtype=torch.int64), max_deg, cost).numel() == 0
 
 
-@pytest.mark.parametrize("rows", [True, False])
-def test_degree_order_bit_identical_and_hub_prefix(rows):
+@pytest.mark.parametrize("rows,prefix", [(True, None), (False, None), (False, 300),
+                                         (True, 1000)])
+def test_degree_order_bit_identical_and_hub_prefix(rows, prefix):
     """graph.degree_order (CPU torch ops): A' = P A P^T (or A P^T) with each row's edges in
     their CSR order, so A' X' equals the original product bit for bit (permuted); the
-    in-degree ranking of hub.hip (descending, ties by ascending id) is then the identity."""
+    in-degree ranking of hub.hip (descending, ties by ascending id) is then the identity.
+    ``prefix``: the first ``prefix`` ids are the full order's, the rest ascending ids."""
     from graphneuralnetwork_amd.graph import CsrGraph, degree_order
     rowptr, col, val = _graph(4000, 50000, 3)
     n = rowptr.size - 1
     g = CsrGraph(torch.from_numpy(rowptr), torch.from_numpy(col.astype(np.int32)),
                  torch.from_numpy(val), n, n)
-    o = degree_order(g, rows=rows)
+    o = degree_order(g, rows=rows, prefix=prefix)
     perm, inv = o.perm.numpy(), o.inv.numpy()
+    if prefix is not None:
+        full = degree_order(g, rows=False).perm.numpy()
+        np.testing.assert_array_equal(perm[:prefix], full[:prefix])
+        np.testing.assert_array_equal(perm[prefix:], np.sort(full[prefix:]))
     np.testing.assert_array_equal(inv[perm], np.arange(n))
     gp = o.graph
     X = np.random.default_rng(5).standard_normal((n, 6))
