@@ -1029,6 +1029,12 @@ def main():
     ap.add_argument("--traffic-json", default=None,
                     help="PMC traffic summary (tools/pmc_traffic.py); default profiles/traffic_<workload>_F<feat>.json")
     args = ap.parse_args()
+    # stdout carries exactly ONE line, the JSON result: whatever the libraries print there
+    # (RCCL's version banner at communicator init, gloo's peer messages) goes to stderr with
+    # the bench's own log lines
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     if os.environ.get("GNN_BENCH_STACKS"):  # rehearsals: every rank dumps its stack periodically
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["GNN_BENCH_STACKS"]), repeat=True)
@@ -1077,7 +1083,8 @@ def main():
         del e10
     if rank == 0:
         res["bench_wall_s"] = time.perf_counter() - t_all
-        print(json.dumps(res), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(res) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
 
