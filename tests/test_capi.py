@@ -55,6 +55,11 @@ def test_argument_rejection_without_launch(lib):
     assert lib.gnn_spmm_plan_count(None, 10, 4, None, None, None) == -1
     assert lib.gnn_spmm_plan_scratch_bytes(-5) < 0
     assert lib.gnn_spmm_plan_scratch_bytes(10_000_000) > 0
+    # the transforms' arithmetic: the previous mode back, anything but 0 / 1 refused
+    prev = lib.gnn_transform_set_precision(0)
+    assert prev in (0, 1)
+    assert lib.gnn_transform_set_precision(prev) == 0
+    assert lib.gnn_transform_set_precision(2) == -1
     # the fused classifier: n_cls outside [1, 4] / missing operands, nothing launched
     for n_cls, wd, lg in ((0, 1, 1), (5, 1, 1), (3, None, 1), (3, 1, None)):
         assert lib.gnn_linear_relu_cls_f32(16, 256, 100, 256, 16, 128, 16, 128, wd, None, n_cls,
