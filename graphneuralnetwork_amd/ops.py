@@ -267,7 +267,7 @@ def _cached_column_order(g: CsrGraph):
     prefix = COLUMN_ORDER_PREFIX
     if prefix is not None and prefix < max(XCD_HUB_ROWS, HUB_ROWS):
         raise ValueError("COLUMN_ORDER_PREFIX must cover the hub rows (XCD_HUB_ROWS, HUB_ROWS)")
-    key = ("_colorder", prefix)
+    key = ("_colorder",) if prefix is None else ("_colorder", prefix)
     o = g._plans.get(key)
     if o is None:
         from .graph import degree_order
