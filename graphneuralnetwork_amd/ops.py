@@ -547,6 +547,9 @@ def linear_relu_classify(x: torch.Tensor, weight: torch.Tensor, wd: torch.Tensor
     m = x.shape[0]
     if out is None:
         out = torch.empty((m, fout), dtype=torch.float32, device=x.device)
+    elif (out.shape != (m, fout) or out.dtype != torch.float32 or out.device != x.device
+          or out.stride(1) != 1 or out.stride(0) % 4 or out.data_ptr() % 16):
+        raise ValueError("out must be float32 [rows, fout] on x's device, 16-B aligned rows")
     logits = torch.empty((m, n_cls), dtype=torch.float32, device=x.device)
     _lib.check(lib.gnn_linear_relu_cls_f32(
         x.data_ptr(), x.stride(0), m, k, w.data_ptr(), fout, out.data_ptr(), out.stride(0),
