@@ -266,6 +266,9 @@ def test_linear_relu_classify_uncovered(dev):
     assert linear_relu_classify(x, w, torch.randn(5, 128, device=dev)) is None
     assert linear_relu_classify(torch.randn(50, 100, device=dev), torch.randn(128, 100, device=dev),
                                 torch.randn(3, 128, device=dev)) is None
+    with pytest.raises(ValueError):  # a caller-supplied out of the wrong shape
+        linear_relu_classify(x, w, torch.randn(3, 128, device=dev),
+                             out=torch.empty(49, 128, device=dev))
 
 
 def test_graphsage_forward_classifier_epilogue(dev, monkeypatch):
