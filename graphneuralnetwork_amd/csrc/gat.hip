@@ -220,7 +220,10 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
   }
 }
 
-constexpr int kGatShortChunk = 8;  // edges whose loads one lane issues together
+#ifndef GNN_GAT_SHORT_CHUNK
+#define GNN_GAT_SHORT_CHUNK 4  // A/B at cfg3 (tools/gat_ab.py, profiles/r03ai_gat_short_chunk_ab.log): 4 0.794, 8 0.803, 16 0.859 ms
+#endif
+constexpr int kGatShortChunk = GNN_GAT_SHORT_CHUNK;  // edges whose loads one lane issues together
 
 // Short rows (deg 2..8 on R-MAT: 35 % of the rows, 6 % of the edges), 64/LPR rows per
 // wave: each LPR-lane group owns one row and every lane runs the edge softmax for the

@@ -37,6 +37,8 @@ VARIANTS = {
     "gs4c16": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_CHUNK=16"],
     "gs4c16u4": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_CHUNK=16", "GNN_GAT_U=4"],
     "gs4np": ["GNN_GAT_SMALL_UNROLL=4", "GNN_GAT_PIPE=0"],
+    "sc4": ["GNN_GAT_SHORT_CHUNK=4"],
+    "sc16": ["GNN_GAT_SHORT_CHUNK=16"],
 }
 
 
