@@ -2,6 +2,7 @@
 one process, on the bench graphs; the outputs are compared too.
 
     python tools/tasks_ab.py [--workload cfg2|ns] [--feat 128] [--grid "64:256,64:128,..."]
+                             [--column-order]
 """
 import argparse
 import statistics
@@ -33,6 +34,8 @@ def main():
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--grid", default="64:256,64:128,64:512,32:256,128:256,16:256")
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--column-order", action="store_true",
+                    help="over the column-degree-ordered graph (ops.column_order), as the bench")
     a = ap.parse_args()
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
@@ -44,6 +47,8 @@ def main():
     g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n)
     del s, d
     F = a.feat
+    if a.column_order:
+        g = ops.column_order(g, F).graph
     X = torch.randn(n, F, device=dev)
     b = torch.randn(F, device=dev)
     Y = torch.empty(n, F, device=dev)
