@@ -33,6 +33,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--ks", default="262144,393216,524288,786432")
+    ap.add_argument("--param", default="XCD_HUB_ROWS",
+                    help="the ops knob swept with --ks (e.g. XCD_MIN_DEG, XCD_CHUNK)")
     a = ap.parse_args()
     import bench
     from graphneuralnetwork_amd import ops
@@ -45,11 +47,12 @@ def main():
     X = torch.randn(g.n_cols, F, device=dev)
     Y = torch.empty(g.n_rows, F, device=dev)
     b = torch.randn(F, device=dev)
-    ops.XCD_HUB_BYTES = 1 << 40
-    res, ref = {"workload": a.workload}, None
+    if a.param == "XCD_HUB_ROWS":
+        ops.XCD_HUB_BYTES = 1 << 40
+    res, ref = {"workload": a.workload, "param": a.param}, None
     for rnd in range(2):  # two interleaved rounds
         for k in [int(v) for v in a.ks.split(",")]:
-            ops.XCD_HUB_ROWS = k
+            setattr(ops, a.param, k)
             fn = lambda: spmm_forward(ga, X, b, out=Y)  # noqa: E731
             fn()
             if ref is None:
