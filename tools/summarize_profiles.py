@@ -94,7 +94,9 @@ def main():
                     s[k.split("(")[0][:90]] = {"l2_hit_rate": round(hit[k] / tot, 3)}
         summary[wl] = s
         print(wl, json.dumps(s.get("_traffic_bytes_per_step")))
-    (ROOT / "profiles" / f"{a.round}_summary.json").write_text(json.dumps(summary, indent=1) + "\n")
+    if summary:
+        (ROOT / "profiles" / f"{a.round}_summary.json").write_text(
+            json.dumps(summary, indent=1) + "\n")
 
 
 if __name__ == "__main__":
