@@ -54,6 +54,7 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
         _vp, _i64, _vp, _i64,           # mid_row, n_mid, task_row, n_task
         _vp, _u32, _vp]),               # partial, flags, stream
+    "gnn_spmm_tasks_check": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp]),
     "gnn_sage_gather_concat_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _i64, _i64, _i64,
                                                    _i64, _i32, _vp, _i64, _vp, _i64, _vp, _vp]),
     "gnn_halo_alltoallv_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp]),
@@ -69,6 +70,7 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_gat_project_supported": (ctypes.c_int, [_i64, _i64, _i64]),
     "gnn_gcn_transform_supported": (ctypes.c_int, [_i64, _i64]),
     "gnn_transform_set_precision": (ctypes.c_int, [ctypes.c_int]),
+    "gnn_transform_get_precision": (ctypes.c_int, []),
     "gnn_gcn_transform_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnn_linear_relu_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnn_linear_relu_cls_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64,

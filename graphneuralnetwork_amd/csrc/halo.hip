@@ -9,11 +9,13 @@
 //
 // The library does not link RCCL: the communicator belongs to whichever RCCL the caller
 // loaded (PyTorch ships its own librccl.so), so ncclAllToAllv is resolved at the first call
-// from the process -- the global scope, then an already-loaded librccl.so / librccl.so.1,
-// then librccl.so.1 from the loader path -- so that the call and the communicator come from
-// the same library.
+// from the process -- the global scope, then an already-loaded librccl.so / librccl.so.1 --
+// so that the call and the communicator come from the same library. An RCCL that is not
+// loaded yet is never loaded here: it could not own the caller's communicator, so the entry
+// returns GNN_E_COMM instead.
 #include <dlfcn.h>
 
+#include <cstdint>
 #include <mutex>
 #include <vector>
 
@@ -36,10 +38,6 @@ static void resolve_a2av() {
   for (const char* nm : names) {
     if (f) break;
     void* h = dlopen(nm, RTLD_LAZY | RTLD_NOLOAD);
-    if (h) f = dlsym(h, "ncclAllToAllv");
-  }
-  if (!f) {
-    void* h = dlopen("librccl.so.1", RTLD_LAZY | RTLD_GLOBAL);
     if (h) f = dlsym(h, "ncclAllToAllv");
   }
   g_a2av = reinterpret_cast<AllToAllvFn>(f);
@@ -67,15 +65,21 @@ extern "C" int gnn_halo_alltoallv_f32(const float* send, const int64_t* send_row
                                       void* comm, void* stream) {
   if (world < 1 || row_floats < 0 || !send_rows || !recv_rows || !comm) return GNN_E_ARG;
   std::vector<size_t> sc(world), sd(world), rc(world), rd(world);
-  size_t so = 0, ro = 0;
+  // element counts and running offsets must stay below 2^62 (no signed / size_t wrap)
+  constexpr int64_t kMax = INT64_C(1) << 62;
+  int64_t so = 0, ro = 0;
   for (int64_t q = 0; q < world; ++q) {
     if (send_rows[q] < 0 || recv_rows[q] < 0) return GNN_E_ARG;
-    sc[q] = static_cast<size_t>(send_rows[q] * row_floats);
-    rc[q] = static_cast<size_t>(recv_rows[q] * row_floats);
-    sd[q] = so;
-    rd[q] = ro;
-    so += sc[q];
-    ro += rc[q];
+    if (row_floats > 0 && (send_rows[q] > kMax / row_floats || recv_rows[q] > kMax / row_floats))
+      return GNN_E_UNSUPPORTED;
+    const int64_t s = send_rows[q] * row_floats, r = recv_rows[q] * row_floats;
+    if (s > kMax - so || r > kMax - ro) return GNN_E_UNSUPPORTED;
+    sc[q] = static_cast<size_t>(s);
+    rc[q] = static_cast<size_t>(r);
+    sd[q] = static_cast<size_t>(so);
+    rd[q] = static_cast<size_t>(ro);
+    so += s;
+    ro += r;
   }
   if ((so && !send) || (ro && !recv)) return GNN_E_ARG;
   std::call_once(g_a2av_once, resolve_a2av);

@@ -282,7 +282,11 @@ __device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int 
   const int sub = lane & (LPR - 1);
   const int grp = lane / LPR;
   const int32_t rb = P.task_row[2 * t];
-  const int nr = P.task_row[2 * t + 1] - rb;  // 1 .. kTaskRows
+  const int32_t re = P.task_row[2 * t + 1];
+  // a task outside the contract (1..kTaskRows rows inside [0, n_rows)) is skipped, never read
+  // out of bounds; gnn_spmm_tasks_check reports such tasks before a launch
+  if (rb < 0 || re <= rb || re - rb > kTaskRows || re > P.n_rows) return;
+  const int nr = re - rb;  // 1 .. kTaskRows
   const int64_t e0 = P.rowptr[rb];
   // lane l < nr: start of row rb + l relative to e0; lanes >= nr: the task's end
   const int rp = static_cast<int>(P.rowptr[rb + min(lane, nr)] - e0);
@@ -305,6 +309,7 @@ __device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int 
   int cur_end = __shfl(rp, min(cur + 1, nr), kWave);  // its end (slot-uniform)
   const int es = __shfl(rp, sb, kWave);          // the slot's edge range [es, ee)
   const int ee = __shfl(rp, se, kWave);
+  int cur_beg = es;                               // its start (slot-uniform, no shuffle later)
   const bool skip_empty = (P.flags & GNN_EPI_SKIP_EMPTY) != 0;
   const uint32_t epi = P.flags & (GNN_EPI_RELU | GNN_EPI_ELU | GNN_EPI_ACCUMULATE);
   typename Vec<VW>::T acc[NCH];
@@ -312,12 +317,15 @@ __device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int 
   for (int ch = 0; ch < NCH; ++ch) acc[ch] = vzero<VW>();
 
   // write every row of the slot that ends at or before edge position `pos` (several when
-  // rows without edges follow each other); the shuffles run with the whole slot active
+  // rows without edges follow each other). The only shuffle runs outside the divergent
+  // branch, with the whole wave active: a ds_bpermute whose source lane (here a row index,
+  // usually in another slot's lane group) is outside EXEC does not return its value. The
+  // row's start is tracked slot-uniformly (the previous row's end), not shuffled.
   auto flush_upto = [&](int pos) {
     bool need = cur < se && pos >= cur_end;
     while (__ballot(need)) {
       if (need) {
-        const bool empty = __shfl(rp, cur, kWave) == cur_end;
+        const bool empty = cur_beg == cur_end;
         if (!(empty && skip_empty))
           store_slot_row<VW, LPR, NCH, NT>(P.y + static_cast<int64_t>(rb + cur) * P.ldy, P.bias,
                                            P.feat, epi, sub, acc);
@@ -326,6 +334,7 @@ __device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int 
       }
       cur += need ? 1 : 0;
       const int nxt = __shfl(rp, min(cur + 1, nr), kWave);
+      cur_beg = need ? cur_end : cur_beg;
       cur_end = need ? nxt : cur_end;
       need = cur < se && pos >= cur_end;
     }
@@ -692,9 +701,35 @@ static int spmm_entry(const int64_t* rowptr, const int32_t* col, const float* va
   return run_spmm(L, x, bias, y, partial, feat, variant);
 }
 
+// err |= 1 for a task with no row, more than kTaskRows rows or rows outside [0, n_rows);
+// err |= 2 for a task that overlaps the previous one (tasks must be disjoint and ascending)
+__global__ __launch_bounds__(kBlock) void spmm_tasks_check_kernel(const int32_t* __restrict__ task_row,
+                                                                  int64_t n_task, int64_t n_rows,
+                                                                  int32_t* __restrict__ err) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (t >= n_task) return;
+  const int32_t rb = task_row[2 * t], re = task_row[2 * t + 1];
+  int32_t e = 0;
+  if (rb < 0 || re <= rb || re - rb > kTaskRows || re > n_rows) e |= 1;
+  if (t > 0 && task_row[2 * t - 1] > rb) e |= 2;
+  if (e) atomicOr(err, e);
+}
+
 }  // namespace gnn
 
 using namespace gnn;
+
+extern "C" int gnn_spmm_tasks_check(const int32_t* task_row, int64_t n_task, int64_t n_rows,
+                                    int32_t* err, void* stream) {
+  if (n_task < 0 || n_rows < 0 || err == nullptr || (n_task > 0 && task_row == nullptr))
+    return GNN_E_ARG;
+  if (n_task == 0) return GNN_OK;
+  const int64_t blocks = (n_task + kBlock - 1) / kBlock;
+  if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
+  hipLaunchKernelGGL(spmm_tasks_check_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), task_row, n_task, n_rows, err);
+  return launch_status();
+}
 
 extern "C" int gnn_spmm_csr_f32(const int64_t* rowptr, const int32_t* col, const float* val,
                                 int64_t n_rows, const float* x, int64_t ldx, int64_t feat,
@@ -753,6 +788,7 @@ extern "C" int gnn_spmm_csr_tasks_f32(const int64_t* rowptr, const int32_t* col,
                                       const int32_t* task_row, int64_t n_task, float* partial,
                                       uint32_t flags, void* stream) {
   if (n_task < 0 || (n_task > 0 && task_row == nullptr) || mid_row == nullptr) return GNN_E_ARG;
+  if (n_task > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   if (xh == nullptr) ldh = 0;
   return spmm_entry(rowptr, col, val, n_rows, x, ldx, feat, bias, y, ldy, seg_len, seg_row,
                     seg_begin, n_seg, long_row, long_seg_ptr, n_long, nullptr, nullptr, nullptr, 0,

@@ -496,6 +496,8 @@ extern "C" int gnn_transform_set_precision(int mode) {
   return prev;
 }
 
+extern "C" int gnn_transform_get_precision(void) { return g_tf_x6; }
+
 extern "C" int gnn_gcn_transform_supported(int64_t k, int64_t fout) {
   const bool kk = k == 16 || k == 32 || k == 64 || k == 128 || k == 256;
   if (!kk) return 0;

@@ -185,6 +185,25 @@ def task_ranges(rowptr: torch.Tensor, max_deg: int, cost: int, rows: int = TASK_
     return torch.stack([tb, te], 1).reshape(-1).to(torch.int32).contiguous()
 
 
+def check_tasks(task_row: torch.Tensor, n_rows: int) -> None:
+    """Raise if a task list breaks gnn_spmm_csr_tasks_f32's contract (1..63 rows inside
+    [0, n_rows), ascending and disjoint): gnn_spmm_tasks_check on the device, one host read.
+    The kernel skips such tasks, so a bad list would leave rows unwritten silently."""
+    n_task = task_row.numel() // 2
+    if n_task == 0 or not task_row.is_cuda:
+        return
+    err = torch.zeros(1, dtype=torch.int32, device=task_row.device)
+    _lib.check(_lib.load().gnn_spmm_tasks_check(task_row.data_ptr(), n_task, n_rows,
+                                                err.data_ptr(),
+                                                _lib.stream_handle(task_row.device)),
+               "gnn_spmm_tasks_check")
+    e = int(err.item())
+    if e:
+        raise ValueError(f"packed row tasks break the kernel contract (gnn_spmm_tasks_check "
+                         f"flags {e}: 1 = a task outside 1..{TASK_ROWS} rows in [0, {n_rows}), "
+                         f"2 = overlapping / descending tasks)")
+
+
 @dataclass
 class HubPlan:
     """Hub staging of a graph's columns (gnn_spmm_csr_hub_f32): the k highest-degree
@@ -455,8 +474,9 @@ class CsrGraph:
             base = self.plan(seg_len)
             deg = self.rowptr[1:] - self.rowptr[:-1]
             mid = torch.nonzero((deg > max_deg) & (deg <= base.seg_len)).view(-1)
-            p = TaskPlan(base.seg_len, base, mid.to(torch.int32).contiguous(),
-                         task_ranges(self.rowptr, min(max_deg, base.seg_len), cost), max_deg,
+            tasks = task_ranges(self.rowptr, min(max_deg, base.seg_len), cost)
+            check_tasks(tasks, self.n_rows)
+            p = TaskPlan(base.seg_len, base, mid.to(torch.int32).contiguous(), tasks, max_deg,
                          cost)
             self._plans[key] = p
         return p

@@ -439,23 +439,25 @@ TRANSFORM_WIDE_MFMA = True
 
 
 TRANSFORM_PRECISIONS = ("split-bf16", "fp32-mfma")
-_TRANSFORM_PRECISION = ["split-bf16"]  # the library's default (gnn_transform_set_precision)
 
 
 def transform_precision() -> str:
-    """The MFMA transforms' arithmetic at K >= 128 (see set_transform_precision)."""
-    return _TRANSFORM_PRECISION[0]
+    """The MFMA transforms' arithmetic at K >= 128 and of the GAT projection at K = 64 (see
+    set_transform_precision), read back from the library (gnn_transform_get_precision), so a
+    direct C call to gnn_transform_set_precision is seen too."""
+    return TRANSFORM_PRECISIONS[0] if _lib.load().gnn_transform_get_precision() == 1 \
+        else TRANSFORM_PRECISIONS[1]
 
 
 def set_transform_precision(mode: str) -> str:
-    """Arithmetic of the MFMA transforms at K >= 128 (gnn_transform_set_precision), returns the
-    previous mode: 'split-bf16' (default: fp32 products from three-piece bf16 splits on
-    v_mfma_f32_16x16x32_bf16, a few fp32 ulps per product) or 'fp32-mfma'
-    (v_mfma_f32_16x16x4_f32, a k-ordered fp32 fmaf chain)."""
+    """Arithmetic of the MFMA transforms at K >= 128 and of the GAT projection at K = 64
+    (gnn_transform_set_precision, process-wide), returns the previous mode: 'split-bf16'
+    (default: fp32 products from three-piece bf16 splits on v_mfma_f32_16x16x32_bf16, a few
+    fp32 ulps per product) or 'fp32-mfma' (v_mfma_f32_16x16x4_f32, a k-ordered fp32 fmaf
+    chain)."""
     if mode not in TRANSFORM_PRECISIONS:
         raise ValueError(f"transform precision must be one of {TRANSFORM_PRECISIONS}")
     prev = _lib.load().gnn_transform_set_precision(0 if mode == "fp32-mfma" else 1)
-    _TRANSFORM_PRECISION[0] = mode
     return TRANSFORM_PRECISIONS[0] if prev == 1 else TRANSFORM_PRECISIONS[1]
 
 

@@ -225,9 +225,12 @@ def degree_ordered(adj: CsrGraph, table: torch.Tensor | None = None):
     n = g.n_rows
     rows = torch.repeat_interleave(torch.arange(n, device=g.device, dtype=torch.int64),
                                    g.rowptr[1:] - g.rowptr[:-1])
-    key = torch.sort(rows * n + g.col.to(torch.int64)).values
+    # each row's neighbours back in ascending order; the values follow their edges (a weighted
+    # adjacency keeps every weight on its own edge)
+    key, perm = torch.sort(rows * n + g.col.to(torch.int64), stable=True)
     del rows
-    g2 = CsrGraph(g.rowptr, (key % n).to(torch.int32).contiguous(), g.val, n, n)
+    g2 = CsrGraph(g.rowptr, (key % n).to(torch.int32).contiguous(), g.val[perm].contiguous(),
+                  n, n)
     return g2, (o.permute_rows(table) if table is not None else None), o
 
 

@@ -115,7 +115,10 @@ int gnn_spmm_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub, const fl
  * optional hub table (col < 0 names row -1-col of xh, as gnn_spmm_csr_hub_f32; NULL: none).
  * flags: GNN_EPI_* including GNN_EPI_SKIP_EMPTY. Needs feat % 4 == 0, 32 < feat,
  * 16-B aligned x / xh / y / bias / partial and ldx, ldh, ldy multiples of 4
- * (else GNN_E_UNSUPPORTED). Each row's sum runs in edge order: deterministic.
+ * (else GNN_E_UNSUPPORTED). Each row's sum runs in edge order: deterministic. A task
+ * outside the contract (no row, more than 63 rows, rows outside [0, n_rows)) is skipped by
+ * the kernel (its rows are left unwritten, nothing is read out of bounds): validate a task
+ * list once with gnn_spmm_tasks_check.
  */
 int gnn_spmm_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, const float* val,
                            int64_t n_rows, const float* x, int64_t ldx, const float* xh,
@@ -125,6 +128,15 @@ int gnn_spmm_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, const floa
                            int64_t n_long, const int32_t* mid_row, int64_t n_mid,
                            const int32_t* task_row, int64_t n_task, float* partial,
                            uint32_t flags, void* stream);
+
+/*
+ * Validates a task list of gnn_spmm_csr_tasks_f32 on the device: *err (device int32, zeroed by
+ * the caller) gets bit 1 for a task with no row, more than 63 rows or rows outside
+ * [0, n_rows), bit 2 for a task that starts before the previous one ends (tasks must be
+ * ascending and disjoint). No host sync.
+ */
+int gnn_spmm_tasks_check(const int32_t* task_row, int64_t n_task, int64_t n_rows, int32_t* err,
+                         void* stream);
 
 /*
  * Hub-staging plan for gnn_spmm_csr_hub_f32 / gnn_gat_csr_hub_f32 (built once per graph
@@ -192,8 +204,10 @@ int gnn_gcn_transform_supported(int64_t k, int64_t fout);
  * fp32 path and a float64 product); mode 0: v_mfma_f32_16x16x4_f32 (a k-ordered fp32 fmaf
  * chain). k < 128 always takes mode 0; the GAT projection (gnn_gat_project_f32 / _rows_f32)
  * follows the same mode at k = 64. Returns the previous mode, GNN_E_ARG for another value.
+ * gnn_transform_get_precision returns the current mode.
  */
 int gnn_transform_set_precision(int mode);
+int gnn_transform_get_precision(void);
 int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,
                           int64_t fout, float* y, int64_t ldy, void* stream);
 
@@ -566,9 +580,11 @@ int gnn_dev_spmm_variant_f32(const int64_t* rowptr, const int32_t* col, const fl
  * with ncclAllToAllv on the caller's communicator `comm` (an ncclComm_t) and HIP stream.
  * send_rows / recv_rows are host arrays [world]. The library does not link RCCL:
  * ncclAllToAllv is resolved from the process at the first call (the global scope, then an
- * already-loaded librccl.so / librccl.so.1, then librccl.so.1), so it is the same RCCL
- * that made `comm`; gnn_halo_rccl_path writes that library's path. No host sync.
- * Returns GNN_E_COMM when RCCL is not found or its call fails.
+ * already-loaded librccl.so / librccl.so.1; an RCCL not yet loaded is never loaded here, it
+ * could not own `comm`), so it is the same RCCL that made `comm`; gnn_halo_rccl_path writes
+ * that library's path. No host sync. Returns GNN_E_COMM when no loaded RCCL exports
+ * ncclAllToAllv or its call fails, GNN_E_UNSUPPORTED when rows * row_floats or the running
+ * offsets would exceed 2^62 elements.
  */
 int gnn_halo_alltoallv_f32(const float* send, const int64_t* send_rows, float* recv,
                            const int64_t* recv_rows, int64_t row_floats, int64_t world,

@@ -58,8 +58,15 @@ def test_argument_rejection_without_launch(lib):
     # the transforms' arithmetic: the previous mode back, anything but 0 / 1 refused
     prev = lib.gnn_transform_set_precision(0)
     assert prev in (0, 1)
+    assert lib.gnn_transform_get_precision() == 0
+    from graphneuralnetwork_amd.ops import transform_precision
+    assert transform_precision() == "fp32-mfma"  # read back from the library, not mirrored
     assert lib.gnn_transform_set_precision(prev) == 0
+    assert lib.gnn_transform_get_precision() == prev
     assert lib.gnn_transform_set_precision(2) == -1
+    # the task-list validator: argument checks before any launch
+    assert lib.gnn_spmm_tasks_check(None, 1, 10, None, None) == -1
+    assert lib.gnn_spmm_tasks_check(None, 0, 10, 16, None) == 0
     # the fused classifier: n_cls outside [1, 4] / missing operands, nothing launched
     for n_cls, wd, lg in ((0, 1, 1), (5, 1, 1), (3, None, 1), (3, 1, None)):
         assert lib.gnn_linear_relu_cls_f32(16, 256, 100, 256, 16, 128, 16, 128, wd, None, n_cls,
@@ -84,6 +91,11 @@ def test_halo_exchange_entry_without_gpu(lib):
     counts = (ctypes.c_int64 * 2)(1, 1)
     assert lib.gnn_halo_alltoallv_f32(None, counts, None, counts, 4, 2, None, None) == -1
     assert lib.gnn_halo_alltoallv_f32(None, counts, None, counts, 4, 0, 1, None) == -1
+    # rows * row_floats (or the running offsets) past 2^62 elements: refused, nothing called
+    huge = (ctypes.c_int64 * 2)(1 << 40, 1)
+    assert lib.gnn_halo_alltoallv_f32(16, huge, 16, counts, 1 << 30, 2, 1, None) == -3
+    big = (ctypes.c_int64 * 2)(1 << 61, 1 << 61)
+    assert lib.gnn_halo_alltoallv_f32(16, big, 16, counts, 2, 2, 1, None) == -3
     buf = ctypes.create_string_buffer(4096)
     assert lib.gnn_halo_rccl_path(buf, 4096) == 0, "ncclAllToAllv not resolvable"
     assert "rccl" in buf.value.decode()

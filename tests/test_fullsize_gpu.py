@@ -152,3 +152,201 @@ def test_graphsage_cfg4_full_size(agg):
     got = sage_gather_aggregate(table, torch.from_numpy(idx).to(dev), agg).cpu().numpy()
     close(got, c_oracle.sage_gather(tn, idx, agg))
     assert int(batch.frontier.max()) >= (1 << 32) // (4 * F)  # sampled rows past 2^32 bytes too
+
+
+# ---------------------------------------------------------------------------------------------
+# The variants bench.py times, pinned at full size: the
+# column-degree-ordered Graph_conv_layer (A P^T, support rows scattered by the MFMA transform,
+# hub rows read in place by the XCD-sliced SpMM) at cfg2 and at the north star; the GAT heads
+# layer through _ordered (gnn_gat_project_rows_f32 + order.graph) at cfg3; the GraphSAGE forward
+# over sampler.degree_ordered at cfg4. Each against the oracle on a row sample holding the 32
+# hottest rows, plus an all-row checksum; each asserts the ordered plan was the one taken.
+# ---------------------------------------------------------------------------------------------
+def _sub_csr(rowptr, col, val, rows):
+    """The CSR of the sampled rows with their columns renumbered into `need` (the distinct
+    columns they gather): (sub_rowptr, sub_col, sub_val, need)."""
+    deg = np.diff(rowptr)[rows]
+    sub_ptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    sub_col = np.concatenate([col[rowptr[r]:rowptr[r + 1]] for r in rows]).astype(np.int64)
+    sub_val = np.concatenate([val[rowptr[r]:rowptr[r + 1]] for r in rows])
+    need, inv = np.unique(sub_col, return_inverse=True)
+    return sub_ptr, inv.astype(np.int32), sub_val, need
+
+
+def _assert_colorder_taken(g):
+    """The layer ran over the cached column-degree order with the XCD-sliced plan reading the
+    hub rows in place (XcdHubPlan.prefix), as bench.py's headline does."""
+    from graphneuralnetwork_amd import ops
+    assert ("_colorder",) in g._plans
+    og = g._plans[("_colorder",)].graph
+    xps = [p for k, p in og._plans.items() if isinstance(k, tuple) and k[0] == "_xcd"]
+    assert xps and all(p is not None and p.prefix for p in xps)
+    assert ops.XCD_DIRECT and ops.DEGREE_ORDER and ops.SPMM_TASKS
+
+
+def _gcn_layer_full_size(g, h, F, seed):
+    from graphneuralnetwork_amd.gcn import Graph_conv_layer
+    dev = g.rowptr.device
+    gen = torch.Generator(dev).manual_seed(seed)
+    layer = Graph_conv_layer(F, F).to(dev).eval()
+    with torch.no_grad():
+        layer.bias.copy_(torch.randn(F, device=dev, generator=gen))
+    X = torch.randn(g.n_rows, F, device=dev, generator=gen)
+    with torch.no_grad():
+        Y = layer(X, g)
+    _assert_colorder_taken(g)
+    W = layer.dense.weight.detach().double().cpu().numpy()
+    bn = layer.bias.detach().cpu().numpy()
+    rows = _sample_rows(h["rowptr"], g.n_rows, 2000, seed)
+    sp, sc, sv, need = _sub_csr(h["rowptr"], h["col"], h["val"], rows)
+    support = (X[torch.from_numpy(need).to(dev)].double().cpu().numpy() @ W.T).astype(np.float32)
+    ref = c_oracle.spmm_csr(sp, sc, sv, support, bn)
+    close(Y[torch.from_numpy(rows).to(dev)].cpu().numpy(), ref)
+    # checksum of checksums over every row: 1^T (A X W^T + 1 b^T) v = (1^T A)(X (W^T v)) + n b.v
+    v = np.random.default_rng(seed + 1).standard_normal(F)
+    lhs = float((Y.double() @ torch.from_numpy(v).to(dev)).sum())
+    xu = (X.double() @ torch.from_numpy(W.T @ v).to(dev)).cpu().numpy()
+    colsum_a = np.bincount(h["col"], weights=h["val"].astype(np.float64), minlength=g.n_cols)
+    rhs = float(colsum_a @ xu) + g.n_rows * float(bn.astype(np.float64) @ v)
+    scale = float(np.abs(colsum_a) @ np.abs(xu))
+    assert abs(lhs - rhs) <= 1e-4 * scale, (lhs, rhs, scale)
+
+
+def test_bench_variant_gcn_layer_north_star(ns_graph):
+    """bench.py's north-star line: Graph_conv_layer(128, 128).eval() over the 10M / 207M graph
+    (GCN/GCN.py:41-47), through the column-degree order with default knobs."""
+    g, h = ns_graph
+    _gcn_layer_full_size(g, h, 128, 11)
+
+
+@pytest.fixture(scope="module")
+def cfg2_graph():
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    dev = torch.device("cuda:0")
+    n = 1_000_000
+    s, d = rmat_edges(n, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n)
+    host = {k: getattr(g, k).cpu().numpy() for k in ("rowptr", "col", "val")}
+    yield g, host
+    del g
+    torch.cuda.empty_cache()
+
+
+def test_bench_variant_gcn_layer_cfg2(cfg2_graph):
+    """bench.py's headline graph (BASELINE configs[1], nnz 20,073,500): the same layer."""
+    g, h = cfg2_graph
+    assert g.nnz == 20_073_500
+    _gcn_layer_full_size(g, h, 128, 12)
+
+
+def test_bench_variant_gcn_spmm_cfg2_all_rows(cfg2_graph):
+    """The headline step itself (bench.py run_gcn: spmm_forward over column_order(g).graph with
+    X = the support in that row order) against the C oracle on EVERY row of cfg2."""
+    from graphneuralnetwork_amd.ops import column_order, spmm_forward
+    g, h = cfg2_graph
+    dev = g.rowptr.device
+    F = 128
+    gen = torch.Generator(dev).manual_seed(3)
+    bias = torch.randn(F, device=dev, generator=gen)
+    X = torch.randn(g.n_cols, F, device=dev, generator=gen)
+    order = column_order(g, F)
+    assert order is not None
+    Y = spmm_forward(order.graph, X, bias)
+    _assert_colorder_taken(g)
+    # X holds the support in the new order: row j of X is old column perm[j]
+    Xold = X[order.inv].cpu().numpy()
+    ref = c_oracle.spmm_csr(h["rowptr"], h["col"], h["val"], Xold, bias.cpu().numpy())
+    close(Y.cpu().numpy(), ref)
+
+
+def test_bench_variant_gat_heads_cfg3():
+    """bench.py's cfg3 line: the 8-head layer of GAT(64, 8, ., 8) at inference (GATBase._heads ->
+    _ordered: gnn_gat_project_rows_f32 writing Wh / er in the column-degree order, the
+    aggregation over order.graph reading the hub rows in place; GAT/models/layers.py:22-37,
+    GAT.py:16) on the 1M / 10M graph, against the oracle on a row sample with the 32 hottest
+    rows, plus every row's attention mass (Wh = 1 aggregates to ELU(1))."""
+    from graphneuralnetwork_amd.gat import GAT
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    dev = torch.device("cuda:0")
+    n, H, fh, Fin = 1_000_000, 8, 8, 64
+    s, d = rmat_edges(n, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n)
+    torch.manual_seed(0)
+    net = GAT(Fin, fh, 7, 0.6, 0.2, H).to(dev).eval()
+    X = torch.randn(n, Fin, device=dev, generator=torch.Generator(dev).manual_seed(4))
+    with torch.no_grad():
+        out = net._heads(X, g)
+    assert ("_colorder",) in g._plans
+    og = g._plans[("_colorder",)].graph
+    hubs = [p for k, p in og._plans.items() if isinstance(k, tuple) and k[0] == "_hub"]
+    assert hubs and all(p.prefix for p in hubs)  # Wh / er hub rows read in place
+    W = torch.cat([m.W for m in net.attentions], 1).detach().double().cpu().numpy()
+    a = [m.a.detach().reshape(-1).cpu().numpy() for m in net.attentions]
+    a_s = np.concatenate([x[:fh] for x in a])
+    a_d = np.concatenate([x[fh:] for x in a])
+    rowptr, col = g.rowptr.cpu().numpy(), g.col.cpu().numpy()
+    rows = _sample_rows(rowptr, n, 3000, 9)
+    sp, sc, _, need = _sub_csr(rowptr, col, np.ones(col.size, np.float32), rows)
+    Xn_need = X[torch.from_numpy(need).to(dev)].double().cpu().numpy()
+    Xn_rows = X[torch.from_numpy(rows).to(dev)].double().cpu().numpy()
+    wh_need = Xn_need @ W
+    el_rows, _ = O.gat_logits(Xn_rows @ W, H, fh, a_s, a_d)
+    _, er_need = O.gat_logits(wh_need, H, fh, a_s, a_d)
+    ref = O.gat_csr(sp, sc, wh_need, el_rows, er_need, H, fh, 0.2, False)
+    ref = np.where(ref > 0, ref, np.expm1(np.minimum(ref, 0)))  # concat heads: ELU
+    close(out[torch.from_numpy(rows).to(dev)].cpu().numpy(), ref)
+    assert bool(torch.isfinite(out).all())
+
+
+def test_bench_variant_graphsage_cfg4_degree_ordered():
+    """bench.py's cfg4 line: the dataset relabelled by sampler.degree_ordered, the device-sampled
+    [25, 10] batch of 8192 seeds, GraphSAGE(2, 128, 128, MEAN).eval() (GraphSAGE.py:38-53):
+    the relabelled adjacency is P A P^T exactly (neighbour sets of sampled rows, bit-exact), and
+    the forward matches the oracle on the same maps within 1e-4."""
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    from graphneuralnetwork_amd.sampler import degree_ordered, sample_batch, symmetric_adjacency
+    dev = torch.device("cuda:0")
+    n, F = 10_000_000, 128
+    s, d = rmat_edges(n, 100_000_000, 0)
+    adj0 = symmetric_adjacency(s, d, n, device=dev)
+    del s, d
+    adj, _, order = degree_ordered(adj0)
+    # structure: new row i lists inv[old neighbours of perm[i]], ascending
+    rp0, c0 = adj0.rowptr.cpu().numpy(), adj0.col.cpu().numpy()
+    rp1, c1 = adj.rowptr.cpu().numpy(), adj.col.cpu().numpy()
+    perm, inv = order.perm.cpu().numpy(), order.inv.cpu().numpy()
+    deg1 = np.diff(rp1)
+    assert np.all(deg1[:-1] >= deg1[1:])  # degree order, hottest first
+    chk = np.unique(np.concatenate([np.arange(32), np.random.default_rng(3).choice(n, 2000)]))
+    for i in chk:
+        o = perm[i]
+        want = np.sort(inv[c0[rp0[o]:rp0[o + 1]]])
+        np.testing.assert_array_equal(c1[rp1[i]:rp1[i + 1]], want)
+    del adj0, rp0, c0
+    gen = torch.Generator(device=dev).manual_seed(0)
+    table = torch.randn(n, F, device=dev, generator=gen)
+    deg = adj.rowptr[1:] - adj.rowptr[:-1]
+    cand = torch.nonzero(deg > 0).view(-1)
+    seeds = cand[torch.randperm(cand.numel(), device=dev, generator=gen)[:8192]]
+    batch = sample_batch(adj, seeds, (25, 10), seed=0)
+    torch.manual_seed(0)
+    net = GraphSAGE(2, F, F, False, agg_func="MEAN", Unsupervised=False, class_size=3).to(dev).eval()
+    with torch.no_grad():
+        emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+    tn = table.cpu().numpy()
+    ws = [blk.weight.weight.detach().cpu().numpy() for blk in net.sage_blocks]
+    dense = (net.dense.weight.detach().cpu().numpy(), net.dense.bias.detach().cpu().numpy())
+    ref_emb, ref_logits = O.graphsage_forward(
+        tn[batch.frontier.cpu().numpy()], [m.cpu().numpy() for m in batch.center_maps],
+        tn[batch.frontier_nbrs.cpu().numpy()], [m.cpu().numpy() for m in batch.neigh_maps],
+        ws, "MEAN", False, dense)
+    close(emb.cpu().numpy(), ref_emb)
+    close(logits.cpu().numpy(), ref_logits)
+    # every sampled neighbour is a true neighbour in the relabelled graph
+    fr = batch.frontier.cpu().numpy()
+    nb = batch.frontier_nbrs.cpu().numpy()
+    for r in range(0, fr.size, max(1, fr.size // 500)):
+        assert np.isin(nb[r], c1[rp1[fr[r]]:rp1[fr[r] + 1]]).all()

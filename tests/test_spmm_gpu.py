@@ -510,6 +510,77 @@ def test_packed_tasks_vs_oracle(dev, F, monkeypatch):
                        ops.spmm_forward(g, Xd, bd, seg_len=256))  # deterministic
 
 
+@pytest.mark.parametrize("F", [64, 128])
+def test_packed_tasks_skip_empty_keeps_negative_zero(dev, F, monkeypatch):
+    """ADVICE r3 (spmm.hip packed_rows): with GNN_EPI_SKIP_EMPTY an edgeless row inside a task
+    is never written, so a -0.0 already in `out` keeps its sign bit (base + 0 would turn it into
+    +0.0). Edgeless rows at every slot position of a task, after rows with edges (rp > 0)."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.graph import CsrGraph
+    rng = np.random.default_rng(F + 1)
+    n = 4000
+    deg = rng.integers(1, 6, n)
+    deg[rng.random(n) < 0.4] = 0                       # edgeless rows scattered through tasks
+    deg[700:760] = 0
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    col = rng.integers(0, n, rowptr[-1]).astype(np.int32)
+    val = rng.standard_normal(rowptr[-1]).astype(np.float32)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.from_numpy(val).to(dev), n, n)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    base = rng.standard_normal((n, F)).astype(np.float32)
+    base[deg == 0] = -0.0
+    for max_deg, cost in ((8, 16), (128, 256)):
+        monkeypatch.setattr(ops, "TASK_MAX_DEG", max_deg)
+        monkeypatch.setattr(ops, "TASK_COST", cost)
+        out = torch.from_numpy(base).to(dev)
+        ops.spmm_forward(g, torch.from_numpy(X).to(dev), None, out=out, accumulate=True,
+                         seg_len=256, hubs=0)
+        assert any(k[0] == "_tasks" for k in g._plans if isinstance(k, tuple))
+        got = out.cpu().numpy()
+        assert np.signbit(got[deg == 0]).all()
+        close(got, base + O.spmm_csr(rowptr, col, val, X))
+
+
+def test_packed_tasks_check(dev):
+    """gnn_spmm_tasks_check flags tasks outside the contract (bit 1: empty, > 63 rows, out of
+    range; bit 2: overlapping); the task kernel skips such tasks without reading past the
+    graph; graph.check_tasks raises on them."""
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd.graph import check_tasks
+    lib = _lib.load()
+    s = torch.cuda.current_stream().cuda_stream
+    n = 200
+    cases = (([0, 63, 63, 126], 0), ([0, 64], 1), ([5, 5], 1), ([190, 201], 1), ([-1, 3], 1),
+             ([0, 10, 5, 20], 2))
+    for tasks, want in cases:
+        t = torch.tensor(tasks, dtype=torch.int32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        assert lib.gnn_spmm_tasks_check(t.data_ptr(), t.numel() // 2, n, err.data_ptr(), s) == 0
+        assert int(err.item()) == want, (tasks, int(err.item()))
+        if want:
+            with pytest.raises(ValueError):
+                check_tasks(t, n)
+    # the kernel itself: a 64-row task and an out-of-range one are skipped, the good one runs
+    rowptr = torch.arange(n + 1, dtype=torch.int64, device=dev)
+    col = torch.arange(n, dtype=torch.int32, device=dev)
+    val = torch.ones(n, device=dev)
+    F = 64
+    X = torch.randn(n, F, device=dev)
+    y = torch.full((n, F), 3.0, device=dev)
+    bad = torch.tensor([0, 64, 100, 110, 150, 260], dtype=torch.int32, device=dev)
+    mid = torch.zeros(1, dtype=torch.int32, device=dev)
+    lsp = torch.zeros(1, dtype=torch.int32, device=dev)
+    rc = lib.gnn_spmm_csr_tasks_f32(rowptr.data_ptr(), col.data_ptr(), val.data_ptr(), n,
+                                    X.data_ptr(), F, None, 0, F, None, y.data_ptr(), F, 256,
+                                    None, None, 0, None, lsp.data_ptr(), 0, mid.data_ptr(), 0,
+                                    bad.data_ptr(), 3, None, 0, s)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y[100:110], X[100:110])
+    assert bool((y[:64] == 3.0).all()) and bool((y[150:] == 3.0).all())
+
+
 def test_packed_tasks_c_abi_contract(dev):
     """gnn_spmm_csr_tasks_f32 rejects what it does not cover (feat <= 32, misaligned
     vectors) with GNN_E_UNSUPPORTED and unknown flags with GNN_E_ARG."""
