@@ -126,9 +126,10 @@ def compulsory_bytes(nnz: int, n_rows: int, n_cols: int, feat: int) -> int:
 
 
 HBM_COPY_GBPS = 6300.0  # achievable HBM rate (MI355X_MICROARCH.md "HBM": ~6.3 TB/s copy)
-# uniformly random 512-B rows of a 4.9 GB table: 12.0 G rows/s = 6.1 TB/s, the copy rate
+# uniformly random 512-B rows of a 4.9 GB table: 12.0 G rows/s = 6.1 TB/s, the copy rate; rows of
+# an XCD-local set that fits the XCDs' L2s: 52 G rows/s = 26.6 TB/s of gathered bytes
 # (tools/workingset_probe.py, profiles/r02y_workingset.log)
-RANDOM_ROW_GRPS_512B = 12.0
+L2_GATHER_GBPS = 26600.0
 
 
 def floor_model(col: torch.Tensor, n_cols: int, k_hub: int, feat: int, comp: int,
@@ -136,26 +137,32 @@ def floor_model(col: torch.Tensor, n_cols: int, k_hub: int, feat: int, comp: int
     """An achievable-floor model of one SpMM step, beside the compulsory ``frac``
     (VERDICT r3 next #3). Priced on a graph whose columns are in degree order (rank < k_hub =
     the hub rows the XCD-sliced plan serves on-chip):
-      * every hub gather is assumed free (served by L2 / the Infinity Cache);
-      * every non-hub column is read once (already in the compulsory bytes), and every
-        further gather of it is a cold HBM row read (R-MAT ids carry no locality: DESIGN.md
-        section 4 "Other graphs");
-      * all bytes move at the HBM copy rate (random 512-B rows measure the same).
-    floor_ms = (compulsory + cold re-reads x 4F) / 6.3 TB/s. ``frac_vs_floor`` = floor_ms /
-    the measured step: 1.0 would mean no time is lost beyond these cold re-reads."""
+      * HBM: every non-hub column is read once (already in the compulsory bytes) and every
+        further gather of it is a cold row read (R-MAT ids carry no locality: DESIGN.md
+        section 4 "Other graphs"), all at the HBM copy rate (random 512-B rows measure the
+        same): hbm_ms = (compulsory + cold re-reads x 4F) / 6.3 TB/s;
+      * on-chip: every hub gather at the best measured gather rate, an XCD-local set that fits
+        the L2s (26.6 TB/s of rows): l2_ms = hub gathers x 4F / 26.6 TB/s;
+      * floor_ms = max(hbm_ms, l2_ms): a lower bound on the step (the two can overlap at best).
+    ``frac_vs_floor`` = floor_ms / the measured step: 1.0 would mean nothing is lost beyond the
+    cold re-reads and the on-chip gather rate."""
     c = col.to(torch.int64)
     nonhub = c >= k_hub
     g_nh = int(nonhub.sum())
+    g_h = int(c.numel()) - g_nh
     d_nh = int((torch.bincount(c[nonhub] - k_hub, minlength=max(1, n_cols - k_hub)) > 0).sum())
     cold = g_nh - d_nh
-    floor_bytes = comp + cold * 4 * feat
-    floor_ms = floor_bytes / (HBM_COPY_GBPS * 1e9) * 1e3
-    return {"hub_rows": k_hub, "nonhub_gathers": g_nh, "nonhub_distinct_rows": d_nh,
-            "cold_rereads": cold, "floor_bytes": floor_bytes, "floor_ms": floor_ms,
+    hbm_bytes = comp + cold * 4 * feat
+    hbm_ms = hbm_bytes / (HBM_COPY_GBPS * 1e9) * 1e3
+    l2_ms = g_h * 4 * feat / (L2_GATHER_GBPS * 1e9) * 1e3
+    floor_ms = max(hbm_ms, l2_ms)
+    return {"hub_rows": k_hub, "hub_gathers": g_h, "nonhub_gathers": g_nh,
+            "nonhub_distinct_rows": d_nh, "cold_rereads": cold, "hbm_bytes": hbm_bytes,
+            "hbm_ms": hbm_ms, "l2_ms": l2_ms, "floor_ms": floor_ms,
             "frac_vs_floor": floor_ms / t_ms,
-            "model": "(compulsory bytes + (non-hub gathers - distinct non-hub rows) x 4F) at the "
-                     "6.3 TB/s HBM copy rate; hub gathers counted free; random 512-B rows "
-                     "measure 12.0 G rows/s = 6.1 TB/s (profiles/r02y_workingset.log)"}
+            "model": "floor = max(HBM: (compulsory bytes + (non-hub gathers - distinct non-hub "
+                     "rows) x 4F) at the 6.3 TB/s copy rate, on-chip: hub gathers x 4F at the "
+                     "26.6 TB/s XCD-local L2 gather rate); profiles/r02y_workingset.log"}
 
 
 BUILD_INFO = {}
@@ -842,9 +849,17 @@ def host_cpu_info(threads: int) -> dict:
     """What the CPU lines ran on: the threads used, the CPUs this process may run on and
     the machine's count. The GPU box allots 16 CPUs per GPU
     (OMP_NUM_THREADS=16 there) even though os.cpu_count() shows the whole machine."""
-    return {"threads": threads, "affinity_cpus": len(os.sched_getaffinity(0)),
+    info = {"threads": threads, "affinity_cpus": len(os.sched_getaffinity(0)),
             "os_cpu_count": os.cpu_count(),
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+    try:  # a CPU quota (cgroup v2 "quota period"): the CPUs' worth of time this job may use
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        info["cgroup_cpu_max"] = f"{q} {per}"
+        if q != "max":
+            info["cgroup_cpu_quota_cpus"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return info
 
 
 def gcn_roofline(nnz: int, n_rows: int, n_cols: int, feat: int, step_ms: list, traffic,

@@ -477,15 +477,52 @@ def _overlaps(a: torch.Tensor, b: torch.Tensor) -> bool:
     return a0 < b1 and b0 < a1
 
 
+def chunk_sizes(counts: list, chunks: int) -> list:
+    """[chunks][world] row counts: peer q's block of counts[q] rows cut into ``chunks``
+    contiguous pieces, piece k = rows [k n_q // C, (k+1) n_q // C). Sender and receiver derive
+    the same pieces from the same count."""
+    return [[(k + 1) * n // chunks - k * n // chunks for n in counts] for k in range(chunks)]
+
+
+def chunk_major(counts: list, chunks: int, device) -> torch.Tensor:
+    """int64 [sum(counts)]: for a buffer laid out peer-major (peer q's rows contiguous, in peer
+    order), the source position of each row of the chunk-major layout (chunk k holds piece k
+    of every peer, in peer order): new_buf = old_buf[chunk_major(...)]."""
+    offs = [0]
+    for n in counts:
+        offs.append(offs[-1] + int(n))
+    parts = []
+    for k in range(chunks):
+        for q, n in enumerate(counts):
+            lo, hi = k * n // chunks, (k + 1) * n // chunks
+            if hi > lo:
+                parts.append(torch.arange(offs[q] + lo, offs[q] + hi, device=device,
+                                          dtype=torch.int64))
+    if not parts:
+        return torch.zeros(0, dtype=torch.int64, device=device)
+    return torch.cat(parts)
+
+
+# Feature-row exchange of the cover SpMM in this many chunked all-to-all-v's (each peer's rows
+# cut into HALO_CHUNKS pieces): the halo_x SpMM of chunk k runs while chunk k+1 is in flight,
+# instead of every halo gather waiting for the whole exchange (VERDICT r3 next #4). Each extra
+# chunk costs one more RCCL launch and one more accumulate pass over the rows it touches.
+HALO_CHUNKS = 2
+
+
 class EdgeCutSpmm:
     """Y_own = (A X)[own rows] (+ bias) for one rank of the edge-cut, halo exchange overlapped.
 
     ``spmm`` / ``gather`` default to the HIP kernels; tests on gloo/CPU pass
     CPU checkers instead (they exercise the partition + exchange logic only).
+
+    ``chunks`` (cover exchange; default HALO_CHUNKS): the feature rows travel in that many
+    all-to-all-v's, laid out chunk-major in the send / receive buffers, and the halo_x SpMM is
+    split by column chunk, so the halo gathers of chunk k start as soon as chunk k has landed.
     """
 
     def __init__(self, part: EdgeCutPartition | CoverExchange, feat: int, device, group=None,
-                 spmm=None, gather=None):
+                 spmm=None, gather=None, chunks: int | None = None):
         self.part = part
         self.feat = feat
         self.group = group
@@ -498,7 +535,9 @@ class EdgeCutSpmm:
         self._gather = gather
         self.cover = isinstance(part, CoverExchange)
         f32 = dict(dtype=torch.float32, device=self.device)
+        self.chunks = max(1, int(HALO_CHUNKS if chunks is None else chunks))
         if self.cover:
+            self._build_chunks()
             self.send_x = torch.empty((sum(part.send_x_counts), feat), **f32)
             self.send_p = torch.empty((sum(part.send_p_counts), feat), **f32)
             self.recv_x = torch.empty((sum(part.recv_x_counts), feat), **f32)
@@ -515,6 +554,39 @@ class EdgeCutSpmm:
         self.cuda = self.device.type == "cuda"
         self.comm_stream = torch.cuda.Stream(self.device) if self.cuda else None
         self._marks = None  # [(name, event)] while profile() runs
+
+    def _build_chunks(self):
+        """Chunk-major send / receive layouts of the feature rows and the halo_x SpMM split by
+        column chunk (see ``chunks``)."""
+        p = self.part
+        C = self.chunks
+        dev = p.halo_x.device
+        self.x_send_chunks = chunk_sizes(p.send_x_counts, C)
+        self.x_recv_chunks = chunk_sizes(p.recv_x_counts, C)
+        self.x_send_off = [0]
+        self.x_recv_off = [0]
+        for k in range(C):
+            self.x_send_off.append(self.x_send_off[-1] + sum(self.x_send_chunks[k]))
+            self.x_recv_off.append(self.x_recv_off[-1] + sum(self.x_recv_chunks[k]))
+        if C == 1:
+            self.send_x_idx = p.send_x_idx
+            self.halo_x_chunks = [p.halo_x]
+            return
+        self.send_x_idx = p.send_x_idx[chunk_major(p.send_x_counts, C,
+                                                   p.send_x_idx.device)].contiguous()
+        src = chunk_major(p.recv_x_counts, C, dev)        # chunk-major position -> receive slot
+        new_of_old = torch.empty_like(src)
+        new_of_old[src] = torch.arange(src.numel(), device=dev, dtype=torch.int64)
+        hx = p.halo_x
+        rows = torch.repeat_interleave(torch.arange(hx.n_rows, device=dev, dtype=torch.int64),
+                                       hx.rowptr[1:] - hx.rowptr[:-1])
+        newc = new_of_old[hx.col.to(torch.int64)] if hx.nnz else hx.col.to(torch.int64)
+        self.halo_x_chunks = []
+        for k in range(C):
+            lo, hi = self.x_recv_off[k], self.x_recv_off[k + 1]
+            m = (newc >= lo) & (newc < hi)
+            self.halo_x_chunks.append(from_coo(rows[m], newc[m] - lo, hx.val[m], hx.n_rows,
+                                               hi - lo, check=False))
 
     def _mark(self, name, stream):
         if self._marks is not None:
@@ -558,7 +630,10 @@ class EdgeCutSpmm:
         finally:
             marks, self._marks = self._marks, None
         res, prev, opened = {}, None, {}
+        t0 = marks[0][1]
+        at = {}  # every mark's time since the start (ms)
         for name, ev in marks:
+            at[name] = t0.elapsed_time(ev)
             if name.endswith(">"):
                 opened[name[:-1]] = ev
             elif name.endswith("<"):
@@ -568,6 +643,14 @@ class EdgeCutSpmm:
                     res[name + "_ms"] = prev.elapsed_time(ev)
                 prev = ev if name != "end" else prev
         res["total_ms"] = marks[0][1].elapsed_time(marks[-1][1])
+        # the pipelined halo pass: when the first halo_x chunk starts (its wait ends) against
+        # when the last feature-row chunk lands; > 0 = halo gathers ran before the last receive
+        if self.cover and self.chunks > 1 and "wait_x0" in at:
+            last = f"a2a_x{self.chunks - 1}<"
+            res["halo_x0_start_at_ms"] = at["wait_x0"]
+            if last in at:
+                res["a2a_x_last_end_at_ms"] = at[last]
+                res["halo_before_last_recv_ms"] = at[last] - at["wait_x0"]
         return res
 
     def _wait(self, ev, cur):
@@ -598,13 +681,18 @@ class EdgeCutSpmm:
         self._last = out
         cur = torch.cuda.current_stream(self.device) if self.cuda else None
         if self.cover:
-            ev_x = ev_p = None
+            C = self.chunks
+            ev_x, ev_p = [None] * C, None
             if p.any_x:
                 if self.send_x.shape[0]:
-                    self._gather(x, p.send_x_idx, self.send_x)
+                    self._gather(x, self.send_x_idx, self.send_x)
                 self._mark("gather_send_x", cur)
-                ev_x = self._exchange(self.recv_x, self.send_x, p.recv_x_counts,
-                                      p.send_x_counts, cur, "a2a_x")
+                so, ro = self.x_send_off, self.x_recv_off
+                for k in range(C):  # every rank issues all C exchanges (some may be empty)
+                    ev_x[k] = self._exchange(self.recv_x[ro[k]:ro[k + 1]],
+                                             self.send_x[so[k]:so[k + 1]], self.x_recv_chunks[k],
+                                             self.x_send_chunks[k], cur,
+                                             "a2a_x" if C == 1 else f"a2a_x{k}")
             if p.any_p:
                 if self.send_p.shape[0]:
                     self._spmm(p.send_p, x, None, out=self.send_p)  # partial sums for peers
@@ -615,11 +703,17 @@ class EdgeCutSpmm:
             self._mark("spmm_interior", cur)
             last = "p" if p.any_p else ("x" if p.any_x else None)
             if p.any_x:
-                self._wait(ev_x, cur)
-                self._mark("wait_x", cur)
-                self._spmm(p.halo_x, self.recv_x, None, out=out, accumulate=True,
-                           activation=activation if last == "x" else None)
-                self._mark("spmm_halo_x", cur)
+                ro = self.x_recv_off
+                for k in range(C):
+                    sfx = "" if C == 1 else str(k)
+                    self._wait(ev_x[k], cur)
+                    self._mark("wait_x" + sfx, cur)
+                    act = activation if (last == "x" and k == C - 1) else None
+                    gk = self.halo_x_chunks[k]
+                    if gk.nnz or act is not None:  # an activation pass touches every row
+                        self._spmm(gk, self.recv_x[ro[k]:ro[k + 1]], None, out=out,
+                                   accumulate=True, activation=act)
+                    self._mark("spmm_halo_x" + sfx, cur)
             if p.any_p:
                 self._wait(ev_p, cur)
                 self._mark("wait_p", cur)

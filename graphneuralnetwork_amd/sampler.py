@@ -185,7 +185,65 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
                  gcn: bool = False) -> SampledBatch:
     """L = len(fanouts) layer frontier for ``seeds`` (get_layer_adj_nodes,
     GraphSAGE/data_utils.py:82-103, with a fanout per layer like GraphSAGE_Pytorch's
-    multihop_sampling): fanouts[i] neighbours for every node of S_i, chained per hop."""
+    multihop_sampling): fanouts[i] neighbours for every node of S_i, chained per hop.
+
+    One library call (gnn_sample_layers) issues every hop's kernels with the list lengths kept
+    on the device, and ONE host read at the end fetches the layer sizes and the error bits:
+    the same tensors as ``sample_batch_stepwise`` (which reads each frontier size back before
+    the next hop), bit for bit."""
+    fanouts = tuple(int(k) for k in fanouts)
+    if not fanouts or min(fanouts) < 1:
+        raise ValueError("fanouts must hold at least one positive neighbour count")
+    if not adj.rowptr.is_cuda:
+        raise RuntimeError("sampling runs on the ROCm device only (no CPU fallback)")
+    seeds = seeds.to(device=adj.device, dtype=torch.int64).contiguous()
+    if seeds.numel() == 0 or max(fanouts) > 256 or adj.n_rows == 0:
+        return sample_batch_stepwise(adj, seeds, fanouts, seed, gcn)
+    dev = adj.device
+    L = len(fanouts)
+    widths = [k + (1 if gcn else 0) for k in fanouts]
+    caps = [seeds.numel()]
+    for i in range(L - 1):
+        caps.append(min(adj.n_rows, caps[i] * (1 + widths[i])))
+    i64 = dict(dtype=torch.int64, device=dev)
+    layers = [seeds] + [torch.empty(caps[i], **i64) for i in range(1, L)]
+    nbrs = [torch.empty((caps[i], widths[i]), **i64) for i in range(L)]
+    cmaps = [torch.empty(caps[i], **i64) for i in range(L - 1)]
+    nmaps = [torch.empty((caps[i], widths[i]), **i64) for i in range(L - 1)]
+    stat = torch.empty(L + 1, **i64)
+    ws = _frontier_ws(adj.n_rows, dev)
+    _FRONTIER_GEN[0] += 1  # the shared workspace is overwritten: older rank() closures refuse
+    import ctypes
+    P = ctypes.c_void_p
+    arr = lambda ts: (P * max(1, len(ts)))(*[t.data_ptr() if t is not None else None  # noqa: E731
+                                              for t in ts])
+    fan_a = (ctypes.c_int64 * L)(*fanouts)
+    seed_a = (ctypes.c_uint64 * L)(*[stream_seed(seed, i) for i in range(L)])
+    cap_a = (ctypes.c_int64 * L)(*caps)
+    lib = _lib.load()
+    _lib.check(lib.gnn_sample_layers(adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.n_rows,
+                                     seeds.data_ptr(), seeds.numel(), L, fan_a, seed_a,
+                                     1 if gcn else 0, arr([None] + layers[1:]), cap_a, arr(nbrs),
+                                     arr(cmaps), arr(nmaps), stat.data_ptr(), ws.data_ptr(),
+                                     ws.numel(), _lib.stream_handle(dev)), "gnn_sample_layers")
+    st = stat.cpu().tolist()  # the one host synchronisation: every layer size + the error bits
+    sizes, e = st[:L], int(st[L]) & 0xFFFFFFFF
+    _raise_sample_error(e & 3)  # the sampler's own errors first, as the step-by-step path
+    if e & 8:
+        raise IndexError("sample_batch: a sampled id outside the graph reached the frontier")
+    if e & 4:
+        raise RuntimeError("sample_batch: a frontier outgrew its buffer (internal bound error)")
+    layers = [seeds] + [layers[i][:sizes[i]] for i in range(1, L)]
+    cmaps = [cmaps[i][:sizes[i]] for i in range(L - 1)]
+    nmaps = [nmaps[i][:sizes[i]] for i in range(L - 1)]
+    return SampledBatch(seeds, layers[-1], nbrs[L - 1][:sizes[L - 1]], cmaps[::-1], nmaps[::-1],
+                        tuple(layers))
+
+
+def sample_batch_stepwise(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int = 0,
+                          gcn: bool = False) -> SampledBatch:
+    """``sample_batch`` hop by hop: gnn_sample_neighbors, then the frontier (gnn_frontier_*,
+    whose size is read back before the next hop), per layer."""
     fanouts = tuple(int(k) for k in fanouts)
     if not fanouts or min(fanouts) < 1:
         raise ValueError("fanouts must hold at least one positive neighbour count")

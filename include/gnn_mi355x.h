@@ -505,6 +505,30 @@ int gnn_frontier_rank(const int64_t* ids, int64_t n, int64_t n_nodes, const void
                       int64_t* pos, void* stream);
 
 /*
+ * The whole L-hop mini-batch of sampler.sample_batch in one call, with no host round trip
+ * between hops (get_layer_adj_nodes + collate_fn's maps, GraphSAGE/data_utils.py:82-162):
+ * S_0 = seeds; for i < L: nbrs[i] = gnn_sample_neighbors(S_i, fanouts[i], layer_seeds[i]) (with
+ * append_self the node itself as column fanouts[i], data_utils.py:95-96); for i < L-1:
+ * S_{i+1} = sorted distinct ids of S_i and nbrs[i] (layers[i+1]), center_maps[i] / neigh_maps[i]
+ * = positions of S_i / nbrs[i] in S_{i+1}. Every list length lives on the device: stat (device
+ * int64 [L + 1]) receives |S_i| in stat[i] and the error bits in the low word of stat[L]
+ * (1 = a node without neighbours, 2 = a node id out of range, 4 = a frontier larger than its
+ * buffer, 8 = an unsampled id reached the frontier), so the caller reads everything with ONE
+ * copy at the end. Host arrays: fanouts, layer_seeds, caps [L] (caps[i] = rows of the S_i /
+ * nbrs[i] / map buffers, caps[0] = n_seeds; caps[i+1] >= min(n_graph, caps[i] (1 + ld_i)) never
+ * overflows), layers, nbrs, center_maps, neigh_maps (device pointers; layers[0] unused).
+ * nbrs[i] / neigh_maps[i] rows have ld_i = fanouts[i] + append_self ids. Workspace:
+ * gnn_frontier_workspace_bytes(n_graph) (the frontier's; not to be shared with a live
+ * gnn_frontier_* sequence). The same draws, frontiers and maps as the step-by-step calls.
+ */
+int gnn_sample_layers(const int64_t* rowptr, const int32_t* col, int64_t n_graph,
+                      const int64_t* seeds, int64_t n_seeds, int32_t n_layers,
+                      const int64_t* fanouts, const uint64_t* layer_seeds, int32_t append_self,
+                      int64_t* const* layers, const int64_t* caps, int64_t* const* nbrs,
+                      int64_t* const* center_maps, int64_t* const* neigh_maps, int64_t* stat,
+                      void* workspace, int64_t workspace_bytes, void* stream);
+
+/*
  * Reference GCN adjacency on the device: D^-1/2 (max(A, A^T) + I)^T D^-1/2 as fp32 CSR
  * (GCN/data_utils.py:32-35 symmetrise, :78 + sp.eye, :54-60 normalize_adj, :63-70 fp32),
  * from a directed edge list (src -> dst, int64, duplicates allowed). Bit-identical to

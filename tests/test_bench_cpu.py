@@ -35,5 +35,7 @@ def test_floor_model_counts():
     col = torch.tensor([0, 1, 0, 2, 2, 3, 5, 5, 5, 1], dtype=torch.int32)
     f = bench.floor_model(col, 6, 2, 128, 10_000, 1.0)
     assert (f["nonhub_gathers"], f["nonhub_distinct_rows"], f["cold_rereads"]) == (6, 3, 3)
-    assert f["floor_bytes"] == 10_000 + 3 * 512
-    assert abs(f["floor_ms"] - f["floor_bytes"] / 6.3e12 * 1e3) < 1e-12
+    assert f["hub_gathers"] == 4 and f["hbm_bytes"] == 10_000 + 3 * 512
+    assert abs(f["hbm_ms"] - f["hbm_bytes"] / 6.3e12 * 1e3) < 1e-12
+    assert abs(f["l2_ms"] - 4 * 512 / 26.6e12 * 1e3) < 1e-12
+    assert f["floor_ms"] == max(f["hbm_ms"], f["l2_ms"])

@@ -232,3 +232,53 @@ def test_degree_ordered_dataset_forward(dev):
                Gathered(table, perm[b.frontier_nbrs], True), b.forward_args(table2)[3])
         e2, c2 = net(*nat, None, None, None, None, None)
     assert torch.equal(e1, e2) and torch.equal(c1, c2)
+
+
+@pytest.mark.parametrize("fanouts", [(5,), (25, 10), (10, 5, 3), (4, 3, 2, 2), (40, 20)])
+@pytest.mark.parametrize("gcn", [False, True])
+def test_fused_batch_equals_stepwise(dev, fanouts, gcn):
+    """gnn_sample_layers (every hop on the device, one host read at the end) returns the same
+    tensors as the hop-by-hop path, bit for bit: layers, neighbour lists and both maps, with
+    repeated seeds; and raises the same errors."""
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.sampler import sample_batch, sample_batch_stepwise
+    adj = _adj(dev, n=20000, e=150000, seed=3)
+    deg = (adj.rowptr[1:] - adj.rowptr[:-1]).cpu().numpy()
+    cand = np.nonzero(deg > 0)[0]
+    seeds = torch.from_numpy(np.concatenate([cand[:300], cand[:5]])).to(dev)
+    a = sample_batch(adj, seeds, fanouts, seed=9, gcn=gcn)
+    b = sample_batch_stepwise(adj, seeds, fanouts, seed=9, gcn=gcn)
+    assert len(a.layers) == len(b.layers) == len(fanouts)
+    for x, y in zip(a.layers, b.layers):
+        assert torch.equal(x, y)
+    assert torch.equal(a.frontier, b.frontier) and torch.equal(a.frontier_nbrs, b.frontier_nbrs)
+    for xs, ys in ((a.center_maps, b.center_maps), (a.neigh_maps, b.neigh_maps)):
+        assert len(xs) == len(ys)
+        for x, y in zip(xs, ys):
+            assert torch.equal(x, y)
+    rowptr = torch.tensor([0, 2, 3, 3], dtype=torch.int64, device=dev)
+    col = torch.tensor([1, 0, 0], dtype=torch.int32, device=dev)
+    g = CsrGraph(rowptr, col, torch.ones(3, device=dev), 3, 3)
+    for fn in (sample_batch, sample_batch_stepwise):
+        with pytest.raises(IndexError, match="empty sequence"):
+            fn(g, torch.tensor([0, 2], device=dev), fanouts, gcn=gcn)
+        with pytest.raises(IndexError, match="out of range"):
+            fn(g, torch.tensor([7, 0], device=dev), fanouts, gcn=gcn)
+
+
+def test_fused_batch_full_size_cfg4(dev):
+    """The cfg4 batch (8192 seeds, [25, 10]) on the 10M-node R-MAT adjacency: fused == stepwise."""
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    from graphneuralnetwork_amd.sampler import (sample_batch, sample_batch_stepwise,
+                                                symmetric_adjacency)
+    n = 10_000_000
+    s, d = rmat_edges(n, 100_000_000, 0)
+    adj = symmetric_adjacency(s, d, n, device=dev)
+    del s, d
+    gen = torch.Generator(device=dev).manual_seed(0)
+    cand = torch.nonzero(adj.rowptr[1:] > adj.rowptr[:-1]).view(-1)
+    seeds = cand[torch.randperm(cand.numel(), device=dev, generator=gen)[:8192]]
+    a = sample_batch(adj, seeds, (25, 10), seed=0)
+    b = sample_batch_stepwise(adj, seeds, (25, 10), seed=0)
+    assert torch.equal(a.frontier, b.frontier) and torch.equal(a.frontier_nbrs, b.frontier_nbrs)
+    assert torch.equal(a.center_map, b.center_map) and torch.equal(a.neigh_map, b.neigh_map)
