@@ -624,7 +624,8 @@ class DegreeOrder:
         return y.index_select(0, self.inv)
 
 
-def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None) -> DegreeOrder:
+def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None,
+                 tail: str | None = None) -> DegreeOrder:
     """Relabel a CSR graph by column in-degree (torch ops on its device). The edges of each
     row keep their CSR order (renamed), so every row sum runs in the same order: the result
     is bit-identical to the original graph's, permuted.
@@ -635,7 +636,11 @@ def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None) ->
     ``prefix``: only the ``prefix`` highest-degree ids are ranked (first, by degree); the rest
     follow in their original id order, so a producer that writes its rows in the new order
     (a transform or projection with scattered output rows) stores all but the prefix rows in
-    ascending address order. The hub ranking of any K <= prefix is the full order's."""
+    ascending address order. The hub ranking of any K <= prefix is the full order's.
+    ``tail`` (with ``prefix``): the order of the ids after the prefix -- "degree" (the full
+    degree order), "id" (ascending ids, the default when only ``prefix`` is given) or
+    "first_use" (by the CSR position of their first edge: the rows a row-ordered SpMM touches
+    for the first time lie together in memory; columns without edges last)."""
     n = g.n_cols
     dev = g.device
     indeg = torch.bincount(g.col.to(torch.int64), minlength=n)
@@ -643,7 +648,18 @@ def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None) ->
     # descending in-degree, ascending id on ties: one stable sort of -indeg
     perm = torch.sort(-indeg, stable=True).indices
     if prefix is not None and prefix < n:
-        perm = torch.cat([perm[:prefix], torch.sort(perm[prefix:]).values])
+        rest = perm[prefix:]
+        if tail == "first_use":
+            nnz = g.col.numel()
+            first = torch.full((n,), nnz, dtype=torch.int64, device=dev)
+            first.scatter_reduce_(0, g.col.to(torch.int64),
+                                  torch.arange(nnz, device=dev, dtype=torch.int64), "amin")
+            rest = rest[torch.sort(first[rest], stable=True).indices]
+        elif tail in (None, "id"):
+            rest = torch.sort(rest).values
+        elif tail != "degree":
+            raise ValueError(f"unknown tail order {tail!r}")
+        perm = torch.cat([perm[:prefix], rest])
     inv = torch.empty_like(perm)
     inv[perm] = idx
     if not rows:

@@ -525,3 +525,50 @@ def test_halo_alltoallv_c_abi_single_rank(dev):
     finally:
         rccl.ncclCommDestroy.argtypes = [ctypes.c_void_p]
         rccl.ncclCommDestroy(comm[0])
+
+
+@pytest.mark.parametrize("chunks", [1, 2, 3])
+def test_chunked_halo_exchange_two_ranks(dev, chunks):
+    """The cover SpMM with its feature rows in `chunks` all-to-all-v's (EdgeCutSpmm chunks=,
+    VERDICT r3 next #4): 2 LocalGroup ranks on one GPU equal the single-GPU SpMM (bias, ReLU on
+    the last pass), and profile() reports when the first halo chunk started against when the
+    last chunk landed."""
+    from graphneuralnetwork_amd import distributed as D
+    from graphneuralnetwork_amd.ops import spmm_forward
+    W, n, F = 2, 20000, 64
+    g = _graph(n, dev)
+    comm = D.LocalGroup(W)
+    _run_ranks.comm = comm
+    parts = [None] * W
+
+    def build(r):
+        comm.bind(r)
+        parts[r] = D.build_cover_exchange(g, r, W, group=comm)
+
+    _run_ranks(W, build)
+    X = torch.randn(n, F, device=dev)
+    b = torch.randn(F, device=dev)
+    Y = torch.empty(n, F, device=dev)
+    profs = [None] * W
+    streams = [torch.cuda.Stream(dev) for _ in range(W)]
+
+    def step(r):
+        comm.bind(r)
+        r0, r1 = parts[r].bounds[r], parts[r].bounds[r + 1]
+        with torch.cuda.stream(streams[r]):
+            run = D.EdgeCutSpmm(parts[r], F, dev, group=comm, chunks=chunks)
+            assert len(run.halo_x_chunks) == chunks
+            x = X[r0:r1].contiguous()
+            Y[r0:r1].copy_(run(x, b, activation="relu"))
+            profs[r] = run.profile(x, b, activation="relu")
+            torch.cuda.synchronize()
+
+    _run_ranks(W, step)
+    ref = torch.relu(spmm_forward(g, X, b))
+    torch.testing.assert_close(Y, ref, rtol=1e-4, atol=1e-5 * float(ref.abs().max()))
+    for p in profs:
+        assert p["total_ms"] > 0
+        if chunks > 1 and parts[0].any_x:
+            assert {"halo_x0_start_at_ms", "a2a_x_last_end_at_ms",
+                    "halo_before_last_recv_ms"} <= set(p)
+            assert all(f"a2a_x{k}_ms" in p for k in range(chunks))

@@ -1,0 +1,41 @@
+import numpy as np, time, sys
+sys.path.insert(0, '/root/repo')
+from graphneuralnetwork_amd.rmat import rmat_edges
+n = int(sys.argv[1]); m = int(sys.argv[2]); K = int(sys.argv[3])
+t=time.time()
+s, d = rmat_edges(n, m, 0)
+key = np.unique(np.concatenate([s * n + d, d * n + s, np.arange(n, dtype=np.int64) * (n + 1)]))
+r = key // n; c = key % n
+print("edges", key.size, time.time()-t, flush=True)
+indeg = np.bincount(c, minlength=n)
+rank = np.empty(n, np.int64); rank[np.argsort(-indeg, kind='stable')] = np.arange(n)
+rc = rank[c]
+nh = rc >= K
+print("nonhub gathers", nh.sum(), "distinct", np.unique(rc[nh]).size, flush=True)
+deg_all = np.bincount(r, minlength=n)
+def gaps(row_pos):
+    # processing position of a row = gathers issued before it (rows in row_pos order)
+    order = np.argsort(row_pos, kind='stable')
+    start = np.zeros(n, np.int64); start[order] = np.cumsum(deg_all[order]) - deg_all[order]
+    cc = rc[nh]; pp = start[r[nh]]
+    o = np.lexsort((pp, cc)); cc = cc[o]; pp = pp[o]
+    same = cc[1:] == cc[:-1]
+    g = (pp[1:] - pp[:-1])[same]
+    tot = nh.sum()
+    return {G: round(float((g < G).sum()) / tot, 4) for G in (1<<16, 1<<18, 1<<20, 1<<22, 1<<24)}
+print("natural", gaps(np.arange(n)), flush=True)
+# rows ordered by their smallest non-hub column rank (a 1-D locality projection)
+mn = np.full(n, np.iinfo(np.int64).max); np.minimum.at(mn, r[nh], rc[nh])
+print("by-min-nonhub-col", gaps(np.argsort(np.argsort(mn, kind='stable'), kind='stable')), flush=True)
+# rows in degree order
+deg = np.bincount(r, minlength=n)
+print("by-degree", gaps(np.argsort(np.argsort(-deg, kind='stable'), kind='stable')), flush=True)
+try:
+    import scipy.sparse as sp
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+    A = sp.csr_matrix((np.ones(key.size, np.int8), (r, c)), shape=(n, n))
+    t=time.time(); p = reverse_cuthill_mckee(A, symmetric_mode=True); print("rcm", time.time()-t, flush=True)
+    pos = np.empty(n, np.int64); pos[p] = np.arange(n)
+    print("rcm", gaps(pos), flush=True)
+except Exception as e:
+    print("rcm failed", e)
