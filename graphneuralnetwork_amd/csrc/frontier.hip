@@ -17,17 +17,64 @@
 
 namespace gnn {
 
-__global__ void frontier_mark_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t n_nodes,
-                                     uint32_t* __restrict__ bits, int32_t* __restrict__ err) {
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+// Marking a power-law frontier: the hub ids appear thousands of times and share a few bitmap
+// words (the degree order puts every hub in the first words), and every thread of the launch is
+// in flight at once, so a global atomicOr per listed id serialises on those words (rocprofv3:
+// 190 us to mark the 213K ids of a cfg4 batch, profiles/r04c_sample_kernel_stats.csv). Each
+// workgroup therefore ORs the ids below kHotIds into an LDS copy of the first words and folds
+// it into the global bitmap once at the end (one atomic per non-zero word and workgroup); ids
+// above it are rare per word and go straight to a global atomic, skipped when a read already
+// shows the bit (bits are only ever set during a build, so a stale read costs an extra atomic,
+// never a missed one).
+constexpr int kHotWords = 2048;                 // 8 KiB of LDS per workgroup
+constexpr int64_t kHotIds = 32 * kHotWords;     // ids 0 .. 65535
+constexpr int kMarkBlocks = 256;                // workgroups of a mark launch (grid-stride)
+
+__device__ __forceinline__ void mark_bit(uint32_t* bits, int64_t v) {
+  uint32_t* w = bits + (v >> 5);
+  const uint32_t m = 1u << (v & 31);
+  if ((__builtin_nontemporal_load(w) & m) == 0) atomicOr(w, m);
+}
+
+// ids a[0 .. na) then b[0 .. nb) (one grid-stride range); sets *err |= errbit for an id outside
+// [0, n_nodes)
+__device__ __forceinline__ void mark_lists(const int64_t* __restrict__ a, int64_t na,
+                                           const int64_t* __restrict__ b, int64_t nb,
+                                           int64_t n_nodes, uint32_t* __restrict__ bits,
+                                           int32_t* __restrict__ err, int32_t errbit) {
+  __shared__ uint32_t hot[kHotWords];
+  for (int i = threadIdx.x; i < kHotWords; i += blockDim.x) hot[i] = 0;
+  __syncthreads();
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < na + nb;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t v = ids[i];
+    const int64_t v = i < na ? a[i] : b[i - na];
     if (v < 0 || v >= n_nodes) {
-      atomicOr(err, 2);
+      atomicOr(err, errbit);
       continue;
     }
-    atomicOr(bits + (v >> 5), 1u << (v & 31));
+    if (v < kHotIds)
+      atomicOr(hot + (v >> 5), 1u << (v & 31));  // LDS atomic, on this CU
+    else
+      mark_bit(bits, v);
   }
+  __syncthreads();
+  const int64_t words = (n_nodes + 31) / 32;
+  for (int i = threadIdx.x; i < kHotWords && i < words; i += blockDim.x)
+    if (hot[i]) atomicOr(bits + i, hot[i]);
+}
+
+static unsigned mark_grid(int64_t n) {
+  const int64_t b = (n + 255) / 256;
+  return static_cast<unsigned>(b < 1 ? 1 : (b > kMarkBlocks ? kMarkBlocks : b));
+}
+
+__global__ __launch_bounds__(256) void frontier_mark_kernel(const int64_t* __restrict__ a,
+                                                             int64_t na,
+                                                             const int64_t* __restrict__ b,
+                                                             int64_t nb, int64_t n_nodes,
+                                                             uint32_t* __restrict__ bits,
+                                                             int32_t* __restrict__ err) {
+  mark_lists(a, na, b, nb, n_nodes, bits, err, 2);
 }
 
 __global__ void frontier_popc_kernel(const uint32_t* __restrict__ bits, int64_t n_words,
@@ -81,21 +128,12 @@ constexpr int32_t kBatchErrMark = 8;      // a listed id outside [0, n_nodes) (a
 
 // rows of list a (a_n rows, live count *a_dev) and of list b (b_rows rows of b_ld ids, live
 // rows *b_dev) in one grid: b's ids are the a rows' sampled neighbours
-__global__ void batch_mark_kernel(const int64_t* __restrict__ a, int64_t a_n,
-                                  const int64_t* __restrict__ a_dev, const int64_t* __restrict__ b,
-                                  int64_t b_rows, const int64_t* __restrict__ b_dev, int64_t b_ld,
-                                  int64_t n_nodes, uint32_t* __restrict__ bits,
-                                  int32_t* __restrict__ err) {
-  const int64_t na = live_rows(a_n, a_dev), nb = live_rows(b_rows, b_dev) * b_ld;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < na + nb;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int64_t v = i < na ? a[i] : b[i - na];
-    if (v < 0 || v >= n_nodes) {
-      atomicOr(err, kBatchErrMark);
-      continue;
-    }
-    atomicOr(bits + (v >> 5), 1u << (v & 31));
-  }
+__global__ __launch_bounds__(256) void batch_mark_kernel(
+    const int64_t* __restrict__ a, int64_t a_n, const int64_t* __restrict__ a_dev,
+    const int64_t* __restrict__ b, int64_t b_rows, const int64_t* __restrict__ b_dev,
+    int64_t b_ld, int64_t n_nodes, uint32_t* __restrict__ bits, int32_t* __restrict__ err) {
+  mark_lists(a, live_rows(a_n, a_dev), b, live_rows(b_rows, b_dev) * b_ld, n_nodes, bits, err,
+             kBatchErrMark);
 }
 
 // frontier[0 .. count) = the set bits in ascending order, *count = their number (clamped to cap)
@@ -223,12 +261,9 @@ extern "C" int gnn_frontier_build(const int64_t* ids_a, int64_t n_a, const int64
   FrontierWs f = fr_layout(workspace, n_nodes, workspace_bytes);
   hipError_t e = hipMemsetAsync(f.bits, 0, 4 * n_words, s);
   if (e != hipSuccess) return static_cast<int>(e);
-  if (n_a > 0)
-    hipLaunchKernelGGL(frontier_mark_kernel, dim3(fr_grid(n_a)), dim3(256), 0, s, ids_a, n_a,
-                       n_nodes, f.bits, err_flag);
-  if (n_b > 0)
-    hipLaunchKernelGGL(frontier_mark_kernel, dim3(fr_grid(n_b)), dim3(256), 0, s, ids_b, n_b,
-                       n_nodes, f.bits, err_flag);
+  if (n_a + n_b > 0)
+    hipLaunchKernelGGL(frontier_mark_kernel, dim3(mark_grid(n_a + n_b)), dim3(256), 0, s, ids_a,
+                       n_a, ids_b, n_b, n_nodes, f.bits, err_flag);
   hipLaunchKernelGGL(frontier_popc_kernel, dim3(fr_grid(n_words)), dim3(256), 0, s, f.bits,
                      n_words, f.cnt);
   e = rocprim::exclusive_scan(f.temp, f.temp_bytes, f.cnt, f.pre, 0u,
@@ -298,7 +333,7 @@ extern "C" int gnn_sample_layers(const int64_t* rowptr, const int32_t* col, int6
     hipError_t e = hipMemsetAsync(f.bits, 0, 4 * n_words, s);
     if (e != hipSuccess) return static_cast<int>(e);
     const int64_t listed = caps[i] * (ld + 1);
-    hipLaunchKernelGGL(batch_mark_kernel, dim3(fr_grid(listed)), dim3(256), 0, s, nodes, caps[i],
+    hipLaunchKernelGGL(batch_mark_kernel, dim3(mark_grid(listed)), dim3(256), 0, s, nodes, caps[i],
                        n_dev, nbrs[i], caps[i], n_dev, ld, n_graph, f.bits, err);
     e = rocprim::exclusive_scan(f.temp, f.temp_bytes, popc_iter(f.bits), f.pre, 0u,
                                 static_cast<size_t>(n_words), rocprim::plus<uint32_t>(), s);

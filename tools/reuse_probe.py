@@ -1,3 +1,15 @@
+"""Reuse distance of the non-hub gathers under different row orders (CPU only, numpy).
+
+For the R-MAT graph of bench.py (symmetrised, self-loops; columns ranked by in-degree, the
+first K = hubs) every gather of a non-hub column after its first one is a potential cache hit
+only if few bytes were gathered since the previous use. For each row order (natural ids, rows
+by their smallest non-hub column, rows by degree, reverse Cuthill-McKee) this prints the share
+of all non-hub gathers whose previous use of the same column lies within G gathers (G x 512 B
+of rows at F = 128): the upper bound on what a locality row order can turn into L2 / Infinity
+Cache hits. VERDICT r3 next #2; result in profiles/r04_reuse_probe_ns.log.
+
+    python tools/reuse_probe.py <nodes> <edges> <hub rows K>
+"""
 import numpy as np, time, sys
 sys.path.insert(0, '/root/repo')
 from graphneuralnetwork_amd.rmat import rmat_edges
