@@ -42,6 +42,10 @@ __device__ __forceinline__ int64_t uniform_below(uint64_t seed, int64_t pos, int
 }
 
 constexpr int kMaxFanout = 256;
+#ifndef GNN_SAMPLE_THREAD_SERIAL
+#define GNN_SAMPLE_THREAD_SERIAL 0  // A/B: the thread-per-node kernels for every k <= 32
+#endif
+constexpr bool kThreadSerialSample = GNN_SAMPLE_THREAD_SERIAL;
 
 __device__ __forceinline__ int64_t live_rows(int64_t n, const int64_t* n_dev) {
   return n_dev ? min(*n_dev, n) : n;
@@ -149,12 +153,93 @@ __global__ __launch_bounds__(256) void sample_kernel(const int64_t* __restrict__
   for (int64_t j = 0; j < k; ++j) o[j] = col[b + o[j]];
 }
 
+// Lane-parallel form of the same draws (fanouts k <= LPN <= 64): a group of LPN lanes per node,
+// lane `sub` owns draw `sub`. The draws of Floyd's algorithm do not depend on earlier picks
+// (draw jj is uniform_below(seed, i, j, j + 1), j = deg - k + jj), only the resolution does
+// ("already picked? then take j"), so every lane draws at once and the resolution runs as k
+// group-wide steps: step jj broadcasts lane jj's draw, the lanes q < jj compare it with their
+// final picks, one ballot decides. Same picks as sample_reg_kernel, bit for bit, with a whole
+// wave per 64 / LPN nodes instead of one thread per node (a thread-serial Floyd over k = 25 took
+// 30.6 us for the 8192 seeds of a cfg4 batch: 128 waves for 256 CUs, profiles/r03ac_cfg4_*).
+template <int LPN>
+__global__ __launch_bounds__(256) void sample_lane_kernel(const int64_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col,
+                                                          int64_t n_graph,
+                                                          const int64_t* __restrict__ nodes,
+                                                          int64_t n, const int64_t* n_dev, int k,
+                                                          int64_t ld, bool self, uint64_t seed,
+                                                          int64_t* __restrict__ out,
+                                                          int32_t* __restrict__ err) {
+  constexpr int GPW = kWave / LPN;  // node groups per wave
+  const int lane = threadIdx.x & (kWave - 1);
+  const int sub = lane & (LPN - 1);
+  const int gbase = lane & ~(LPN - 1);
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t i = wave * GPW + lane / LPN;
+  const int64_t live = live_rows(n, n_dev);
+  if (wave * GPW >= live) return;  // wave-uniform: every group of the wave is past the end
+  const bool act = i < live;
+  int64_t v = act ? nodes[i] : -1;
+  int64_t b = 0, deg = 0;
+  const bool ok = act && v >= 0 && v < n_graph;
+  if (ok) {
+    b = rowptr[v];
+    deg = rowptr[v + 1] - b;
+  }
+  if (act && sub == 0) {
+    if (!ok) atomicOr(err, kSampleErrRange);
+    else if (deg == 0) atomicOr(err, kSampleErrEmpty);
+  }
+  const bool good = ok && deg > 0;
+  const bool floyd = good && deg > k;
+  int64_t pick = 0;
+  if (good && sub < k) {
+    if (!floyd)
+      pick = uniform_below(seed, i, sub, deg);      // random.choices: independent draws
+    else {
+      const int64_t j = deg - k + sub;
+      pick = uniform_below(seed, i, j, j + 1);       // Floyd's draw jj = sub
+    }
+  }
+  // Floyd's resolution, in draw order: lane jj's draw stands unless a lane q < jj already
+  // holds it, then lane jj takes j = deg - k + jj (never held: earlier picks are < j)
+  for (int jj = 1; jj < LPN; ++jj) {
+    const int64_t t = __shfl(pick, gbase + jj, kWave);
+    const uint64_t hit = __ballot(floyd && sub < jj && pick == t);
+    const uint64_t gmask = (LPN == 64 ? ~0ull : ((1ull << LPN) - 1)) << gbase;
+    if (floyd && sub == jj && jj < k && (hit & gmask)) pick = deg - k + jj;
+  }
+  if (!act) return;
+  int64_t* o = out + i * ld;
+  if (sub < k) o[sub] = good ? static_cast<int64_t>(col[b + pick]) : -1;
+  if (self && sub == 0) o[k] = v;
+}
+
 // one launch of the right kernel for fanout k (k <= kMaxFanout): rows [0, min(*n_dev, n))
 inline void launch_sample(const int64_t* rowptr, const int32_t* col, int64_t n_graph,
                           const int64_t* nodes, int64_t n, const int64_t* n_dev, int k,
                           int64_t ld, bool self, uint64_t seed, int64_t* out, int32_t* err,
                           hipStream_t s) {
   const dim3 g(static_cast<unsigned>((n + 255) / 256)), t(256);
+  auto lane_grid = [&](int lpn) {  // 4 waves of 64 / lpn nodes per workgroup
+    const int64_t per_block = 4 * (kWave / lpn);
+    return dim3(static_cast<unsigned>((n + per_block - 1) / per_block));
+  };
+  if (k <= 16 && !kThreadSerialSample) {
+    hipLaunchKernelGGL(sample_lane_kernel<16>, lane_grid(16), t, 0, s, rowptr, col, n_graph, nodes,
+                       n, n_dev, k, ld, self, seed, out, err);
+    return;
+  }
+  if (k <= 32 && !kThreadSerialSample) {
+    hipLaunchKernelGGL(sample_lane_kernel<32>, lane_grid(32), t, 0, s, rowptr, col, n_graph, nodes,
+                       n, n_dev, k, ld, self, seed, out, err);
+    return;
+  }
+  if (k <= 64 && !kThreadSerialSample) {
+    hipLaunchKernelGGL(sample_lane_kernel<64>, lane_grid(64), t, 0, s, rowptr, col, n_graph, nodes,
+                       n, n_dev, k, ld, self, seed, out, err);
+    return;
+  }
   if (k <= 16)
     hipLaunchKernelGGL(sample_reg_kernel<16>, g, t, 0, s, rowptr, col, n_graph, nodes, n, n_dev,
                        k, ld, self, seed, out, err);
