@@ -212,11 +212,13 @@ def _gcn_layer_full_size(g, h, F, seed):
     assert abs(lhs - rhs) <= 1e-4 * scale, (lhs, rhs, scale)
 
 
-def test_bench_variant_gcn_layer_north_star(ns_graph):
-    """bench.py's north-star line: Graph_conv_layer(128, 128).eval() over the 10M / 207M graph
-    (GCN/GCN.py:41-47), through the column-degree order with default knobs."""
+@pytest.mark.parametrize("F", [128, 256])
+def test_bench_variant_gcn_layer_north_star(ns_graph, F):
+    """bench.py's north-star line (F=128) and the cfg5 layer at one GPU (F=256):
+    Graph_conv_layer(F, F).eval() over the 10M / 207M graph (GCN/GCN.py:41-47), through the
+    column-degree order with default knobs (F=256: the one-launch 256-column transform)."""
     g, h = ns_graph
-    _gcn_layer_full_size(g, h, 128, 11)
+    _gcn_layer_full_size(g, h, F, 11 + F)
 
 
 @pytest.fixture(scope="module")
@@ -260,13 +262,14 @@ def test_bench_variant_gcn_spmm_cfg2_all_rows(cfg2_graph):
     close(Y.cpu().numpy(), ref)
 
 
-def test_bench_variant_gat_heads_cfg3():
+@pytest.mark.parametrize("model", ["GAT", "SpGAT"])
+def test_bench_variant_gat_heads_cfg3(model):
     """bench.py's cfg3 line: the 8-head layer of GAT(64, 8, ., 8) at inference (GATBase._heads ->
     _ordered: gnn_gat_project_rows_f32 writing Wh / er in the column-degree order, the
     aggregation over order.graph reading the hub rows in place; GAT/models/layers.py:22-37,
     GAT.py:16) on the 1M / 10M graph, against the oracle on a row sample with the 32 hottest
     rows, plus every row's attention mass (Wh = 1 aggregates to ELU(1))."""
-    from graphneuralnetwork_amd.gat import GAT
+    from graphneuralnetwork_amd import gat as gat_mod
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     from graphneuralnetwork_amd.rmat import rmat_edges
     dev = torch.device("cuda:0")
@@ -274,7 +277,7 @@ def test_bench_variant_gat_heads_cfg3():
     s, d = rmat_edges(n, 10_000_000, 0)
     g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n)
     torch.manual_seed(0)
-    net = GAT(Fin, fh, 7, 0.6, 0.2, H).to(dev).eval()
+    net = getattr(gat_mod, model)(Fin, fh, 7, 0.6, 0.2, H).to(dev).eval()
     X = torch.randn(n, Fin, device=dev, generator=torch.Generator(dev).manual_seed(4))
     with torch.no_grad():
         out = net._heads(X, g)
@@ -294,7 +297,7 @@ def test_bench_variant_gat_heads_cfg3():
     wh_need = Xn_need @ W
     el_rows, _ = O.gat_logits(Xn_rows @ W, H, fh, a_s, a_d)
     _, er_need = O.gat_logits(wh_need, H, fh, a_s, a_d)
-    ref = O.gat_csr(sp, sc, wh_need, el_rows, er_need, H, fh, 0.2, False)
+    ref = O.gat_csr(sp, sc, wh_need, el_rows, er_need, H, fh, 0.2, model == "SpGAT")
     ref = np.where(ref > 0, ref, np.expm1(np.minimum(ref, 0)))  # concat heads: ELU
     close(out[torch.from_numpy(rows).to(dev)].cpu().numpy(), ref)
     assert bool(torch.isfinite(out).all())
