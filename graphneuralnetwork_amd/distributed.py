@@ -519,6 +519,8 @@ class EdgeCutSpmm:
     ``chunks`` (cover exchange; default HALO_CHUNKS): the feature rows travel in that many
     all-to-all-v's, laid out chunk-major in the send / receive buffers, and the halo_x SpMM is
     split by column chunk, so the halo gathers of chunk k start as soon as chunk k has landed.
+    With chunks > 1 the constructor is a collective (every rank's chunk sizes are gathered
+    once, so that all ranks skip the same globally empty chunks): construct it on every rank.
     """
 
     def __init__(self, part: EdgeCutPartition | CoverExchange, feat: int, device, group=None,
@@ -568,6 +570,15 @@ class EdgeCutSpmm:
         for k in range(C):
             self.x_send_off.append(self.x_send_off[-1] + sum(self.x_send_chunks[k]))
             self.x_recv_off.append(self.x_recv_off[-1] + sum(self.x_recv_chunks[k]))
+        # chunks that move no row on ANY rank are not issued at all (every rank sees the same
+        # totals, so every rank skips the same collectives); a chunk empty on some ranks only
+        # is an all-to-all-v with zero counts there, as any exchange can be
+        self.x_chunk_live = [True] * C
+        if C > 1 and p.any_x:
+            mine = [float(sum(self.x_send_chunks[k]) + sum(self.x_recv_chunks[k]))
+                    for k in range(C)]
+            tot = _all_gather_floats(mine, p.world, self.device, self.group).sum(0)
+            self.x_chunk_live = [bool(v > 0) for v in tot.tolist()]
         if C == 1:
             self.send_x_idx = p.send_x_idx
             self.halo_x_chunks = [p.halo_x]
@@ -688,7 +699,9 @@ class EdgeCutSpmm:
                     self._gather(x, self.send_x_idx, self.send_x)
                 self._mark("gather_send_x", cur)
                 so, ro = self.x_send_off, self.x_recv_off
-                for k in range(C):  # every rank issues all C exchanges (some may be empty)
+                for k in range(C):  # every rank issues the same (globally non-empty) chunks
+                    if not self.x_chunk_live[k]:
+                        continue
                     ev_x[k] = self._exchange(self.recv_x[ro[k]:ro[k + 1]],
                                              self.send_x[so[k]:so[k + 1]], self.x_recv_chunks[k],
                                              self.x_send_chunks[k], cur,
