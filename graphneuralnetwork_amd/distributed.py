@@ -29,7 +29,8 @@ row of every remote column, each cut block is covered by feature rows AND
 remotely computed partial row sums (a greedy vertex cover of the block's
 bipartite edge set), which ships 2-3x fewer rows on an RMAT cut; the two kinds
 travel in two all-to-all-v's that pipeline with the partial-sum, interior and
-halo SpMMs.
+halo SpMMs. The feature rows go in ``HALO_CHUNKS`` chunked all-to-all-v's, so that the halo
+SpMM of one chunk runs while the next is in flight (``EdgeCutSpmm(chunks=...)``).
 
 GraphSAGE (``sage_forward_sharded``) needs no exchange on its forward path: seed batches
 shard across ranks and the feature table is replicated (5.1 GB at 10M x 128 fits 288 GB).
