@@ -624,6 +624,22 @@ class DegreeOrder:
         return y.index_select(0, self.inv)
 
 
+def in_degree(g: "CsrGraph") -> torch.Tensor:
+    """int64 [n_cols] column in-degrees. On the device: gnn_in_degree_u32 (LDS-privatised
+    counts for the hot ids; torch.bincount serialises on the hub columns: 26 ms at the north
+    star, profiles/r04d_sample_kernel_stats.csv); on the CPU: torch.bincount."""
+    n = g.n_cols
+    if not g.col.is_cuda or g.nnz == 0 or n == 0:
+        return torch.bincount(g.col.to(torch.int64), minlength=n)
+    deg = torch.empty(n, dtype=torch.int32, device=g.device)
+    err = torch.zeros(1, dtype=torch.int32, device=g.device)
+    _lib.check(_lib.load().gnn_in_degree_u32(g.col.data_ptr(), g.nnz, n, deg.data_ptr(),
+                                             err.data_ptr(), _lib.stream_handle(g.device)),
+               "gnn_in_degree_u32")
+    # uint32 counts < 2^31 here (nnz < 2^31 per column): the int32 view is exact
+    return deg.to(torch.int64)
+
+
 def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None,
                  tail: str | None = None) -> DegreeOrder:
     """Relabel a CSR graph by column in-degree (torch ops on its device). The edges of each
@@ -643,7 +659,7 @@ def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None,
     for the first time lie together in memory; columns without edges last)."""
     n = g.n_cols
     dev = g.device
-    indeg = torch.bincount(g.col.to(torch.int64), minlength=n)
+    indeg = in_degree(g)
     idx = torch.arange(n, device=dev, dtype=torch.int64)
     # descending in-degree, ascending id on ties: one stable sort of -indeg
     perm = torch.sort(-indeg, stable=True).indices

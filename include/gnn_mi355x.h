@@ -139,6 +139,15 @@ int gnn_spmm_tasks_check(const int32_t* task_row, int64_t n_task, int64_t n_rows
                          void* stream);
 
 /*
+ * In-degree of every column of a CSR (deg[c] = number of entries with column c, uint32,
+ * device), the histogram of gnn_hub_plan_build: LDS-privatised counts for the hottest ids, so
+ * the hub columns' counters do not serialise. A column id outside [0, n_cols) sets
+ * *err_flag |= 1 (not counted). No host sync. (graph.degree_order's in-degree.)
+ */
+int gnn_in_degree_u32(const int32_t* col, int64_t nnz, int64_t n_cols, uint32_t* deg,
+                      int32_t* err_flag, void* stream);
+
+/*
  * Hub-staging plan for gnn_spmm_csr_hub_f32 / gnn_gat_csr_hub_f32 (built once per graph
  * and hub count k, 1 <= k <= n_cols):
  *   hub_ids[r] (int64 [k]) = the column of in-degree rank r (degree descending, ties by

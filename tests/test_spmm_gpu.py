@@ -733,3 +733,18 @@ def test_gcn_layer_column_order(dev, monkeypatch):
     support = (X.double() @ layer.dense.weight.detach().double().T).cpu().numpy()
     close(y.cpu().numpy(), O.spmm_csr(rowptr, col, val, support, layer.bias.detach().cpu().numpy()),
           rtol=1e-4)
+
+
+def test_in_degree_matches_bincount(dev):
+    """gnn_in_degree_u32 (LDS-privatised counts for the hot ids, the hub plan's histogram) ==
+    torch.bincount, on a power-law graph whose hubs are the smallest ids (degree-ordered) and
+    on its natural order, incl. columns past the LDS range and columns without edges."""
+    from graphneuralnetwork_amd.graph import CsrGraph, degree_order, in_degree
+    rowptr, col, val = _rand_graph(50000, 900000, 3, hub_deg=40000)
+    g = _graph(rowptr, col, val, 50000, dev)
+    for gg in (g, degree_order(g, rows=False).graph):
+        want = torch.bincount(gg.col.to(torch.int64), minlength=gg.n_cols)
+        assert torch.equal(in_degree(gg), want)
+    empty = CsrGraph(torch.zeros(3, dtype=torch.int64, device=dev),
+                     torch.zeros(0, dtype=torch.int32, device=dev), torch.zeros(0, device=dev), 2, 9)
+    assert torch.equal(in_degree(empty), torch.zeros(9, dtype=torch.int64, device=dev))
