@@ -73,6 +73,9 @@ def main():
     ap.add_argument("world", nargs="?", type=int, default=8)
     ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--exchange", default="cover", choices=["cover", "gather", "balanced"])
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="time the halo_x pass split into this many column chunks "
+                         "(EdgeCutSpmm chunks=, the chunked feature-row exchange)")
     ap.add_argument("--strong", action="store_true",
                     help="cfg5: the fixed 10M / 100M graph cut W ways (default: W x 1M / 10M)")
     args = ap.parse_args()
@@ -110,7 +113,8 @@ def main():
     th = [threading.Thread(target=build, args=(r,)) for r in range(W)]
     [t.start() for t in th]
     [t.join() for t in th]
-    print(json.dumps({"world": W, "feat": F, "nnz": g.nnz, "exchange": args.exchange}), flush=True)
+    print(json.dumps({"world": W, "feat": F, "nnz": g.nnz, "exchange": args.exchange,
+                      "halo_chunks": args.chunks}), flush=True)
     rows = []
     for r in range(W):
         p = parts[r]
@@ -128,7 +132,19 @@ def main():
             if sp.shape[0]:
                 ph["spmm_send_p"] = _time(lambda: spmm_forward(p.send_p, x, None, out=sp))
             ph["spmm_interior"] = _time(lambda: spmm_forward(p.interior, x, None, out=out))
-            if rx.shape[0]:
+            if rx.shape[0] and args.chunks > 1:
+                hx = D.split_halo_chunks(p.halo_x, p.recv_x_counts, args.chunks)
+                offs = [0]
+                for gk in hx:
+                    offs.append(offs[-1] + gk.n_cols)
+
+                def halo_chunks():
+                    for k, gk in enumerate(hx):
+                        if gk.nnz:
+                            spmm_forward(gk, rx[offs[k]:offs[k + 1]], None, out=out,
+                                         accumulate=True)
+                ph["spmm_halo_x"] = _time(halo_chunks)
+            elif rx.shape[0]:
                 ph["spmm_halo_x"] = _time(lambda: spmm_forward(p.halo_x, rx, None, out=out,
                                                                accumulate=True))
             if rp.shape[0]:
