@@ -525,26 +525,6 @@ def split_halo_chunks(halo_x: CsrGraph, recv_counts: list, chunks: int) -> list:
     return out
 
 
-def chunk_spmm_kwargs(whole: CsrGraph, chunks: list, feat: int) -> list:
-    """``spmm_forward`` keyword arguments for the column chunks of one halo pass: the hub
-    staging the whole pass would get (ops.spmm_forward's size rules on ``whole``), its hub
-    rows shared out between the chunks in proportion to their edges. Each chunk's default
-    would stage as many hub rows as the whole pass (K = 256 Ki rows of a 256 MB chunk table),
-    so C chunks copied C times the hub bytes per step."""
-    from . import ops
-    xcd = (whole.nnz >= ops.XCD_MIN_NNZ and ops.xcd_hub_rows_for(whole.n_cols, feat) > 0)
-    k_all = (ops.xcd_hub_rows_for(whole.n_cols, feat) if xcd
-             else ops.hub_rows_for(whole.n_cols, feat))
-    if k_all == 0:
-        return [{"hubs": 0, "xcd": False} for _ in chunks]
-    out = []
-    for gk in chunks:
-        k = int(round(k_all * gk.nnz / max(1, whole.nnz)))
-        k = min(gk.n_cols, max(8 * ops.XCD_PHASES if xcd else 1, k))
-        out.append({"hubs": k, "xcd": xcd})
-    return out
-
-
 # Feature-row exchange of the cover SpMM in this many chunked all-to-all-v's (each peer's rows
 # cut into HALO_CHUNKS pieces): the halo_x SpMM of chunk k runs while chunk k+1 is in flight,
 # instead of every halo gather waiting for the whole exchange (VERDICT r3 next #4). Each extra
@@ -571,7 +551,6 @@ class EdgeCutSpmm:
         self.feat = feat
         self.group = group
         self.device = torch.device(device)
-        self._hip_spmm = spmm is None
         if spmm is None or gather is None:
             from .ops import gather_rows, spmm_forward
             spmm = spmm or spmm_forward
@@ -621,7 +600,6 @@ class EdgeCutSpmm:
                     for k in range(C)]
             tot = _all_gather_floats(mine, p.world, self.device, self.group).sum(0)
             self.x_chunk_live = [bool(v > 0) for v in tot.tolist()]
-        self.x_chunk_kw = [{} for _ in range(C)]
         if C == 1:
             self.send_x_idx = p.send_x_idx
             self.halo_x_chunks = [p.halo_x]
@@ -629,8 +607,6 @@ class EdgeCutSpmm:
         self.send_x_idx = p.send_x_idx[chunk_major(p.send_x_counts, C,
                                                    p.send_x_idx.device)].contiguous()
         self.halo_x_chunks = split_halo_chunks(p.halo_x, p.recv_x_counts, C)
-        if self._hip_spmm:
-            self.x_chunk_kw = chunk_spmm_kwargs(p.halo_x, self.halo_x_chunks, self.feat)
 
     def _mark(self, name, stream):
         if self._marks is not None:
@@ -758,7 +734,7 @@ class EdgeCutSpmm:
                     gk = self.halo_x_chunks[k]
                     if gk.nnz or act is not None:  # an activation pass touches every row
                         self._spmm(gk, self.recv_x[ro[k]:ro[k + 1]], None, out=out,
-                                   accumulate=True, activation=act, **self.x_chunk_kw[k])
+                                   accumulate=True, activation=act)
                     self._mark("spmm_halo_x" + sfx, cur)
             if p.any_p:
                 self._wait(ev_p, cur)

@@ -76,8 +76,6 @@ def main():
     ap.add_argument("--chunks", type=int, default=1,
                     help="time the halo_x pass split into this many column chunks "
                          "(EdgeCutSpmm chunks=, the chunked feature-row exchange)")
-    ap.add_argument("--chunk-default-hubs", action="store_true",
-                    help="chunks stage hub rows by their own size rule (before chunk_spmm_kwargs)")
     ap.add_argument("--strong", action="store_true",
                     help="cfg5: the fixed 10M / 100M graph cut W ways (default: W x 1M / 10M)")
     args = ap.parse_args()
@@ -140,14 +138,11 @@ def main():
                 for gk in hx:
                     offs.append(offs[-1] + gk.n_cols)
 
-                kw = (D.chunk_spmm_kwargs(p.halo_x, hx, F) if not args.chunk_default_hubs
-                      else [{} for _ in hx])
-
                 def halo_chunks():
                     for k, gk in enumerate(hx):
                         if gk.nnz:
                             spmm_forward(gk, rx[offs[k]:offs[k + 1]], None, out=out,
-                                         accumulate=True, **kw[k])
+                                         accumulate=True)
                 ph["spmm_halo_x"] = _time(halo_chunks)
             elif rx.shape[0]:
                 ph["spmm_halo_x"] = _time(lambda: spmm_forward(p.halo_x, rx, None, out=out,
