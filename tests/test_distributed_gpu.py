@@ -572,3 +572,36 @@ def test_chunked_halo_exchange_two_ranks(dev, chunks):
             assert {"halo_x0_start_at_ms", "a2a_x_last_end_at_ms",
                     "halo_before_last_recv_ms"} <= set(p)
             assert all(f"a2a_x{k}_ms" in p for k in range(chunks))
+
+
+def test_rccl_world1_zero_and_chunked_all_to_all(dev):
+    """The nccl (= RCCL) backend at world 1 (one GPU cannot host two RCCL ranks): the
+    all-to-all-v calls the edge-cut path makes -- a zero-row chunk, a non-empty one, int64 and
+    float64 handshakes, the float all-gather -- run through torch.distributed on RCCL."""
+    from graphneuralnetwork_amd import distributed as D
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=dev)
+    try:
+        for rows in (0, 5, 1000):
+            inp = torch.randn(rows, 64, device=dev)
+            out = torch.empty_like(inp)
+            D._all_to_all_v(out, inp, [rows], [rows])
+            torch.cuda.synchronize()
+            assert torch.equal(out, inp)
+        for dt in (torch.int64, torch.float64):
+            inp = torch.arange(12, device=dev).to(dt)
+            out = torch.empty_like(inp)
+            D._all_to_all_v(out, inp, [12], [12])
+            assert torch.equal(out, inp)
+        g = D._all_gather_floats([1.5, -2.0], 1, dev)
+        assert g.tolist() == [[1.5, -2.0]]
+        assert D._global_sum(7, dev) == 7
+    finally:
+        dist.destroy_process_group()
