@@ -1066,9 +1066,11 @@ def run_gcn(args, dev, rank: int, world: int, workload: str, edges_np=None, extr
     res = None
     if rank == 0:
         kernel = HUB_INFO["kernel"] if HUB_INFO.get("kernel") else (
-            "EdgeCutSpmm step: send-side SpMM + 2 RCCL all-to-all-v (comm stream) overlapping "
-            "the interior SpMM (hub-staged when its X is >= 192 MiB), then the halo SpMMs; "
-            "per-step HIP events, max over ranks" if world > 1 else
+            "EdgeCutSpmm step: send-side SpMM; the feature rows in %d chunked RCCL "
+            "all-to-all-v's and the partial rows in one more (comm stream) overlapping the "
+            "interior SpMM (hub-staged when its X is >= 192 MiB); the halo SpMM of each chunk as "
+            "it lands, then the partial-row pass; per-step HIP events, max over ranks"
+            % (runner.chunks if args.exchange == "cover" else 1) if world > 1 else
             "spmm_csr_kernel (+ spmm_fixup_kernel), per-step HIP events")
         roof = gcn_roofline(nnz_local, rows_local,
                             rows_local + halo_rows if world > 1 else g.n_cols, F, step_ms,
