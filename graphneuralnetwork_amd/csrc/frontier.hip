@@ -320,7 +320,8 @@ extern "C" int gnn_sample_layers(const int64_t* rowptr, const int32_t* col, int6
   const int64_t n_words = (n_graph + 31) / 32;
   FrontierWs f = fr_layout(workspace, n_graph, workspace_bytes);
   int32_t* err = reinterpret_cast<int32_t*>(stat + n_layers);  // low word of the last entry
-  hipLaunchKernelGGL(batch_init_kernel, dim3(1), dim3(64), 0, s, stat, n_layers, n_seeds);
+  // n_layers + 1 <= 65 entries (sizes, then the error word): one workgroup of 128 threads
+  hipLaunchKernelGGL(batch_init_kernel, dim3(1), dim3(128), 0, s, stat, n_layers, n_seeds);
   for (int i = 0; i < n_layers; ++i) {
     const int64_t* nodes = i == 0 ? seeds : layers[i];
     const int64_t* n_dev = stat + i;
