@@ -330,3 +330,24 @@ def test_draws_match_restatement(dev, k):
     got = sample_neighbors(adj, torch.from_numpy(nodes).to(dev), k, seed=11, layer=1).cpu().numpy()
     want = _draws_ref(rowptr, col, nodes, k, stream_seed(11, 1))
     np.testing.assert_array_equal(got, want)
+
+
+def test_degree_ordered_keeps_edge_values(dev):
+    """sampler.degree_ordered re-sorts each row's neighbours; a weighted adjacency
+    keeps every value on its own edge (the (row, col, val) triplets are P A P^T's)."""
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.sampler import degree_ordered
+    adj = _adj(dev, n=2000, e=20000, seed=4)
+    rowptr, col = adj.rowptr.cpu().numpy(), adj.col.cpu().numpy()
+    rng = np.random.default_rng(0)
+    val = rng.standard_normal(col.size).astype(np.float32)          # distinct per edge
+    g = CsrGraph(adj.rowptr, adj.col, torch.from_numpy(val).to(dev), adj.n_rows, adj.n_cols)
+    g2, _, o = degree_ordered(g)
+    inv = o.inv.cpu().numpy()
+    rows = np.repeat(np.arange(adj.n_rows), np.diff(rowptr))
+    want = sorted(zip(inv[rows].tolist(), inv[col].tolist(), val.tolist()))
+    rp2, c2, v2 = g2.rowptr.cpu().numpy(), g2.col.cpu().numpy(), g2.val.cpu().numpy()
+    rows2 = np.repeat(np.arange(adj.n_rows), np.diff(rp2))
+    assert sorted(zip(rows2.tolist(), c2.tolist(), v2.tolist())) == want
+    for r in range(0, adj.n_rows, 97):                               # ascending neighbours
+        assert np.all(np.diff(c2[rp2[r]:rp2[r + 1]]) > 0)
