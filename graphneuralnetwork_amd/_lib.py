@@ -61,6 +61,16 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_halo_rccl_path": (ctypes.c_int, [ctypes.c_char_p, _i64]),
     "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
     "gnn_hub_plan_workspace_bytes": (_i64, [_i64]),
+    "gnn_spmm_tasks_workspace_bytes": (_i64, [_i64]),
+    "gnn_spmm_tasks_build": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _i64,
+                                            _vp]),
+    "gnn_column_order_workspace_bytes": (_i64, [_i64]),
+    "gnn_column_order": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "gnn_xcd_hub_plan_workspace_bytes": (_i64, [_i64, _i64]),
+    "gnn_xcd_hub_plan_build": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+                                              _i64, _vp, _vp, _i64, _vp]),
+    "gnn_xcd_hub_plan_fill": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp,
+                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gnn_in_degree_u32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gnn_hub_plan_build": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "gnn_spmm_plan_count": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),

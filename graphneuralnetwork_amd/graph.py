@@ -20,6 +20,7 @@ device by the C-ABI (``gnn_spmm_plan_*``); it is cached per ``seg_len``.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass, field
 
 import torch
@@ -153,10 +154,40 @@ class TaskPlan:
                 self.task_row.data_ptr() if self.n_task else None, self.n_task)
 
 
+# The schedule builders run natively on the device (csrc/plan_build.hip: gnn_spmm_tasks_build,
+# gnn_column_order, gnn_xcd_hub_plan_*), the same C-ABI a C caller uses; the torch versions
+# below are the CPU path and the cross-check (tests/test_plan_build_gpu.py: equal arrays).
+NATIVE_PLANS = True
+
+
 def task_ranges(rowptr: torch.Tensor, max_deg: int, cost: int, rows: int = TASK_ROWS):
     """[2 * n_task] int32 [begin, end) row ranges: maximal runs of consecutive rows of degree
     <= max_deg, cut where the (edges + rows) prefix inside the run crosses a multiple of
-    ``cost`` and every ``rows`` rows (torch ops on any device)."""
+    ``cost`` and every ``rows`` rows. On the device: gnn_spmm_tasks_build; else torch ops."""
+    if NATIVE_PLANS and rowptr.is_cuda and rows == TASK_ROWS and cost >= 1:
+        return task_ranges_native(rowptr, max_deg, cost)
+    return task_ranges_torch(rowptr, max_deg, cost, rows)
+
+
+def task_ranges_native(rowptr: torch.Tensor, max_deg: int, cost: int) -> torch.Tensor:
+    """``task_ranges`` by gnn_spmm_tasks_build (one host sync for the count)."""
+    n = rowptr.numel() - 1
+    dev = rowptr.device
+    if n <= 0:
+        return torch.zeros(0, dtype=torch.int32, device=dev)
+    lib = _lib.load()
+    ws = torch.empty(int(lib.gnn_spmm_tasks_workspace_bytes(n)), dtype=torch.uint8, device=dev)
+    out = torch.empty(2 * n, dtype=torch.int32, device=dev)
+    nt = ctypes.c_int64(0)
+    _lib.check(lib.gnn_spmm_tasks_build(rowptr.data_ptr(), n, int(max_deg), int(cost),
+                                        out.data_ptr(), n, ctypes.addressof(nt), ws.data_ptr(),
+                                        ws.numel(), _lib.stream_handle(dev)),
+               "gnn_spmm_tasks_build")
+    return out[:2 * nt.value].clone()
+
+
+def task_ranges_torch(rowptr: torch.Tensor, max_deg: int, cost: int, rows: int = TASK_ROWS):
+    """``task_ranges`` in torch ops (any device)."""
     dev = rowptr.device
     n = rowptr.numel() - 1
     if n == 0:
@@ -592,6 +623,8 @@ def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int, phases: i
         return None
     if item_k is not None and min(int(item_k), hub.k) < XCDS * phases:
         return None
+    if NATIVE_PLANS and g.rowptr.is_cuda:
+        return _build_xcd_hub_plan_native(g, hub, min_deg, chunk, phases, item_k, small_item)
     coo = xcd_hub_coo(g.rowptr, hub.col_hub, g.val, hub.k, min_deg, chunk, phases=phases,
                       item_k=item_k, small_item=small_item)
     if coo is None:
@@ -601,6 +634,48 @@ def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int, phases: i
         return None  # partial refs must fit int32 column ids
     items = from_coo(ir, ic, iv, n_pos, hub.k, check=False)
     rest = from_coo(rr, rc, rv, g.n_rows, g.n_cols, check=False)
+    return XcdHubPlan(hub, items, rest, n_items, min_deg, chunk, pos_row)
+
+
+def _build_xcd_hub_plan_native(g: CsrGraph, hub: HubPlan, min_deg: int, chunk: int,
+                               phases: int, item_k: int | None,
+                               small_item: int | None) -> "XcdHubPlan | None":
+    """``_build_xcd_hub_plan`` by gnn_xcd_hub_plan_build / _fill (the same CSR arrays)."""
+    if chunk < 4:
+        raise ValueError("xcd hub staging needs chunk >= 4 and k >= xcds * phases")
+    if small_item is not None and small_item < 2:
+        raise ValueError("small_item must be >= 2")
+    lib = _lib.load()
+    dev = g.device
+    stream = _lib.stream_handle(dev)
+    ws = torch.empty(int(lib.gnn_xcd_hub_plan_workspace_bytes(g.n_rows, g.nnz)),
+                     dtype=torch.uint8, device=dev)
+    counts = (ctypes.c_int64 * 4)()
+    _lib.check(lib.gnn_xcd_hub_plan_build(g.rowptr.data_ptr(), hub.col_hub.data_ptr(), g.n_rows,
+                                          g.nnz, hub.k, int(min_deg), int(chunk), int(phases),
+                                          0 if item_k is None else int(item_k),
+                                          0 if small_item is None else int(small_item),
+                                          ctypes.addressof(counts), ws.data_ptr(), ws.numel(),
+                                          stream), "gnn_xcd_hub_plan_build")
+    n_items, n_pos, nnz_items, nnz_rest = (int(v) for v in counts)
+    if n_items == 0 or hub.k + n_pos > 0x7fffffff:
+        return None
+    i64, i32, f32 = (dict(dtype=t, device=dev) for t in (torch.int64, torch.int32, torch.float32))
+    irp = torch.empty(n_pos + 1, **i64)
+    icol = torch.empty(nnz_items, **i32)
+    ival = torch.empty(nnz_items, **f32)
+    pos_row = torch.empty(n_pos, **i64)
+    rrp = torch.empty(g.n_rows + 1, **i64)
+    rcol = torch.empty(nnz_rest, **i32)
+    rval = torch.empty(nnz_rest, **f32)
+    _lib.check(lib.gnn_xcd_hub_plan_fill(ws.data_ptr(), g.rowptr.data_ptr(),
+                                         hub.col_hub.data_ptr(), g.val.data_ptr(), g.n_rows, g.nnz,
+                                         hub.k, int(phases), ctypes.addressof(counts),
+                                         irp.data_ptr(), icol.data_ptr(), ival.data_ptr(),
+                                         pos_row.data_ptr(), rrp.data_ptr(), rcol.data_ptr(),
+                                         rval.data_ptr(), stream), "gnn_xcd_hub_plan_fill")
+    items = CsrGraph(irp, icol, ival, n_pos, hub.k)
+    rest = CsrGraph(rrp, rcol, rval, g.n_rows, g.n_cols)
     return XcdHubPlan(hub, items, rest, n_items, min_deg, chunk, pos_row)
 
 
@@ -642,7 +717,8 @@ def in_degree(g: "CsrGraph") -> torch.Tensor:
 
 def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None,
                  tail: str | None = None) -> DegreeOrder:
-    """Relabel a CSR graph by column in-degree (torch ops on its device). The edges of each
+    """Relabel a CSR graph by column in-degree (gnn_column_order on the device, torch ops on
+    the CPU; tail "first_use" in torch ops everywhere). The edges of each
     row keep their CSR order (renamed), so every row sum runs in the same order: the result
     is bit-identical to the original graph's, permuted.
 
@@ -657,6 +733,56 @@ def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None,
     degree order), "id" (ascending ids, the default when only ``prefix`` is given) or
     "first_use" (by the CSR position of their first edge: the rows a row-ordered SpMM touches
     for the first time lie together in memory; columns without edges last)."""
+    n = g.n_cols
+    dev = g.device
+    idx = torch.arange(n, device=dev, dtype=torch.int64)
+    if tail not in (None, "id", "degree", "first_use"):
+        raise ValueError(f"unknown tail order {tail!r}")
+    col_new = None
+    if NATIVE_PLANS and g.col.is_cuda and n > 0 and tail != "first_use":
+        ranked = prefix if (prefix is not None and prefix < n and tail != "degree") else -1
+        perm, inv, col_new = column_order_native(g, ranked)
+    else:
+        perm, inv = _degree_perm_torch(g, prefix, tail)
+    if not rows:
+        col = col_new if col_new is not None else inv[g.col.to(torch.int64)].to(torch.int32)
+        return DegreeOrder(perm, inv, CsrGraph(g.rowptr, col.contiguous(), g.val, g.n_rows, n))
+    if g.n_rows != g.n_cols:
+        raise ValueError("degree_order(rows=True) needs a square adjacency")
+    deg = g.rowptr[1:] - g.rowptr[:-1]
+    new_deg = deg[perm]
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(new_deg, 0, out=rowptr[1:])
+    # edge e of new row i is edge (rowptr_old[perm[i]] + j) of the old graph
+    rows_new = torch.repeat_interleave(idx, new_deg)
+    src = g.rowptr[perm][rows_new] + (torch.arange(rows_new.numel(), device=dev,
+                                                   dtype=torch.int64) - rowptr[rows_new])
+    if col_new is not None:
+        col = col_new[src].contiguous()
+    else:
+        col = inv[g.col.to(torch.int64)[src]].to(torch.int32).contiguous()
+    val = g.val[src].contiguous()
+    return DegreeOrder(perm, inv, CsrGraph(rowptr, col, val, n, n))
+
+
+def column_order_native(g: "CsrGraph", prefix: int = -1):
+    """(perm, inv, renamed int32 columns) of ``degree_order`` by gnn_column_order
+    (``prefix`` < 0: every id ranked)."""
+    n = g.n_cols
+    dev = g.device
+    lib = _lib.load()
+    ws = torch.empty(int(lib.gnn_column_order_workspace_bytes(n)), dtype=torch.uint8, device=dev)
+    perm = torch.empty(n, dtype=torch.int64, device=dev)
+    inv = torch.empty(n, dtype=torch.int64, device=dev)
+    col = torch.empty_like(g.col)
+    _lib.check(lib.gnn_column_order(_lib.ptr(g.col), g.nnz, n, int(prefix), perm.data_ptr(),
+                                    inv.data_ptr(), _lib.ptr(col), ws.data_ptr(), ws.numel(),
+                                    _lib.stream_handle(dev)), "gnn_column_order")
+    return perm, inv, col
+
+
+def _degree_perm_torch(g: "CsrGraph", prefix: int | None, tail: str | None):
+    """(perm, inv) of ``degree_order`` in torch ops (any device)."""
     n = g.n_cols
     dev = g.device
     indeg = in_degree(g)
@@ -678,22 +804,7 @@ def degree_order(g: "CsrGraph", rows: bool = True, prefix: int | None = None,
         perm = torch.cat([perm[:prefix], rest])
     inv = torch.empty_like(perm)
     inv[perm] = idx
-    if not rows:
-        col = inv[g.col.to(torch.int64)].to(torch.int32).contiguous()
-        return DegreeOrder(perm, inv, CsrGraph(g.rowptr, col, g.val, g.n_rows, n))
-    if g.n_rows != g.n_cols:
-        raise ValueError("degree_order(rows=True) needs a square adjacency")
-    deg = g.rowptr[1:] - g.rowptr[:-1]
-    new_deg = deg[perm]
-    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(new_deg, 0, out=rowptr[1:])
-    # edge e of new row i is edge (rowptr_old[perm[i]] + j) of the old graph
-    rows_new = torch.repeat_interleave(idx, new_deg)
-    src = g.rowptr[perm][rows_new] + (torch.arange(rows_new.numel(), device=dev,
-                                                   dtype=torch.int64) - rowptr[rows_new])
-    col = inv[g.col.to(torch.int64)[src]].to(torch.int32).contiguous()
-    val = g.val[src].contiguous()
-    return DegreeOrder(perm, inv, CsrGraph(rowptr, col, val, n, n))
+    return perm, inv
 
 
 # ---------------------------------------------------------------- builders

@@ -164,6 +164,72 @@ int gnn_hub_plan_build(const int32_t* col, int64_t nnz, int64_t n_cols, int64_t 
                        int64_t workspace_bytes, void* stream);
 
 /*
+ * Schedule builders of the default aggregation path (csrc/plan_build.hip). Each one returns
+ * the arrays the Python builder named in brackets makes, bit for bit; they synchronise the
+ * stream to size their stages (once per graph, never per forward). New in this library: the
+ * reference has no plans; they serve GCN/GCN.py:43-45 through the SpMM entries above.
+ *
+ * gnn_spmm_tasks_build (graph.task_ranges): the packed row tasks of gnn_spmm_csr_tasks_f32 --
+ *   maximal runs of consecutive rows of degree <= max_deg, cut every 63 rows and where the
+ *   (edges + rows) prefix inside the run crosses a multiple of `cost` (>= 1). *n_task (host)
+ *   receives the task count; the [begin, end) pairs go to task_row (int32 [2 * cap_tasks],
+ *   device) when task_row is non-null and n_task <= cap_tasks (else GNN_E_ARG with *n_task
+ *   set: call again with room for it; n_rows pairs always suffice). Ascending, disjoint,
+ *   1..63 rows each (gnn_spmm_tasks_check accepts them). Pass min(max_deg, seg_len).
+ *   workspace: gnn_spmm_tasks_workspace_bytes(n_rows) bytes of device memory.
+ */
+int64_t gnn_spmm_tasks_workspace_bytes(int64_t n_rows);
+int gnn_spmm_tasks_build(const int64_t* rowptr, int64_t n_rows, int64_t max_deg, int64_t cost,
+                         int32_t* task_row, int64_t cap_tasks, int64_t* n_task, void* workspace,
+                         int64_t workspace_bytes, void* stream);
+
+/*
+ * gnn_column_order (graph.degree_order(g, rows=False, prefix)): the column relabelling of the
+ * column-degree order A P^T. perm[i] (int64 [n_cols]) = the old id of new column i: in-degree
+ * descending, ties by ascending id; with 0 <= prefix < n_cols only the first `prefix` ids are
+ * ranked and the rest follow in ascending id order (prefix < 0: all ranked). inv[perm[i]] = i;
+ * col_out[e] = inv[col[e]] (col_out may be col). Y = (A P^T)(P X) = A X with every row's sum
+ * in its CSR order: bit-identical. A column id outside [0, n_cols) -> GNN_E_ARG.
+ * workspace: gnn_column_order_workspace_bytes(n_cols) bytes of device memory.
+ */
+int64_t gnn_column_order_workspace_bytes(int64_t n_cols);
+int gnn_column_order(const int32_t* col, int64_t nnz, int64_t n_cols, int64_t prefix,
+                     int64_t* perm, int64_t* inv, int32_t* col_out, void* workspace,
+                     int64_t workspace_bytes, void* stream);
+
+/*
+ * gnn_xcd_hub_plan_build / _fill (graph.xcd_hub_coo + from_coo): the XCD-sliced hub staging
+ * of gnn_spmm_csr_hub_f32 / gnn_spmm_csr_tasks_f32 for a column array renamed by
+ * gnn_hub_plan_build (col_hub; k hub ranks). The hub ranks are dealt to S = 8 * phases slices
+ * (rank % S). For every row of degree >= min_deg (>= 2 with small_item >= 2), the edges to
+ * the item_k hottest ranks (item_k <= 0: all k) that fall in one slice form a group; groups of
+ * >= 2 edges (and, with small_item, rows of degree >= min_deg or groups of >= small_item edges)
+ * are cut into ceil(m / chunk) balanced items. Pass 1 ("items") reduces each item into a
+ * partial row at a position laid out so that workgroup w (4 waves) holds items of slice
+ * w % 8 only; pass 2 ("rest") is every row's unmoved edges in CSR order followed by one edge
+ * -1 - (k + position) of value 1.0 per item of the row.
+ *   build: counts[4] (host) = n_items, n_pos, nnz_items, nnz_rest; n_items == 0 means no
+ *          row has two hub edges in one slice (no plan). chunk >= 4, k >= S, item_k >= S,
+ *          8 * phases <= 1024, else GNN_E_ARG.
+ *   fill:  with the same workspace, rowptr, col_hub, n_rows, nnz, k, phases and the counts:
+ *          items CSR (rowptr int64 [n_pos + 1], col int32 / val fp32 [nnz_items]; a pad
+ *          position holds two zero-valued edges of its slice), pos_row (int64 [n_pos]: the
+ *          graph row of each position, pads 0) and rest CSR (rowptr int64 [n_rows + 1],
+ *          col int32 / val fp32 [nnz_rest]). All device memory.
+ * workspace: gnn_xcd_hub_plan_workspace_bytes(n_rows, nnz) bytes of device memory.
+ */
+int64_t gnn_xcd_hub_plan_workspace_bytes(int64_t n_rows, int64_t nnz);
+int gnn_xcd_hub_plan_build(const int64_t* rowptr, const int32_t* col_hub, int64_t n_rows,
+                           int64_t nnz, int64_t k, int64_t min_deg, int64_t chunk, int64_t phases,
+                           int64_t item_k, int64_t small_item, int64_t* counts, void* workspace,
+                           int64_t workspace_bytes, void* stream);
+int gnn_xcd_hub_plan_fill(const void* workspace, const int64_t* rowptr, const int32_t* col_hub,
+                          const float* val, int64_t n_rows, int64_t nnz, int64_t k, int64_t phases,
+                          const int64_t* counts, int64_t* items_rowptr, int32_t* items_col,
+                          float* items_val, int64_t* pos_row, int64_t* rest_rowptr,
+                          int32_t* rest_col, float* rest_val, void* stream);
+
+/*
  * Row-class plan for gnn_spmm_csr_f32 / gnn_gat_csr_f32 (built once per graph).
  *
  * gnn_spmm_plan_count: classifies the rows and writes four int64 counters into
