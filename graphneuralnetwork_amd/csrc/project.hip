@@ -9,7 +9,8 @@
 // in registers for the whole launch, Wh stored straight from the accumulator layout
 // (16 lanes = 64 contiguous bytes of a row). The logits ride along as one more
 // 16-column MFMA tile: [el | er] = X (W A) with A the block-diagonal [fout, 2 heads]
-// matrix of a_src / a_dst, folded into W once per workgroup (W2 = W A in LDS).
+// matrix of a_src / a_dst, folded into W once per workgroup (W2 = W A in LDS, computed by
+// the workgroup itself: no separate launch).
 //
 // MFMA operand maps (16x16x4 f32): lane l holds A[l & 15][k = l >> 4] and
 // B[k = l >> 4][l & 15]; C/D: col = l & 15, row = 4 * (l >> 4) + reg. The kernel
@@ -32,22 +33,17 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 // w2[k][c] = W[k, head c] . a_src[head c] (c < heads), W[k, head c-heads] . a_dst[head
 // c-heads] (heads <= c < 2 heads), 0 beyond: the logits as a [K, 16] weight tile.
-__global__ __launch_bounds__(256) void gat_project_w2_kernel(const float* __restrict__ w, int k,
-                                                             int fout, const float* __restrict__ a_src,
-                                                             const float* __restrict__ a_dst,
-                                                             int heads, int fh,
-                                                             float* __restrict__ w2) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= k * 16) return;
-  const int kk = e >> 4, c = e & 15;
+// (w and a read from the workgroup's LDS copies: wl = W [K, fout], al = [a_src | a_dst])
+__device__ __forceinline__ float logit_weight(const float* wl, int kk, int fout, const float* al,
+                                              int heads, int fh, int c) {
   float v = 0.f;
   if (c < 2 * heads) {
     const int h = c < heads ? c : c - heads;
-    const float* av = (c < heads ? a_src : a_dst) + h * fh;
-    const float* wr = w + kk * fout + h * fh;
+    const float* av = al + (c < heads ? 0 : fout) + h * fh;
+    const float* wr = wl + kk * fout + h * fh;
     for (int f = 0; f < fh; ++f) v = fmaf(wr[f], av[f], v);
   }
-  w2[e] = v;
+  return v;
 }
 
 // The A tile's LDS image (row pitch and xor swizzle per K): TileLds in common.hpp.
@@ -79,7 +75,8 @@ __device__ __forceinline__ void proj_tile_sync() {
 template <int K, int NT, bool COLROW, bool X6 = false>
 __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
-    const float* __restrict__ w2, int heads, float* __restrict__ wh, int64_t ldwh,
+    const float* __restrict__ a_src, const float* __restrict__ a_dst, int fh, int heads,
+    float* __restrict__ wh, int64_t ldwh,
     float* __restrict__ el, float* __restrict__ er, int64_t lde,
     const int64_t* __restrict__ col_row) {
   constexpr int S = K / 4;   // MFMA k-steps
@@ -96,10 +93,19 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
   const bool vec_logits = heads % 4 == 0 && lde % 4 == 0 &&
                           ((reinterpret_cast<uintptr_t>(el) | reinterpret_cast<uintptr_t>(er)) & 15) == 0;
 
-  // Logit weights as one more 16-column tile (w2 = W A, gat_project_w2_kernel):
+  // Logit weights as one more 16-column tile (w2 = W A, folded here per workgroup):
   // [el | er] = X w2 comes out of the same MFMA k-loop as Wh = X W.
+  // W and a are copied to LDS first (independent loads, one round trip), the fold reads them
+  // there (a loop of dependent global loads per entry would stall every workgroup's start)
   __shared__ float w2s[K * 16];
-  for (int e = threadIdx.x; e < K * 16; e += kProjBlock) w2s[e] = w2[e];
+  __shared__ float wl[K * FO];
+  __shared__ float al[2 * FO];
+  for (int e = threadIdx.x; e < K * FO; e += kProjBlock) wl[e] = w[e];
+  for (int e = threadIdx.x; e < 2 * FO; e += kProjBlock) al[e] = e < FO ? a_src[e] : a_dst[e - FO];
+  __syncthreads();
+  for (int e = threadIdx.x; e < K * 16; e += kProjBlock)
+    w2s[e] = logit_weight(wl, e >> 4, FO, al, heads, fh, e & 15);
+  __syncthreads();
 #ifdef GNN_PROJ_B_LDS
   // B fragments read from LDS at every step (fewer VGPRs, more waves per SIMD)
   __shared__ float ws[K * FO];
@@ -117,7 +123,7 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = q * S + 8 * s6 + j;
-          const float v = t < NT ? w[k * FO + 16 * t + r] : w2[k * 16 + r];
+          const float v = t < NT ? wl[k * FO + 16 * t + r] : w2s[k * 16 + r];
           __bf16 p0, p1, p2;
           split3(v, p0, p1, p2);
           bx[t][s6][0][j] = p0;
@@ -128,7 +134,7 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int s = 0; s < S; ++s) b[t][s] = w[(q * S + s) * FO + 16 * t + r];
+      for (int s = 0; s < S; ++s) b[t][s] = wl[(q * S + s) * FO + 16 * t + r];
   }
   __syncthreads();
   if constexpr (!X6) {
@@ -326,8 +332,9 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
 
 template <int K, int NT>
 static int launch_project(const float* x, int64_t ldx, int64_t n_rows, const float* w,
-                          const float* w2, int heads, float* wh, int64_t ldwh, float* el,
-                          float* er, int64_t lde, const int64_t* col_row, hipStream_t s) {
+                          const float* a_src, const float* a_dst, int fh, int heads, float* wh,
+                          int64_t ldwh, float* el, float* er, int64_t lde,
+                          const int64_t* col_row, hipStream_t s) {
   const int64_t groups = (n_rows + 16 * kProjG * kProjWaves - 1) / (16 * kProjG * kProjWaves);
 #ifndef GNN_PROJ_GRID
 // 512 = the resident workgroups at 2 waves/SIMD (144 VGPRs): A/B at cfg3 with isolated
@@ -344,33 +351,34 @@ static int launch_project(const float* x, int64_t ldx, int64_t n_rows, const flo
     if (g_tf_x6) {  // the transforms' arithmetic (gnn_transform_set_precision)
       if (col_row != nullptr)
         hipLaunchKernelGGL((gat_project_kernel<K, NT, true, true>), g, dim3(kProjBlock), 0, s, x,
-                           ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row);
+                           ldx, n_rows, w, a_src, a_dst, fh, heads, wh, ldwh, el, er, lde, col_row);
       else
         hipLaunchKernelGGL((gat_project_kernel<K, NT, false, true>), g, dim3(kProjBlock), 0, s, x,
-                           ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row);
+                           ldx, n_rows, w, a_src, a_dst, fh, heads, wh, ldwh, el, er, lde, col_row);
       return launch_status();
     }
   }
   if (col_row != nullptr)
     hipLaunchKernelGGL((gat_project_kernel<K, NT, true>), g, dim3(kProjBlock), 0, s, x, ldx,
-                       n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row);
+                       n_rows, w, a_src, a_dst, fh, heads, wh, ldwh, el, er, lde, col_row);
   else
     hipLaunchKernelGGL((gat_project_kernel<K, NT, false>), g, dim3(kProjBlock), 0, s, x, ldx,
-                       n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row);
+                       n_rows, w, a_src, a_dst, fh, heads, wh, ldwh, el, er, lde, col_row);
   return launch_status();
 }
 
 template <int K>
 static int dispatch_project_nt(int64_t fout, const float* x, int64_t ldx, int64_t n_rows,
-                               const float* w, const float* w2, int heads, float* wh,
+                               const float* w, const float* a_src, const float* a_dst, int fh,
+                               int heads, float* wh,
                                int64_t ldwh, float* el, float* er, int64_t lde,
                                const int64_t* col_row, hipStream_t s) {
   // B fragments live in registers: (K / 4) * NT <= 64
-  if (fout == 16) return launch_project<K, 1>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row, s);
+  if (fout == 16) return launch_project<K, 1>(x, ldx, n_rows, w, a_src, a_dst, fh, heads, wh, ldwh, el, er, lde, col_row, s);
   if constexpr (K <= 128)
-    if (fout == 32) return launch_project<K, 2>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row, s);
+    if (fout == 32) return launch_project<K, 2>(x, ldx, n_rows, w, a_src, a_dst, fh, heads, wh, ldwh, el, er, lde, col_row, s);
   if constexpr (K <= 64)
-    if (fout == 64) return launch_project<K, 4>(x, ldx, n_rows, w, w2, heads, wh, ldwh, el, er, lde, col_row, s);
+    if (fout == 64) return launch_project<K, 4>(x, ldx, n_rows, w, a_src, a_dst, fh, heads, wh, ldwh, el, er, lde, col_row, s);
   return GNN_E_UNSUPPORTED;
 }
 
@@ -397,20 +405,18 @@ static int project_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
     return GNN_E_ARG;
   if (!gnn_gat_project_supported(k, fout, fh)) return GNN_E_UNSUPPORTED;
   if (n_rows == 0) return GNN_OK;
-  if (!x || !w || !a_src || !a_dst || !wh || !el || !er || !w2_scratch) return GNN_E_ARG;
+  if (!x || !w || !a_src || !a_dst || !wh || !el || !er) return GNN_E_ARG;
   if (ldx % 4 || ldwh % 4 || !aligned_to(x, 16) || !aligned_to(wh, 16)) return GNN_E_ALIGN;
+  (void)w2_scratch;  // the logit weights are folded inside the kernel (kept for the ABI)
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int h = static_cast<int>(heads);
-  hipLaunchKernelGGL(gat_project_w2_kernel, dim3(static_cast<unsigned>((k * 16 + 255) / 256)),
-                     dim3(256), 0, s, w, static_cast<int>(k), static_cast<int>(fout), a_src,
-                     a_dst, h, static_cast<int>(fh), w2_scratch);
-  const float* w2 = w2_scratch;
+  const int f = static_cast<int>(fh);
   switch (k) {
-    case 16: return dispatch_project_nt<16>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
-    case 32: return dispatch_project_nt<32>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
-    case 64: return dispatch_project_nt<64>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
-    case 128: return dispatch_project_nt<128>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
-    default: return dispatch_project_nt<256>(fout, x, ldx, n_rows, w, w2, h, wh, ldwh, el, er, lde, col_row, s);
+    case 16: return dispatch_project_nt<16>(fout, x, ldx, n_rows, w, a_src, a_dst, f, h, wh, ldwh, el, er, lde, col_row, s);
+    case 32: return dispatch_project_nt<32>(fout, x, ldx, n_rows, w, a_src, a_dst, f, h, wh, ldwh, el, er, lde, col_row, s);
+    case 64: return dispatch_project_nt<64>(fout, x, ldx, n_rows, w, a_src, a_dst, f, h, wh, ldwh, el, er, lde, col_row, s);
+    case 128: return dispatch_project_nt<128>(fout, x, ldx, n_rows, w, a_src, a_dst, f, h, wh, ldwh, el, er, lde, col_row, s);
+    default: return dispatch_project_nt<256>(fout, x, ldx, n_rows, w, a_src, a_dst, f, h, wh, ldwh, el, er, lde, col_row, s);
   }
 }
 

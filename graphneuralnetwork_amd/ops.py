@@ -415,19 +415,18 @@ def gat_project(x: torch.Tensor, w: torch.Tensor, heads: int, fh: int, a_src: to
         wh = torch.empty((n, fout), dtype=torch.float32, device=x.device)
         el = torch.empty((n, heads), dtype=torch.float32, device=x.device)
         er = torch.empty((n, heads), dtype=torch.float32, device=x.device)
-    w2 = torch.empty((k, 16), dtype=torch.float32, device=x.device)
     if col_rows is not None:
         _lib.check(lib.gnn_gat_project_rows_f32(
             x.data_ptr(), x.stride(0), n, k, w.contiguous().data_ptr(), fout,
             a_src.contiguous().data_ptr(), a_dst.contiguous().data_ptr(), heads, fh,
             wh.data_ptr(), wh.stride(0), el.data_ptr(), er.data_ptr(), el.stride(0),
-            col_rows.data_ptr(), w2.data_ptr(), _lib.stream_handle(x.device)),
+            col_rows.data_ptr(), None, _lib.stream_handle(x.device)),
             "gnn_gat_project_rows_f32")
         return wh, el, er
     _lib.check(lib.gnn_gat_project_f32(
         x.data_ptr(), x.stride(0), n, k, w.contiguous().data_ptr(), fout,
         a_src.contiguous().data_ptr(), a_dst.contiguous().data_ptr(), heads, fh, wh.data_ptr(),
-        wh.stride(0), el.data_ptr(), er.data_ptr(), el.stride(0), w2.data_ptr(),
+        wh.stride(0), el.data_ptr(), er.data_ptr(), el.stride(0), None,
         _lib.stream_handle(x.device)), "gnn_gat_project_f32")
     return wh, el, er
 

@@ -5,8 +5,11 @@
  * Every entry point:
  *   - takes plain device pointers, sizes and a hipStream_t passed as `void*`
  *     (NULL = the null stream); no torch / C++ types cross this boundary;
- *   - never allocates device memory and never synchronises the host: buffers
- *     (outputs, workspaces) are owned and preallocated by the caller;
+ *   - never allocates device memory: buffers (outputs, workspaces) are owned and
+ *     preallocated by the caller;
+ *   - never synchronises the host, except the once-per-graph builders that size their
+ *     outputs (gnn_gcn_adjacency_build, gnn_spmm_tasks_build, gnn_column_order,
+ *     gnn_xcd_hub_plan_build), which say so;
  *   - enqueues its kernels on `stream` and returns 0 on success, a positive
  *     hipError_t on a launch/runtime failure, or a negative GNN_E_* code when an
  *     argument is rejected before anything is launched. It never throws.
@@ -345,8 +348,9 @@ int gnn_linear_relu_cls_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t
  * gnn_gat_logits_f32 on wh to fp32 rounding, not bitwise). Shapes:
  * gnn_gat_project_supported(k, fout, fh) != 0 (k in {16,32,64,128,256}, fout in
  * {16,32,64} with (k/4)*(fout/16) <= 64, heads = fout/fh <= 8); otherwise
- * GNN_E_UNSUPPORTED. x / wh rows 16-B aligned (GNN_E_ALIGN). w2_scratch: k * 16
- * floats of device memory (the folded logit weights w A).
+ * GNN_E_UNSUPPORTED. x / wh rows 16-B aligned (GNN_E_ALIGN). w2_scratch: unused (may be
+ * null; each workgroup folds the logit weights w A itself, one launch in all), kept so that
+ * existing callers link.
  */
 int gnn_gat_project_supported(int64_t k, int64_t fout, int64_t fh);
 int gnn_gat_project_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,

@@ -1,4 +1,5 @@
-"""A/B of gnn_gat_project_f32 builds (lib/variants) at the cfg3 shape.
+"""A/B of gnn_gat_project_rows_f32 builds (lib/variants) at the cfg3 shape (rows scattered
+into a column order as bench.py's cfg3 step writes them).
 
     python tools/project_ab.py --build      (CPU side)
     python tools/project_ab.py              (GPU)
@@ -18,7 +19,8 @@ VARIANTS = {"base": [], "d1": ["GNN_PROJ_DEPTH=1"], "d3": ["GNN_PROJ_DEPTH=3"],
             "g1024": ["GNN_PROJ_GRID=1024"], "g4096": ["GNN_PROJ_GRID=4096"],
             "g8192": ["GNN_PROJ_GRID=8192"], "blds_g4096": ["GNN_PROJ_B_LDS", "GNN_PROJ_GRID=4096"],
             "nomfma": ["GNN_PROJ_NO_MFMA"], "nomfma_nowh": ["GNN_PROJ_NO_MFMA", "GNN_PROJ_NO_WH"],
-            "g2": ["GNN_PROJ_G=2"], "g2_512": ["GNN_PROJ_G=2", "GNN_PROJ_GRID=512"]}
+            "g2": ["GNN_PROJ_G=2"], "g2_512": ["GNN_PROJ_G=2", "GNN_PROJ_GRID=512"],
+            "old": None}  # "old": lib/variants/libgnn_proj_old.so, built from another tree
 
 
 def main():
@@ -30,16 +32,37 @@ def main():
     if args.build:
         from graphneuralnetwork_amd.build import build_variant
         for n in names:
-            print(build_variant("proj_" + n, VARIANTS[n], only=["project.hip"]))
+            if VARIANTS[n] is not None:
+                print(build_variant("proj_" + n, VARIANTS[n], only=["project.hip"]))
         return
     import torch
     from graphneuralnetwork_amd import _lib
-    from graphneuralnetwork_amd.ops import gat_project
     dev = torch.device("cuda:0")
     n, k, H, fh = 1_000_000, 64, 8, 8
     x = torch.randn(n, k, device=dev)
     w = torch.randn(k, H * fh, device=dev)
     s, d = torch.randn(H * fh, device=dev), torch.randn(H * fh, device=dev)
+    # cfg3's column order: 262,144 "hub" ids (random here) first in random order, the rest
+    # ascending (graph.degree_order(prefix=...)); inv = old -> new row
+    g = torch.Generator(device=dev).manual_seed(3)
+    hub = torch.randperm(n, device=dev, generator=g)[:262144]
+    is_hub = torch.zeros(n, dtype=torch.bool, device=dev)
+    is_hub[hub] = True
+    perm = torch.cat([hub, torch.nonzero(~is_hub).view(-1)])
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(n, device=dev)
+    w2 = torch.empty(k * 16, device=dev)  # the scratch older builds fold the logits into
+
+    def gat_project(x, w, H, fh, s, d):
+        lib = _lib.load()
+        wh = torch.empty(n, H * fh, device=dev)
+        el = torch.empty(n, H, device=dev)
+        er = torch.empty(n, H, device=dev)
+        _lib.check(lib.gnn_gat_project_rows_f32(
+            x.data_ptr(), k, n, k, w.data_ptr(), H * fh, s.data_ptr(), d.data_ptr(), H, fh,
+            wh.data_ptr(), H * fh, el.data_ptr(), er.data_ptr(), H, inv.data_ptr(),
+            w2.data_ptr(), _lib.stream_handle(dev)), "gnn_gat_project_rows_f32")
+        return wh, el, er
     res = {v: [] for v in names}
     ref = None
     import statistics
