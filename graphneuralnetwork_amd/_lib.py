@@ -66,6 +66,14 @@ SIGNATURES: dict[str, tuple] = {
                                             _vp]),
     "gnn_column_order_workspace_bytes": (_i64, [_i64]),
     "gnn_column_order": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "gnn_cover_workspace_bytes": (_i64, [_i64, _i64, _i64, _i32]),
+    "gnn_cover_build": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i32, _i32, _vp, _vp, _i64, _vp]),
+    "gnn_cover_fill": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _i32, _i32, _vp,
+                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                      _vp, _vp, _vp, _vp]),
+    "gnn_cover_send_workspace_bytes": (_i64, [_i64]),
+    "gnn_cover_send_partials": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _vp,
+                                               _vp, _vp, _vp, _i64, _vp]),
     "gnn_xcd_hub_plan_workspace_bytes": (_i64, [_i64, _i64]),
     "gnn_xcd_hub_plan_build": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
                                               _i64, _vp, _vp, _i64, _vp]),

@@ -297,6 +297,11 @@ def _global_sum(v: int, device, group=None) -> int:
     return int(t.item())
 
 
+# build the cover on the device through the C-ABI (csrc/cover_build.hip: gnn_cover_build /
+# _fill / _send_partials, the arrays of the torch restatement below; up to 64 ranks)
+NATIVE_COVER = True
+
+
 def build_cover_exchange(g: CsrGraph, rank: int, world: int, group=None,
                          bounds: torch.Tensor | None = None) -> CoverExchange:
     """Rank ``rank``'s block of the cover exchange (see ``CoverExchange``).
@@ -307,11 +312,58 @@ def build_cover_exchange(g: CsrGraph, rank: int, world: int, group=None,
     j has from p's rows", then tightened in two passes (an edge whose row is
     already shipped as a partial joins it; an edge whose column is already
     shipped drops its partial). The edges to be reduced remotely are handed to
-    their column owners once, here.
+    their column owners once, here. On the device the local choice and the
+    partial-sum CSR are built by the C-ABI (``NATIVE_COVER``), the handshake is
+    this module's collectives either way.
     """
     if bounds is None:
         bounds = nnz_balanced_bounds(g.rowptr, world)
     b = [int(v) for v in bounds.cpu().tolist()]
+    r0, r1 = b[rank], b[rank + 1]
+    n_own = r1 - r0
+    dev = g.device
+    i64 = torch.int64
+    native = NATIVE_COVER and g.rowptr.is_cuda and world <= 64
+    local = (_cover_local_native if native else _cover_local_torch)(g, rank, world, b)
+    interior, xcols, nx, (pe_src_i, pe_src_j, pe_src_v), np_, npe, halo_x, halo_p = local
+
+    # ---- one-time handshake -----------------------------------------------------------------
+    mine = torch.stack([nx, np_, npe], 1).contiguous()        # [world, 3] what I ask of each peer
+    theirs = torch.empty_like(mine)
+    _all_to_all_v(theirs.view(-1), mine.view(-1), [3] * world, [3] * world, group)
+    mine_l, theirs_l = mine.cpu().tolist(), theirs.cpu().tolist()
+    req_x = torch.empty(sum(t[0] for t in theirs_l), dtype=i64, device=dev)
+    _all_to_all_v(req_x, xcols.contiguous(), [t[0] for t in theirs_l], [m[0] for m in mine_l], group)
+    spl_out, spl_in = [t[2] for t in theirs_l], [m[2] for m in mine_l]
+    n_pe_in = sum(spl_out)
+    pe_i = torch.empty(n_pe_in, dtype=i64, device=dev)
+    pe_j = torch.empty(n_pe_in, dtype=i64, device=dev)
+    pe_v = torch.empty(n_pe_in, dtype=g.val.dtype, device=dev)
+    _all_to_all_v(pe_i, pe_src_i.contiguous(), spl_out, spl_in, group)
+    _all_to_all_v(pe_j, pe_src_j.contiguous(), spl_out, spl_in, group)
+    _all_to_all_v(pe_v, pe_src_v.contiguous(), spl_out, spl_in, group)
+
+    # ---- what this rank computes / copies for its peers ------------------------------------
+    n_p_send = sum(t[1] for t in theirs_l)
+    if native:
+        send_p = _cover_send_partials_native(pe_i, pe_j, pe_v, spl_out, world, r0, n_own, n_p_send)
+    else:
+        peer_e = torch.repeat_interleave(torch.arange(world, device=dev, dtype=i64),
+                                         torch.tensor(spl_out, dtype=i64, device=dev))
+        _, p_slot = torch.unique_consecutive(peer_e * b[-1] + pe_i, return_inverse=True)
+        send_p = from_coo(p_slot.view(-1), pe_j - r0, pe_v, n_p_send, n_own)
+    any_x = _global_sum(int(xcols.numel()), dev, group) > 0
+    any_p = _global_sum(int(halo_p.n_cols), dev, group) > 0
+    return CoverExchange(rank, world, b, interior, (req_x - r0).contiguous(), send_p, halo_x,
+                         halo_p, [t[0] for t in theirs_l], [t[1] for t in theirs_l],
+                         [int(v) for v in nx.cpu().tolist()], [int(v) for v in np_.cpu().tolist()],
+                         any_x, any_p)
+
+
+def _cover_local_torch(g: CsrGraph, rank: int, world: int, b: list):
+    """The local half of ``build_cover_exchange`` in torch ops: (interior, requested columns,
+    feature rows asked of each peer, the partial edges (global row, global column, value) in
+    (owner, row) order, partial rows / partial edges asked of each peer, halo_x, halo_p)."""
     r0, r1 = b[rank], b[rank + 1]
     n_own = r1 - r0
     dev = g.device
@@ -353,41 +405,79 @@ def build_cover_exchange(g: CsrGraph, rank: int, world: int, group=None,
     np_ = torch.bincount(pkeys // stride, minlength=world).to(i64)
     npe = torch.bincount(pq, minlength=world).to(i64)
 
-    # ---- one-time handshake -----------------------------------------------------------------
-    mine = torch.stack([nx, np_, npe], 1).contiguous()        # [world, 3] what I ask of each peer
-    theirs = torch.empty_like(mine)
-    _all_to_all_v(theirs.view(-1), mine.view(-1), [3] * world, [3] * world, group)
-    mine_l, theirs_l = mine.cpu().tolist(), theirs.cpu().tolist()
-    req_x = torch.empty(sum(t[0] for t in theirs_l), dtype=i64, device=dev)
-    _all_to_all_v(req_x, xcols.contiguous(), [t[0] for t in theirs_l], [m[0] for m in mine_l], group)
-    spl_out, spl_in = [t[2] for t in theirs_l], [m[2] for m in mine_l]
-    n_pe_in = sum(spl_out)
-    pe_i = torch.empty(n_pe_in, dtype=i64, device=dev)
-    pe_j = torch.empty(n_pe_in, dtype=i64, device=dev)
-    pe_v = torch.empty(n_pe_in, dtype=val.dtype, device=dev)
-    _all_to_all_v(pe_i, (pr + r0).contiguous(), spl_out, spl_in, group)
-    _all_to_all_v(pe_j, pc.contiguous(), spl_out, spl_in, group)
-    _all_to_all_v(pe_v, pv.contiguous(), spl_out, spl_in, group)
-
-    # ---- what this rank computes / copies for its peers ------------------------------------
-    peer_e = torch.repeat_interleave(torch.arange(world, device=dev, dtype=i64),
-                                     torch.tensor(spl_out, dtype=i64, device=dev))
-    _, p_slot = torch.unique_consecutive(peer_e * b[-1] + pe_i, return_inverse=True)
-    n_p_send = sum(t[1] for t in theirs_l)
-    send_p = from_coo(p_slot.view(-1), pe_j - r0, pe_v, n_p_send, n_own)
-
     # ---- how this rank folds in what it receives ------------------------------------------
     halo_x = from_coo(xr, torch.searchsorted(xcols, xc), xv, n_own, int(xcols.numel()))
     ki = pkeys - (pkeys // stride) * stride
     halo_p = from_coo(ki, torch.arange(pkeys.numel(), device=dev, dtype=i64),
                       torch.ones(pkeys.numel(), dtype=val.dtype, device=dev), n_own,
                       int(pkeys.numel()))
-    any_x = _global_sum(int(xcols.numel()), dev, group) > 0
-    any_p = _global_sum(int(pkeys.numel()), dev, group) > 0
-    return CoverExchange(rank, world, b, interior, (req_x - r0).contiguous(), send_p, halo_x,
-                         halo_p, [t[0] for t in theirs_l], [t[1] for t in theirs_l],
-                         [int(v) for v in nx.cpu().tolist()], [int(v) for v in np_.cpu().tolist()],
-                         any_x, any_p)
+    return interior, xcols, nx, (pr + r0, pc, pv), np_, npe, halo_x, halo_p
+
+
+def _cover_local_native(g: CsrGraph, rank: int, world: int, b: list):
+    """``_cover_local_torch`` by gnn_cover_build / gnn_cover_fill (the same tensors)."""
+    import ctypes
+    from . import _lib
+    lib = _lib.load()
+    dev = g.device
+    r0, r1 = b[rank], b[rank + 1]
+    n_own = r1 - r0
+    e_loc = int(g.rowptr[r1]) - int(g.rowptr[r0])
+    stream = _lib.stream_handle(dev)
+    hb = (ctypes.c_int64 * (world + 1))(*b)
+    ws = torch.empty(int(lib.gnn_cover_workspace_bytes(g.n_rows, e_loc, n_own, world)),
+                     dtype=torch.uint8, device=dev)
+    counts = (ctypes.c_int64 * (4 + 3 * world))()
+    _lib.check(lib.gnn_cover_build(g.rowptr.data_ptr(), _lib.ptr(g.col), g.n_rows,
+                                   ctypes.addressof(hb), rank, world, ctypes.addressof(counts),
+                                   ws.data_ptr(), ws.numel(), stream), "gnn_cover_build")
+    c = [int(v) for v in counts]
+    n_int, n_x, n_hx, n_pk = c[:4]
+    nx = torch.tensor(c[4:4 + world], dtype=torch.int64, device=dev)
+    np_ = torch.tensor(c[4 + world:4 + 2 * world], dtype=torch.int64, device=dev)
+    npe = torch.tensor(c[4 + 2 * world:4 + 3 * world], dtype=torch.int64, device=dev)
+    n_pe = sum(c[4 + 2 * world:])
+    i64, i32, f32 = (dict(dtype=t, device=dev) for t in (torch.int64, torch.int32, torch.float32))
+    int_rp, int_col, int_val = (torch.empty(n_own + 1, **i64), torch.empty(n_int, **i32),
+                                torch.empty(n_int, **f32))
+    xcols = torch.empty(n_x, **i64)
+    hx_rp, hx_col, hx_val = (torch.empty(n_own + 1, **i64), torch.empty(n_hx, **i32),
+                             torch.empty(n_hx, **f32))
+    pe_i, pe_j, pe_v = torch.empty(n_pe, **i64), torch.empty(n_pe, **i64), torch.empty(n_pe, **f32)
+    hp_rp, hp_col, hp_val = (torch.empty(n_own + 1, **i64), torch.empty(n_pk, **i32),
+                             torch.empty(n_pk, **f32))
+    P = _lib.ptr
+    _lib.check(lib.gnn_cover_fill(ws.data_ptr(), g.rowptr.data_ptr(), P(g.col), P(g.val), g.n_rows,
+                                  ctypes.addressof(hb), rank, world, ctypes.addressof(counts),
+                                  int_rp.data_ptr(), P(int_col), P(int_val), P(xcols),
+                                  hx_rp.data_ptr(), P(hx_col), P(hx_val), P(pe_i), P(pe_j),
+                                  P(pe_v), hp_rp.data_ptr(), P(hp_col), P(hp_val), stream),
+               "gnn_cover_fill")
+    interior = CsrGraph(int_rp, int_col, int_val, n_own, n_own)
+    halo_x = CsrGraph(hx_rp, hx_col, hx_val, n_own, n_x)
+    halo_p = CsrGraph(hp_rp, hp_col, hp_val, n_own, n_pk)
+    return interior, xcols, nx, (pe_i, pe_j, pe_v), np_, npe, halo_x, halo_p
+
+
+def _cover_send_partials_native(pe_i, pe_j, pe_v, recv_edges: list, world: int, r0: int,
+                                n_own: int, n_p_send: int) -> CsrGraph:
+    """The partial-sum CSR this rank computes for its peers (gnn_cover_send_partials)."""
+    import ctypes
+    from . import _lib
+    lib = _lib.load()
+    dev = pe_i.device
+    m = int(sum(recv_edges))
+    ws = torch.empty(int(lib.gnn_cover_send_workspace_bytes(m)), dtype=torch.uint8, device=dev)
+    he = (ctypes.c_int64 * world)(*[int(v) for v in recv_edges])
+    rp = torch.empty(n_p_send + 1, dtype=torch.int64, device=dev)
+    col = torch.empty(m, dtype=torch.int32, device=dev)
+    val = torch.empty(m, dtype=torch.float32, device=dev)
+    P = _lib.ptr
+    _lib.check(lib.gnn_cover_send_partials(P(pe_i), P(pe_j), P(pe_v), ctypes.addressof(he), world,
+                                           r0, n_own, n_p_send, rp.data_ptr(), P(col), P(val),
+                                           ws.data_ptr(), ws.numel(), _lib.stream_handle(dev)),
+               "gnn_cover_send_partials")
+    return CsrGraph(rp, col, val, n_p_send, n_own)
 
 
 def _all_gather_floats(v: list, world: int, device, group=None) -> torch.Tensor:

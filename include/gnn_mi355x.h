@@ -9,7 +9,7 @@
  *     preallocated by the caller;
  *   - never synchronises the host, except the once-per-graph builders that size their
  *     outputs (gnn_gcn_adjacency_build, gnn_spmm_tasks_build, gnn_column_order,
- *     gnn_xcd_hub_plan_build), which say so;
+ *     gnn_xcd_hub_plan_build, gnn_cover_*), which say so;
  *   - enqueues its kernels on `stream` and returns 0 on success, a positive
  *     hipError_t on a launch/runtime failure, or a negative GNN_E_* code when an
  *     argument is rejected before anything is launched. It never throws.
@@ -231,6 +231,47 @@ int gnn_xcd_hub_plan_fill(const void* workspace, const int64_t* rowptr, const in
                           const int64_t* counts, int64_t* items_rowptr, int32_t* items_col,
                           float* items_val, int64_t* pos_row, int64_t* rest_rowptr,
                           int32_t* rest_col, float* rest_val, void* stream);
+
+/*
+ * Edge-cut cover exchange of the N-rank SpMM (distributed.build_cover_exchange; csrc/
+ * cover_build.hip), rank `rank` of `world` (<= 64), row blocks bounds[0..world] (host int64,
+ * bounds[0] = 0, bounds[world] = n_rows, non-decreasing). Rank p owns rows [b_p, b_{p+1}) of
+ * the CSR and of X; each cut edge (i, j) is covered by shipping X_j to p (a feature row) or by
+ * the owner q of j computing the partial row sum over its columns (a partial row), per the
+ * greedy rule documented there. New in this library (the reference is single-device); it
+ * shards GCN/GCN.py:43-45 across ranks with gnn_halo_alltoallv_f32 + the SpMM entries.
+ *   gnn_cover_build: counts (host int64 [4 + 3 world]) = interior nnz, requested feature rows,
+ *     halo_x nnz, partial rows received, then per peer q: feature rows asked of q, partial
+ *     rows asked of q, partial edges handed to q. Synchronises the stream.
+ *   gnn_cover_fill (same workspace and arguments + the counts): the interior CSR (local rows x
+ *     local columns), xcols (the requested global ids, ascending = grouped by owner), halo_x CSR
+ *     (local rows x positions in xcols), the partial edges (pe_i global row, pe_j global
+ *     column, pe_v value; grouped by owner q, then row, CSR order inside a row) and halo_p CSR
+ *     (local rows x partial-row index, values 1.0).
+ *   Handshake (the caller's collectives): all-to-all of the 3 per-peer counts, then
+ *     all-to-all-v of xcols (-> the rows this rank sends, minus b_p) and of pe_i / pe_j / pe_v.
+ *   gnn_cover_send_partials: from the received partial edges (recv_edges[q] from peer q, host),
+ *     the CSR of the partial rows this rank computes for its peers: n_p_send rows (the sum of
+ *     the partial rows peers asked of it; another total -> GNN_E_ARG) x local columns.
+ * workspaces: gnn_cover_workspace_bytes(n_rows, local nnz, b_{p+1} - b_p, world),
+ * gnn_cover_send_workspace_bytes(received partial edges) bytes of device memory.
+ */
+int64_t gnn_cover_workspace_bytes(int64_t n_rows, int64_t nnz_local, int64_t n_own, int32_t world);
+int gnn_cover_build(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                    const int64_t* bounds, int32_t rank, int32_t world, int64_t* counts,
+                    void* workspace, int64_t workspace_bytes, void* stream);
+int gnn_cover_fill(const void* workspace, const int64_t* rowptr, const int32_t* col,
+                   const float* val, int64_t n_rows, const int64_t* bounds, int32_t rank,
+                   int32_t world, const int64_t* counts, int64_t* int_rowptr, int32_t* int_col,
+                   float* int_val, int64_t* xcols, int64_t* hx_rowptr, int32_t* hx_col,
+                   float* hx_val, int64_t* pe_i, int64_t* pe_j, float* pe_v, int64_t* hp_rowptr,
+                   int32_t* hp_col, float* hp_val, void* stream);
+int64_t gnn_cover_send_workspace_bytes(int64_t n_edges);
+int gnn_cover_send_partials(const int64_t* pe_i, const int64_t* pe_j, const float* pe_v,
+                            const int64_t* recv_edges, int32_t world, int64_t r0, int64_t n_own,
+                            int64_t n_p_send, int64_t* sp_rowptr, int32_t* sp_col, float* sp_val,
+                            void* workspace, int64_t workspace_bytes, void* stream);
+
 
 /*
  * Row-class plan for gnn_spmm_csr_f32 / gnn_gat_csr_f32 (built once per graph).
