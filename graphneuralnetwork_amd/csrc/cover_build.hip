@@ -76,6 +76,7 @@ struct CoverWs {
   int64_t* hp_cnt;   // [n_own + 1] partial rows per row (halo_p degrees)
   int64_t* qb;       // [2 W] first / end of each owner's partial edges in sorted order
   int64_t* cnt;      // [4] select counts
+  int32_t* err;      // [1] a column id outside [0, n_rows)
   void* temp;
   size_t temp_bytes;
   int64_t bytes;
@@ -152,6 +153,7 @@ static CoverWs cover_carve(void* ws, int64_t E, int64_t n, int64_t n_own, int wo
   w.hp_cnt = c.take<int64_t>(n_own + 1);
   w.qb = c.take<int64_t>(2 * kMaxWorld);
   w.cnt = c.take<int64_t>(4);
+  w.err = c.take<int32_t>(1);
   w.temp_bytes = cover_temp_bytes(E, n, P, n_own);
   w.temp = c.take<char>(static_cast<int64_t>(w.temp_bytes));
   w.bytes = c.used;
@@ -162,7 +164,8 @@ static CoverWs cover_carve(void* ws, int64_t E, int64_t n, int64_t n_own, int wo
 __global__ void cover_count_kernel(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                    int64_t r0, int64_t n_own, int64_t e0, int64_t E, Bounds B,
                                    int32_t* __restrict__ e_row, uint8_t* __restrict__ e_cls,
-                                   int32_t* __restrict__ cnt_pair, int32_t* __restrict__ cnt_col) {
+                                   int32_t* __restrict__ cnt_pair, int32_t* __restrict__ cnt_col,
+                                   int32_t* __restrict__ err) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= E) return;
   const int64_t e = e0 + t;
@@ -173,6 +176,11 @@ __global__ void cover_count_kernel(const int64_t* __restrict__ rp, const int32_t
   }
   e_row[t] = static_cast<int32_t>(lo);
   const int64_t c = col[e];
+  if (c < 0 || c >= B.b[B.world]) {  // counted as interior so no later pass indexes with it
+    atomicOr(err, 1);
+    e_cls[t] = kInterior;
+    return;
+  }
   if (c >= r0 && c < r0 + n_own) {
     e_cls[t] = kInterior;
     return;
@@ -413,9 +421,14 @@ extern "C" int gnn_cover_build(const int64_t* rowptr, const int32_t* col, int64_
   CB_TRY(hipMemsetAsync(w.hx, 0, static_cast<size_t>(n_rows), s));
   CB_TRY(hipMemsetAsync(w.qb, 0, 2 * kMaxWorld * 8, s));
   CB_TRY(hipMemsetAsync(w.cnt, 0, 4 * 8, s));
+  CB_TRY(hipMemsetAsync(w.err, 0, 4, s));
   if (E > 0) {
     hipLaunchKernelGGL(cover_count_kernel, dim3(grid(E)), dim3(kT), 0, s, rowptr, col, r0, n_own, e0,
-                       E, B, w.e_row, w.e_cls, w.cnt_pair, w.cnt_col);
+                       E, B, w.e_row, w.e_cls, w.cnt_pair, w.cnt_col, w.err);
+    int32_t herr = 0;
+    CB_TRY(hipMemcpyAsync(&herr, w.err, 4, hipMemcpyDeviceToHost, s));
+    CB_TRY(hipStreamSynchronize(s));
+    if (herr) return GNN_E_ARG;  // a column id outside [0, n_rows)
     hipLaunchKernelGGL(cover_rule_kernel, dim3(grid(E)), dim3(kT), 0, s, col, e0, E, n_own, B, w.e_row,
                        w.e_cls, w.cnt_pair, w.cnt_col, w.hp);
     hipLaunchKernelGGL(cover_cols_kernel, dim3(grid(E)), dim3(kT), 0, s, col, e0, E, n_own, B, w.e_row,

@@ -242,7 +242,8 @@ int gnn_xcd_hub_plan_fill(const void* workspace, const int64_t* rowptr, const in
  * shards GCN/GCN.py:43-45 across ranks with gnn_halo_alltoallv_f32 + the SpMM entries.
  *   gnn_cover_build: counts (host int64 [4 + 3 world]) = interior nnz, requested feature rows,
  *     halo_x nnz, partial rows received, then per peer q: feature rows asked of q, partial
- *     rows asked of q, partial edges handed to q. Synchronises the stream.
+ *     rows asked of q, partial edges handed to q. Synchronises the stream. A column id
+ *     outside [0, n_rows) in this rank's rows -> GNN_E_ARG.
  *   gnn_cover_fill (same workspace and arguments + the counts): the interior CSR (local rows x
  *     local columns), xcols (the requested global ids, ascending = grouped by owner), halo_x CSR
  *     (local rows x positions in xcols), the partial edges (pe_i global row, pe_j global

@@ -121,6 +121,12 @@ def test_cover_capi_rejects_bad_bounds(dev):
     hb = (ctypes.c_int64 * 3)(0, 50, 100)
     assert lib.gnn_cover_build(g.rowptr.data_ptr(), g.col.data_ptr(), 100, ctypes.addressof(hb), 2,
                                2, ctypes.addressof(counts), ws.data_ptr(), ws.numel(), s) == -1
+    # a column id outside [0, n_rows) in this rank's rows
+    bad_col = g.col.clone()
+    bad_col[int(g.rowptr[60])] = 100
+    hb = (ctypes.c_int64 * 3)(0, 50, 100)
+    assert lib.gnn_cover_build(g.rowptr.data_ptr(), bad_col.data_ptr(), 100, ctypes.addressof(hb),
+                               1, 2, ctypes.addressof(counts), ws.data_ptr(), ws.numel(), s) == -1
     # the handshake's partial-row total must match the received edges' slots
     pe_i = torch.tensor([3, 3, 4], dtype=torch.int64, device=dev)
     pe_j = torch.tensor([0, 1, 1], dtype=torch.int64, device=dev)
