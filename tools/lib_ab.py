@@ -79,6 +79,8 @@ def main():
                     help="--build: csrc files compiled with the variant's defines (the rest "
                          "link from the main build)")
     ap.add_argument("--seg-lens", default="", help="also time the default build at these seg_len")
+    ap.add_argument("--ordered", action="store_true",
+                    help="time the column-ordered graph A P^T, as bench.py does")
     ap.add_argument("--op", default="spmm", choices=["spmm", "sage"],
                     help="sage: the fused gather-mean over [M=62,401, k=10] uniform-degree-weighted "
                          "samples of the workload's graph (the cfg4 layer-0 shape)")
@@ -99,6 +101,10 @@ def main():
     s, d = rmat_edges(n, e, 0)
     g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n, device=dev)
     F = args.feat
+    if args.ordered:
+        from graphneuralnetwork_amd.ops import column_order
+        o = column_order(g, F)
+        g = g if o is None else o.graph
     X = torch.randn(n, F, device=dev)
     Y = torch.empty(n, F, device=dev)
     nbytes = g.nnz * (8 + 4 * F) + n * (8 + 4 * F)
