@@ -105,7 +105,33 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
         os.replace(tmp, LIB_PATH)
+    build_examples(force)
     return LIB_PATH
+
+
+EXAMPLES_DIR = REPO_DIR / "examples"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+
+
+def build_examples(force: bool = False) -> list[Path]:
+    """The plain-C callers under examples/ (gcc, linked against the library and the HIP
+    runtime only), next to the library in lib/: the C-ABI exercised without Python."""
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        raise RuntimeError("no C compiler for examples/")
+    outs = []
+    for src in sorted(EXAMPLES_DIR.glob("*.c")):
+        out = LIB_DIR / src.stem
+        if force or _stale(out, [src, HEADER, LIB_PATH]):
+            cmd = [cc, "-O2", "-std=c11", "-Wall", "-D__HIP_PLATFORM_AMD__",
+                   f"-I{ROCM / 'include'}", str(src), "-o", str(out), f"-L{LIB_DIR}",
+                   "-lgnn_mi355x", f"-L{ROCM / 'lib'}", "-lamdhip64", "-Wl,-rpath,$ORIGIN",
+                   f"-Wl,-rpath,{ROCM / 'lib'}"]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"{src.name} failed:\n" + r.stdout + r.stderr)
+        outs.append(out)
+    return outs
 
 
 def build_variant(tag: str, defines: list[str], only: list[str] | None = None) -> Path:
