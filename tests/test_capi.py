@@ -99,3 +99,15 @@ def test_halo_exchange_entry_without_gpu(lib):
     buf = ctypes.create_string_buffer(4096)
     assert lib.gnn_halo_rccl_path(buf, 4096) == 0, "ncclAllToAllv not resolvable"
     assert "rccl" in buf.value.decode()
+
+
+def test_c_program_links_and_checks_usage():
+    """examples/capi_gcn_spmm.c is built next to the library (build.py) from the header alone and
+    loads here (no GPU): the usage check runs before any HIP call."""
+    import subprocess
+    from graphneuralnetwork_amd import build as B
+    exe = B.LIB_DIR / "capi_gcn_spmm"
+    if not exe.exists():
+        B.build()
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
