@@ -153,24 +153,52 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
   // before its MFMAs, so the HBM latency (several microseconds under load) is covered by
   // DEPTH tiles of MFMA work, not one
   constexpr int DEPTH = K >= 128 ? 1 : GNN_PROJ_DEPTH;  // K >= 128: 64+ VGPRs per tile
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   float4 pre[DEPTH][NV];
+  // COLROW: the column-order ids of a tile's output rows travel with its X loads (requested a
+  // tile ahead, like them): a plain load of them after the MFMAs is where the compiler would
+  // put it, and its wait would also wait for the refill issued before -- the next tile's whole
+  // latency, once per tile
+  int64_t cidx[DEPTH][G];
+  auto fetch_ids = [&](int64_t (&dst)[G], int64_t g) {
+    if constexpr (COLROW) {
+      const int64_t r0 = (g * kProjWaves + wave) * 16 * G;
+      const int64_t live =
+          (g < n_groups && r0 < n_rows) ? (n_rows - r0 < 16 * G ? n_rows - r0 : 16 * G) : 0;
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<int64_t*>(col_row + (live > 0 ? r0 : 0)), 0, static_cast<int>(live * 8),
+          0x00020000);
+#pragma unroll
+      for (int j = 0; j < G; ++j)
+        dst[j] = __builtin_bit_cast(int64_t,
+                                    __builtin_amdgcn_raw_buffer_load_b64(rsrc, (16 * j + r) * 8, 0, 0));
+    }
+  };
+  // The wave's tile rows through a buffer descriptor: the range check returns 0 past the last
+  // row, so the loads carry no per-lane branch (under one, the compiler cannot count them and
+  // waits for all outstanding loads -- the prefetch -- before the MFMAs; transform.hip).
   auto fetch = [&](float4 (&dst)[NV], int64_t g) {
-    const int64_t r0 = (g * kProjWaves + (threadIdx.x >> 6)) * 16 * G;
+    const int64_t r0 = (g * kProjWaves + wave) * 16 * G;
+    const int64_t live =
+        (g < n_groups && r0 < n_rows) ? (n_rows - r0 < 16 * G ? n_rows - r0 : 16 * G) : 0;
+    const float* base = x + (live > 0 ? r0 : 0) * ldx;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base), 0, static_cast<int>(live * ldx * 4), 0x00020000);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = v * kWave + lane;
       const int rr = e / (K / 4), c4 = e - rr * (K / 4);
-      dst[v] = (e < V4 && g < n_groups && r0 + rr < n_rows)
-                   ? *reinterpret_cast<const float4*>(x + (r0 + rr) * ldx + 4 * c4)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int off = e < V4 ? (rr * static_cast<int>(ldx) + 4 * c4) * 4 : 0x7ffffff0;
+      dst[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
     }
   };
-  auto tile = [&](int64_t g, float4 (&src)[NV]) {
+  constexpr bool kFullTile = NV * kWave == V4;
+  auto tile = [&](int64_t g, float4 (&src)[NV], int64_t (&ids)[G]) {
     const int64_t row0 = (g * kProjWaves + (threadIdx.x >> 6)) * 16 * G;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = v * kWave + lane;
-      if (e < V4) {
+      if (kFullTile || e < V4) {
         const int rr = e / (K / 4), c4 = e - rr * (K / 4);
         if constexpr (X6) {
           const float tv[4] = {src[v].x, src[v].y, src[v].z, src[v].w};
@@ -194,7 +222,12 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
       }
     }
     proj_tile_sync();
+    int64_t crow_pre[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) crow_pre[j] = COLROW ? ids[j] : row0 + 16 * j + r;
     fetch(src, g + DEPTH * static_cast<int64_t>(gridDim.x));  // refill this slot
+    fetch_ids(ids, g + DEPTH * static_cast<int64_t>(gridDim.x));
+    __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk to the next tile's staging
     float a[X6 ? 1 : G][X6 ? 1 : S];
     if constexpr (!X6)
 #pragma unroll
@@ -280,18 +313,19 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const int64_t orow = row0 + 16 * j + r;
+      // col_row: Wh and er are the column side of the aggregation -- rows in the column
+      // order of a degree-ordered graph; el (the row side) stays in place (a template flag:
+      // the index load and range check cost 10 % of the in-order launch when compiled in,
+      // profiles/r03i_proj_colrow_ab.log). Resolved outside the row guard below, so the
+      // compiler keeps the index load where it was issued, ahead of the MFMAs.
+      int64_t crow = orow;
+      bool cok = true;
+      if constexpr (COLROW) {
+        crow = crow_pre[j];
+        cok = crow >= 0 && crow < n_rows;  // an id out of range is not stored
+        crow = cok ? crow : 0;
+      }
       if (orow < n_rows) {
-        // col_row: Wh and er are the column side of the aggregation -- rows in the
-        // column order of a degree-ordered graph; el (the row side) stays in place
-        // (a template flag: the index load and range check cost 10 % of the in-order
-        // launch when compiled in, profiles/r03i_proj_colrow_ab.log)
-        int64_t crow = orow;
-        bool cok = true;
-        if constexpr (COLROW) {
-          crow = col_row[orow];
-          cok = crow >= 0 && crow < n_rows;  // an id out of range is not stored
-          crow = cok ? crow : 0;
-        }
 #ifndef GNN_PROJ_NO_WH
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -320,12 +354,15 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
     proj_tile_sync();  // the next group overwrites the A tile
   };
 #pragma unroll
-  for (int d = 0; d < DEPTH; ++d) fetch(pre[d], blockIdx.x + d * static_cast<int64_t>(gridDim.x));
+  for (int d = 0; d < DEPTH; ++d) {
+    fetch(pre[d], blockIdx.x + d * static_cast<int64_t>(gridDim.x));
+    fetch_ids(cidx[d], blockIdx.x + d * static_cast<int64_t>(gridDim.x));
+  }
   for (int64_t g = blockIdx.x; g < n_groups; g += DEPTH * static_cast<int64_t>(gridDim.x)) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {  // uniform over the block
       const int64_t gg = g + d * static_cast<int64_t>(gridDim.x);
-      if (gg < n_groups) tile(gg, pre[d]);
+      if (gg < n_groups) tile(gg, pre[d], cidx[d]);
     }
   }
 }

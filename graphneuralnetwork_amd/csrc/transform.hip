@@ -15,6 +15,8 @@
 // columns of one Y row (16-B stores), and the K axis is permuted so that lane quarter q
 // owns k in [q*S, q*S + S): its X values are one contiguous run of an LDS row (float4
 // reads, rows padded by 4 floats so the 16 rows of a read hit distinct banks).
+#include <type_traits>
+
 #include "common.hpp"
 
 extern "C" int gnn_gcn_transform_supported(int64_t k, int64_t fout);
@@ -53,6 +55,9 @@ using tf32x4 = __attribute__((ext_vector_type(4))) float;
 #endif
 #ifndef GNN_TF_ONE256
 #define GNN_TF_ONE256 1  // 0 = A/B: 256 output columns at K >= 128 as two 128-column launches
+#endif
+#ifndef GNN_TF_PREFETCH
+#define GNN_TF_PREFETCH 1  // X tiles in flight in registers ahead of the one being multiplied
 #endif
 
 // NW waves per workgroup, each owning CB 16-column blocks of W (FO = NW * CB * 16); a tile is
@@ -140,26 +145,39 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
   }
 
   const int64_t n_tiles = (n_rows + TR - 1) / TR;
-  float4 pre[NV];
-  auto fetch = [&](int64_t g) {
+  // PF tiles in flight in registers: tile it + PF is requested while tile it is multiplied
+  // (slot it % PF; the loop is unrolled by PF so every slot index is a constant)
+  constexpr int PF = GNN_TF_PREFETCH;
+  static_assert(PF >= 1 && PF <= 4 && (PF == 1 || NBUF == 2), "prefetch depth 1..4");
+  float4 pre[PF][NV];
+  // Tile loads through a buffer descriptor of the tile's rows: the hardware range check
+  // returns 0 for rows past the end (and for a tile past the last), so the loads need no
+  // per-lane branch. Under such a branch the compiler cannot count the outstanding loads at
+  // the join and waits for all of them (s_waitcnt vmcnt(0)), which exposed the next tile's
+  // whole load latency instead of hiding it under this tile's MFMAs.
+  auto fetch = [&](float4 (&p)[NV], int64_t g) {
     const int64_t r0 = g * TR;
+    const int64_t live = g < n_tiles ? (n_rows - r0 < TR ? n_rows - r0 : TR) : 0;
+    const float* base = x + (live > 0 ? r0 : 0) * ldx;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base), 0, static_cast<int>(live * ldx * 4), 0x00020000);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = v * kTfBlock + static_cast<int>(threadIdx.x);
       const int rr = e / (K / 4), c4 = e - rr * (K / 4);
-      pre[v] = (e < V4 && g < n_tiles && r0 + rr < n_rows)
-                   ? *reinterpret_cast<const float4*>(x + (r0 + rr) * ldx + 4 * c4)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int off = e < V4 ? (rr * static_cast<int>(ldx) + 4 * c4) * 4 : 0x7ffffff0;
+      p[v] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
     }
   };
-  auto stage = [&](float* buf) {
+  constexpr bool kFullTile = NV * kTfBlock == V4;  // every thread stages NV float4s
+  auto stage = [&](float* buf, const float4 (&p)[NV]) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = v * kTfBlock + static_cast<int>(threadIdx.x);
-      if (e < V4) {
+      if (kFullTile || e < V4) {
         const int rr = e / (K / 4), c4 = e - rr * (K / 4);
         if constexpr (X6) {  // 4 floats -> 4 bf16 of each plane (8 B), chunk c4 / 2 swizzled
-          const float tv[4] = {pre[v].x, pre[v].y, pre[v].z, pre[v].w};
+          const float tv[4] = {p[v].x, p[v].y, p[v].z, p[v].w};
           bf16x4 p0, p1, p2;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -175,33 +193,42 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
           *reinterpret_cast<bf16x4*>(base + PLANE) = p1;
           *reinterpret_cast<bf16x4*>(base + 2 * PLANE) = p2;
         } else {
-          *reinterpret_cast<float4*>(buf + rr * LDA + 4 * (c4 ^ TileLds<K>::swz(rr))) = pre[v];
+          *reinterpret_cast<float4*>(buf + rr * LDA + 4 * (c4 ^ TileLds<K>::swz(rr))) = p[v];
         }
       }
     }
   };
-  fetch(blockIdx.x);
+  fetch(pre[0], blockIdx.x);
   if (NBUF == 2) {
-    stage(xt[0]);
+    stage(xt[0], pre[0]);
     __syncthreads();
   }
+#pragma unroll
+  for (int f = 1; f < PF; ++f) fetch(pre[f], blockIdx.x + static_cast<int64_t>(f) * gridDim.x);
   int it = 0;
-  for (int64_t g = blockIdx.x; g < n_tiles; g += gridDim.x, ++it) {  // uniform over the block
+  auto body = [&](auto slot, int64_t g) {  // one tile; uniform over the block
+    constexpr int SL = decltype(slot)::value;  // this tile's register slot (already staged)
+    constexpr int SN = (SL + 1) % PF;          // the next tile's
     const float* cur = xt[NBUF == 2 ? (it & 1) : 0];
     if (NBUF == 1) {
-      stage(xt[0]);
+      stage(xt[0], pre[0]);
       __syncthreads();
     }
-    fetch(g + gridDim.x);  // the next tile, in flight during this tile's MFMAs
     const int64_t row0 = g * TR;
-    int64_t dst[TR / 16];  // output rows of this lane's rows (loaded before the MFMAs)
+    // output rows of this lane's rows, requested first: the epilogue's wait for them then does
+    // not also wait for the prefetch issued after them (the counter retires in order)
+    int64_t dst[TR / 16];
 #pragma unroll
     for (int j = 0; j < TR / 16; ++j) {
       const int64_t orow = row0 + j * 16 + r;
       dst[j] = orow;
-      if constexpr (SCATTER)
-        if (orow < n_rows) dst[j] = y_row[orow];
+      if constexpr (SCATTER) dst[j] = y_row[orow < n_rows ? orow : n_rows - 1];
     }
+    // tile it + PF into the slot this tile left, in flight during the next PF tiles' MFMAs
+    fetch(pre[SL], g + static_cast<int64_t>(PF) * gridDim.x);
+    // keep the loads here: left to itself the scheduler sinks them to their use in stage(),
+    // after the MFMAs, and the tile waits for its own prefetch
+    __builtin_amdgcn_sched_barrier(0);
     tf32x4 acc[TR / 16][CB];
     if constexpr (X6) {
 #pragma unroll
@@ -282,7 +309,8 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
     }
     // the next tile goes to the other buffer while the last MFMAs drain (nobody reads it:
     // the barrier that ended the previous tile saw every wave's reads of it complete)
-    if (NBUF == 2) stage(xt[(it + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);  // ... and the staging (which waits for them) after the MFMAs
+    if (NBUF == 2) stage(xt[(it + 1) & 1], pre[SN]);
 #pragma unroll
     for (int j = 0; j < TR / 16; ++j) {
       // acc[j][cb][i] = Y[row0 + 16 j + r][(wv*CB + cb)*16 + 4q + i]
@@ -341,6 +369,29 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
           cls.logits[(row0 + rr) * cls.ldl + c] = v;
         }
       }
+    }
+  };
+  for (int64_t g = blockIdx.x; g < n_tiles;) {  // unrolled by PF: constant slot indices
+    body(std::integral_constant<int, 0>{}, g);
+    g += gridDim.x;
+    ++it;
+    if constexpr (PF > 1) {
+      if (g >= n_tiles) break;
+      body(std::integral_constant<int, 1 % PF>{}, g);
+      g += gridDim.x;
+      ++it;
+    }
+    if constexpr (PF > 2) {
+      if (g >= n_tiles) break;
+      body(std::integral_constant<int, 2 % PF>{}, g);
+      g += gridDim.x;
+      ++it;
+    }
+    if constexpr (PF > 3) {
+      if (g >= n_tiles) break;
+      body(std::integral_constant<int, 3 % PF>{}, g);
+      g += gridDim.x;
+      ++it;
     }
   }
 }

@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--variants", default=",".join(VARIANTS))
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--ordered", action="store_true",
+                    help="the column-ordered graph with Wh / er rows in that order, as bench.py")
     ap.add_argument("--short-degs", default="",
                     help="instead of library variants: time the default build with these "
                          "GAT_SHORT_MAX_DEG values (0 = short-row path off)")
@@ -72,6 +74,10 @@ def main():
     a_s = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
     a_d = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
     el, er = gat_logits(Wh, H, Fh, a_s, a_d)
+    if args.ordered:
+        from graphneuralnetwork_amd.ops import gat_column_order
+        o = gat_column_order(g, H, Fh)
+        g, Wh, er = o.graph, Wh[o.perm].contiguous(), er[o.perm].contiguous()
     out = torch.empty_like(Wh)
     from graphneuralnetwork_amd import ops as _ops
     _deg, _ops.GAT_SHORT_MAX_DEG = _ops.GAT_SHORT_MAX_DEG, 0

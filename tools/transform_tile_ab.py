@@ -16,7 +16,9 @@ VARIANTS = {"base": [], "tr32_1m": ["GNN_TF_TR32_ROWS=1000000"],
             "tr32": ["GNN_TF_TR32_ROWS=(1LL<<40)"],
             "tr16": ["GNN_TF_TR32_ROWS=(1LL<<40)", "GNN_TF_TR16_ROWS=(1LL<<40)"],
             "grid1024": ["GNN_TF_GRID=1024"],
-            "one256": ["GNN_TF_ONE256=1"], "cb2": ["GNN_TF_K256_CB2=1"]}
+            "one256": ["GNN_TF_ONE256=1"], "cb2": ["GNN_TF_K256_CB2=1"],
+            "pf2": ["GNN_TF_PREFETCH=2"], "pf3": ["GNN_TF_PREFETCH=3"],
+            "old": None}  # "old": lib/variants/libgnn_tf_old.so, built from another tree
 
 
 def main():
@@ -30,7 +32,8 @@ def main():
     if a.build:
         from graphneuralnetwork_amd.build import build_variant
         for n in names:
-            print(build_variant("tf_" + n, VARIANTS[n], only=["transform.hip"]))
+            if VARIANTS[n] is not None:
+                print(build_variant("tf_" + n, VARIANTS[n], only=["transform.hip"]))
         return
     import torch
     from graphneuralnetwork_amd import _lib
