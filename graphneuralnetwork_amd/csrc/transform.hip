@@ -467,8 +467,8 @@ static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const f
   // X6 at K = 256: 16-row tiles at every size (in one process, tools/transform_x6_ab.py,
   // profiles/r03x_transform_x6_ab.log: 62K / 200K x 256 -> 128 30.9 / 79.9 vs 32.9 / 89.7 us
   // with 32-row tiles; K = 128 keeps 32: 1M x 128 -> 128 205 vs 211 us)
-  if ((GNN_TF_MIN_TR <= 16 && n_rows < 32 * 2 * slots) ||
-      (K == 256 && g_tf_x6 && !(CB == 2 && K == 256)))
+  if (GNN_TF_MIN_TR <= 16 &&
+      (n_rows < 32 * 2 * slots || (K == 256 && g_tf_x6 && !(CB == 2 && K == 256))))
     return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
   if (GNN_TF_MIN_TR <= 32 && (K > GNN_TF_TR64_MAX_K || n_rows < 64 * 2 * slots))
     return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, s);

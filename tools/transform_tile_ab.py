@@ -18,6 +18,7 @@ VARIANTS = {"base": [], "tr32_1m": ["GNN_TF_TR32_ROWS=1000000"],
             "grid1024": ["GNN_TF_GRID=1024"],
             "one256": ["GNN_TF_ONE256=1"], "cb2": ["GNN_TF_K256_CB2=1"],
             "pf2": ["GNN_TF_PREFETCH=2"], "pf3": ["GNN_TF_PREFETCH=3"],
+            "mt32": ["GNN_TF_MIN_TR=32"], "mt32pf2": ["GNN_TF_MIN_TR=32", "GNN_TF_PREFETCH=2"],
             "old": None}  # "old": lib/variants/libgnn_tf_old.so, built from another tree
 
 
