@@ -260,6 +260,18 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
           const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(xp);
           const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(xp + PLANE);
           const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(xp + 2 * PLANE);
+#ifdef GNN_PROJ_NO_MFMA  // A/B only: the tile's LDS reads without its MFMAs
+#pragma unroll
+          for (int t = 0; t <= NT; ++t) {
+            const f32x4 c = f32x4{static_cast<float>(x0[t & 7]), static_cast<float>(x1[t & 7]),
+                                  static_cast<float>(x2[t & 7]), static_cast<float>(s6)};
+            if (t < NT)
+              acc[j][t] += c;
+            else
+              acc2[j] += c;
+          }
+          continue;
+#endif
 #pragma unroll
           for (int t = 0; t <= NT; ++t) {  // smallest terms first; t == NT: the logit tile
             f32x4 c = t < NT ? acc[j][t] : acc2[j];

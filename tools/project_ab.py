@@ -27,6 +27,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--inorder", action="store_true",
+                    help="gnn_gat_project_f32 (rows in place) instead of the column-order scatter")
     args = ap.parse_args()
     names = args.variants.split(",")
     if args.build:
@@ -58,6 +60,12 @@ def main():
         wh = torch.empty(n, H * fh, device=dev)
         el = torch.empty(n, H, device=dev)
         er = torch.empty(n, H, device=dev)
+        if args.inorder:
+            _lib.check(lib.gnn_gat_project_f32(
+                x.data_ptr(), k, n, k, w.data_ptr(), H * fh, s.data_ptr(), d.data_ptr(), H, fh,
+                wh.data_ptr(), H * fh, el.data_ptr(), er.data_ptr(), H, w2.data_ptr(),
+                _lib.stream_handle(dev)), "gnn_gat_project_f32")
+            return wh, el, er
         _lib.check(lib.gnn_gat_project_rows_f32(
             x.data_ptr(), k, n, k, w.data_ptr(), H * fh, s.data_ptr(), d.data_ptr(), H, fh,
             wh.data_ptr(), H * fh, el.data_ptr(), er.data_ptr(), H, inv.data_ptr(),
