@@ -15,6 +15,9 @@ sys.path.insert(0, str(ROOT))
 # Measured and not kept (profiles/r02x_gat_pipe2.log): a depth-2 chunk pipeline (chunk
 # k+1's er / Wh loads in flight while chunk k is reduced, two register buffers) -- 0.98 ms
 # against 0.80: 84 VGPRs (5 waves/SIMD) cost more than the deeper pipeline gains.
+# Also measured and not kept (round 4, profiles/r04gs_gat_short_rows_per_group_ab.log, --ordered):
+# gat_short_kernel with RPG = 2 / 3 / 4 rows per lane group, their chains issued together:
+# 0.809 / 0.837 / 0.883 ms against 0.783 at one row per group (RPG 2 + short chunk 8: 0.839).
 VARIANTS = {
     "j1u2": ["GNN_GAT_CHUNK=1", "GNN_GAT_U=2"],     # one pass per chunk (previous kernel)
     "c32u2": ["GNN_GAT_CHUNK=32", "GNN_GAT_U=2"],
