@@ -26,6 +26,14 @@ constexpr int kTaskRows = 63;  // spmm.hip kTaskRows
 constexpr int kXcds = 8;       // graph.XCDS: workgroup w runs on XCD w % 8
 constexpr int kWaves = 4;      // graph.SPMM_WAVES_PER_WG
 constexpr int64_t kMaxSlices = 1024;
+// Hub rank r belongs to slice (r / G) % S (graph.XCD_SLICE_GROUP): G = 4 consecutive ranks, 2 KiB
+// of X at F = 128, stay together. With G = 1 an XCD's hub rows sit 4 KiB apart and the step
+// is 2.8 % slower at cfg2 (tools/slice_group_ab.py, profiles/r04sg_slice_group_ab.log). G drops
+// to 1 when fewer than S * G ranks may form items.
+#ifndef GNN_XCD_SLICE_GROUP
+#define GNN_XCD_SLICE_GROUP 4
+#endif
+constexpr int64_t kSliceGroup = GNN_XCD_SLICE_GROUP;
 
 static inline unsigned grid(int64_t n) { return static_cast<unsigned>((n + kT - 1) / kT); }
 static inline int64_t up(int64_t v) { return (v + 255) / 256 * 256; }
@@ -234,7 +242,7 @@ static OrderWs order_carve(void* ws, int64_t n) {
 // ------------------------------------------------------------------------- XCD hub plan
 // State kept in the workspace from gnn_xcd_hub_plan_build to gnn_xcd_hub_plan_fill.
 // hdr: [0] selected edges, [1] groups, [2] items, [3] moved edges, [4] positions,
-//      [8 ..] phase bases (phases + 1)
+//      [5] slice group G (ranks r of slice (r / G) % S), [8 ..] phase bases (phases + 1)
 struct XcdWs {
   int64_t* hdr;
   int32_t* row_e;      // [E] row of each edge
@@ -343,13 +351,17 @@ __global__ void edge_row_kernel(const int64_t* __restrict__ rp, int64_t n, int64
   row_e[e] = static_cast<int32_t>(lo);
 }
 
+__global__ void xcd_group_kernel(int64_t* __restrict__ hdr, int64_t gsz) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) hdr[5] = gsz;
+}
+
 __global__ void xcd_keys_kernel(const int64_t* __restrict__ eid, const int64_t* __restrict__ hdr,
                                 const int32_t* __restrict__ col, const int32_t* __restrict__ row_e,
                                 int64_t S, uint64_t* __restrict__ key) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= hdr[0]) return;
   const int64_t e = eid[t];
-  const int64_t s = (-1 - static_cast<int64_t>(col[e])) % S;
+  const int64_t s = ((-1 - static_cast<int64_t>(col[e])) / hdr[5]) % S;
   key[t] = static_cast<uint64_t>(row_e[e]) * static_cast<uint64_t>(S) + static_cast<uint64_t>(s);
 }
 
@@ -464,7 +476,8 @@ __global__ void xcd_first_item_kernel(const int64_t* __restrict__ it_row, int64_
   if (i == 0 || it_row[i - 1] != it_row[i]) first_item[it_row[i]] = i;
 }
 
-__global__ void xcd_fill_items_kernel(PosMap pm, int64_t n_pos, const int64_t* __restrict__ irp,
+__global__ void xcd_fill_items_kernel(PosMap pm, const int64_t* __restrict__ hdr, int64_t n_pos,
+                                      const int64_t* __restrict__ irp,
                                       const int64_t* __restrict__ it_e0, const int32_t* __restrict__ it_cnt,
                                       const int64_t* __restrict__ it_row, const int64_t* __restrict__ eid1,
                                       const int32_t* __restrict__ col, const float* __restrict__ val,
@@ -484,7 +497,7 @@ __global__ void xcd_fill_items_kernel(PosMap pm, int64_t n_pos, const int64_t* _
     }
     pos_row[p] = it_row[it];
   } else {  // a pad: two zero-valued edges to a row of its own slice
-    const int64_t pc = -1 - (ph * kXcds + ((p - pm.base[ph]) / kWaves) % kXcds);
+    const int64_t pc = -1 - (ph * kXcds + ((p - pm.base[ph]) / kWaves) % kXcds) * hdr[5];
     icol[o] = static_cast<int32_t>(pc);
     icol[o + 1] = static_cast<int32_t>(pc);
     ival[o] = 0.f;
@@ -721,6 +734,8 @@ extern "C" int gnn_xcd_hub_plan_build(const int64_t* rowptr, const int32_t* col_
   hipStream_t s = static_cast<hipStream_t>(stream);
   XcdWs w = xcd_carve(workspace, nnz, n_rows);
   PB_TRY(hipMemsetAsync(w.hdr, 0, (16 + kMaxSlices) * sizeof(int64_t), s));
+  const int64_t gsz = kSliceGroup > 1 && ik >= S * kSliceGroup ? kSliceGroup : 1;
+  hipLaunchKernelGGL(xcd_group_kernel, dim3(1), dim3(64), 0, s, w.hdr, gsz);
   hipLaunchKernelGGL(edge_row_kernel, dim3(grid(nnz)), dim3(kT), 0, s, rowptr, n_rows, nnz, w.row_e);
   // 1. the hub edges that may form items, by (row, slice), CSR order kept inside a group
   size_t tb = w.temp_bytes;
@@ -813,7 +828,8 @@ extern "C" int gnn_xcd_hub_plan_fill(const void* workspace, const int64_t* rowpt
   const auto p_it = rocprim::make_transform_iterator(Count(0), PosCount{pm, w.it_cnt, n_pos});
   PB_TRY(rocprim::exclusive_scan(w.temp, tb, p_it, items_rowptr, int64_t(0),
                                  static_cast<size_t>(n_pos + 1), rocprim::plus<int64_t>(), s));
-  hipLaunchKernelGGL(xcd_fill_items_kernel, dim3(grid(n_pos)), dim3(kT), 0, s, pm, n_pos, items_rowptr,
+  hipLaunchKernelGGL(xcd_fill_items_kernel, dim3(grid(n_pos)), dim3(kT), 0, s, pm, w.hdr, n_pos,
+                     items_rowptr,
                      w.it_e0, w.it_cnt, w.it_row, w.eid1, col_hub, val, items_col, items_val, pos_row);
   tb = w.temp_bytes;
   const auto r_it = rocprim::make_transform_iterator(Count(0), RestCount{rowptr, w.row_delta, n_rows});

@@ -266,15 +266,18 @@ class HubPlan:
 # workgroup (spmm.hip kBlock = 256), one row per wave.
 XCDS = 8
 SPMM_WAVES_PER_WG = 4
+# hub ranks per slice group of the XCD-sliced plan (xcd_hub_coo); plan_build.hip's
+# GNN_XCD_SLICE_GROUP is the same constant for the device builder
+XCD_SLICE_GROUP = 4
 
 
 @dataclass
 class XcdHubPlan:
     """XCD-sliced hub staging (built once per graph, hub count and row threshold).
 
-    The staged hub ranks are dealt to the 8 XCDs (rank % 8). For every row of degree
-    >= ``min_deg``, the hub edges that fall in one slice form an *item* (chunked to at
-    most ``chunk`` edges). Pass 1 (``items``) reduces each item into one partial row;
+    The staged hub ranks are dealt to the 8 XCDs ((rank // XCD_SLICE_GROUP) % 8). For every
+    row of degree >= ``min_deg``, the hub edges that fall in one slice form an *item* (chunked
+    to at most ``chunk`` edges). Pass 1 (``items``) reduces each item into one partial row;
     its rows are laid out so that workgroup w holds only items of slice w % 8, so each
     XCD's L2 serves 1/8 of the hub table. Pass 2 (``rest``) is every row's remaining
     edges followed by one edge of value 1.0 per partial row of that row.
@@ -370,9 +373,12 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     Item edges keep their CSR order; rest rows list their unmoved edges in CSR order,
     then their partial refs in (slice, chunk) order.
 
-    ``phases`` > 1 deals the hub ranks to xcds * phases slices (rank % S); the items of
-    slice s run on XCD s % xcds in phase s // xcds, the phases one after another in the
-    launch order, so each XCD's L2 holds 1 / (xcds * phases) of the table at a time.
+    Hub rank r belongs to slice (r // G) % S, S = xcds * phases, G = ``XCD_SLICE_GROUP``
+    consecutive ranks (1 when fewer than S * G ranks may form items): G = 4 keeps 2 KiB of a
+    slice's rows together in X at F = 128, 2.8 % faster at cfg2 than dealing single ranks
+    (``profiles/r04sg_slice_group_ab.log``). ``phases`` > 1: the items of slice s run on XCD
+    s % xcds in phase s // xcds, the phases one after another in the launch order, so each
+    XCD's L2 holds 1 / (xcds * phases) of the table at a time.
 
     ``item_k`` < k limits the items to the item_k hottest hub rows (a smaller set per XCD
     slice); the edges to the other hub rows stay in ``rest`` and read the whole table.
@@ -398,7 +404,8 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
         eid = torch.nonzero((c < 0) & (c >= -ik) & (deg[rows_e] >= min_deg)).view(-1)
     else:
         eid = torch.nonzero((c < 0) & (c >= -ik) & (deg[rows_e] >= 2)).view(-1)
-    s_e = (-1 - c[eid]) % S
+    G = XCD_SLICE_GROUP if XCD_SLICE_GROUP > 1 and ik >= S * XCD_SLICE_GROUP else 1
+    s_e = ((-1 - c[eid]) // G) % S
     key = rows_e[eid] * S + s_e
     order = torch.argsort(key, stable=True)                  # by (row, slice), CSR order kept
     eid, key, s_e = eid[order], key[order], s_e[order]
@@ -440,7 +447,7 @@ def xcd_hub_coo(rowptr: torch.Tensor, col_hub: torch.Tensor, val: torch.Tensor, 
     filled[pos] = True
     pad = torch.nonzero(~filled).view(-1)                    # 2 zero-valued edges of its slice
     pad_phase = torch.searchsorted(base, pad, right=True) - 1
-    pad_col = -1 - (pad_phase * xcds + ((pad - base[pad_phase]) // W) % xcds)
+    pad_col = -1 - (pad_phase * xcds + ((pad - base[pad_phase]) // W) % xcds) * G
     items = (torch.cat([pos[item], pad, pad]), torch.cat([c[eid], pad_col, pad_col]),
              torch.cat([val[eid], torch.zeros(2 * pad.numel(), dtype=val.dtype, device=dev)]),
              n_pos, n_items)

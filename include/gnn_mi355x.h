@@ -204,7 +204,8 @@ int gnn_column_order(const int32_t* col, int64_t nnz, int64_t n_cols, int64_t pr
  * gnn_xcd_hub_plan_build / _fill (graph.xcd_hub_coo + from_coo): the XCD-sliced hub staging
  * of gnn_spmm_csr_hub_f32 / gnn_spmm_csr_tasks_f32 for a column array renamed by
  * gnn_hub_plan_build (col_hub; k hub ranks). The hub ranks are dealt to S = 8 * phases slices
- * (rank % S). For every row of degree >= min_deg (>= 2 with small_item >= 2), the edges to
+ * in groups of G = 4 consecutive ranks (rank r in slice (r / 4) % S; G = 1 when the item ranks
+ * number fewer than 4 S). For every row of degree >= min_deg (>= 2 with small_item >= 2), the edges to
  * the item_k hottest ranks (item_k <= 0: all k) that fall in one slice form a group; groups of
  * >= 2 edges (and, with small_item, rows of degree >= min_deg or groups of >= small_item edges)
  * are cut into ceil(m / chunk) balanced items. Pass 1 ("items") reduces each item into a

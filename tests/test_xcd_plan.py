@@ -47,8 +47,14 @@ def _csr_spmm(rows, cols, vals, n_rows, src):
     (3000, 1, 4, 1, None, None), (3000, 1, 5, 1, None, None), (500, 16, 8, 2, None, None),
     (3000, 2, 4, 4, None, None), (3000, 2, 8, 1, 100, None), (500, 16, 8, 2, 64, None),
     (500, 64, 128, 1, None, 3), (3000, 32, 8, 1, None, 4), (500, 10 ** 9, 16, 1, None, 2)])
-def test_xcd_plan_algebra_and_layout(k, min_deg, chunk, phases, item_k, small_item):
+@pytest.mark.parametrize("group", [1, 4])
+def test_xcd_plan_algebra_and_layout(monkeypatch, k, min_deg, chunk, phases, item_k, small_item,
+                                     group):
+    from graphneuralnetwork_amd import graph as G
     from graphneuralnetwork_amd.graph import xcd_hub_coo
+    monkeypatch.setattr(G, "XCD_SLICE_GROUP", group)
+    S = XCDS * phases
+    gs = group if (item_k or k) >= S * group else 1  # hub rank r in slice (r // gs) % S
     rowptr, col, val = _graph()
     n = rowptr.size - 1
     hub, ch = _hub_rename(col, n, k)
@@ -59,10 +65,10 @@ def test_xcd_plan_algebra_and_layout(k, min_deg, chunk, phases, item_k, small_it
     (ir, ic, iv, n_pos, n_items), (rr, rc, rv), pos_row = res
     ir, ic, iv, rr, rc, rv = (t.numpy() for t in (ir, ic, iv, rr, rc, rv))
     # layout: positions fill whole workgroups of every XCD; an item only reads its slice
-    # (slice = rank % (XCDS * phases), on XCD slice % XCDS), the phases in launch order
+    # (slice = (rank // gs) % (XCDS * phases), on XCD slice % XCDS), the phases in launch order
     assert n_pos % (XCDS * W) == 0
     assert ((ic < 0) & (ic >= -(item_k or k))).all()
-    sl = (-1 - ic) % (XCDS * phases)
+    sl = ((-1 - ic) // gs) % S
     np.testing.assert_array_equal(sl % XCDS, (ir // W) % XCDS)
     o = np.argsort(ir, kind="stable")
     assert (np.diff((sl // XCDS)[o]) >= 0).all()
@@ -88,7 +94,7 @@ def test_xcd_plan_algebra_and_layout(k, min_deg, chunk, phases, item_k, small_it
     np.testing.assert_array_equal(both[:, np.lexsort(both[::-1])], orig[:, np.lexsort(orig[::-1])])
     # items of rows below min_deg only for (row, slice) groups of >= small_item hub edges
     deg_item = deg[moved_rows]
-    grp = moved_rows * (XCDS * phases) + (-1 - ic[~pads]) % (XCDS * phases)
+    grp = moved_rows * S + ((-1 - ic[~pads]) // gs) % S
     _, inv, gsize = np.unique(grp, return_inverse=True, return_counts=True)
     low = deg_item < min_deg
     if small_item is None:
