@@ -361,7 +361,12 @@ __global__ void xcd_keys_kernel(const int64_t* __restrict__ eid, const int64_t* 
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= hdr[0]) return;
   const int64_t e = eid[t];
+#ifdef GNN_XCD_SLICE_SNAKE  // A/B only: groups dealt back and forth (0..S-1, S-1..0, ...)
+  const int64_t q = (-1 - static_cast<int64_t>(col[e])) / hdr[5];
+  const int64_t s = (q / S) % 2 ? S - 1 - q % S : q % S;
+#else
   const int64_t s = ((-1 - static_cast<int64_t>(col[e])) / hdr[5]) % S;
+#endif
   key[t] = static_cast<uint64_t>(row_e[e]) * static_cast<uint64_t>(S) + static_cast<uint64_t>(s);
 }
 

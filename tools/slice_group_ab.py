@@ -25,12 +25,18 @@ def main():
     ap.add_argument("--groups", default="1,8,64")
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--snake", default="", help="group sizes dealt back and forth (variant sg<G>s)")
     a = ap.parse_args()
     groups = [int(v) for v in a.groups.split(",")]
+    names = [f"sg{gsz}" for gsz in groups] + [f"sg{v}s" for v in a.snake.split(",") if v]
     if a.build:
         from graphneuralnetwork_amd.build import build_variant
         for gsz in groups:
             print(build_variant(f"sg{gsz}", [f"GNN_XCD_SLICE_GROUP={gsz}"], only=["plan_build.hip"]))
+        for gsz in a.snake.split(","):
+            if gsz:
+                print(build_variant(f"sg{gsz}s", [f"GNN_XCD_SLICE_GROUP={gsz}", "GNN_XCD_SLICE_SNAKE"],
+                                    only=["plan_build.hip"]))
         return
     import torch
     from graphneuralnetwork_amd import _lib
@@ -45,11 +51,11 @@ def main():
     X = torch.randn(n, 128, device=dev)
     Y = torch.empty(n, 128, device=dev)
     ref = spmm_forward(g, X).clone()
-    graphs = {gsz: CsrGraph(g.rowptr, g.col, g.val, g.n_rows, g.n_cols) for gsz in groups}
-    times = {gsz: [] for gsz in groups}
+    graphs = {gsz: CsrGraph(g.rowptr, g.col, g.val, g.n_rows, g.n_cols) for gsz in names}
+    times = {gsz: [] for gsz in names}
     for r in range(a.rounds):
-        for gsz in groups:
-            _lib.use_variant(ROOT / "graphneuralnetwork_amd" / "lib" / "variants" / f"libgnn_sg{gsz}.so")
+        for gsz in names:
+            _lib.use_variant(ROOT / "graphneuralnetwork_amd" / "lib" / "variants" / f"libgnn_{gsz}.so")
             gv = graphs[gsz]
             spmm_forward(gv, X, out=Y)
             torch.cuda.synchronize()
