@@ -94,8 +94,7 @@ def gcn_normalized_csr(src, dst, n: int, device=None) -> CsrGraph:
     r, c = merged // n, merged % n
     del merged
     # rowsum(A_til): keys are row-major sorted -> one segmented sum per row
-    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(torch.bincount(r, minlength=n), 0, out=offs[1:])
+    offs = torch.searchsorted(r, torch.arange(n + 1, dtype=torch.int64, device=dev))
     rowsum = torch.segment_reduce(w3, "sum", offsets=offs)
     w = w3
     d = rowsum.pow(-0.5)

@@ -301,6 +301,7 @@ def symmetric_adjacency(src, dst, n: int, device=None) -> CsrGraph:
     s, d = s[keep], d[keep]
     key = torch.unique(torch.cat([s * n + d, d * n + s]))
     r, c = key // n, key % n
-    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=s.device)
-    torch.cumsum(torch.bincount(r, minlength=n), 0, out=rowptr[1:])
+    # r is sorted (torch.unique): row starts by binary search, not a histogram whose atomics
+    # serialise on equal neighbours (torch.bincount took 33 ms at the cfg4 graph's 197M keys)
+    rowptr = torch.searchsorted(r, torch.arange(n + 1, dtype=torch.int64, device=s.device))
     return CsrGraph(rowptr, c.to(torch.int32), torch.ones(c.numel(), device=s.device), n, n)
