@@ -2,6 +2,7 @@
 default path of bench.py (hub rows read in place; one plan per K, cached on the graph).
 
     python tools/xcd_k_ab.py [--workload cfg2|ns] [--ks 196608,262144,327680] [--rounds 6]
+    python tools/xcd_k_ab.py --min-degs 64,96,128,192      (ops.XCD_MIN_DEG at the default K)
 """
 import argparse
 import json
@@ -19,6 +20,7 @@ def main():
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--ks", default="196608,262144,327680,393216")
     ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--min-degs", default="", help="sweep ops.XCD_MIN_DEG instead of K")
     a = ap.parse_args()
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
@@ -31,11 +33,15 @@ def main():
     X = torch.randn(n, 128, device=dev)
     Y = torch.empty(n, 128, device=dev)
     ref = ops.spmm_forward(g, X).clone()
-    ks = [int(v) for v in a.ks.split(",")]
+    sweep_deg = bool(a.min_degs)
+    ks = [int(v) for v in (a.min_degs if sweep_deg else a.ks).split(",")]
     times = {k: [] for k in ks}
     for r in range(a.rounds):
         for k in ks:
-            ops.XCD_HUB_ROWS, ops.XCD_HUB_BYTES = k, k * 512
+            if sweep_deg:
+                ops.XCD_MIN_DEG = k
+            else:
+                ops.XCD_HUB_ROWS, ops.XCD_HUB_BYTES = k, k * 512
             ops.spmm_forward(g, X, out=Y)
             torch.cuda.synchronize()
             if r == 0:
@@ -48,7 +54,7 @@ def main():
             ev[1].record()
             torch.cuda.synchronize()
             times[k].append(ev[0].elapsed_time(ev[1]) / 5)
-    print(json.dumps({"workload": a.workload,
+    print(json.dumps({"workload": a.workload, "swept": "XCD_MIN_DEG" if sweep_deg else "K",
                       "median_ms": {k: round(statistics.median(t), 4) for k, t in times.items()}}))
 
 
