@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--groups", default="1,8,64")
     ap.add_argument("--workload", default="cfg2")
+    ap.add_argument("--feat", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--snake", default="", help="group sizes dealt back and forth (variant sg<G>s)")
     a = ap.parse_args()
@@ -47,9 +48,10 @@ def main():
     dev = torch.device("cuda:0")
     n, e = (1_000_000, 10_000_000) if a.workload == "cfg2" else (10_000_000, 100_000_000)
     s, d = rmat_edges(n, e, 0)
-    g = column_order(gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n), 128).graph
-    X = torch.randn(n, 128, device=dev)
-    Y = torch.empty(n, 128, device=dev)
+    F = a.feat
+    g = column_order(gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n), F).graph
+    X = torch.randn(n, F, device=dev)
+    Y = torch.empty(n, F, device=dev)
     ref = spmm_forward(g, X).clone()
     graphs = {gsz: CsrGraph(g.rowptr, g.col, g.val, g.n_rows, g.n_cols) for gsz in names}
     times = {gsz: [] for gsz in names}
@@ -69,7 +71,7 @@ def main():
             ev[1].record()
             torch.cuda.synchronize()
             times[gsz].append(ev[0].elapsed_time(ev[1]) / 5)
-    print(json.dumps({"workload": a.workload,
+    print(json.dumps({"workload": a.workload, "feat": F,
                       "median_ms": {gsz: round(statistics.median(t), 4) for gsz, t in times.items()}}))
 
 
