@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--ks", default="196608,262144,327680,393216")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--min-degs", default="", help="sweep ops.XCD_MIN_DEG instead of K")
+    ap.add_argument("--phases", default="", help="sweep ops.XCD_PHASES instead of K")
     a = ap.parse_args()
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
@@ -33,13 +34,15 @@ def main():
     X = torch.randn(n, 128, device=dev)
     Y = torch.empty(n, 128, device=dev)
     ref = ops.spmm_forward(g, X).clone()
-    sweep_deg = bool(a.min_degs)
-    ks = [int(v) for v in (a.min_degs if sweep_deg else a.ks).split(",")]
+    sweep_deg, sweep_ph = bool(a.min_degs), bool(a.phases)
+    ks = [int(v) for v in (a.min_degs if sweep_deg else a.phases if sweep_ph else a.ks).split(",")]
     times = {k: [] for k in ks}
     for r in range(a.rounds):
         for k in ks:
             if sweep_deg:
                 ops.XCD_MIN_DEG = k
+            elif sweep_ph:
+                ops.XCD_PHASES = k
             else:
                 ops.XCD_HUB_ROWS, ops.XCD_HUB_BYTES = k, k * 512
             ops.spmm_forward(g, X, out=Y)
@@ -54,7 +57,7 @@ def main():
             ev[1].record()
             torch.cuda.synchronize()
             times[k].append(ev[0].elapsed_time(ev[1]) / 5)
-    print(json.dumps({"workload": a.workload, "swept": "XCD_MIN_DEG" if sweep_deg else "K",
+    print(json.dumps({"workload": a.workload, "swept": "XCD_MIN_DEG" if sweep_deg else "XCD_PHASES" if sweep_ph else "K",
                       "median_ms": {k: round(statistics.median(t), 4) for k, t in times.items()}}))
 
 
