@@ -11,7 +11,7 @@
  *         -> gnn_spmm_csr_f32 (pass 1), gnn_spmm_csr_tasks_f32 (pass 2)
  *
  * with ops.py's default knobs (XCD_MIN_DEG 128, XCD_CHUNK 128, TASK_MAX_DEG 128, TASK_COST
- * 256, seg_len = max(64, 192 KiB / 4F), K = min(n, 262144, 128 MiB / 4F)). The output must
+ * 128, seg_len = max(64, 192 KiB / 4F), K = min(n, 262144, 128 MiB / 4F)). The output must
  * equal ops.spmm_forward(column_order(g).graph, X[perm]) bit for bit
  * (tests/test_capi_program_gpu.py).
  *
@@ -232,7 +232,7 @@ int main(int argc, char** argv) {
   int64_t n_task = 0;
   ws_bytes = gnn_spmm_tasks_workspace_bytes(n);
   ws = dmalloc((size_t)ws_bytes);
-  CHECK(gnn_spmm_tasks_build(rrp, n, max_deg, 256, task_row, n, &n_task, ws, ws_bytes, S));
+  CHECK(gnn_spmm_tasks_build(rrp, n, max_deg, 128, task_row, n, &n_task, ws, ws_bytes, S));
   CHECK(gnn_spmm_tasks_check(task_row, n_task, n, err, S));
   float* partial = p2.n_seg ? (float*)dmalloc((size_t)p2.n_seg * F * 4) : NULL;
   float* y = (float*)dmalloc((size_t)n * F * 4);

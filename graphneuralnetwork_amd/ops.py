@@ -87,7 +87,7 @@ def xcd_hub_rows_for(n_cols: int, feat: int) -> int:
 # task. Needs the 16-B vector path and feat > 32 (two or fewer edge slots per 16 lanes).
 SPMM_TASKS = True
 TASK_MAX_DEG = 128
-TASK_COST = 256
+TASK_COST = 128  # 256 until late round 4: 128 is 0.7 % faster with the slice groups (cfg2, north star)
 
 
 def _tasks_ok(feat: int, *ts) -> bool:

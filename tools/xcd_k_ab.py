@@ -3,6 +3,7 @@ default path of bench.py (hub rows read in place; one plan per K, cached on the 
 
     python tools/xcd_k_ab.py [--workload cfg2|ns] [--ks 196608,262144,327680] [--rounds 6]
     python tools/xcd_k_ab.py --min-degs 64,96,128,192      (ops.XCD_MIN_DEG at the default K)
+    python tools/xcd_k_ab.py --knob TASK_COST --values 128,256,512   (any integer ops knob)
 """
 import argparse
 import json
@@ -22,6 +23,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--min-degs", default="", help="sweep ops.XCD_MIN_DEG instead of K")
     ap.add_argument("--phases", default="", help="sweep ops.XCD_PHASES instead of K")
+    ap.add_argument("--knob", default="", help="sweep this integer ops knob over --values")
+    ap.add_argument("--values", default="")
     a = ap.parse_args()
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
@@ -34,12 +37,17 @@ def main():
     X = torch.randn(n, 128, device=dev)
     Y = torch.empty(n, 128, device=dev)
     ref = ops.spmm_forward(g, X).clone()
+    if a.knob:
+        a.min_degs = a.phases = ""
     sweep_deg, sweep_ph = bool(a.min_degs), bool(a.phases)
-    ks = [int(v) for v in (a.min_degs if sweep_deg else a.phases if sweep_ph else a.ks).split(",")]
+    src = a.values if a.knob else a.min_degs if sweep_deg else a.phases if sweep_ph else a.ks
+    ks = [int(v) for v in src.split(",")]
     times = {k: [] for k in ks}
     for r in range(a.rounds):
         for k in ks:
-            if sweep_deg:
+            if a.knob:
+                setattr(ops, a.knob, k)
+            elif sweep_deg:
                 ops.XCD_MIN_DEG = k
             elif sweep_ph:
                 ops.XCD_PHASES = k
@@ -57,7 +65,7 @@ def main():
             ev[1].record()
             torch.cuda.synchronize()
             times[k].append(ev[0].elapsed_time(ev[1]) / 5)
-    print(json.dumps({"workload": a.workload, "swept": "XCD_MIN_DEG" if sweep_deg else "XCD_PHASES" if sweep_ph else "K",
+    print(json.dumps({"workload": a.workload, "swept": a.knob or ("XCD_MIN_DEG" if sweep_deg else "XCD_PHASES" if sweep_ph else "K"),
                       "median_ms": {k: round(statistics.median(t), 4) for k, t in times.items()}}))
 
 
