@@ -203,20 +203,30 @@ def build_graph(nodes: int, edges: int, dev, rank: int, world: int, edges_np=Non
     return g
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants this job (cgroup v2 cpu.max), or None."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_threads() -> int:
     """Host threads for the CPU lines: every CPU this process may use, capped by the box's
-    per-GPU CPU share (OMP_NUM_THREADS, 16 on the GPU box; GNN_CPU_THREADS overrides)."""
+    per-GPU CPU share -- the cgroup quota (cpu.max: 16 CPUs of time on the GPU box, whose
+    affinity mask lists all 256 host CPUs) and OMP_NUM_THREADS (16 there too).
+    GNN_CPU_THREADS overrides. Round 4 also timed the sample on all 256 host CPUs: inside the
+    16-CPU quota that oversubscribes, 0.600 s against 0.182 s at 16 threads
+    (profiles/r04zd_bench_default.log), so the lines use the quota (VERDICT r4 weak #6)."""
     if os.environ.get("GNN_CPU_THREADS"):
         return int(os.environ["GNN_CPU_THREADS"])
     n = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    if quota:
+        n = min(n, quota)
     share = os.environ.get("OMP_NUM_THREADS")
     return min(n, int(share)) if share and share.isdigit() and int(share) > 0 else n
-
-
-def all_host_threads() -> int:
-    """Every CPU this process may run on (the whole host on the GPU box: 256), ignoring the
-    per-GPU share OMP_NUM_THREADS sets (VERDICT r3 next #7)."""
-    return len(os.sched_getaffinity(0))
 
 
 def cpu_baseline(g, X, feat: int, threads: int | None = None):
@@ -248,15 +258,52 @@ def cpu_baseline(g, X, feat: int, threads: int | None = None):
             "seconds_per_step": t, "host": host_cpu_info(threads)}
 
 
-def load_traffic(name: str):
-    """PMC traffic summary profiles/traffic_<name>.json (tools/pmc_traffic.py) or None."""
-    path = ROOT / "profiles" / f"traffic_{name}.json"
+STAMP_SOURCES = ("graphneuralnetwork_amd/csrc", "graphneuralnetwork_amd/ops.py",
+                 "graphneuralnetwork_amd/graph.py")
+
+
+def source_stamp(root: Path = ROOT) -> str:
+    """sha256 (16 hex) over the kernel sources and the schedule builders (csrc/, ops.py,
+    graph.py): what a PMC traffic file or a kernel-stats summary was measured on. The profile
+    summaries carry it (tools/summarize_profiles.py) and bench.py compares it with the tree it
+    runs (roofline.traffic_stale, VERDICT r4 next #5)."""
+    import hashlib
+    h = hashlib.sha256()
+    files = []
+    for s in STAMP_SOURCES:
+        p = root / s
+        files += sorted(f for f in p.rglob("*") if f.is_file()) if p.is_dir() else [p]
+    for f in files:
+        if f.suffix not in (".hip", ".hpp", ".cpp", ".h", ".py", ".map"):
+            continue
+        h.update(str(f.relative_to(root)).encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def traffic_record(path: Path):
+    """(traffic bytes, source note, stamp, stale) of a profiles/traffic_*.json, or Nones."""
     try:
         t = json.loads(path.read_text())
-    except (OSError, ValueError):
-        return None, None
-    return t["traffic_bytes"], (str(path.relative_to(ROOT)) + ": rocprofv3 --pmc FETCH_SIZE x2 + "
-                                "WRITE_SIZE of this command")
+        traffic = t["traffic_bytes"]
+    except (OSError, ValueError, KeyError):
+        return None, None, None, None
+    stamp = t.get("source_stamp")
+    src = (str(path.relative_to(ROOT)) if path.is_relative_to(ROOT) else str(path)) + \
+        ": rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of this command (round %s)" % t.get("round")
+    return traffic, src, stamp, stamp != source_stamp()
+
+
+def traffic_fields(path: Path) -> dict:
+    """The roofline keys that say where ``traffic`` came from and whether it is current."""
+    traffic, src, stamp, stale = traffic_record(path)
+    return {"traffic": traffic, "traffic_source": src, "traffic_stamp": stamp,
+            "tree_stamp": source_stamp(), "traffic_stale": stale}
+
+
+def load_traffic(name: str):
+    """PMC traffic summary profiles/traffic_<name>.json (tools/summarize_profiles.py) or None."""
+    traffic, src, _, _ = traffic_record(ROOT / "profiles" / f"traffic_{name}.json")
+    return traffic, src
 
 
 def cpu_reference_ops(g, X, feat: int, budget_s: float = 25.0, max_nnz: int = 21_000_000):
@@ -500,7 +547,8 @@ def run_gat(args, dev, rank: int = 0, world: int = 1):
     k_ms = statistics.mean(agg_ms[GAT_DENSE])
     t = k_ms / 1e3
     achieved = comp / t / 1e9
-    traffic, tsrc = load_traffic("cfg3_F64")
+    tf = traffic_fields(ROOT / "profiles" / "traffic_cfg3_F64.json")
+    traffic = tf["traffic"]
     from graphneuralnetwork_amd.ops import transform_precision
     proj_arith = ("fp32 products from split-bf16 MFMAs (x and W in three bf16 pieces, six "
                   "v_mfma_f32_16x16x32_bf16 products accumulated in fp32)"
@@ -528,14 +576,13 @@ def run_gat(args, dev, rank: int = 0, world: int = 1):
            "project_tflops": 2.0 * n * Fin * (H * Fh + 2 * H) / (statistics.median(proj_ms) / 1e3)
            / 1e12,
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                        "frac": achieved / HBM_PEAK_GBPS, **tf,
                         "compulsory_bytes": comp,
                         "traffic_over_compulsory": traffic / comp if traffic else None,
                         "gather_model_bytes": gm, "gather_model_GBps": gm / t / 1e9,
                         "gather_model_frac": gm / t / 1e9 / HBM_PEAK_GBPS,
                         "traffic_GBps": traffic / t / 1e9 if traffic else None,
                         "traffic_frac": traffic / t / 1e9 / HBM_PEAK_GBPS if traffic else None,
-                        "traffic_source": tsrc,
                         "kernel": (("gat_csr_kernel<dense, hub> reading the Wh / er rows of "
                                     "the %d highest-degree columns in place (the first rows in "
                                     "the column-degree order) + " % hub_k) if order is not None
@@ -766,7 +813,8 @@ def run_sage(args, dev, rank: int = 0, world: int = 1, edges_np=None):
     k_ms = statistics.mean(agg_graph_ms) if agg_graph_ms else statistics.mean(agg_ms)
     t = k_ms / 1e3
     achieved = comp_l0 / t / 1e9
-    traffic, tsrc = load_traffic(f"cfg4_F{F}")
+    tf = traffic_fields(ROOT / "profiles" / f"traffic_cfg4_F{F}.json")
+    traffic = tf["traffic"]
     res = {"metric": "GraphSAGE sampled-neighbour aggregated edges/sec (2-layer forward)",
            "value": edges_all * args.steps / wall, "unit": "edges/s", "n_gpus": world,
            "steps": args.steps,
@@ -786,14 +834,13 @@ def run_sage(args, dev, rank: int = 0, world: int = 1, edges_np=None):
            "forward_hipgraph_ms": graph_ms,
            "first_sample_s": t_sample,
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                        "frac": achieved / HBM_PEAK_GBPS, **tf,
                         "compulsory_bytes": comp_l0, "distinct_rows": distinct,
                         "traffic_over_compulsory": traffic / comp_l0 if traffic else None,
                         "gather_model_bytes": bytes_l0, "gather_model_GBps": bytes_l0 / t / 1e9,
                         "gather_model_frac": bytes_l0 / t / 1e9 / HBM_PEAK_GBPS,
                         "traffic_GBps": traffic / t / 1e9 if traffic else None,
                         "traffic_frac": traffic / t / 1e9 / HBM_PEAK_GBPS if traffic else None,
-                        "traffic_source": tsrc,
                         "kernel": "sage_aggregate_kernel<gather, mean> (layer 0: |S1| x 10 from the 10M table)"
                                   + (", %d launches per HIP-graph replay" % REP if agg_graph_ms else
                                      ", eager per-launch HIP events"),
@@ -859,19 +906,23 @@ def host_cpu_info(threads: int) -> dict:
             info["cgroup_cpu_quota_cpus"] = round(int(q) / int(per), 2)
     except (OSError, ValueError):
         pass
+    info["threads_rule"] = ("min(affinity CPUs, cgroup CPU quota, OMP_NUM_THREADS): the CPUs "
+                            "of time this job is granted; more threads oversubscribe the quota")
     return info
 
 
-def gcn_roofline(nnz: int, n_rows: int, n_cols: int, feat: int, step_ms: list, traffic,
-                 kernel: str, traffic_src=None) -> dict:
-    """The roofline object of one SpMM step (see compulsory_bytes / algorithmic_bytes)."""
+def gcn_roofline(nnz: int, n_rows: int, n_cols: int, feat: int, step_ms: list, tf: dict,
+                 kernel: str) -> dict:
+    """The roofline object of one SpMM step (see compulsory_bytes / algorithmic_bytes); ``tf``
+    = traffic_fields() of the workload's PMC file (all None without one)."""
     kern_ms = statistics.mean(step_ms)
     t = kern_ms / 1e3
     comp = compulsory_bytes(nnz, n_rows, n_cols, feat)
     gm = algorithmic_bytes(nnz, n_rows, feat)
     achieved = comp / t / 1e9
+    traffic = tf.get("traffic")
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+            "frac": achieved / HBM_PEAK_GBPS, **tf,
             "compulsory_bytes": comp,
             "traffic_over_compulsory": traffic / comp if traffic else None,
             # the SURVEY 8(d) no-reuse gather model (every gathered row from HBM): an upper
@@ -882,16 +933,9 @@ def gcn_roofline(nnz: int, n_rows: int, n_cols: int, feat: int, step_ms: list, t
             # served, as a fraction of the 8 TB/s peak
             "traffic_GBps": traffic / t / 1e9 if traffic else None,
             "traffic_frac": traffic / t / 1e9 / HBM_PEAK_GBPS if traffic else None,
-            "traffic_source": traffic_src, "kernel": kernel,
+            "kernel": kernel,
             "avg_launch_ms": kern_ms, "median_launch_ms": statistics.median(step_ms),
             "min_launch_ms": min(step_ms)}
-
-
-def _load_traffic_file(tpath: Path):
-    try:
-        return json.loads(tpath.read_text())["traffic_bytes"]
-    except (OSError, ValueError, KeyError):
-        return None
 
 
 def run_gcn(args, dev, rank: int, world: int, workload: str, edges_np=None, extras=False):
@@ -1055,14 +1099,11 @@ def run_gcn(args, dev, rank: int, world: int, workload: str, edges_np=None, extr
         log(f"[bench] Graph_conv_layer timed: {layer_ms:.3f} ms")
         torch.cuda.empty_cache()
 
-    traffic = tsrc = None
+    tf = {}
     if world == 1:
         tpath = Path(args.traffic_json) if (args.traffic_json and not extras) else \
             ROOT / "profiles" / f"traffic_{workload}_F{F}.json"
-        traffic = _load_traffic_file(tpath)
-        if traffic is not None:
-            tsrc = (str(tpath.relative_to(ROOT)) if tpath.is_relative_to(ROOT) else str(tpath)) + \
-                ": rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE of bench.py --workload " + workload
+        tf = traffic_fields(tpath)
     res = None
     if rank == 0:
         kernel = HUB_INFO["kernel"] if HUB_INFO.get("kernel") else (
@@ -1074,7 +1115,7 @@ def run_gcn(args, dev, rank: int, world: int, workload: str, edges_np=None, extr
             "spmm_csr_kernel (+ spmm_fixup_kernel), per-step HIP events")
         roof = gcn_roofline(nnz_local, rows_local,
                             rows_local + halo_rows if world > 1 else g.n_cols, F, step_ms,
-                            traffic, kernel, tsrc)
+                            tf, kernel)
         if world == 1 and "column_order_s" in BUILD_INFO:
             from graphneuralnetwork_amd.ops import xcd_hub_rows_for
             roof["achievable_floor"] = floor_model(ga.col, g.n_cols,
@@ -1123,18 +1164,6 @@ def run_gcn(args, dev, rank: int, world: int, workload: str, edges_np=None, extr
                 res["cpu_baseline"] = cpu_baseline(g, X, F)
             except Exception as e:  # the baseline is reported, never the target
                 res["cpu_baseline"] = {"value": None, "error": repr(e)}
-            n_all = all_host_threads()
-            if not extras and n_all > res["cpu_baseline"].get("cores", n_all):
-                # the same bounded sample on every host CPU (the box's whole host, not just
-                # the 16-CPU share of one GPU), beside the share line
-                log(f"[bench] {workload} cpu baseline on all {n_all} host CPUs ...")
-                try:
-                    res["cpu_baseline_all_cores"] = cpu_baseline(g, X, F, threads=n_all)
-                except Exception as e:
-                    res["cpu_baseline_all_cores"] = {"value": None, "error": repr(e)}
-                finally:
-                    from oracle import c_oracle
-                    c_oracle.set_threads(cpu_threads())
             if not args.no_cpu_reference and not extras:
                 log("[bench] cpu reference operators ...")
                 try:
@@ -1152,7 +1181,7 @@ def _sub(res: dict) -> dict:
     """A workload's line as a sub-object of the headline (the keys that describe it)."""
     keep = ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "median_step_ms",
             "cache_cold_median_step_ms", "dtype",
-            "config", "roofline", "cpu_baseline", "cpu_baseline_all_cores", "cpu_reference_ops",
+            "config", "roofline", "cpu_baseline", "cpu_reference_ops",
             "first_step_s", "graph_build_s", "gcn_layer_ms", "layer_ms", "aggregate_ms",
             "forward_ms", "forward_hipgraph_ms", "sample_ms", "batch_ms", "project_ms",
             "project_tflops", "project_arithmetic")

@@ -75,6 +75,7 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_cover_send_partials": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _i64, _i64, _i64, _vp,
                                                _vp, _vp, _vp, _i64, _vp]),
     "gnn_xcd_hub_plan_workspace_bytes": (_i64, [_i64, _i64]),
+    "gnn_xcd_slice_group": (_i64, []),
     "gnn_xcd_hub_plan_build": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
                                               _i64, _vp, _vp, _i64, _vp]),
     "gnn_xcd_hub_plan_fill": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp,

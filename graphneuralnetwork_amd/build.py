@@ -11,6 +11,7 @@ from __future__ import annotations
 import os
 import shutil
 import subprocess
+import warnings
 import sys
 from pathlib import Path
 
@@ -105,7 +106,12 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
         os.replace(tmp, LIB_PATH)
-    build_examples(force)
+    # the plain-C example is optional: a missing C compiler or a failing example build warns
+    # and leaves the library usable; tests/test_capi.py builds it explicitly
+    try:
+        build_examples(force)
+    except (RuntimeError, OSError) as e:
+        warnings.warn(f"examples/ not built: {e}", RuntimeWarning, stacklevel=2)
     return LIB_PATH
 
 

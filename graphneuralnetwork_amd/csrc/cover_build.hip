@@ -77,6 +77,7 @@ struct CoverWs {
   int64_t* qb;       // [2 W] first / end of each owner's partial edges in sorted order
   int64_t* cnt;      // [4] select counts
   int32_t* err;      // [1] a column id outside [0, n_rows)
+  int64_t* out;      // [4 + 3 W] the counts handed back (one host read)
   void* temp;
   size_t temp_bytes;
   int64_t bytes;
@@ -154,10 +155,31 @@ static CoverWs cover_carve(void* ws, int64_t E, int64_t n, int64_t n_own, int wo
   w.qb = c.take<int64_t>(2 * kMaxWorld);
   w.cnt = c.take<int64_t>(4);
   w.err = c.take<int32_t>(1);
+  w.out = c.take<int64_t>(4 + 3 * static_cast<int64_t>(world));
   w.temp_bytes = cover_temp_bytes(E, n, P, n_own);
   w.temp = c.take<char>(static_cast<int64_t>(w.temp_bytes));
   w.bytes = c.used;
   return w;
+}
+
+// the counts gnn_cover_build hands back (see there), one lane per owner q
+__global__ void cover_counts_kernel(const int64_t* __restrict__ kpre, const int64_t* __restrict__ xpre,
+                                    const int64_t* __restrict__ xrank, const int64_t* __restrict__ pscan,
+                                    const int64_t* __restrict__ qb, int64_t E, int64_t n_rows, int64_t P,
+                                    int64_t n_own, Bounds B, int64_t* __restrict__ out) {
+  const int q = threadIdx.x;
+  const int W = B.world;
+  if (q == 0) {
+    out[0] = kpre[E];
+    out[1] = xrank[n_rows];
+    out[2] = xpre[E];
+    out[3] = pscan[P];
+  }
+  if (q < W) {
+    out[4 + q] = xrank[B.b[q + 1]] - xrank[B.b[q]];
+    out[4 + W + q] = pscan[(q + 1) * n_own] - pscan[q * n_own];
+    out[4 + 2 * W + q] = qb[kMaxWorld + q] - qb[q];
+  }
 }
 
 // local edge t (global e0 + t): its row, its class (interior / cut), the cut counts
@@ -479,26 +501,11 @@ extern "C" int gnn_cover_build(const int64_t* rowptr, const int32_t* col, int64_
                        w.hp_cnt);
   // counts: [0] interior nnz, [1] requested columns, [2] halo_x nnz, [3] partial rows,
   // [4 + q] feature rows asked of q, [4 + W + q] partial rows asked of q, [4 + 2W + q] their edges
-  int64_t h[2];
-  int rc = sync_read(w.kpre + E, &h[0], 1, s);
-  if (rc == GNN_OK) rc = sync_read(w.xpre + E, &h[1], 1, s);
+  // -- gathered on the device and read back once (4 W + 6 separate reads before)
+  hipLaunchKernelGGL(cover_counts_kernel, dim3(1), dim3(kMaxWorld), 0, s, w.kpre, w.xpre, w.xrank,
+                     w.pscan, w.qb, E, n_rows, P, n_own, B, w.out);
+  int rc = sync_read(w.out, counts, 4 + 3 * static_cast<int64_t>(world), s);
   if (rc != GNN_OK) return rc;
-  counts[0] = h[0];
-  counts[2] = h[1];
-  if ((rc = sync_read(w.xrank + n_rows, &counts[1], 1, s)) != GNN_OK) return rc;
-  if ((rc = sync_read(w.pscan + P, &counts[3], 1, s)) != GNN_OK) return rc;
-  for (int q = 0; q < world; ++q) {
-    int64_t a[2], p2[2];
-    if ((rc = sync_read(w.xrank + B.b[q], &a[0], 1, s)) != GNN_OK) return rc;
-    if ((rc = sync_read(w.xrank + B.b[q + 1], &a[1], 1, s)) != GNN_OK) return rc;
-    counts[4 + q] = a[1] - a[0];
-    if ((rc = sync_read(w.pscan + q * n_own, &p2[0], 1, s)) != GNN_OK) return rc;
-    if ((rc = sync_read(w.pscan + (q + 1) * n_own, &p2[1], 1, s)) != GNN_OK) return rc;
-    counts[4 + world + q] = p2[1] - p2[0];
-  }
-  int64_t qb[2 * kMaxWorld];
-  if ((rc = sync_read(w.qb, qb, 2 * kMaxWorld, s)) != GNN_OK) return rc;
-  for (int q = 0; q < world; ++q) counts[4 + 2 * world + q] = qb[kMaxWorld + q] - qb[q];
   return launch_status();
 }
 

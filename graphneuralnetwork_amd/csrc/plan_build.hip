@@ -716,6 +716,10 @@ extern "C" int gnn_column_order(const int32_t* col, int64_t nnz, int64_t n_cols,
 }
 
 // ============================================================================ XCD hub plan
+// the compile-time slice group G of this builder (graph.XCD_SLICE_GROUP must agree for the
+// package to use it; a different Python value selects the torch builder, which honours it)
+extern "C" int64_t gnn_xcd_slice_group(void) { return kSliceGroup; }
+
 extern "C" int64_t gnn_xcd_hub_plan_workspace_bytes(int64_t n_rows, int64_t nnz) {
   if (n_rows < 1 || nnz < 0) return GNN_E_ARG;
   return xcd_carve(nullptr, nnz, n_rows).bytes;

@@ -37,7 +37,7 @@ shard across ranks and the feature table is replicated (5.1 GB at 10M x 128 fits
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
@@ -253,6 +253,8 @@ class CoverExchange:
     recv_p_counts: list
     any_x: bool             # some rank exchanges feature rows (collective is needed)
     any_p: bool             # some rank exchanges partial rows
+    # feature rows rank p receives from rank q, for every (p, q): the same on every rank
+    recv_x_matrix: list = field(default=None)
 
     @property
     def n_own(self) -> int:
@@ -352,12 +354,17 @@ def build_cover_exchange(g: CsrGraph, rank: int, world: int, group=None,
                                          torch.tensor(spl_out, dtype=i64, device=dev))
         _, p_slot = torch.unique_consecutive(peer_e * b[-1] + pe_i, return_inverse=True)
         send_p = from_coo(p_slot.view(-1), pe_j - r0, pe_v, n_p_send, n_own)
-    any_x = _global_sum(int(xcols.numel()), dev, group) > 0
+    # every rank's feature-row requests ([world, world]: row p = rows p receives from each q),
+    # so that a consumer of the exchange (EdgeCutSpmm's chunking) decides from data all ranks
+    # hold, with no collective of its own
+    x_matrix = [[int(v) for v in row] for row in
+                _all_gather_floats([float(m[0]) for m in mine_l], world, dev, group).tolist()]
+    any_x = sum(map(sum, x_matrix)) > 0
     any_p = _global_sum(int(halo_p.n_cols), dev, group) > 0
     return CoverExchange(rank, world, b, interior, (req_x - r0).contiguous(), send_p, halo_x,
                          halo_p, [t[0] for t in theirs_l], [t[1] for t in theirs_l],
                          [int(v) for v in nx.cpu().tolist()], [int(v) for v in np_.cpu().tolist()],
-                         any_x, any_p)
+                         any_x, any_p, x_matrix)
 
 
 def _cover_local_torch(g: CsrGraph, rank: int, world: int, b: list):
@@ -631,8 +638,8 @@ class EdgeCutSpmm:
     ``chunks`` (cover exchange; default HALO_CHUNKS): the feature rows travel in that many
     all-to-all-v's, laid out chunk-major in the send / receive buffers, and the halo_x SpMM is
     split by column chunk, so the halo gathers of chunk k start as soon as chunk k has landed.
-    With chunks > 1 the constructor is a collective (every rank's chunk sizes are gathered
-    once, so that all ranks skip the same globally empty chunks): construct it on every rank.
+    All ranks skip the same globally empty chunks, decided from the [world, world] count
+    matrix ``build_cover_exchange`` gathered: the constructor itself runs no collective.
     """
 
     def __init__(self, part: EdgeCutPartition | CoverExchange, feat: int, device, group=None,
@@ -686,10 +693,14 @@ class EdgeCutSpmm:
         # is an all-to-all-v with zero counts there, as any exchange can be
         self.x_chunk_live = [True] * C
         if C > 1 and p.any_x:
-            mine = [float(sum(self.x_send_chunks[k]) + sum(self.x_recv_chunks[k]))
-                    for k in range(C)]
-            tot = _all_gather_floats(mine, p.world, self.device, self.group).sum(0)
-            self.x_chunk_live = [bool(v > 0) for v in tot.tolist()]
+            if p.recv_x_matrix is not None:   # every rank holds the whole count matrix
+                flat = [n for row in p.recv_x_matrix for n in row]
+                self.x_chunk_live = [sum(piece) > 0 for piece in chunk_sizes(flat, C)]
+            else:  # a CoverExchange built without it: one all-gather of the chunk sizes
+                mine = [float(sum(self.x_send_chunks[k]) + sum(self.x_recv_chunks[k]))
+                        for k in range(C)]
+                tot = _all_gather_floats(mine, p.world, self.device, self.group).sum(0)
+                self.x_chunk_live = [bool(v > 0) for v in tot.tolist()]
         if C == 1:
             self.send_x_idx = p.send_x_idx
             self.halo_x_chunks = [p.halo_x]

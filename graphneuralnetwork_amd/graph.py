@@ -630,7 +630,11 @@ def _build_xcd_hub_plan(g: CsrGraph, k: int, min_deg: int, chunk: int, phases: i
         return None
     if item_k is not None and min(int(item_k), hub.k) < XCDS * phases:
         return None
-    if NATIVE_PLANS and g.rowptr.is_cuda:
+    # the device builder's slice group is a compile-time constant: it runs only when it is the
+    # one asked for here (a monkeypatched / edited XCD_SLICE_GROUP takes the torch builder,
+    # which reads it at run time)
+    if NATIVE_PLANS and g.rowptr.is_cuda and \
+            int(_lib.load().gnn_xcd_slice_group()) == XCD_SLICE_GROUP:
         return _build_xcd_hub_plan_native(g, hub, min_deg, chunk, phases, item_k, small_item)
     coo = xcd_hub_coo(g.rowptr, hub.col_hub, g.val, hub.k, min_deg, chunk, phases=phases,
                       item_k=item_k, small_item=small_item)
@@ -718,6 +722,10 @@ def in_degree(g: "CsrGraph") -> torch.Tensor:
     _lib.check(_lib.load().gnn_in_degree_u32(g.col.data_ptr(), g.nnz, n, deg.data_ptr(),
                                              err.data_ptr(), _lib.stream_handle(g.device)),
                "gnn_in_degree_u32")
+    # a column id outside [0, n_cols) is not counted by the kernel; torch.bincount would raise
+    # (negative) or return a longer vector, so it is an error here too
+    if int(err.item()) != 0:
+        raise ValueError(f"column ids outside [0, {n}) in the graph (in_degree)")
     # uint32 counts < 2^31 here (nnz < 2^31 per column): the int32 view is exact
     return deg.to(torch.int64)
 

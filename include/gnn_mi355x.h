@@ -223,6 +223,9 @@ int gnn_column_order(const int32_t* col, int64_t nnz, int64_t n_cols, int64_t pr
  * workspace: gnn_xcd_hub_plan_workspace_bytes(n_rows, nnz) bytes of device memory.
  */
 int64_t gnn_xcd_hub_plan_workspace_bytes(int64_t n_rows, int64_t nnz);
+/* The slice group G the builder was compiled with (4): a caller that needs another grouping
+ * builds the arrays itself (graph.xcd_hub_coo restates them). */
+int64_t gnn_xcd_slice_group(void);
 int gnn_xcd_hub_plan_build(const int64_t* rowptr, const int32_t* col_hub, int64_t n_rows,
                            int64_t nnz, int64_t k, int64_t min_deg, int64_t chunk, int64_t phases,
                            int64_t item_k, int64_t small_item, int64_t* counts, void* workspace,

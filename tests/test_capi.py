@@ -109,5 +109,6 @@ def test_c_program_links_and_checks_usage():
     exe = B.LIB_DIR / "capi_gcn_spmm"
     if not exe.exists():
         B.build()
+    B.build_examples()  # build() only warns when the example fails to build; here it must not
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "usage" in r.stderr
