@@ -618,9 +618,138 @@ def run_gat(args, dev, rank: int = 0, world: int = 1):
                                                          H, Fh)
             except Exception as e:
                 res["cpu_reference_ops"] = {"error": repr(e)}
-    del g, X, Wh, out
+    del Wh, out, Wh_o, el_o, er_o
+    torch.cuda.empty_cache()
+    if not args.no_train:
+        res["train_step"] = gat_train_step(g, X, H, Fh, args, dev)
+    del g, X
     torch.cuda.empty_cache()
     return res
+
+
+def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
+    """One training step of the drop-in 8-head GAT attention block at cfg3 (GAT.py:16's heads
+    through GATBase._heads: one X W GEMM for all heads, the fused edge-softmax aggregation with
+    ELU; GAT/train_eval.py:75-76's loss.backward()): forward + backward with W, a_src, a_dst
+    requiring grad (X is the input features). The backward's three HIP passes
+    (csrc/gat_bwd.hip: prep, SDDMM edge pass, transposed node pass; replacing the autograd of
+    GAT/models/layers.py:22-37 and SpecialSpmmFunction.backward :54-64) are also timed alone,
+    each with a roofline on its compulsory bytes."""
+    from graphneuralnetwork_amd.gat import GAT
+    from graphneuralnetwork_amd.ops import GAT_DENSE, gat_aggregate, gat_backward, gat_logits
+    gen = torch.Generator(device=dev).manual_seed(3)
+    net = GAT(X.shape[1], Fh, 3, dropout=0.0, alpha=0.2, nheads=H).to(dev).train()
+    gy = torch.randn(g.n_rows, H * Fh, device=dev, generator=gen)
+    steps = max(3, min(args.steps, 10))
+
+    def step():
+        net.zero_grad(set_to_none=True)
+        net._heads(X, g).backward(gy)
+
+    step_ms = time_steps(step, steps, 2, dev)[0]
+    fwd_ms = time_steps(lambda: net._heads(X, g), steps, 2, dev)[0]
+    keep = {"y": net._heads(X, g)}
+    bwd_ms = time_steps(lambda: keep["y"].backward(gy, retain_graph=True), steps, 2, dev)[0]
+    del keep
+    # the three backward passes alone (the tensors the autograd Function saves)
+    W = torch.cat([m.W for m in net.attentions], 1).detach()
+    a_s = torch.cat([m._a_parts()[0] for m in net.attentions]).detach()
+    a_d = torch.cat([m._a_parts()[1] for m in net.attentions]).detach()
+    Wh = torch.mm(X, W)
+    el, er = gat_logits(Wh, H, Fh, a_s, a_d)
+    stats = torch.empty((g.n_rows, H), device=dev)
+    out = gat_aggregate(g, Wh, el, er, H, Fh, 0.2, GAT_DENSE, "elu", stats=stats)
+    per = {}
+    for i in range(steps + 2):
+        tl = []
+        gat_backward(g, Wh, el, er, stats, out, gy, a_s, a_d, H, Fh, 0.2, GAT_DENSE, True,
+                     timings=tl)
+        torch.cuda.synchronize(dev)
+        if i >= 2:
+            for name, a, b in tl:
+                per.setdefault(name, []).append(a.elapsed_time(b))
+    n, nnz, feat = g.n_rows, g.nnz, H * Fh
+    comp = {"prep": n * 4 * (3 * feat + H),
+            "edges": nnz * (4 + 8 * H) + n * (8 + 16 * H + 4 * feat) + g.n_cols * (4 * H + 4 * feat),
+            "nodes": nnz * (12 + 8 * H) + n * (8 + 8 * feat + 8 * H)}
+    what = {"prep": "gat_bwd_prep_kernel: dout = dy ELU'(out), D = dout . out",
+            "edges": "gat_bwd_edge_kernel (+ del fix-up): SDDMM g = dout_i . Wh_j, edge weights "
+                     "w_ij and softmax/LeakyReLU gradients ds_ij written per (edge, head)",
+            "nodes": "gat_bwd_node_kernel (+ fix-up) over the transposed CSR: dWh_j = sum_i w_ij "
+                     "dout_i + der_j a_dst + del_j a_src"}
+    kernels = {}
+    for name, ms in per.items():
+        t = statistics.mean(ms) / 1e3
+        kernels[name] = {"median_ms": statistics.median(ms), "kernel": what[name],
+                         "roofline": {"bound": "hbm", "achieved": comp[name] / t / 1e9,
+                                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                      "frac": comp[name] / t / 1e9 / HBM_PEAK_GBPS,
+                                      "compulsory_bytes": comp[name], "avg_launch_ms": t * 1e3}}
+    res = {"what": "GAT %d-head attention block (%d -> %dx%d, dense softmax, ELU) forward + "
+                   "loss.backward() at cfg3; W, a_src, a_dst require grad" % (H, X.shape[1], H, Fh),
+           "step_ms": statistics.median(step_ms), "forward_ms": statistics.median(fwd_ms),
+           "backward_ms": statistics.median(bwd_ms),
+           "edges_per_s": nnz / (statistics.median(step_ms) / 1e3),
+           "forward_path": "torch.mm (X W, autograd) + gat_logits + gat_aggregate with per-row "
+                           "log-sum-exp stats (hub-staged Wh / er)",
+           "backward_kernels": kernels,
+           "compulsory_bytes_model": {
+               "prep": "4 N (3 H Fh + H)",
+               "edges": "nnz (4 + 8 H) + N (8 + 16 H + 4 H Fh) + N (4 H + 4 H Fh)",
+               "nodes": "nnz (12 + 8 H) + N (8 + 8 H Fh + 8 H)"}}
+    if not args.no_cpu_baseline:
+        try:
+            res["cpu_reference_ops"] = cpu_gat_train_ops(g, X.cpu(), W.cpu(), a_s.cpu(),
+                                                         a_d.cpu(), H, Fh)
+        except Exception as e:
+            res["cpu_reference_ops"] = {"error": repr(e)}
+    del net, gy, Wh, out, stats
+    torch.cuda.empty_cache()
+    return res
+
+
+def cpu_gat_train_ops(g, X, W, a_s, a_d, H: int, Fh: int, max_edges: int = 1_000_000,
+                      budget_s: float = 10.0) -> dict:
+    """The sparse attention layer's math (GAT/models/layers.py:94-131 per head, softmax-
+    normalised and ELU as the dense layer) forward + backward by torch CPU autograd on an edge
+    list (index_select / index_add: the reference's own backward materialises dense N x N
+    gradients and cannot run at this size), on the leading rows holding <= max_edges edges,
+    every allowed host thread."""
+    threads = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        rowptr = g.rowptr.cpu()
+        r1 = max(1, min(g.n_rows, int(torch.searchsorted(rowptr, max_edges, right=True)) - 1))
+        e1 = int(rowptr[r1])
+        src = torch.repeat_interleave(torch.arange(r1), rowptr[1:r1 + 1] - rowptr[:r1])
+        dst = g.col[:e1].cpu().to(torch.int64)
+        Wp = W.clone().requires_grad_(True)
+        asp = a_s.clone().requires_grad_(True)
+        adp = a_d.clone().requires_grad_(True)
+        gy = torch.randn(r1, H * Fh)
+
+        def step():
+            for t in (Wp, asp, adp):
+                t.grad = None
+            Wh = (X @ Wp).view(-1, H, Fh)
+            el = (Wh[:r1] * asp.view(H, Fh)).sum(-1)
+            er = (Wh * adp.view(H, Fh)).sum(-1)
+            z = torch.nn.functional.leaky_relu(el[src] + er[dst], 0.2)
+            m = torch.zeros(r1, H).index_reduce_(0, src, z.detach(), "amax", include_self=False)
+            p = torch.exp(z - m[src])
+            den = torch.zeros(r1, H).index_add_(0, src, p)
+            num = torch.zeros(r1, H, Fh).index_add_(0, src, p.unsqueeze(-1) * Wh[dst])
+            out = torch.nn.functional.elu(num / den.unsqueeze(-1))
+            out.view(r1, -1).backward(gy)
+
+        t, runs = _cpu_time(step, budget_s)
+        return {"torch_cpu_train_step": {"value": e1 / t, "unit": "edges/s", "threads": threads,
+                                         "seconds_per_step": t, "runs": runs},
+                "note": f"torch CPU autograd of the edge-list attention layer, {H} heads, rows "
+                        f"0..{r1} ({e1} edges; X W over all {X.shape[0]} rows)"}
+    finally:
+        torch.set_num_threads(prev)
 
 
 def run_gat_edgecut(args, dev, rank: int, world: int):
@@ -847,6 +976,9 @@ def run_sage(args, dev, rank: int = 0, world: int = 1, edges_np=None):
                         "eager_launch_ms": statistics.median(agg_ms),
                         "avg_launch_ms": k_ms,
                         "median_launch_ms": statistics.median(agg_graph_ms or agg_ms)}}
+    if world == 1 and not args.no_variants:
+        res["aggregators"] = sage_aggregator_variants(args, dev, table, batch, fargs, F, H,
+                                                      distinct)
     if world > 1:
         res["config"]["global_seeds"] = 8192 * world
         res["config"]["parallelism"] = f"seed-sharded{world} (replicated table, no collective)"
@@ -877,6 +1009,62 @@ def run_sage(args, dev, rank: int = 0, world: int = 1, edges_np=None):
     del table, adj, batch, fargs
     torch.cuda.empty_cache()
     return res
+
+
+def sage_aggregator_variants(args, dev, table, batch, fargs, F: int, H: int,
+                             distinct: int) -> dict:
+    """cfg4 with the other aggregators the reference exposes: 'MAX'
+    (graph_utils.py:7-8: torch.argmax over the neighbours, int64 indices, bit-exact) and the
+    north star's value max-pool 'MAXPOOL' (torch.max(dim=1).values): the 2-layer forward on the
+    same sampled batch and the layer-0 gather-reduce kernel alone, with its roofline
+    (compulsory bytes: the index map, each distinct table row once, the output: 8 B per
+    element for the argmax) and the C oracle's rate on the same gather (16 threads)."""
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    from graphneuralnetwork_amd.ops import sage_gather_aggregate
+    from oracle import c_oracle
+    M, k1 = batch.frontier_nbrs.shape
+    steps = max(3, min(args.steps, 10))
+    out = {}
+    for agg in ("MAX", "MAXPOOL"):
+        net = GraphSAGE(2, F, H, False, agg_func=agg, Unsupervised=False,
+                        class_size=3).to(dev).eval()
+        with torch.no_grad():
+            fwd_ms = time_steps(lambda: net(*fargs, None, None, None, None, None), steps, 2,
+                                dev)[0]
+            k_ms = time_steps(lambda: sage_gather_aggregate(table, batch.frontier_nbrs, agg,
+                                                            check=False), steps, 2, dev)[0]
+        out_bytes = M * F * (8 if agg == "MAX" else 4)
+        comp = M * k1 * 8 + distinct * 4 * F + out_bytes
+        t = statistics.mean(k_ms) / 1e3
+        r = {"forward_ms": statistics.median(fwd_ms),
+             "value": batch.sampled_edges / (statistics.median(fwd_ms) / 1e3),
+             "unit": "edges/s",
+             "layer0_kernel_ms": statistics.median(k_ms),
+             "roofline": {"bound": "hbm", "achieved": comp / t / 1e9, "peak": HBM_PEAK_GBPS,
+                          "unit": "GB/s", "frac": comp / t / 1e9 / HBM_PEAK_GBPS,
+                          "compulsory_bytes": comp, "avg_launch_ms": t * 1e3,
+                          "kernel": "sage_aggregate_kernel<gather, %s> (layer 0: %d frontier "
+                                    "rows x %d from the 10M table), eager per-launch HIP events"
+                                    % (agg.lower(), M, k1)}}
+        if not args.no_cpu_baseline:
+            threads = cpu_threads()
+            c_oracle.set_threads(threads)
+            tn = table.cpu().numpy()
+            idx = batch.frontier_nbrs.cpu().numpy()
+            fn = ((lambda: c_oracle.sage_argmax(tn, idx)) if agg == "MAX" else
+                  (lambda: c_oracle.sage_gather(tn, idx, "MAXPOOL")))
+            tc, runs = _cpu_time(fn, 5.0)
+            r["cpu_baseline"] = {"value": idx.size / tc, "unit": "edges/s", "cores": threads,
+                                 "kind": "port", "seconds_per_step": tc,
+                                 "sample": "layer-0 gather-%s of the same batch (%d x %d) by "
+                                           "oracle/spmm_oracle.c %s, median of %d runs"
+                                           % (agg.lower(), M, k1,
+                                              "oracle_sage_argmax" if agg == "MAX"
+                                              else "oracle_sage_gather", runs),
+                                 "host": host_cpu_info(threads)}
+        out[agg] = r
+        del net
+    return out
 
 
 def transform_note() -> str:
@@ -936,6 +1124,183 @@ def gcn_roofline(nnz: int, n_rows: int, n_cols: int, feat: int, step_ms: list, t
             "kernel": kernel,
             "avg_launch_ms": kern_ms, "median_launch_ms": statistics.median(step_ms),
             "min_launch_ms": min(step_ms)}
+
+
+def _ms_stats(ms: list) -> dict:
+    return {"median_ms": statistics.median(ms), "mean_ms": statistics.mean(ms)}
+
+
+def gcn_train_step(g, F: int, args, dev) -> dict:
+    """One training step of the drop-in Graph_conv_layer(F, F) at cfg2 (GCN/GCN.py:41-47 under
+    GCN/train_eval.py:43-48's loss.backward()), as a hidden layer (dX needed too): forward =
+    MFMA transform into the column-degree order + XCD-sliced SpMM with the bias epilogue;
+    backward = SpMM over A^T (A itself: the normalised adjacency is symmetric) + MFMA transform
+    (dX = dS W) + hipBLASLt GEMM (dW = dS^T X) + column sums (db). Each backward component is
+    also timed alone; the backward SpMM carries its own roofline (compulsory bytes, as the
+    forward's)."""
+    from graphneuralnetwork_amd.gcn import Graph_conv_layer
+    from graphneuralnetwork_amd.ops import gcn_transform, spmm_forward
+    gen = torch.Generator(device=dev).manual_seed(1)
+    layer = Graph_conv_layer(F, F).to(dev)
+    X = torch.randn(g.n_cols, F, device=dev, generator=gen).requires_grad_(True)
+    gy = torch.randn(g.n_rows, F, device=dev, generator=gen)
+    steps = max(3, min(args.steps, 10))
+
+    def step():
+        X.grad = None
+        layer.zero_grad(set_to_none=True)
+        layer(X, g).backward(gy)
+
+    step_ms = time_steps(step, steps, 2, dev)[0]
+    fwd_ms = time_steps(lambda: layer(X, g), steps, 2, dev)[0]
+    keep = {"y": layer(X, g)}
+    bwd_ms = time_steps(lambda: keep["y"].backward(gy, retain_graph=True), steps, 2, dev)[0]
+    del keep
+    gt = g.transpose()
+    ds = torch.empty(g.n_rows, F, device=dev)
+    spmm_ms = time_steps(lambda: spmm_forward(gt, gy, out=ds), steps, 2, dev)[0]
+    Wt = layer.dense.weight.detach().t().contiguous()
+    Xd = X.detach()
+    dx_ms = time_steps(lambda: gcn_transform(ds, Wt), steps, 2, dev)[0]
+    dw_ms = time_steps(lambda: torch.mm(ds.t(), Xd), steps, 2, dev)[0]
+    db_ms = time_steps(lambda: gy.sum(0), steps, 2, dev)[0]
+    comp = compulsory_bytes(g.nnz, g.n_rows, g.n_cols, F)
+    t_sp = statistics.mean(spmm_ms) / 1e3
+    nbytes_rows = g.n_rows * 4 * F
+    res = {
+        "what": "Graph_conv_layer(%d, %d) forward + loss.backward() at cfg2, X requiring grad "
+                "(a hidden layer: dX, dW, db)" % (F, F),
+        "step_ms": statistics.median(step_ms), "forward_ms": statistics.median(fwd_ms),
+        "backward_ms": statistics.median(bwd_ms),
+        "edges_per_s": 2 * g.nnz / (statistics.median(step_ms) / 1e3),
+        "edges_note": "two SpMM passes per step (forward A S, backward A^T dY)",
+        "backward_components_ms": {
+            "spmm_dS_AT_dY": statistics.median(spmm_ms),
+            "transform_dX_dS_W": statistics.median(dx_ms),
+            "gemm_dW_dST_X_hipblaslt": statistics.median(dw_ms),
+            "colsum_db": statistics.median(db_ms)},
+        "backward_spmm_graph": "A itself (symmetric: no transposed copy)" if gt is g else
+                               "transposed CSR",
+        "roofline_backward_spmm": {
+            "bound": "hbm", "achieved": comp / t_sp / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": comp / t_sp / 1e9 / HBM_PEAK_GBPS, "compulsory_bytes": comp,
+            "avg_launch_ms": t_sp * 1e3,
+            "kernel": "spmm_csr_kernel pass 1 + pass 2 (XCD-sliced hub staging of the natural-"
+                      "order graph: dY is not in the column order) + fix-up"},
+        "roofline_backward_gemm_dW": {
+            "bound": "hbm", "achieved": 2 * nbytes_rows / (statistics.mean(dw_ms) / 1e3) / 1e9,
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": 2 * nbytes_rows / (statistics.mean(dw_ms) / 1e3) / 1e9 / HBM_PEAK_GBPS,
+            "bytes": 2 * nbytes_rows,
+            "note": "dS and X read once (K = n_rows reduction, %.1f GFLOP)"
+                    % (2 * g.n_rows * F * F / 1e9)},
+        "roofline_backward_transform_dX": {
+            "bound": "hbm", "achieved": 2 * nbytes_rows / (statistics.mean(dx_ms) / 1e3) / 1e9,
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": 2 * nbytes_rows / (statistics.mean(dx_ms) / 1e3) / 1e9 / HBM_PEAK_GBPS,
+            "bytes": 2 * nbytes_rows, "note": "dS read, dX written"},
+    }
+    if not args.no_cpu_baseline:
+        try:
+            res["cpu_reference_ops"] = cpu_gcn_train_ops(g, F)
+        except Exception as e:  # reported, never the target
+            res["cpu_reference_ops"] = {"error": repr(e)}
+    del X, gy, ds, layer
+    torch.cuda.empty_cache()
+    return res
+
+
+def cpu_gcn_train_ops(g, F: int, max_nnz: int = 2_000_000, budget_s: float = 10.0) -> dict:
+    """The reference's CPU training step of one Graph_conv_layer (GCN/GCN.py:41-47: nn.Linear +
+    torch.spmm on the uncoalesced COO + bias; loss.backward()) with torch CPU autograd, every
+    allowed host thread, on the leading rows holding <= max_nnz edges (the COO is [rows, n]:
+    X and dX stay full size)."""
+    threads = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        rowptr = g.rowptr.cpu()
+        r1 = max(1, min(g.n_rows, int(torch.searchsorted(rowptr, max_nnz, right=True)) - 1))
+        e1 = int(rowptr[r1])
+        rows = torch.repeat_interleave(torch.arange(r1), rowptr[1:r1 + 1] - rowptr[:r1])
+        cols = g.col[:e1].cpu().to(torch.int64)
+        order = torch.argsort(cols, stable=True)
+        coo = torch.sparse_coo_tensor(torch.stack([rows[order], cols[order]]),
+                                      g.val[:e1].cpu()[order], (r1, g.n_cols))
+        lin = torch.nn.Linear(F, F, bias=False)
+        bias = torch.nn.Parameter(torch.zeros(F))
+        X = torch.randn(g.n_cols, F, requires_grad=True)
+        gy = torch.randn(r1, F)
+
+        def step():
+            X.grad = None
+            lin.zero_grad(set_to_none=True)
+            bias.grad = None
+            (torch.spmm(coo, lin(X)) + bias).backward(gy)
+
+        t, runs = _cpu_time(step, budget_s)
+        return {"torch_cpu_train_step": {"value": 2 * e1 / t, "unit": "edges/s",
+                                         "threads": threads, "seconds_per_step": t,
+                                         "runs": runs},
+                "note": f"torch CPU forward + backward of the reference layer on rows 0..{r1} "
+                        f"({e1} edges; the X W^T transform and its backward over all "
+                        f"{g.n_cols} rows), edges counted twice (forward + backward SpMM)"}
+    finally:
+        torch.set_num_threads(prev)
+
+
+def gcn_model_forward(g, F: int, args, dev) -> dict:
+    """The drop-in two-layer GCN_Model(F, F, F, 2) forward at the north star (GCN/GCN.py:21-27:
+    Graph_conv_layer -> ReLU -> Dropout (eval: identity) -> Graph_conv_layer), each layer the
+    MFMA transform into the column order + the XCD-sliced SpMM."""
+    from graphneuralnetwork_amd.gcn import GCN_Model
+    gen = torch.Generator(device=dev).manual_seed(2)
+    net = GCN_Model(F, F, F, 2, 0.5).to(dev).eval()
+    X = torch.randn(g.n_cols, F, device=dev, generator=gen)
+    with torch.no_grad():
+        ms = time_steps(lambda: net(X, g), max(3, min(args.steps, 10)), 2, dev)[0]
+    t = statistics.median(ms)
+    res = {"what": "GCN_Model(%d, %d, %d, num_layers=2).eval() forward at the north star" % (F, F, F),
+           "forward_ms": t, "value": 2 * g.nnz / (t / 1e3), "unit": "edges/s",
+           "edges_note": "two aggregation layers per forward"}
+    if not args.no_cpu_baseline:
+        try:
+            res["cpu_baseline"] = cpu_gcn_layer_rate(g, F)
+        except Exception as e:
+            res["cpu_baseline"] = {"value": None, "error": repr(e)}
+    del X, net
+    torch.cuda.empty_cache()
+    return res
+
+
+def cpu_gcn_layer_rate(g, F: int, max_nnz: int = 25_000_000) -> dict:
+    """The CPU rate of the GCN layer math on a row block (rows 0..r1 holding <= max_nnz
+    entries): the dense transform of those rows (torch CPU, row-separable) + the C oracle's
+    SpMM of those rows; a 2-layer forward is two such passes, so edges/s is the same."""
+    from oracle import c_oracle
+    threads = cpu_threads()
+    c_oracle.set_threads(threads)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        rowptr = g.rowptr.cpu().numpy()
+        r1 = max(1, min(g.n_rows, int(np.searchsorted(rowptr, max_nnz, side="right")) - 1))
+        e1 = int(rowptr[r1])
+        Xs = torch.randn(r1, F)
+        W = torch.randn(F, F)
+        S = torch.randn(g.n_cols, F).numpy()
+        col, val = g.col.cpu().numpy(), g.val.cpu().numpy()
+        t_mm, _ = _cpu_time(lambda: Xs @ W.t(), 5.0)
+        c_oracle.spmm_csr(rowptr, col, val, S, None, 0, min(r1, 20000))
+        t_sp, runs = _cpu_time(lambda: c_oracle.spmm_csr(rowptr, col, val, S, None, 0, r1), 10.0)
+        return {"value": e1 / (t_mm + t_sp), "unit": "edges/s", "cores": threads, "kind": "port",
+                "seconds_per_layer_sample": t_mm + t_sp,
+                "sample": f"one layer on rows 0..{r1} ({e1} entries): torch CPU X W^T of those "
+                          f"rows ({t_mm:.3f} s) + oracle/spmm_oracle.c SpMM of those rows "
+                          f"({t_sp:.3f} s, median of {runs})",
+                "host": host_cpu_info(threads)}
+    finally:
+        torch.set_num_threads(prev)
 
 
 def run_gcn(args, dev, rank: int, world: int, workload: str, edges_np=None, extras=False):
@@ -1099,6 +1464,12 @@ def run_gcn(args, dev, rank: int, world: int, workload: str, edges_np=None, extr
         log(f"[bench] Graph_conv_layer timed: {layer_ms:.3f} ms")
         torch.cuda.empty_cache()
 
+    train = model_fwd = None
+    if world == 1 and not args.no_train and workload == "cfg2":
+        train = gcn_train_step(g, F, args, dev)
+    if world == 1 and not args.no_layer and workload == "ns":
+        model_fwd = gcn_model_forward(g, F, args, dev)
+
     tf = {}
     if world == 1:
         tpath = Path(args.traffic_json) if (args.traffic_json and not extras) else \
@@ -1151,6 +1522,8 @@ def run_gcn(args, dev, rank: int, world: int, workload: str, edges_np=None, extr
             "first_step_s": BUILD_INFO.get("first_step_s"),
             **({"gcn_layer_ms": layer_ms, "gcn_layer_transform": transform_note()}
                if layer_ms is not None else {}),
+            **({"train_step": train} if train is not None else {}),
+            **({"gcn_model_forward": model_fwd} if model_fwd is not None else {}),
             **({"partition_build_s": BUILD_INFO.get("partition_build_s"),
                 "row_bounds": part.bounds,
                 "balance_max_mean_cost": BUILD_INFO.get("balance_max_mean_cost"),
@@ -1184,7 +1557,8 @@ def _sub(res: dict) -> dict:
             "config", "roofline", "cpu_baseline", "cpu_reference_ops",
             "first_step_s", "graph_build_s", "gcn_layer_ms", "layer_ms", "aggregate_ms",
             "forward_ms", "forward_hipgraph_ms", "sample_ms", "batch_ms", "project_ms",
-            "project_tflops", "project_arithmetic")
+            "project_tflops", "project_arithmetic", "train_step", "gcn_model_forward",
+            "aggregators")
     return {k: res[k] for k in keep if k in res}
 
 
@@ -1204,7 +1578,14 @@ def main():
     ap.add_argument("--no-cold", action="store_true",
                     help="skip the cache-cold step timing (profiling runs: exactly warmup + steps)")
     ap.add_argument("--no-layer", action="store_true",
-                    help="skip the Graph_conv_layer (GEMM + SpMM) timing beside the aggregation")
+                    help="skip the Graph_conv_layer (GEMM + SpMM) timing beside the aggregation "
+                         "(and the two-layer GCN_Model forward at the north star)")
+    ap.add_argument("--no-train", action="store_true",
+                    help="skip the training-step (forward + backward) sub-objects (cfg2 GCN "
+                         "layer, cfg3 GAT layer)")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the cfg4 MAX / MAXPOOL aggregator sub-object (profiling runs: "
+                         "only the headline kernels launch)")
     ap.add_argument("--no-cpu-reference", action="store_true",
                     help="skip the torch CPU operator lines (torch.spmm COO / sparse.mm CSR)")
     ap.add_argument("--exchange", default="cover", choices=["cover", "gather"],

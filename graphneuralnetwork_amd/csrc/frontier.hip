@@ -30,6 +30,8 @@ constexpr int kHotWords = 2048;                 // 8 KiB of LDS per workgroup
 constexpr int64_t kHotIds = 32 * kHotWords;     // ids 0 .. 65535
 constexpr int kMarkBlocks = 256;                // workgroups of a mark launch (grid-stride)
 
+static inline int64_t fr_align_bytes(int64_t v) { return (v + 255) / 256 * 256; }
+
 __device__ __forceinline__ void mark_bit(uint32_t* bits, int64_t v) {
   uint32_t* w = bits + (v >> 5);
   const uint32_t m = 1u << (v & 31);
@@ -125,6 +127,7 @@ __global__ void frontier_rank_kernel(const int64_t* __restrict__ ids, int64_t n,
 constexpr int32_t kBatchErrOverflow = 4;  // a frontier larger than its buffer (cannot happen
                                           // with the caller's bounds; checked anyway)
 constexpr int32_t kBatchErrMark = 8;      // a listed id outside [0, n_nodes) (a failed draw)
+constexpr int32_t kBatchErrInternal = 16; // the frontier scan's look-back did not complete
 
 // rows of list a (a_n rows, live count *a_dev) and of list b (b_rows rows of b_ld ids, live
 // rows *b_dev) in one grid: b's ids are the a rows' sampled neighbours
@@ -184,6 +187,269 @@ __global__ void batch_rank_kernel(const int64_t* __restrict__ a, int64_t a_n,
 __global__ void batch_init_kernel(int64_t* __restrict__ stat, int n_layers, int64_t n_seeds) {
   const int i = threadIdx.x;
   if (i <= n_layers) stat[i] = i == 0 ? n_seeds : 0;  // sizes |S_i|, then the error word
+}
+
+// ---- the 3-launch L-hop batch (gnn_sample_layers) -------------------------------------------
+// The frontier marks are byte flags (flags[v] = 1, plain stores: idempotent, no atomics), set by
+// the hop's sampling kernel itself. One scan kernel per hop transition turns them into the
+// frontier: a workgroup per tile of 1024 words (32 flags per word), the tile prefixes chained
+// by a decoupled look-back (each tile publishes its count, then its inclusive prefix, in ONE
+// 8-byte agent-scope atomic word {tag, kind, value}); it writes the frontier ids, the word
+// prefixes / bitmaps the position lookups need, and clears the flags it read (the workspace
+// is left all-zero for the next call: no memset). The next hop's sampling kernel also ranks the
+// previous hop's lists (its extra workgroups) and derives the previous hop's sampler errors.
+// For L = 2 ([25, 10]): sample + mark, scan + emit, sample + rank = 3 launches.
+constexpr int kScanTileWords = 1024;  // 256 threads x 4 words
+constexpr uint64_t kTileAgg = 1, kTileInc = 2;
+
+struct SampleWs {
+  uint8_t* flags;   // [32 * n_words] (zero between calls)
+  uint32_t* bits;   // [n_words] flag bitmap of the marked words (written where non-zero)
+  uint32_t* pre;    // [n_words] frontier position of each marked word's first id
+  uint64_t* tile;   // [n_tiles] look-back words {tag:30 | kind:2 | value:32}
+  uint64_t* ctl;    // [0] tag base (bumped by L per call), [1] tile ticket of the next scan
+};
+
+static int64_t sw_tiles(int64_t n_words) { return (n_words + kScanTileWords - 1) / kScanTileWords; }
+
+static int64_t sw_bytes(int64_t n_graph, SampleWs* w, char* base) {
+  const int64_t n_words = (n_graph + 31) / 32;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += fr_align_bytes(bytes);
+    return p;
+  };
+  char* f = take(32 * n_words);
+  char* b = take(4 * n_words);
+  char* pr = take(4 * n_words);
+  char* t = take(8 * sw_tiles(n_words));
+  char* c = take(64);
+  if (w) {
+    w->flags = reinterpret_cast<uint8_t*>(f);
+    w->bits = reinterpret_cast<uint32_t*>(b);
+    w->pre = reinterpret_cast<uint32_t*>(pr);
+    w->tile = reinterpret_cast<uint64_t*>(t);
+    w->ctl = reinterpret_cast<uint64_t*>(c);
+  }
+  return off;
+}
+
+struct HopArgs {
+  const int64_t* rowptr;
+  const int32_t* col;
+  int64_t n_graph;
+  // this hop's draw: rows [0, live) of nodes, live = min(*n_dev, cap) (n_dev NULL: cap)
+  const int64_t* nodes;
+  int64_t cap;
+  const int64_t* n_dev;
+  int k;
+  int64_t ld;
+  bool self;
+  uint64_t seed;
+  int64_t* out;
+  int32_t* err;        // stat[L]'s low word
+  bool own_err;        // the last hop: the sampler records its own errors
+  uint8_t* flags;      // non-NULL: mark (a scan follows)
+  // first launch: stat[0..L] and the control words
+  int64_t* stat;
+  int n_layers;
+  int64_t n_seeds;
+  uint64_t* ctl;       // non-NULL: reset the next scan's tile ticket (and, first launch, bump the tag)
+  bool first;
+  // the previous hop's lists to rank (NULL: none)
+  const int64_t* p_nodes;
+  int64_t p_cap;
+  const int64_t* p_dev;
+  const int64_t* p_nbrs;
+  int64_t p_ld;
+  const uint32_t* bits;
+  const uint32_t* pre;
+  int64_t* p_cmap;
+  int64_t* p_nmap;
+  int64_t sample_blocks;
+};
+
+template <int LPN>
+__global__ __launch_bounds__(256) void batch_hop_kernel(HopArgs A) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && A.ctl != nullptr) {
+    if (A.first) A.ctl[0] += static_cast<uint64_t>(A.n_layers);  // this call's scan tags
+    A.ctl[1] = 0;                                                 // the next scan's tickets
+  }
+  if (A.first && blockIdx.x == 0 && threadIdx.x <= A.n_layers)
+    A.stat[threadIdx.x] = threadIdx.x == 0 ? A.n_seeds : 0;      // sizes, then the error word
+  if (static_cast<int64_t>(blockIdx.x) < A.sample_blocks) {
+    const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+    const int64_t live = live_rows(A.cap, A.n_dev);
+    int32_t* err = A.own_err ? A.err : nullptr;
+    if (A.flags)
+      sample_lane_wave<LPN, true>(A.rowptr, A.col, A.n_graph, A.nodes, live, wave, A.k, A.ld,
+                                  A.self, A.seed, A.out, err, A.flags);
+    else
+      sample_lane_wave<LPN, false>(A.rowptr, A.col, A.n_graph, A.nodes, live, wave, A.k, A.ld,
+                                   A.self, A.seed, A.out, err, nullptr);
+    return;
+  }
+  if (A.p_nodes == nullptr) return;
+  // positions of the previous hop's nodes and neighbour ids in the frontier just built, and
+  // that hop's sampler errors, derived from its lists (its draw ran with err == NULL):
+  // node outside [0, n) -> 2 | 8, node without neighbours -> 1, listed id outside -> 8
+  const int64_t live = live_rows(A.p_cap, A.p_dev);
+  const int64_t total = live * (1 + A.p_ld);
+  const int64_t stride = (static_cast<int64_t>(gridDim.x) - A.sample_blocks) * blockDim.x;
+  int32_t e = 0;
+  for (int64_t t = (static_cast<int64_t>(blockIdx.x) - A.sample_blocks) * blockDim.x + threadIdx.x;
+       t < total; t += stride) {
+    const bool node = t < live;
+    const int64_t v = node ? A.p_nodes[t] : A.p_nbrs[t - live];
+    int64_t p = -1;
+    if (v >= 0 && v < A.n_graph) {
+      const int64_t w = v >> 5;
+      p = static_cast<int64_t>(A.pre[w]) + __popc(A.bits[w] & ((1u << (v & 31)) - 1u));
+      if (node && A.rowptr[v + 1] == A.rowptr[v]) e |= kSampleErrEmpty;
+    } else {
+      e |= node ? (kSampleErrRange | kBatchErrMark) : kBatchErrMark;
+    }
+    if (node)
+      A.p_cmap[t] = p;
+    else
+      A.p_nmap[t - live] = p;
+  }
+  if (e) atomicOr(A.err, e);
+}
+
+__device__ __forceinline__ uint64_t tile_word(uint64_t tag, uint64_t kind, uint32_t v) {
+  return (tag << 34) | (kind << 32) | v;
+}
+
+// frontier = the flagged ids in ascending order (out[0 .. min(total, cap)), *count), the word
+// prefixes and bitmaps of the flagged words, flags cleared; one workgroup per tile, tiles taken
+// by ticket (ctl[1], reset by the launch before) so that a tile waits only on tiles that an
+// earlier-started workgroup holds
+__global__ __launch_bounds__(256) void batch_scan_kernel(uint8_t* __restrict__ flags,
+                                                         int64_t n_words, uint32_t* __restrict__ bits,
+                                                         uint32_t* __restrict__ pre,
+                                                         uint64_t* __restrict__ tile_st,
+                                                         uint64_t* __restrict__ ctl, int tag_off,
+                                                         int64_t cap, int64_t* __restrict__ out,
+                                                         int64_t* __restrict__ count,
+                                                         int32_t* __restrict__ err) {
+  __shared__ int64_t s_tile;
+  __shared__ uint32_t s_wave[4];
+  __shared__ uint32_t s_prefix;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0)
+    s_tile = static_cast<int64_t>(__hip_atomic_fetch_add(ctl + 1, uint64_t(1), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT));
+  __syncthreads();
+  const int64_t tile = s_tile;
+  if (tile >= (n_words + kScanTileWords - 1) / kScanTileWords) {  // tickets not reset: never
+    if (tid == 0) atomicOr(err, kBatchErrInternal);                // writes out of range
+    return;
+  }
+  const uint64_t tag = (ctl[0] + static_cast<uint64_t>(static_cast<int64_t>(tag_off))) & 0x3fffffffull;
+  const int64_t w0 = tile * kScanTileWords + tid * 4;
+  uint32_t mask[4];
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t w = w0 + q;
+    mask[q] = 0;
+    if (w < n_words) {
+      const uint4* f = reinterpret_cast<const uint4*>(flags + 32 * w);
+      const uint4 a = f[0], b = f[1];
+      const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      uint32_t m = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+          m |= ((d[j] >> (8 * bb)) & 0xffu ? 1u : 0u) << (4 * j + bb);
+      }
+      mask[q] = m;
+      cnt += __popc(m);
+    }
+  }
+  // block-wide exclusive scan of the thread counts
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_wave[wid] = incl;
+  __syncthreads();
+  uint32_t wave_off = 0, agg = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    wave_off += q < wid ? s_wave[q] : 0;
+    agg += s_wave[q];
+  }
+  const uint32_t excl = wave_off + incl - cnt;
+  // publish the tile's count, look back for the prefix of the tiles before it
+  if (wid == 0) {
+    if (lane == 0)
+      __hip_atomic_store(tile_st + tile, tile_word(tag, tile == 0 ? kTileInc : kTileAgg, agg),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t prefix = 0;
+    int64_t look = tile - 1;  // the nearest tile not yet summed
+    uint32_t polls = 0;       // every wave leaves: a tile that never publishes is an error
+    while (look >= 0) {
+      const int64_t j = look - lane;
+      uint64_t sw = tile_word(tag, kTileInc, 0);  // before tile 0: an inclusive prefix of 0
+      bool ready = true;
+      if (j >= 0) {
+        sw = __hip_atomic_load(tile_st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ready = (sw >> 34) == tag && ((sw >> 32) & 3) != 0;
+      }
+      if (__ballot(!ready)) {  // a tile of this window has not published yet
+        if (++polls > (1u << 22)) {
+          if (lane == 0) atomicOr(err, kBatchErrInternal);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      const uint64_t inc = __ballot(((sw >> 32) & 3) == kTileInc);
+      const int stop = inc ? __ffsll(static_cast<unsigned long long>(inc)) - 1 : 63;
+      uint32_t v = lane <= stop ? static_cast<uint32_t>(sw) : 0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      prefix += v;
+      if (inc) break;
+      look -= 64;
+    }
+    if (lane == 0) {
+      if (tile > 0)
+        __hip_atomic_store(tile_st + tile, tile_word(tag, kTileInc, prefix + agg),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_prefix = prefix;
+      if ((tile + 1) * kScanTileWords >= n_words) {  // the last tile: the frontier size
+        const int64_t total = static_cast<int64_t>(prefix) + agg;
+        if (total > cap) atomicOr(err, kBatchErrOverflow);
+        count[0] = total < cap ? total : cap;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t o = s_prefix + excl;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t m = mask[q];
+    if (m == 0) continue;
+    const int64_t w = w0 + q;
+    bits[w] = m;
+    pre[w] = o;
+    uint4* f = reinterpret_cast<uint4*>(flags + 32 * w);
+    f[0] = make_uint4(0, 0, 0, 0);
+    f[1] = make_uint4(0, 0, 0, 0);
+    while (m) {
+      const int t = __ffs(m) - 1;
+      if (o < cap) out[o] = w * 32 + t;
+      ++o;
+      m &= m - 1;
+    }
+  }
 }
 
 static unsigned fr_grid(int64_t n) {
@@ -293,6 +559,28 @@ extern "C" int gnn_frontier_rank(const int64_t* ids, int64_t n, int64_t n_nodes,
   return launch_status();
 }
 
+extern "C" int64_t gnn_sample_layers_workspace_bytes(int64_t n_graph) {
+  if (n_graph < 1) return GNN_E_ARG;
+  return sw_bytes(n_graph, nullptr, nullptr);
+}
+
+template <int LPN>
+static void launch_hop(HopArgs A, int64_t rank_blocks, hipStream_t s) {
+  const int64_t per_block = 4 * (kWave / LPN);  // 4 waves of 64 / LPN nodes
+  A.sample_blocks = (A.cap + per_block - 1) / per_block;
+  hipLaunchKernelGGL(batch_hop_kernel<LPN>, dim3(static_cast<unsigned>(A.sample_blocks + rank_blocks)),
+                     dim3(256), 0, s, A);
+}
+
+static void launch_hop_k(const HopArgs& A, int64_t rank_blocks, hipStream_t s) {
+  if (A.k <= 16)
+    launch_hop<16>(A, rank_blocks, s);
+  else if (A.k <= 32)
+    launch_hop<32>(A, rank_blocks, s);
+  else
+    launch_hop<64>(A, rank_blocks, s);
+}
+
 extern "C" int gnn_sample_layers(const int64_t* rowptr, const int32_t* col, int64_t n_graph,
                                  const int64_t* seeds, int64_t n_seeds, int32_t n_layers,
                                  const int64_t* fanouts, const uint64_t* layer_seeds,
@@ -304,46 +592,70 @@ extern "C" int gnn_sample_layers(const int64_t* rowptr, const int32_t* col, int6
       !fanouts || !layer_seeds || !caps || !nbrs || !stat || !workspace)
     return GNN_E_ARG;
   if (n_layers > 1 && (!layers || !center_maps || !neigh_maps)) return GNN_E_ARG;
-  if (workspace_bytes < gnn_frontier_workspace_bytes(n_graph)) return GNN_E_ARG;
+  if (workspace_bytes < gnn_sample_layers_workspace_bytes(n_graph)) return GNN_E_ARG;
   if (caps[0] != n_seeds) return GNN_E_ARG;
   for (int i = 0; i < n_layers; ++i) {
-    if (fanouts[i] < 1 || fanouts[i] > kMaxFanout || caps[i] < 1 || !nbrs[i]) return GNN_E_ARG;
+    if (fanouts[i] < 1 || caps[i] < 1 || !nbrs[i]) return GNN_E_ARG;
+    if (fanouts[i] > 64) return GNN_E_UNSUPPORTED;  // the lane sampler's widest group
     const int64_t ld = fanouts[i] + (append_self ? 1 : 0);
     if (caps[i] > (INT64_C(1) << 40) / ld) return GNN_E_UNSUPPORTED;
     if (i + 1 < n_layers) {
       if (!layers[i + 1] || !center_maps[i] || !neigh_maps[i] || caps[i + 1] < 1)
         return GNN_E_ARG;
-      if (caps[i] * (ld + 1) > 0xffffffffLL) return GNN_E_UNSUPPORTED;  // 32-bit word prefixes
+      if (caps[i] * (ld + 1) > 0xffffffffLL) return GNN_E_UNSUPPORTED;  // 32-bit prefixes
     }
   }
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t n_words = (n_graph + 31) / 32;
-  FrontierWs f = fr_layout(workspace, n_graph, workspace_bytes);
+  SampleWs w;
+  sw_bytes(n_graph, &w, static_cast<char*>(workspace));
   int32_t* err = reinterpret_cast<int32_t*>(stat + n_layers);  // low word of the last entry
-  // n_layers + 1 <= 65 entries (sizes, then the error word): one workgroup of 128 threads
-  hipLaunchKernelGGL(batch_init_kernel, dim3(1), dim3(128), 0, s, stat, n_layers, n_seeds);
+  if (n_layers == 1) {  // one hop: no frontier; the sizes / error word first
+    hipLaunchKernelGGL(batch_init_kernel, dim3(1), dim3(128), 0, s, stat, n_layers, n_seeds);
+    launch_sample(rowptr, col, n_graph, seeds, n_seeds, nullptr, static_cast<int>(fanouts[0]),
+                  fanouts[0] + (append_self ? 1 : 0), append_self != 0, layer_seeds[0], nbrs[0],
+                  err, s);
+    return launch_status();
+  }
+  const int64_t rank_blocks = 512;  // grid-stride over the ranked lists
   for (int i = 0; i < n_layers; ++i) {
-    const int64_t* nodes = i == 0 ? seeds : layers[i];
-    const int64_t* n_dev = stat + i;
-    const int k = static_cast<int>(fanouts[i]);
-    const int64_t ld = k + (append_self ? 1 : 0);
-    launch_sample(rowptr, col, n_graph, nodes, caps[i], n_dev, k, ld, append_self != 0,
-                  layer_seeds[i], nbrs[i], err, s);
+    HopArgs A{};
+    A.rowptr = rowptr;
+    A.col = col;
+    A.n_graph = n_graph;
+    A.nodes = i == 0 ? seeds : layers[i];
+    A.cap = caps[i];
+    A.n_dev = i == 0 ? nullptr : stat + i;
+    A.k = static_cast<int>(fanouts[i]);
+    A.ld = fanouts[i] + (append_self ? 1 : 0);
+    A.self = append_self != 0;
+    A.seed = layer_seeds[i];
+    A.out = nbrs[i];
+    A.err = err;
+    A.own_err = i + 1 == n_layers;
+    A.flags = i + 1 < n_layers ? w.flags : nullptr;
+    A.stat = stat;
+    A.n_layers = n_layers;
+    A.n_seeds = n_seeds;
+    A.ctl = w.ctl;
+    A.first = i == 0;
+    if (i > 0) {  // rank hop i - 1's lists in the frontier S_i the scan just built
+      A.p_nodes = i == 1 ? seeds : layers[i - 1];
+      A.p_cap = caps[i - 1];
+      A.p_dev = i == 1 ? nullptr : stat + i - 1;
+      A.p_nbrs = nbrs[i - 1];
+      A.p_ld = fanouts[i - 1] + (append_self ? 1 : 0);
+      A.bits = w.bits;
+      A.pre = w.pre;
+      A.p_cmap = center_maps[i - 1];
+      A.p_nmap = neigh_maps[i - 1];
+    }
+    launch_hop_k(A, i > 0 ? rank_blocks : 0, s);
     if (i + 1 == n_layers) break;
-    // S_{i+1} = sorted distinct ids of S_i and its sampled neighbours, and the maps into it
-    hipError_t e = hipMemsetAsync(f.bits, 0, 4 * n_words, s);
-    if (e != hipSuccess) return static_cast<int>(e);
-    const int64_t listed = caps[i] * (ld + 1);
-    hipLaunchKernelGGL(batch_mark_kernel, dim3(mark_grid(listed)), dim3(256), 0, s, nodes, caps[i],
-                       n_dev, nbrs[i], caps[i], n_dev, ld, n_graph, f.bits, err);
-    e = rocprim::exclusive_scan(f.temp, f.temp_bytes, popc_iter(f.bits), f.pre, 0u,
-                                static_cast<size_t>(n_words), rocprim::plus<uint32_t>(), s);
-    if (e != hipSuccess) return static_cast<int>(e);
-    hipLaunchKernelGGL(batch_emit_kernel, dim3(fr_grid(n_words)), dim3(256), 0, s, f.bits, f.pre,
-                       n_words, caps[i + 1], layers[i + 1], stat + i + 1, err);
-    hipLaunchKernelGGL(batch_rank_kernel, dim3(fr_grid(listed)), dim3(256), 0, s, nodes, caps[i],
-                       n_dev, nbrs[i], caps[i], n_dev, ld, n_graph, f.bits, f.pre, center_maps[i],
-                       neigh_maps[i]);
+    // S_{i+1} = the flagged ids of S_i and nbrs[i] (tag i of this call's L)
+    hipLaunchKernelGGL(batch_scan_kernel, dim3(static_cast<unsigned>(sw_tiles(n_words))), dim3(256),
+                       0, s, w.flags, n_words, w.bits, w.pre, w.tile, w.ctl, i + 1 - n_layers,
+                       caps[i + 1], layers[i + 1], stat + i + 1, err);
   }
   return launch_status();
 }

@@ -161,22 +161,23 @@ __global__ __launch_bounds__(256) void sample_kernel(const int64_t* __restrict__
 // final picks, one ballot decides. Same picks as sample_reg_kernel, bit for bit, with a whole
 // wave per 64 / LPN nodes instead of one thread per node (a thread-serial Floyd over k = 25 took
 // 30.6 us for the 8192 seeds of a cfg4 batch: 128 waves for 256 CUs, profiles/r03ac_cfg4_*).
-template <int LPN>
-__global__ __launch_bounds__(256) void sample_lane_kernel(const int64_t* __restrict__ rowptr,
-                                                          const int32_t* __restrict__ col,
-                                                          int64_t n_graph,
-                                                          const int64_t* __restrict__ nodes,
-                                                          int64_t n, const int64_t* n_dev, int k,
-                                                          int64_t ld, bool self, uint64_t seed,
-                                                          int64_t* __restrict__ out,
-                                                          int32_t* __restrict__ err) {
+// The body of the lane-parallel sampler for one wave: node groups of LPN lanes, node i of
+// `nodes` = wave * (64 / LPN) + lane / LPN. err == nullptr: the caller derives the sampler's
+// error bits elsewhere (the fused batch does, in the next hop's rank pass). MARK: every drawn
+// neighbour id and the node itself (ids inside [0, n_graph)) get flags[id] = 1 -- the batch
+// frontier's marks, fused into the draw (frontier.hip, gnn_sample_layers).
+template <int LPN, bool MARK>
+__device__ __forceinline__ void sample_lane_wave(const int64_t* __restrict__ rowptr,
+                                                 const int32_t* __restrict__ col, int64_t n_graph,
+                                                 const int64_t* __restrict__ nodes, int64_t live,
+                                                 int64_t wave, int k, int64_t ld, bool self,
+                                                 uint64_t seed, int64_t* __restrict__ out,
+                                                 int32_t* err, uint8_t* __restrict__ flags) {
   constexpr int GPW = kWave / LPN;  // node groups per wave
   const int lane = threadIdx.x & (kWave - 1);
   const int sub = lane & (LPN - 1);
   const int gbase = lane & ~(LPN - 1);
-  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t i = wave * GPW + lane / LPN;
-  const int64_t live = live_rows(n, n_dev);
   if (wave * GPW >= live) return;  // wave-uniform: every group of the wave is past the end
   const bool act = i < live;
   int64_t v = act ? nodes[i] : -1;
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(256) void sample_lane_kernel(const int64_t* __restr
     b = rowptr[v];
     deg = rowptr[v + 1] - b;
   }
-  if (act && sub == 0) {
+  if (err != nullptr && act && sub == 0) {
     if (!ok) atomicOr(err, kSampleErrRange);
     else if (deg == 0) atomicOr(err, kSampleErrEmpty);
   }
@@ -211,8 +212,37 @@ __global__ __launch_bounds__(256) void sample_lane_kernel(const int64_t* __restr
   }
   if (!act) return;
   int64_t* o = out + i * ld;
-  if (sub < k) o[sub] = good ? static_cast<int64_t>(col[b + pick]) : -1;
-  if (self && sub == 0) o[k] = v;
+  if (sub < k) {
+    const int64_t id = good ? static_cast<int64_t>(col[b + pick]) : -1;
+    o[sub] = id;
+    if (MARK && id >= 0 && id < n_graph) flags[id] = 1;
+  }
+  if (sub == 0) {
+    if (self) o[k] = v;
+    if (MARK && ok) flags[v] = 1;
+  }
+}
+
+// Lane-parallel form of the same draws (fanouts k <= LPN <= 64): a group of LPN lanes per node,
+// lane `sub` owns draw `sub`. The draws of Floyd's algorithm do not depend on earlier picks
+// (draw jj is uniform_below(seed, i, j, j + 1), j = deg - k + jj), only the resolution does
+// ("already picked? then take j"), so every lane draws at once and the resolution runs as k
+// group-wide steps: step jj broadcasts lane jj's draw, the lanes q < jj compare it with their
+// final picks, one ballot decides. Same picks as sample_reg_kernel, bit for bit, with a whole
+// wave per 64 / LPN nodes instead of one thread per node (a thread-serial Floyd over k = 25 took
+// 30.6 us for the 8192 seeds of a cfg4 batch: 128 waves for 256 CUs, profiles/r03ac_cfg4_*).
+template <int LPN>
+__global__ __launch_bounds__(256) void sample_lane_kernel(const int64_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col,
+                                                          int64_t n_graph,
+                                                          const int64_t* __restrict__ nodes,
+                                                          int64_t n, const int64_t* n_dev, int k,
+                                                          int64_t ld, bool self, uint64_t seed,
+                                                          int64_t* __restrict__ out,
+                                                          int32_t* __restrict__ err) {
+  const int64_t wave = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  sample_lane_wave<LPN, false>(rowptr, col, n_graph, nodes, live_rows(n, n_dev), wave, k, ld,
+                               self, seed, out, err, nullptr);
 }
 
 // one launch of the right kernel for fanout k (k <= kMaxFanout): rows [0, min(*n_dev, n))

@@ -10,10 +10,12 @@ exactly like GCN/GCN.py:23, which is why the layer class keeps the name
 The aggregation ``torch.spmm(adj, support) + bias`` (GCN/GCN.py:43-45) runs
 as ONE gfx950 kernel launch (CSR SpMM with the bias fused into its epilogue);
 the feature transform ``support = dense(X)`` is an fp32 MFMA GEMM: the hand-written
-``gnn_gcn_transform_f32`` at inference for the shapes it covers (F_in/F_out 64-256),
-otherwise (training, other shapes) nn.Linear on hipBLASLt.  ``adj`` may be the reference's sparse COO tensor, a sparse CSR
-tensor, a dense tensor or a prebuilt ``CsrGraph``; the CSR form is cached on
-the adjacency tensor.
+``gnn_gcn_transform_f32`` for the shapes it covers (F_in/F_out 64-256), otherwise nn.Linear
+on hipBLASLt. Under autograd the layer is one differentiable op (``ops.gcn_layer``): the same
+forward, and a backward of the SpMM over A^T (A itself: the normalised adjacency is
+symmetric), the MFMA transform for dX and a hipBLASLt GEMM for dW. ``adj`` may be the
+reference's sparse COO tensor, a sparse CSR tensor, a dense tensor or a prebuilt ``CsrGraph``;
+the CSR form is cached on the adjacency tensor.
 
 On graphs large enough for the XCD-sliced hub staging, the inference layer runs over the
 column-degree-ordered graph A P^T (``ops.column_order``): the transform writes the support
@@ -25,7 +27,7 @@ import torch
 from torch import nn
 
 from .graph import as_csr
-from .ops import column_order, gcn_transform, spmm
+from .ops import column_order, gcn_layer, gcn_transform, spmm
 
 
 class GCN_Model(nn.Module):
@@ -71,8 +73,15 @@ class Graph_conv_layer(nn.Module):
     def forward(self, X_input, adj):
         g = as_csr(adj)
         support = None
-        if X_input.is_cuda and not (torch.is_grad_enabled() and
-                                    (X_input.requires_grad or self.dense.weight.requires_grad)):
+        training = torch.is_grad_enabled() and (
+            X_input.requires_grad or self.dense.weight.requires_grad
+            or (self.bias is not None and self.bias.requires_grad))
+        if X_input.is_cuda and training and X_input.dtype == torch.float32 \
+                and X_input.shape[0] == g.n_cols:
+            # one differentiable op: MFMA transform + SpMM forward, SpMM + MFMA transform +
+            # dW GEMM backward (ops._GcnLayerFn)
+            return gcn_layer(g, X_input, self.dense.weight, self.bias)
+        if X_input.is_cuda and not training:
             order = column_order(g, self.out_features)
             if order is not None and X_input.shape[0] == g.n_cols:
                 # support rows in the column-degree order of A P^T: the SpMM then reads its hub

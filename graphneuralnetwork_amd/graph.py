@@ -472,6 +472,10 @@ class CsrGraph:
     n_cols: int
     _plans: dict = field(default_factory=dict, repr=False)
     _transpose: "CsrGraph | None" = field(default=None, repr=False)
+    # A == A^T (structure, and values to fp32 rounding): the SpMM backward's dX = A^T dY then
+    # runs over A itself, with A's cached plans and no transposed copy. Set by the GCN
+    # adjacency builders (D^-1/2 (A_sym + I) D^-1/2 is symmetric), or found by ``transpose``.
+    symmetric: bool = False
 
     @property
     def nnz(self) -> int:
@@ -540,13 +544,24 @@ class CsrGraph:
         return self._plans[key]
 
     def transpose(self) -> "CsrGraph":
-        """CSR of A^T (used by the SpMM backward: dX = A^T dY)."""
+        """CSR of A^T (used by the SpMM backward: dX = A^T dY). A symmetric graph is its own
+        transpose (no copy, its plans reused); a graph not marked symmetric whose transpose
+        turns out equal to it (same structure, values within one fp32 rounding: the
+        reference's scipy normalisation rounds v_ij and v_ji separately) is marked so and the
+        copy dropped."""
+        if self.symmetric:
+            return self
         if self._transpose is None:
             rows = torch.repeat_interleave(
                 torch.arange(self.n_rows, device=self.device, dtype=torch.int64),
                 self.rowptr[1:] - self.rowptr[:-1])
-            self._transpose = from_coo(self.col.to(torch.int64), rows, self.val,
-                                       self.n_cols, self.n_rows)
+            t = from_coo(self.col.to(torch.int64), rows, self.val, self.n_cols, self.n_rows)
+            if (self.n_rows == self.n_cols and torch.equal(t.rowptr, self.rowptr)
+                    and torch.equal(t.col, self.col)
+                    and torch.allclose(t.val, self.val, rtol=2.0 ** -23, atol=0.0)):
+                self.symmetric = True
+                return self
+            self._transpose = t
         return self._transpose
 
     def transpose_eid(self):
@@ -570,7 +585,7 @@ class CsrGraph:
 
     def to(self, device) -> "CsrGraph":
         return CsrGraph(self.rowptr.to(device), self.col.to(device), self.val.to(device),
-                        self.n_rows, self.n_cols)
+                        self.n_rows, self.n_cols, symmetric=self.symmetric)
 
 
 def _build_plan(g: CsrGraph, seg_len: int) -> RowSplitPlan:

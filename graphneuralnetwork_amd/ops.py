@@ -355,6 +355,66 @@ def spmm(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None) -> torc
     return spmm_forward(g, x, bias)
 
 
+def _transform_or_mm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x @ w^T: the MFMA transform where it covers the shape, else torch.mm (hipBLASLt)."""
+    y = gcn_transform(x, w)
+    return y if y is not None else torch.mm(x, w.t())
+
+
+class _GcnLayerFn(torch.autograd.Function):
+    """Graph_conv_layer (GCN/GCN.py:41-47) as one differentiable op, trained the way the
+    reference's loop runs it (GCN/train_eval.py:43-48: forward, loss.backward()):
+
+    forward   S = X W^T on the MFMA transform -- scattered into the column-degree order of
+              A P^T when the graph takes that path (``column_order``), as at inference --
+              then Y = A S + b (the forward SpMM path, bias in its epilogue);
+    backward  dS = A^T dY (the same SpMM kernels; A itself when it is symmetric, as the GCN
+              normalisation is: no transposed copy), dX = dS W on the MFMA transform,
+              dW = dS^T X (torch.mm: a K = n_rows reduction, hipBLASLt), db = column sums of dY.
+    The support S is not kept for backward (dW needs X and dS only)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, g):
+        order = column_order(g, weight.shape[0]) if x.shape[0] == g.n_cols else None
+        s = None
+        if order is not None:
+            s = gcn_transform(x, weight, out_rows=order.inv, check_rows=False)
+        if s is not None:
+            y = spmm_forward(order.graph, s, bias)
+        else:
+            y = spmm_forward(g, _transform_or_mm(x, weight), bias)
+        ctx.save_for_backward(x, weight)
+        ctx.g = g
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous()
+        ds = spmm_forward(ctx.g.transpose(), gy)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = _transform_or_mm(ds, weight.t().contiguous())
+        if ctx.needs_input_grad[1]:
+            gw = torch.mm(ds.t(), x)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum(0)
+        return gx, gw, gb, None
+
+
+def gcn_layer(g: CsrGraph, x: torch.Tensor, weight: torch.Tensor,
+              bias: torch.Tensor | None = None) -> torch.Tensor:
+    """A_hat (x W^T) + b, differentiable w.r.t. x, W and b (``_GcnLayerFn``)."""
+    _require_device(g.rowptr, x, weight, bias)
+    if x.dtype != torch.float32 or weight.dtype != torch.float32:
+        raise TypeError("gcn_layer runs in float32")
+    if x.dim() != 2 or weight.dim() != 2 or x.shape[1] != weight.shape[1] \
+            or x.shape[0] != g.n_cols:
+        raise ValueError("x must be [n_cols, F_in] and weight [F_out, F_in]")
+    return _GcnLayerFn.apply(x, weight, bias, g)
+
+
 # ---------------------------------------------------------------------- GAT
 GAT_DENSE = 0   # GraphAttentionLayer   (GAT/models/layers.py:22-37)
 GAT_SPARSE = 1  # SpGraphAttentionLayer (GAT/models/layers.py:94-131)
@@ -1010,10 +1070,12 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
                  stats: torch.Tensor, y: torch.Tensor, dy: torch.Tensor, a_src: torch.Tensor,
                  a_dst: torch.Tensor, heads: int, fh: int, negative_slope: float, mode: int,
                  elu: bool, dropout_p: float = 0.0, seed: int = 0,
-                 seg_len: int | None = None):
+                 seg_len: int | None = None, timings: list | None = None):
     """dWh (incl. the el/er terms), del, der for one GAT layer (three HIP passes).
 
-    Returns (dwh [N, H*fh], dout [N, H*fh], del [N, H], der [N, H])."""
+    Returns (dwh [N, H*fh], dout [N, H*fh], del [N, H], der [N, H]). ``timings`` (a list):
+    (pass name, start event, end event) of each pass on the current stream is appended
+    (bench.py's per-kernel backward times)."""
     _require_device(wh, dy)
     n = g.n_rows
     feat = heads * fh
@@ -1024,6 +1086,17 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
     y = y.contiguous()
     dout = torch.empty((n, feat), dtype=torch.float32, device=dev)
     D = torch.empty((n, heads), dtype=torch.float32, device=dev)
+
+    def mark(name):
+        if timings is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.current_stream(dev))
+            if timings and timings[-1][2] is None:
+                timings[-1] = (timings[-1][0], timings[-1][1], ev)
+            if name:
+                timings.append((name, ev, None))
+
+    mark("prep")
     _lib.check(lib.gnn_gat_backward_prep_f32(dy.data_ptr(), y.data_ptr(), feat, n, heads, fh,
                                              int(elu), dout.data_ptr(), D.data_ptr(), stream),
                "gnn_gat_backward_prep_f32")
@@ -1035,6 +1108,7 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
     dl = torch.zeros((n, heads), dtype=torch.float32, device=dev)
     del_part = torch.empty((max(plan.n_seg, 1), heads), dtype=torch.float32, device=dev)
     rows = plan.row_list()
+    mark("edges")
     _lib.check(lib.gnn_gat_backward_edges_f32(
         g.rowptr.data_ptr(), g.col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
         el.data_ptr(), er.data_ptr(), stats.data_ptr(), dout.data_ptr(), D.data_ptr(),
@@ -1052,6 +1126,7 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
     a_src = a_src.contiguous().float()
     a_dst = a_dst.contiguous().float()
     # one node pass for every head (the kernel sums der over groups of 8 heads itself)
+    mark("nodes")
     _lib.check(lib.gnn_gat_backward_nodes_f32(
         rowptr_t.data_ptr(), src_t.data_ptr(), eid_t.data_ptr(), n, heads, fh,
         dout.data_ptr(), w_edge.data_ptr(), ds_edge.data_ptr(), dl.data_ptr(),
@@ -1059,4 +1134,5 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
         _lib.ptr(pt.seg_row), _lib.ptr(pt.seg_begin), pt.n_seg, _lib.ptr(pt.long_row),
         pt.long_seg_ptr.data_ptr(), pt.n_long, _lib.ptr(rows_t), rows_t.numel(),
         part.data_ptr(), stream), "gnn_gat_backward_nodes_f32")
+    mark(None)
     return dwh, dout, dl, der

@@ -57,7 +57,9 @@ def gcn_adjacency(src, dst, n: int, device=None) -> CsrGraph:
     _lib.check(lib.gnn_gcn_adjacency_fill(ws.data_ptr(), e, n, m, rowptr.data_ptr(),
                                           col.data_ptr(), val.data_ptr(), stream),
                "gnn_gcn_adjacency_fill")
-    return CsrGraph(rowptr, col, val, n, n)
+    # D^-1/2 (max(A, A^T) + I) D^-1/2: symmetric in structure; v_ij and v_ji are the same
+    # float64 product in two orders, equal after the fp32 rounding to within one ulp
+    return CsrGraph(rowptr, col, val, n, n, symmetric=True)
 
 
 def gcn_normalized_csr(src, dst, n: int, device=None) -> CsrGraph:
@@ -104,7 +106,8 @@ def gcn_normalized_csr(src, dst, n: int, device=None) -> CsrGraph:
     order = torch.argsort(c * n + r)
     rowptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     torch.cumsum(torch.bincount(c, minlength=n), 0, out=rowptr[1:])
-    return CsrGraph(rowptr, r[order].to(torch.int32).contiguous(), val[order].contiguous(), n, n)
+    return CsrGraph(rowptr, r[order].to(torch.int32).contiguous(), val[order].contiguous(), n, n,
+                    symmetric=True)
 
 
 def normalize_features(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

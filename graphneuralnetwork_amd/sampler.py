@@ -95,6 +95,22 @@ def _frontier_ws(n_nodes: int, dev) -> torch.Tensor:
     return ws
 
 
+_SAMPLE_WS = {}
+
+
+def _sample_ws(n_nodes: int, dev) -> torch.Tensor:
+    """gnn_sample_layers' workspace for an n_nodes graph: zero-filled once here; every call
+    leaves it zero-filled again (the frontier flags are cleared by the scan that reads them)."""
+    key = (dev, n_nodes)
+    ws = _SAMPLE_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(int(_lib.load().gnn_sample_layers_workspace_bytes(n_nodes)),
+                         dtype=torch.uint8, device=dev)
+        _SAMPLE_WS.clear()  # one graph at a time
+        _SAMPLE_WS[key] = ws
+    return ws
+
+
 def build_frontier(ids_a: torch.Tensor, ids_b: torch.Tensor, n_nodes: int, err: torch.Tensor):
     """(sorted distinct ids of ids_a and ids_b, rank function) on the device: the
     reference's set union + index remap (GraphSAGE/data_utils.py:100-116), as
@@ -188,7 +204,8 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
     multihop_sampling): fanouts[i] neighbours for every node of S_i, chained per hop.
 
     One library call (gnn_sample_layers) issues every hop's kernels with the list lengths kept
-    on the device, and ONE host read at the end fetches the layer sizes and the error bits:
+    on the device -- for [25, 10] three launches: draw + frontier marks, the frontier scan,
+    draw + the maps -- and ONE host read at the end fetches the layer sizes and the error bits:
     the same tensors as ``sample_batch_stepwise`` (which reads each frontier size back before
     the next hop), bit for bit."""
     fanouts = tuple(int(k) for k in fanouts)
@@ -197,7 +214,8 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
     if not adj.rowptr.is_cuda:
         raise RuntimeError("sampling runs on the ROCm device only (no CPU fallback)")
     seeds = seeds.to(device=adj.device, dtype=torch.int64).contiguous()
-    if seeds.numel() == 0 or max(fanouts) > 256 or adj.n_rows == 0:
+    if seeds.numel() == 0 or max(fanouts) > 64 or adj.n_rows == 0:
+        # fanouts above the lane sampler's 64 (and empty inputs) take the hop-by-hop path
         return sample_batch_stepwise(adj, seeds, fanouts, seed, gcn)
     dev = adj.device
     L = len(fanouts)
@@ -211,8 +229,7 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
     cmaps = [torch.empty(caps[i], **i64) for i in range(L - 1)]
     nmaps = [torch.empty((caps[i], widths[i]), **i64) for i in range(L - 1)]
     stat = torch.empty(L + 1, **i64)
-    ws = _frontier_ws(adj.n_rows, dev)
-    _FRONTIER_GEN[0] += 1  # the shared workspace is overwritten: older rank() closures refuse
+    ws = _sample_ws(adj.n_rows, dev)
     import ctypes
     P = ctypes.c_void_p
     arr = lambda ts: (P * max(1, len(ts)))(*[t.data_ptr() if t is not None else None  # noqa: E731
@@ -233,6 +250,9 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
         raise IndexError("sample_batch: a sampled id outside the graph reached the frontier")
     if e & 4:
         raise RuntimeError("sample_batch: a frontier outgrew its buffer (internal bound error)")
+    if e & 16:
+        raise RuntimeError("sample_batch: the frontier scan's look-back did not complete "
+                           "(internal error)")
     layers = [seeds] + [layers[i][:sizes[i]] for i in range(1, L)]
     cmaps = [cmaps[i][:sizes[i]] for i in range(L - 1)]
     nmaps = [nmaps[i][:sizes[i]] for i in range(L - 1)]

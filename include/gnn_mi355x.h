@@ -638,14 +638,22 @@ int gnn_frontier_rank(const int64_t* ids, int64_t n, int64_t n_nodes, const void
  * = positions of S_i / nbrs[i] in S_{i+1}. Every list length lives on the device: stat (device
  * int64 [L + 1]) receives |S_i| in stat[i] and the error bits in the low word of stat[L]
  * (1 = a node without neighbours, 2 = a node id out of range, 4 = a frontier larger than its
- * buffer, 8 = an unsampled id reached the frontier), so the caller reads everything with ONE
+ * buffer, 8 = an unsampled id reached the frontier, 16 = internal: the frontier scan's
+ * look-back gave up), so the caller reads everything with ONE
  * copy at the end. Host arrays: fanouts, layer_seeds, caps [L] (caps[i] = rows of the S_i /
  * nbrs[i] / map buffers, caps[0] = n_seeds; caps[i+1] >= min(n_graph, caps[i] (1 + ld_i)) never
  * overflows), layers, nbrs, center_maps, neigh_maps (device pointers; layers[0] unused).
- * nbrs[i] / neigh_maps[i] rows have ld_i = fanouts[i] + append_self ids. Workspace:
- * gnn_frontier_workspace_bytes(n_graph) (the frontier's; not to be shared with a live
- * gnn_frontier_* sequence). The same draws, frontiers and maps as the step-by-step calls.
+ * nbrs[i] / neigh_maps[i] rows have ld_i = fanouts[i] + append_self ids. fanouts[i] <= 64
+ * (GNN_E_UNSUPPORTED above: use the step-by-step calls). The same draws, frontiers and maps as
+ * the step-by-step calls. Launches: 2 L - 1 (L = 1: 2) -- each hop's draw also sets the
+ * frontier flags of its ids, one scan per hop builds S_{i+1} (decoupled look-back over the
+ * flags, which it clears), and the next hop's draw computes the maps and the previous hop's
+ * error bits.
+ * Workspace: gnn_sample_layers_workspace_bytes(n_graph) bytes, ZERO-FILLED before its first
+ * use; every call leaves it zero-filled again. One workspace per stream (calls sharing one
+ * must be ordered).
  */
+int64_t gnn_sample_layers_workspace_bytes(int64_t n_graph);
 int gnn_sample_layers(const int64_t* rowptr, const int32_t* col, int64_t n_graph,
                       const int64_t* seeds, int64_t n_seeds, int32_t n_layers,
                       const int64_t* fanouts, const uint64_t* layer_seeds, int32_t append_self,

@@ -39,6 +39,8 @@ def load():
         lib.oracle_gat_csr.restype = None
         lib.oracle_sage_gather.argtypes = [vp, i64, vp, i64, i64, i64, i64, ctypes.c_int, vp, i64]
         lib.oracle_sage_gather.restype = None
+        lib.oracle_sage_argmax.argtypes = [vp, i64, vp, i64, i64, i64, i64, vp, i64]
+        lib.oracle_sage_argmax.restype = None
         _lib = lib
     return _lib
 
@@ -93,6 +95,21 @@ def gat_csr(rowptr, col, wh, el, er, heads: int, fh: int, slope: float, sparse: 
 
 
 _SAGE_MODES = {"MEAN": 0, "SUM": 2, "MAXPOOL": 3}
+
+
+def sage_argmax(table, idx):
+    """int64 [M, F] argmax over k of table[idx[m, j]] (Aggregator 'MAX', graph_utils.py:7-8:
+    torch.argmax order -- NaN largest, first index on ties)."""
+    lib = load()
+    table = np.ascontiguousarray(table, dtype=np.float32)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    M, k = idx.shape
+    F = table.shape[1]
+    out = np.empty((M, F), dtype=np.int64)
+    if k:
+        lib.oracle_sage_argmax(table.ctypes.data, F, idx.ctypes.data, k, M, k, F, out.ctypes.data,
+                               F)
+    return out
 
 
 def sage_gather(table, idx, mode: str = "MEAN"):

@@ -115,6 +115,30 @@ void oracle_gat_csr(const int64_t* rowptr, const int32_t* col, int64_t row0, int
 }
 
 /*
+ * Fused gather + argmax over the neighbours (graph_utils.py:7-8, Aggregator 'MAX':
+ * torch.argmax(neigh_feat, dim=1)): out[m, f] = the first j < k whose table[idx[m, j], f] is
+ * the maximum under torch's order (a NaN is larger than every number; the first NaN wins).
+ */
+void oracle_sage_argmax(const float* table, int64_t ldt, const int64_t* idx, int64_t ldi,
+                        int64_t M, int64_t k, int64_t feat, int64_t* out, int64_t ldo) {
+#pragma omp parallel for schedule(dynamic, 256)
+  for (int64_t m = 0; m < M; ++m) {
+    for (int64_t f = 0; f < feat; ++f) {
+      int64_t best = 0;
+      float bv = table[idx[m * ldi] * ldt + f];
+      for (int64_t j = 1; j < k && bv == bv; ++j) {
+        const float v = table[idx[m * ldi + j] * ldt + f];
+        if (v != v || v > bv) {
+          best = j;
+          bv = v;
+        }
+      }
+      out[m * ldo + f] = best;
+    }
+  }
+}
+
+/*
  * Fused gather + neighbour reduction (GraphSAGE/GraphSAGE.py:47-49 + graph_utils.py:6):
  * out[m] = reduce_j table[idx[m*ldi + j]] over j < k, float64 accumulation.
  * mode 0 mean (torch.mean), 2 sum (NeighborAggregator 'sum'), 3 max-pool

@@ -266,6 +266,32 @@ def test_fused_batch_equals_stepwise(dev, fanouts, gcn):
             fn(g, torch.tensor([7, 0], device=dev), fanouts, gcn=gcn)
 
 
+def test_fused_batch_leaves_workspace_clean(dev):
+    """gnn_sample_layers' workspace contract: zero-filled before the first call, zero-filled
+    flags again after every call (the scan clears what it reads), so back-to-back batches on
+    different seeds and an erroring batch in between all give the step-by-step results."""
+    from graphneuralnetwork_amd import sampler as S
+    adj = _adj(dev, n=30000, e=200000, seed=5)
+    deg = (adj.rowptr[1:] - adj.rowptr[:-1]).cpu().numpy()
+    cand = np.nonzero(deg > 0)[0]
+    empty = np.nonzero(deg == 0)[0]
+    n_words = (adj.n_rows + 31) // 32
+    for it in range(4):
+        seeds = torch.from_numpy(cand[it * 500:(it + 1) * 500]).to(dev)
+        a = S.sample_batch(adj, seeds, (6, 4, 3), seed=it)
+        b = S.sample_batch_stepwise(adj, seeds, (6, 4, 3), seed=it)
+        assert torch.equal(a.frontier, b.frontier) and torch.equal(a.neigh_map, b.neigh_map)
+        for x, y in zip(a.center_maps, b.center_maps):
+            assert torch.equal(x, y)
+        ws = S._SAMPLE_WS[(adj.device, adj.n_rows)]
+        assert int(ws[:32 * n_words].count_nonzero()) == 0
+        if empty.size and it == 1:
+            with pytest.raises(IndexError):
+                S.sample_batch(adj, torch.from_numpy(np.concatenate([cand[:10], empty[:1]])).to(dev),
+                               (6, 4))
+            assert int(ws[:32 * n_words].count_nonzero()) == 0
+
+
 def test_fused_batch_full_size_cfg4(dev):
     """The cfg4 batch (8192 seeds, [25, 10]) on the 10M-node R-MAT adjacency: fused == stepwise."""
     from graphneuralnetwork_amd.rmat import rmat_edges

@@ -443,7 +443,8 @@ def test_transform_split_bf16_accuracy(dev, k, fout, n, scale):
 
 
 def test_gcn_transform_fallback_and_training(dev):
-    """Uncovered shapes return None (nn.Linear runs); with autograd the layer uses nn.Linear."""
+    """Uncovered shapes return None (nn.Linear runs); with autograd the layer is ops.gcn_layer
+    (its own backward, tests/test_training_gpu.py) and equals the inference path."""
     from graphneuralnetwork_amd.gcn import Graph_conv_layer
     from graphneuralnetwork_amd.ops import gcn_transform
     x = torch.randn(100, 7, device=dev)

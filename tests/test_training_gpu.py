@@ -1,0 +1,122 @@
+"""Training path of Graph_conv_layer (GCN/GCN.py:41-47 under GCN/train_eval.py:43-48's
+loss.backward()): ops.gcn_layer / _GcnLayerFn against float64 references.
+
+Tolerance (north_star): fp32 within 1e-4 relative (atol scaled by max |ref|).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import c_oracle
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+
+
+def close(a, b, rtol=RTOL):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    scale = max(1.0, float(np.nanmax(np.abs(b)))) if b.size else 1.0
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=1e-5 * scale)
+
+
+def _rand_graph(n, m, seed):
+    rng = np.random.default_rng(seed)
+    r = rng.integers(0, n, m)
+    c = np.where(rng.random(m) < 0.3, rng.integers(0, 8, m), rng.integers(0, n, m))
+    order = np.lexsort((c, r))
+    r, c = r[order], c[order]
+    rowptr = np.zeros(n + 1, np.int64)
+    np.add.at(rowptr, r + 1, 1)
+    return np.cumsum(rowptr), c.astype(np.int32), rng.standard_normal(m).astype(np.float32)
+
+
+@pytest.mark.parametrize("bias", [True, False])
+def test_gcn_layer_grads_vs_float64(dev, bias):
+    """A non-symmetric graph (transposed CSR built for dX): Y, dX, dW, db against float64
+    dense autograd of A (X W^T) + b."""
+    from graphneuralnetwork_amd.gcn import Graph_conv_layer
+    from graphneuralnetwork_amd.graph import CsrGraph
+    n = 400
+    rowptr, col, val = _rand_graph(n, 5000, 3)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.from_numpy(val).to(dev), n, n)
+    A = torch.zeros(n, n, dtype=torch.float64)
+    rows = np.repeat(np.arange(n), np.diff(rowptr))
+    A.index_put_((torch.from_numpy(rows), torch.from_numpy(col.astype(np.int64))),
+                 torch.from_numpy(val.astype(np.float64)), accumulate=True)
+    layer = Graph_conv_layer(128, 64, is_bias=bias).to(dev)
+    if bias:
+        torch.nn.init.normal_(layer.bias)
+    X = torch.randn(n, 128, device=dev, requires_grad=True)
+    y = layer(X, g)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    assert not g.symmetric and g._transpose is not None
+    Xd = X.detach().cpu().double().requires_grad_()
+    Wd = layer.dense.weight.detach().cpu().double().requires_grad_()
+    bd = layer.bias.detach().cpu().double().requires_grad_() if bias else None
+    yd = A @ (Xd @ Wd.t()) + (bd if bias else 0)
+    yd.backward(gy.cpu().double())
+    close(y.detach().cpu().numpy(), yd.detach().numpy())
+    close(X.grad.cpu().numpy(), Xd.grad.numpy())
+    close(layer.dense.weight.grad.cpu().numpy(), Wd.grad.numpy())
+    if bias:
+        close(layer.bias.grad.cpu().numpy(), bd.grad.numpy())
+
+
+def test_symmetric_graph_is_its_own_transpose(dev):
+    """The GCN builders mark D^-1/2 (A_sym + I) D^-1/2 symmetric (no transposed copy); an
+    unmarked graph whose transpose equals it (the reference's COO) is found to be so."""
+    from graphneuralnetwork_amd.graph import CsrGraph, from_coo
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    s, d = rmat_edges(50_000, 400_000, 1)
+    g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), 50_000, device=dev)
+    assert g.symmetric and g.transpose() is g
+    rows = torch.repeat_interleave(torch.arange(g.n_rows, device=dev), g.rowptr[1:] - g.rowptr[:-1])
+    t = from_coo(g.col.to(torch.int64), rows, g.val, g.n_cols, g.n_rows)
+    assert torch.equal(t.rowptr, g.rowptr) and torch.equal(t.col, g.col)
+    assert torch.allclose(t.val, g.val, rtol=2.0 ** -23, atol=0)
+    plain = CsrGraph(g.rowptr, g.col, g.val, g.n_rows, g.n_cols)
+    assert not plain.symmetric
+    assert plain.transpose() is plain and plain.symmetric and plain._transpose is None
+
+
+def test_gcn_layer_training_cfg2_full_size(dev):
+    """The benchmarked training step at BASELINE cfg2 size (R-MAT 1M / 20.1M nnz, 128 -> 128):
+    the forward takes the column-ordered path and equals the inference layer bit for bit; the
+    gradients equal float64 references built from the C oracle's SpMM (dS = A dY, A
+    symmetric) and numpy products (dX = dS W, dW = dS^T X, db = sum dY) on every row."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.gcn import Graph_conv_layer
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    n = 1_000_000
+    s, d = rmat_edges(n, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
+    assert g.nnz == 20_073_500 and g.symmetric
+    assert ops.column_order(g, 128) is not None
+    gen = torch.Generator(device=dev).manual_seed(5)
+    layer = Graph_conv_layer(128, 128).to(dev)
+    with torch.no_grad():
+        layer.bias.normal_(generator=gen)
+    X = torch.randn(n, 128, device=dev, generator=gen)
+    with torch.no_grad():
+        y_inf = layer(X, g)
+    y = layer(X, g)
+    assert torch.equal(y.detach(), y_inf)
+    gy = torch.randn(n, 128, device=dev, generator=gen)
+    y.backward(gy)
+    assert g._transpose is None  # the symmetric graph served the backward itself
+    rp, col, val = (t.cpu().numpy() for t in (g.rowptr, g.col, g.val))
+    gyn = gy.cpu().numpy()
+    dS = c_oracle.spmm_csr(rp, col, val, gyn).astype(np.float64)   # double accumulation
+    Xn = X.cpu().numpy().astype(np.float64)
+    W = layer.dense.weight.detach().cpu().numpy().astype(np.float64)
+    close(layer.dense.weight.grad.cpu().numpy(), dS.T @ Xn)
+    close(layer.bias.grad.cpu().numpy(), gyn.astype(np.float64).sum(0))
+    X.requires_grad_(True)
+    layer.zero_grad()
+    layer(X, g).backward(gy)
+    close(X.grad.cpu().numpy(), dS @ W)
