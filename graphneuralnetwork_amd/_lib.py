@@ -128,7 +128,19 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _i64, _vp, _i64,           # mid_row, n_mid, short_row, n_short
         _vp, _vp,                       # partial, stats
         _u32, _vp,                      # flags, stream
-        _vp, _i64, _vp, _i64]),         # whh, ldwh, erh, ldeh
+        _vp, _i64, _vp, _i64]),
+    "gnn_gat_csr_tasks_f32": (ctypes.c_int, [
+        _vp, _vp, _i64,                 # rowptr, col (hub ranks -1-k when staged), n_rows
+        _vp, _i64, _i64, _i64,          # wh, ldw, heads, fh
+        _vp, _vp, _i64,                 # el, er, lde
+        ctypes.c_float, _i32, _vp,      # negative_slope, mode, empty_row_fill
+        ctypes.c_float, ctypes.c_uint64,  # dropout_p, dropout_seed
+        _vp, _i64,                      # out, ldo
+        _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
+        _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
+        _vp, _i64, _vp, _i64,           # mid_row, n_mid, task_row, n_task
+        _vp, _vp, _u32, _vp,            # partial, stats, flags, stream
+        _vp, _i64, _vp, _i64]),         # whh, ldwh, erh, ldeh (NULL: no staged tables)         # whh, ldwh, erh, ldeh
     "gnn_gat_backward_prep_f32": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp,
                                                  _vp]),
     "gnn_gat_backward_edges_f32": (ctypes.c_int, [

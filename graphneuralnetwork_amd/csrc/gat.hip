@@ -108,6 +108,10 @@ struct GatParams {
   int64_t ldwh;
   const float* erh;
   int64_t ldeh;
+  // packed row tasks (gnn_gat_csr_tasks_f32): task t = rows [task_row[2t], task_row[2t+1]),
+  // at most kGatTaskRows consecutive rows of low degree (edgeless and one-edge rows included)
+  const int32_t* task_row;
+  int64_t n_task;
 };
 
 // Wh row / er entry of column c (hub-staged when c < 0). Without staging no column id is
@@ -296,6 +300,161 @@ template <int VW, int LPR, bool SPARSE>
 __global__ __launch_bounds__(kGatBlock) void gat_short_kernel(GatParams P) {
   gat_short_rows<VW, LPR, SPARSE>(P, static_cast<int64_t>(blockIdx.x) * kGatWaves + (threadIdx.x >> 6),
                                   threadIdx.x & (kWave - 1));
+}
+
+#ifndef GNN_GAT_TASK_U
+#define GNN_GAT_TASK_U 4  // edges whose er / Wh loads a slot issues together in a packed task
+#endif
+constexpr int kGatTaskRows = 63;  // a task's rowptr values fit one VGPR (lane = row)
+
+// Packed row tasks for the low-degree rows (the SpMM's packed_rows with an edge softmax): a
+// wave takes <= 63 consecutive rows of degree <= the plan's threshold, splits them between its
+// EPI edge slots by cost (edges + rows), and every slot streams ITS rows' edges in CSR order --
+// column ids loaded coalesced by the slot's LPR lanes and broadcast, U edges' er entries and Wh
+// rows in flight -- with a lane-private online softmax for the head of the lane's VW features,
+// writing a row (out = acc / l, stats) as soon as the stream passes its end. The rowptr ->
+// col -> (er, Wh) chain is paid once per task instead of per row (gat_short_kernel: 4 rows per
+// wave, one chain each), and the row's el values come from an LDS copy of the task's el rows.
+// Edgeless rows: dense -> the column mean (empty_fill), sparse -> 0/0 = NaN; one-edge rows
+// give the edge's Wh row (dense, weight exp(0) = 1) or (p Wh) / p (sparse), as the small-row
+// path. Requires NCH == 1 and fh % VW == 0 (the launcher's condition).
+template <int VW, int LPR, bool SPARSE, int U>
+__device__ __forceinline__ void gat_packed_rows(const GatParams& P, int64_t t, int lane,
+                                                float* __restrict__ el_lds) {
+  constexpr int EPI = kWave / LPR;
+  static_assert(LPR % U == 0, "a batch of U edges never straddles a chunk of LPR edges");
+  const int sub = lane & (LPR - 1);
+  const int grp = lane / LPR;
+  const int32_t rb = P.task_row[2 * t];
+  const int32_t re = P.task_row[2 * t + 1];
+  if (rb < 0 || re <= rb || re - rb > kGatTaskRows || re > P.n_rows) return;
+  const int nr = re - rb;
+  const int H = P.heads;
+  // the task's el rows into this wave's LDS slice (row r, head h at r * H + h)
+  for (int i = lane; i < nr * H; i += kWave) {
+    const int r = i / H, hh = i - r * H;
+    el_lds[i] = P.el[static_cast<int64_t>(rb + r) * P.lde + hh];
+  }
+  const int64_t e0 = P.rowptr[rb];
+  const int rp = static_cast<int>(P.rowptr[rb + min(lane, nr)] - e0);
+  const int E = __shfl(rp, nr, kWave);
+  int sb = 0, se = nr;
+  if (EPI > 1) {
+    const int64_t total = static_cast<int64_t>(E) + nr;
+#pragma unroll
+    for (int b = 1; b < EPI; ++b) {
+      const int64_t target = total * b / EPI;
+      const uint64_t m = __ballot(lane <= nr && static_cast<int64_t>(rp) + lane >= target);
+      const int row_b = m ? (__ffsll(static_cast<unsigned long long>(m)) - 1) : nr;
+      if (grp == b) sb = row_b;
+      if (grp == b - 1) se = row_b;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int64_t f = static_cast<int64_t>(sub) * VW;
+  const bool fok = f < P.feat;
+  const int h = fok ? static_cast<int>(f / P.fh) : 0;
+  int cur = sb;
+  int cur_end = __shfl(rp, min(cur + 1, nr), kWave);
+  const int es = __shfl(rp, sb, kWave);
+  const int ee = __shfl(rp, se, kWave);
+  int cur_beg = es;
+  float eli = cur < se ? el_lds[cur * H + h] : 0.f;
+  float m = SPARSE ? 0.f : -INFINITY, l = 0.f;
+  typename Vec<VW>::T acc = vzero<VW>();
+
+  auto flush_upto = [&](int pos) {
+    bool need = cur < se && pos >= cur_end;
+    while (__ballot(need)) {
+      if (need) {
+        const int64_t row = rb + cur;
+        const bool empty = cur_beg == cur_end;
+        if (P.stats && fok && f % P.fh == 0)
+          P.stats[row * P.lds + h] = empty ? -INFINITY : (SPARSE ? 0.f : m) + __logf(l);
+        if (fok) {
+          typename Vec<VW>::T r;
+          if (!SPARSE && empty)
+            r = P.empty_fill ? vload<VW>(P.empty_fill + f) : typename Vec<VW>::T(NAN);
+          else
+            r = acc / l;  // sparse, no edge: 0/0 = NaN like the reference
+#pragma unroll
+          for (int k = 0; k < VW; ++k) vset(r, k, act_apply(vget(r, k), P.flags));
+          vstore<VW>(P.out + row * P.ldo + f, r);
+        }
+        m = SPARSE ? 0.f : -INFINITY;
+        l = 0.f;
+        acc = vzero<VW>();
+      }
+      cur += need ? 1 : 0;
+      const int nxt = __shfl(rp, min(cur + 1, nr), kWave);
+      cur_beg = need ? cur_end : cur_beg;
+      cur_end = need ? nxt : cur_end;
+      if (need && cur < se) eli = el_lds[cur * H + h];
+      need = cur < se && pos >= cur_end;
+    }
+  };
+
+  int len = ee - es;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) len = max(len, __shfl_xor(len, o, kWave));
+  flush_upto(es);  // leading rows without edges
+  for (int off = 0; off < len; off += LPR) {
+    const int cb = es + off;  // this slot's chunk: lane `sub` holds edge cb + sub
+    const int c = cb + sub < ee ? P.col[e0 + cb + sub] : 0;
+    const int n = min(LPR, len - off);  // wave-uniform
+    for (int k = 0; k < n; k += U) {
+      float erv[U];
+      typename Vec<VW>::T xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int ce = __shfl(c, grp * LPR + ((k + u) & (LPR - 1)), kWave);
+        const bool ok = cb + k + u < ee;
+        erv[u] = ok ? er_at(P, ce, h) : 0.f;
+        xv[u] = (ok && fok) ? vload<VW>(wh_row(P, ce) + f) : vzero<VW>();
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        flush_upto(cb + k + u);  // rows that end before this edge
+        if (cb + k + u < ee) {
+          const float sv = eli + erv[u];
+          const float x = sv > 0.f ? sv : P.slope * sv;
+          float p;
+          if (SPARSE) {
+            p = __expf(-x);  // exp(-LeakyReLU), no max subtraction
+          } else {
+            if (x > m) {  // online softmax: rescale the row's state to the new maximum
+              const float sc = __expf(m - x);  // 0 on the row's first edge (m = -inf)
+              acc *= sc;
+              l *= sc;
+              m = x;
+            }
+            p = __expf(x - m);
+          }
+          l += p;
+          float w = p;
+          if (P.drop_p > 0.f) {
+            const uint32_t r = hash3(P.drop_seed, e0 + cb + k + u, P.head0 + h);
+            w = (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f
+                                                                                : w * P.drop_scale;
+          }
+          acc += w * xv[u];
+        }
+      }
+    }
+  }
+  flush_upto(0x7fffffff);  // the last row and trailing rows without edges
+}
+
+template <int VW, int LPR, bool SPARSE>
+__global__ __launch_bounds__(kGatBlock) void gat_task_kernel(GatParams P) {
+  __shared__ float el_lds[kGatWaves][kGatTaskRows * kMaxHeads];
+  const int wid = threadIdx.x >> 6;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * kGatWaves + wid;
+  if (t < P.n_task)
+    gat_packed_rows<VW, LPR, SPARSE, (LPR < GNN_GAT_TASK_U ? LPR : GNN_GAT_TASK_U)>(
+        P, t, threadIdx.x & (kWave - 1), el_lds[wid]);
 }
 
 #ifndef GNN_GAT_LDS_PAD
@@ -686,6 +845,11 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
     hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U, J>),
                        dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), GNN_GAT_LDS_PAD, s, Q);
   if constexpr (NCH == 1) {
+    if (P.n_task > 0) {
+      hipLaunchKernelGGL((gat_task_kernel<VW, LPR, SPARSE>),
+                         dim3(static_cast<unsigned>((P.n_task + kGatWaves - 1) / kGatWaves)),
+                         dim3(kGatBlock), 0, s, Q);
+    }
     if (P.n_short > 0) {
       const int64_t sw = (P.n_short + EPI - 1) / EPI;
       hipLaunchKernelGGL((gat_short_kernel<VW, LPR, SPARSE>),
@@ -864,9 +1028,12 @@ static int gat_entry(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
                      int64_t n_small, const int32_t* mid_row, int64_t n_mid,
                      const int32_t* short_row, int64_t n_short,
                      float* partial, float* stats, uint32_t flags, void* stream,
-                     const float* whh, int64_t ldwh, const float* erh, int64_t ldeh) {
+                     const float* whh, int64_t ldwh, const float* erh, int64_t ldeh,
+                     const int32_t* task_row = nullptr, int64_t n_task = 0) {
   if (n_rows < 0 || heads < 1 || fh < 1 || seg_len < 1 || n_seg < 0 || n_long < 0 || n_small < 0)
     return GNN_E_ARG;
+  if (n_task < 0 || (n_task > 0 && (task_row == nullptr || mid_row == nullptr))) return GNN_E_ARG;
+  if (n_task > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
   const bool plan = mid_row != nullptr;
   if (plan && (n_mid < 0 || n_short < 0 || n_mid + n_short + n_small + n_long > n_rows))
     return GNN_E_ARG;
@@ -937,11 +1104,14 @@ static int gat_entry(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
     P.ldwh = ldwh;
     P.erh = erh ? erh + h0 : nullptr;
     P.ldeh = ldeh;
+    P.task_row = task_row;
+    P.n_task = plan ? n_task : 0;
     const bool vec4 = (fh % 4 == 0) && (ldw % 4 == 0) && (ldo % 4 == 0) && aligned_to(P.wh, 16) &&
                       (P.whh == nullptr || (aligned_to(P.whh, 16) && ldwh % 4 == 0)) &&
                       aligned_to(P.out, 16) &&
                       (P.empty_fill == nullptr || aligned_to(P.empty_fill, 16)) &&
                       (P.partial == nullptr || (aligned_to(P.partial, 16) && ldp % 4 == 0));
+    if (P.n_task > 0 && !(vec4 && P.feat <= 64 * 4 && fh % 4 == 0)) return GNN_E_UNSUPPORTED;
     int rc;
     if (mode == 1)
       rc = vec4 ? dispatch_gat<4, true>(P, s) : dispatch_gat<1, true>(P, s);
@@ -991,4 +1161,34 @@ extern "C" int gnn_gat_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub
                    seg_begin, n_seg, long_row, long_seg_ptr, n_long, small_row, small_col,
                    n_small, mid_row, n_mid, short_row, n_short, partial, stats, flags, stream,
                    whh, ldwh, erh, ldeh);
+}
+
+// ---- packed row tasks for the low-degree rows (GAT/models/layers.py:22-37 / :94-131, the
+// same softmax + aggregation): see gat_packed_rows. The small / short row classes are replaced
+// by tasks (ranges of consecutive rows of degree <= the threshold, edgeless rows included); the
+// plan's segments and mid rows run as in gnn_gat_csr_hub_f32. whh / erh: hub tables (c < 0) or
+// NULL (ldwh / ldeh ignored). Requires fh % 4 == 0, heads * fh <= 256 per group of 8 heads,
+// 16-B aligned rows (GNN_E_UNSUPPORTED otherwise).
+extern "C" int gnn_gat_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                                     const float* wh, int64_t ldw, int64_t heads, int64_t fh,
+                                     const float* el, const float* er, int64_t lde,
+                                     float negative_slope, int32_t mode,
+                                     const float* empty_row_fill, float dropout_p,
+                                     uint64_t dropout_seed, float* out, int64_t ldo,
+                                     int64_t seg_len, const int32_t* seg_row,
+                                     const int64_t* seg_begin, int64_t n_seg,
+                                     const int32_t* long_row, const int32_t* long_seg_ptr,
+                                     int64_t n_long, const int32_t* mid_row, int64_t n_mid,
+                                     const int32_t* task_row, int64_t n_task, float* partial,
+                                     float* stats, uint32_t flags, void* stream,
+                                     const float* whh, int64_t ldwh, const float* erh,
+                                     int64_t ldeh) {
+  if (mid_row == nullptr) return GNN_E_ARG;
+  if ((whh == nullptr) != (erh == nullptr)) return GNN_E_ARG;
+  if (whh == nullptr) ldwh = ldeh = 0;
+  return gat_entry(rowptr, col, n_rows, wh, ldw, heads, fh, el, er, lde, negative_slope, mode,
+                   empty_row_fill, dropout_p, dropout_seed, out, ldo, seg_len, seg_row, seg_begin,
+                   n_seg, long_row, long_seg_ptr, n_long, nullptr, nullptr, 0, mid_row, n_mid,
+                   nullptr, 0, partial, stats, flags, stream, whh, ldwh, erh, ldeh, task_row,
+                   n_task);
 }

@@ -634,6 +634,21 @@ def col_mean(x: torch.Tensor) -> torch.Tensor:
 
 
 GAT_SHORT_MAX_DEG = 16  # rows with 2..16 edges take the short-row path (A/B at cfg3: 16 best)
+# Packed row tasks for the rows of degree <= GAT_SHORT_MAX_DEG (gnn_gat_csr_tasks_f32,
+# gat.hip gat_packed_rows): runs of consecutive low-degree rows, edgeless and one-edge rows
+# included, cut at GAT_TASK_COST edges + rows, one wave per task -- in place of the packed
+# small rows and gat_short_kernel's four rows per wave
+GAT_TASKS = True
+GAT_TASK_COST = 128
+
+
+def _gat_tasks_ok(heads, fh, *ts) -> bool:
+    # the task kernel's geometry: one 16-B vector per lane, one chunk of <= 64 lanes per row of a
+    # head group (<= 8 heads x fh <= 256 features), a lane's features inside one head
+    if not GAT_TASKS or fh % 4 or min(heads, 8) * fh > 256:
+        return False
+    return all(t is None or (t.data_ptr() % 16 == 0 and (t.dim() == 1 or t.stride(0) % 4 == 0))
+               for t in ts)
 # XCD-sliced hub staging for GAT (``_gat_xcd``) is built and tested but not the default: at
 # cfg3 it loses or ties at every setting (tools/xcd_ab.py --op gat, profiles/r02z_xcd_ab_gat_*:
 # single pass 0.79 ms; rows of >= 128 edges 0.88, >= 256 0.86, >= 1024 0.79). The edge
@@ -820,6 +835,8 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
             short.data_ptr() if short.numel() else None, short.numel(), _lib.ptr(partial),
             _lib.ptr(stats), _ACT_FLAGS[activation], stream)
     k = hub_rows_for(g.n_cols, feat + heads) if hubs is None else min(int(hubs), g.n_cols)
+    hp = whh = erh = None
+    ldwh = lderh = 0
     if k > 0 and g.nnz:
         hp = g.hub_plan(k)
         if XCD_DIRECT and hp.prefix:  # degree-ordered columns: hub rows read in place
@@ -833,6 +850,25 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
                                                    hp.hub_ids.data_ptr(), hp.k, w,
                                                    dst.data_ptr(), w, hp.err.data_ptr(), stream),
                            "gnn_gather_rows_f32")
+    col = hp.col_hub if hp is not None else g.col
+    if _gat_tasks_ok(heads, fh, wh, out, fill, whh):
+        tp = g.task_plan(plan.seg_len, GAT_SHORT_MAX_DEG, GAT_TASK_COST)
+        b = tp.base
+        if b.n_seg and partial is None:
+            partial = torch.empty((b.n_seg, feat + 2 * heads), dtype=torch.float32,
+                                  device=wh.device)
+        _lib.check(lib.gnn_gat_csr_tasks_f32(
+            g.rowptr.data_ptr(), col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
+            el.data_ptr(), er.data_ptr(), lde, float(negative_slope), int(mode), _lib.ptr(fill),
+            float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), out.stride(0),
+            tp.seg_len, _lib.ptr(b.seg_row), _lib.ptr(b.seg_begin), b.n_seg, _lib.ptr(b.long_row),
+            b.long_seg_ptr.data_ptr(), b.n_long,
+            tp.mid_row.data_ptr() if tp.n_mid else b.long_seg_ptr.data_ptr(), tp.n_mid,
+            tp.task_row.data_ptr() if tp.n_task else None, tp.n_task, _lib.ptr(partial),
+            _lib.ptr(stats), _ACT_FLAGS[activation], stream, _lib.ptr(whh), ldwh, _lib.ptr(erh),
+            lderh), "gnn_gat_csr_tasks_f32")
+        return out
+    if hp is not None:
         rc = lib.gnn_gat_csr_hub_f32(g.rowptr.data_ptr(), hp.col_hub.data_ptr(), *args,
                                      whh.data_ptr(), ldwh, erh.data_ptr(), lderh)
         _lib.check(rc, "gnn_gat_csr_hub_f32")

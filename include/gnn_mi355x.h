@@ -471,6 +471,27 @@ int gnn_gat_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub, int64_t n
                         int64_t ldwh, const float* erh, int64_t ldeh);
 
 /*
+ * The same layer with the low-degree rows as packed row tasks (the package's default at fh % 4
+ * == 0): task_row [2 n_task] = [begin, end) ranges of <= 63 consecutive rows of degree <= the
+ * plan's threshold (edgeless and one-edge rows included; gnn_spmm_tasks_build builds them),
+ * mid_row = the rows above the threshold up to seg_len, segments / long rows as above; there is
+ * no small / short class. One wave streams a task's edges with a lane-private online softmax per
+ * row (same weights and ELU, rounding of a streamed softmax). whh / erh: hub tables (column
+ * c < 0 reads row -1-c) or NULL. GNN_E_UNSUPPORTED unless fh % 4 == 0, <= 256 features per
+ * group of 8 heads and 16-B aligned rows.
+ */
+int gnn_gat_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                          const float* wh, int64_t ldw, int64_t heads, int64_t fh, const float* el,
+                          const float* er, int64_t lde, float negative_slope, int32_t mode,
+                          const float* empty_row_fill, float dropout_p, uint64_t dropout_seed,
+                          float* out, int64_t ldo, int64_t seg_len, const int32_t* seg_row,
+                          const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
+                          const int32_t* long_seg_ptr, int64_t n_long, const int32_t* mid_row,
+                          int64_t n_mid, const int32_t* task_row, int64_t n_task, float* partial,
+                          float* stats, uint32_t flags, void* stream, const float* whh,
+                          int64_t ldwh, const float* erh, int64_t ldeh);
+
+/*
  * Column mean of x[n_rows, feat] (double accumulation, deterministic): the dense
  * GAT layer's output for an edgeless row (uniform softmax over all N nodes,
  * GAT/models/layers.py:29-32). scratch: gnn_col_mean_scratch_bytes(n_rows, feat).

@@ -143,6 +143,50 @@ def test_gat_hub_staging_bitexact(dev, heads, fh, sparse):
             assert torch.equal(torch.nan_to_num(st, 1.5), torch.nan_to_num(st0, 1.5))
 
 
+@pytest.mark.parametrize("heads,fh", [(8, 8), (12, 4), (1, 64), (2, 128)])
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gat_packed_tasks_vs_short_rows(dev, heads, fh, sparse, monkeypatch):
+    """gnn_gat_csr_tasks_f32 (low-degree rows as packed tasks, the default at fh % 4 == 0)
+    against the row-class path it replaces (packed small rows + gat_short_kernel) and the
+    oracle: edgeless rows (dense: column mean; sparse: NaN), one-edge rows, runs longer than a
+    task, long-row segments, two head groups (12 heads), hub staging, dropout (the same
+    (edge, head) masks), ELU and the log-sum-exp stats."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.graph import CsrGraph
+    n = 3000
+    rng = np.random.default_rng(heads * fh)
+    deg = rng.integers(0, 14, n)
+    deg[rng.integers(0, n, 40)] = rng.integers(17, 400, 40)
+    deg[200:330] = 0                       # a run of edgeless rows longer than a task
+    deg[600:700] = 1
+    rowptr = np.zeros(n + 1, np.int64)
+    rowptr[1:] = np.cumsum(deg)
+    col = np.concatenate([np.sort(rng.choice(n, d, replace=False)) for d in deg]).astype(np.int32)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.ones(col.size, device=dev), n, n)
+    wh = torch.randn(n, heads * fh, device=dev) * 0.5
+    el, er = torch.randn(n, heads, device=dev) * 0.7, torch.randn(n, heads, device=dev) * 0.7
+    mode = ops.GAT_SPARSE if sparse else ops.GAT_DENSE
+    ref_o = O.gat_csr(rowptr, col, wh.cpu().numpy(), el.cpu().numpy(), er.cpu().numpy(), heads,
+                      fh, 0.2, sparse)
+    for seg_len, p, hubs in ((None, 0.0, 0), (32, 0.0, 0), (32, 0.0, 100), (None, 0.3, 0)):
+        outs = {}
+        for tasks in (True, False):
+            monkeypatch.setattr(ops, "GAT_TASKS", tasks)
+            st = torch.empty(n, heads, device=dev)
+            out = ops.gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, activation="elu",
+                                    seg_len=seg_len, dropout_p=p, seed=11, stats=st, hubs=hubs)
+            outs[tasks] = (out.cpu().numpy(), st.cpu().numpy())
+        (a, sa), (b, sb) = outs[True], outs[False]
+        np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+        close(np.nan_to_num(a), np.nan_to_num(b), rtol=1e-5)
+        close(np.nan_to_num(sa, neginf=-1e30), np.nan_to_num(sb, neginf=-1e30), rtol=1e-5)
+        if p == 0.0:
+            elu = np.where(ref_o > 0, ref_o, np.expm1(np.minimum(ref_o, 0)))
+            np.testing.assert_array_equal(np.isnan(a), np.isnan(elu))
+            close(np.nan_to_num(a), np.nan_to_num(elu))
+
+
 def _xcd_gat_graph(n, seed):
     """Edge set with hub columns 0..79 of strictly decreasing in-degree (hub rank = id), a
     hub row, one-edge rows into hub 0 (rows 0-99), edgeless rows (100-109), and rows whose
