@@ -1,0 +1,73 @@
+"""A/B of the GAT low-degree row schedule at cfg3 (8 x 8 heads over the 1M / 10M R-MAT graph in
+the column-degree order, as bench.py run_gat): packed row tasks (gnn_gat_csr_tasks_f32, task
+cost 64 / 128 / 256 edges + rows, degree threshold 16 / 32) against the row classes they replace
+(packed small rows + gat_short_kernel), interleaved in one process, HIP events per launch;
+outputs compared with the row-class path.
+
+    python tools/gat_tasks_ab.py [--reps 30]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=30)
+    a = ap.parse_args()
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    dev = torch.device("cuda:0")
+    s, d = rmat_edges(1_000_000, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), 1_000_000, device=dev)
+    H, Fh, Fin = 8, 8, 64
+    gen = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(g.n_rows, Fin, device=dev, generator=gen)
+    W = torch.randn(Fin, H * Fh, device=dev, generator=gen) * 0.2
+    a_s = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
+    a_d = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
+    order = ops.gat_column_order(g, H, Fh)
+    ga = order.graph
+    wh, el, er = ops.gat_project(X, W, H, Fh, a_s, a_d, col_rows=order.inv)
+    out = torch.empty_like(wh)
+    variants = [("rowclass", False, 128, 16), ("tasks_c64", True, 64, 16),
+                ("tasks_c128", True, 128, 16), ("tasks_c256", True, 256, 16),
+                ("tasks_c128_d32", True, 128, 32)]
+
+    def run(v):
+        _, tasks, cost, deg = v
+        ops.GAT_TASKS, ops.GAT_TASK_COST, ops.GAT_SHORT_MAX_DEG = tasks, cost, deg
+        return ops.gat_aggregate(ga, wh, el, er, H, Fh, 0.2, ops.GAT_DENSE, "elu", out=out)
+
+    ref = run(variants[0]).clone()
+    times = {v[0]: [] for v in variants}
+    err = {}
+    for v in variants:  # warm-up (plans) and the comparison
+        y = run(v)
+        torch.cuda.synchronize()
+        err[v[0]] = float(((y - ref).abs().max() / ref.abs().max()).item())
+    for _ in range(a.reps):
+        for v in variants:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            run(v)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v[0]].append(e0.elapsed_time(e1))
+    print(json.dumps({k: {"median_ms": round(statistics.median(t), 4),
+                          "max_rel_diff_vs_rowclass": err[k]} for k, t in times.items()}),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
