@@ -857,7 +857,7 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
         if b.n_seg and partial is None:
             partial = torch.empty((b.n_seg, feat + 2 * heads), dtype=torch.float32,
                                   device=wh.device)
-        _lib.check(lib.gnn_gat_csr_tasks_f32(
+        rc = lib.gnn_gat_csr_tasks_f32(
             g.rowptr.data_ptr(), col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
             el.data_ptr(), er.data_ptr(), lde, float(negative_slope), int(mode), _lib.ptr(fill),
             float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr(), out.stride(0),
@@ -866,8 +866,11 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
             tp.mid_row.data_ptr() if tp.n_mid else b.long_seg_ptr.data_ptr(), tp.n_mid,
             tp.task_row.data_ptr() if tp.n_task else None, tp.n_task, _lib.ptr(partial),
             _lib.ptr(stats), _ACT_FLAGS[activation], stream, _lib.ptr(whh), ldwh, _lib.ptr(erh),
-            lderh), "gnn_gat_csr_tasks_f32")
-        return out
+            lderh)
+        if rc != _lib.E_UNSUPPORTED:  # e.g. a 4-float vector path the row pitches do not allow
+            _lib.check(rc, "gnn_gat_csr_tasks_f32")
+            return out
+        # the row-class launch below (same plan, same partial buffer) covers the shape
     if hp is not None:
         rc = lib.gnn_gat_csr_hub_f32(g.rowptr.data_ptr(), hp.col_hub.data_ptr(), *args,
                                      whh.data_ptr(), ldwh, erh.data_ptr(), lderh)

@@ -4,7 +4,10 @@ cost 64 / 128 / 256 edges + rows, degree threshold 16 / 32) against the row clas
 (packed small rows + gat_short_kernel), interleaved in one process, HIP events per launch;
 outputs compared with the row-class path.
 
-    python tools/gat_tasks_ab.py [--reps 30]
+    python tools/gat_tasks_ab.py [--reps 30] [--libs gatpipe2]
+
+--libs: variant libraries (lib/variants/libgnn_<tag>.so, build.build_variant) timed with the
+default schedule beside the main library (e.g. gatpipe2 = GNN_GAT_PIPE=2: two chunks in flight).
 """
 from __future__ import annotations
 
@@ -23,6 +26,7 @@ sys.path.insert(0, str(ROOT))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--libs", default="")
     a = ap.parse_args()
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
@@ -40,13 +44,25 @@ def main():
     ga = order.graph
     wh, el, er = ops.gat_project(X, W, H, Fh, a_s, a_d, col_rows=order.inv)
     out = torch.empty_like(wh)
-    variants = [("rowclass", False, 128, 16), ("tasks_c64", True, 64, 16),
-                ("tasks_c128", True, 128, 16), ("tasks_c256", True, 256, 16),
-                ("tasks_c128_d32", True, 128, 32)]
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd.build import LIB_DIR
+    variants = [("rowclass", False, 128, 16, None), ("tasks_c64", True, 64, 16, None),
+                ("tasks_c128", True, 128, 16, None), ("tasks_c256", True, 256, 16, None),
+                ("tasks_c128_d32", True, 128, 32, None)]
+    variants += [(f"tasks_c128_{t}", True, 128, 16, LIB_DIR / "variants" / f"libgnn_{t}.so")
+                 for t in a.libs.split(",") if t]
+
+    current = {"lib": "unset"}
+
+    def prep(v):  # outside the timed region: a library switch rebinds every symbol
+        _, tasks, cost, deg, lib = v
+        ops.GAT_TASKS, ops.GAT_TASK_COST, ops.GAT_SHORT_MAX_DEG = tasks, cost, deg
+        if current["lib"] != lib:
+            _lib.use_variant(lib)
+            current["lib"] = lib
 
     def run(v):
-        _, tasks, cost, deg = v
-        ops.GAT_TASKS, ops.GAT_TASK_COST, ops.GAT_SHORT_MAX_DEG = tasks, cost, deg
+        prep(v)
         return ops.gat_aggregate(ga, wh, el, er, H, Fh, 0.2, ops.GAT_DENSE, "elu", out=out)
 
     ref = run(variants[0]).clone()
@@ -58,6 +74,8 @@ def main():
         err[v[0]] = float(((y - ref).abs().max() / ref.abs().max()).item())
     for _ in range(a.reps):
         for v in variants:
+            prep(v)
+            torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             run(v)
