@@ -180,6 +180,10 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_frontier_emit": (ctypes.c_int, [_i64, _vp, _vp, _vp]),
     "gnn_frontier_rank": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gnn_sample_layers_workspace_bytes": (ctypes.c_int64, [_i64]),
+    "gnn_gemm_tn_supported": (ctypes.c_int, [_i64, _i64]),
+    "gnn_gemm_tn_workspace_bytes": (_i64, [_i64, _i64, _i64]),
+    "gnn_gemm_tn_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i32,
+                                       _vp, _i64, _vp, _vp, _i64, _vp]),
     "gnn_sample_layers": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp, _i32, _vp,
                                          _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     # CPython-exact host sampler (pysample.cpp): host pointers, no stream

@@ -141,7 +141,8 @@ constexpr int gat_small_unroll() {
 #define GNN_GAT_U 4  // feature-row gathers in flight per lane in phase B (capped at the chunk's slots)
 #endif
 #ifndef GNN_GAT_PIPE
-#define GNN_GAT_PIPE 1  // pipelined chunk loop in gat_csr_kernel (A/B: tools/gat_ab.py)
+#define GNN_GAT_PIPE 1  // pipelined chunk loop in gat_csr_kernel (0: plain loop; a depth-2 form,
+                        // two chunks in flight, was slower: profiles/r05b_gat_tasks_ab.log)
 #endif
 #ifndef GNN_GAT_CHUNK
 #define GNN_GAT_CHUNK 8  // edges per phase-A chunk (A/B at cfg3 with the short-row path: 8 > 16 > 32 > 64)
@@ -520,79 +521,7 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
   }
 
   constexpr int CE = (C + EPI - 1) / EPI;  // gather slots per chunk
-  if constexpr (GNN_GAT_PIPE == 2 && J == 1 && NCH == 1 && CE <= 4) {
-    // Two chunks in flight: chunk k + 1's er entries and Wh rows (and chunk k + 2's column
-    // ids) are issued before chunk k's softmax arithmetic, from unconditional addresses (a
-    // dead slot reads row 0 and is masked), so that the compiler can keep them outstanding
-    // across the arithmetic. Same arithmetic in the same order as the depth-1 loop below.
-    const int64_t f0 = static_cast<int64_t>(sub) * VW;
-    const bool fok = f0 < P.feat;
-    int np = static_cast<int>(min(static_cast<int64_t>(C), end - beg));
-    int cj = ae < np ? P.col[beg + ae] : 0;
-    int c_next = beg + C + ae < end ? P.col[beg + C + ae] : 0;
-    float erv = er_at(P, cj, head_ok ? ah : 0);
-    typename Vec<VW>::T xv[CE];
-#pragma unroll
-    for (int q = 0; q < CE; ++q) {
-      const int e = q * EPI + grp;
-      const int ce = __shfl(cj, (e < EPP ? e : 0) * HP, kWave);
-      xv[q] = vload<VW>(wh_row(P, ce) + (fok ? f0 : 0));
-    }
-    for (int64_t b = beg; b < end; b += C) {
-      // ---- issue chunk b + C (masked past the row's end) and chunk b + 2C's column ids
-      const int64_t b1 = b + C;
-      const int np1 = b1 < end ? static_cast<int>(min(static_cast<int64_t>(C), end - b1)) : 0;
-      const int cj1 = ae < np1 ? c_next : 0;
-      c_next = b1 + C + ae < end ? P.col[b1 + C + ae] : 0;
-      const float erv1 = er_at(P, cj1, head_ok ? ah : 0);
-      typename Vec<VW>::T xv1[CE];
-#pragma unroll
-      for (int q = 0; q < CE; ++q) {
-        const int e = q * EPI + grp;
-        const int ce = __shfl(cj1, (e < EPP ? e : 0) * HP, kWave);
-        xv1[q] = vload<VW>(wh_row(P, ce) + (fok ? f0 : 0));
-      }
-      // ---- chunk b
-      const bool live = ae < np && head_ok;
-      float z = -INFINITY;
-      if (live) {
-        const float sv = eli + erv;
-        const float x = sv > 0.f ? sv : P.slope * sv;
-        z = SPARSE ? -x : x;
-      }
-      float pv;
-      if (!SPARSE) {
-        float pm = z;
-#pragma unroll
-        for (int o = HP; o < kWave; o <<= 1) pm = fmaxf(pm, __shfl_xor(pm, o, kWave));
-        const float mn = fmaxf(m, pm);
-        const float scale = __expf(m - mn);  // 0 on the first chunk (m = -inf)
-        m = mn;
-        pv = z == -INFINITY ? 0.f : __expf(z - mn);
-        lsum = lsum * scale + pv;
-        acc[0] *= __shfl(scale, hid[0], kWave);
-      } else {
-        pv = z == -INFINITY ? 0.f : __expf(z);  // exp(-LeakyReLU), no max subtraction
-        lsum += pv;
-      }
-#pragma unroll
-      for (int q = 0; q < CE; ++q) {
-        const int e = q * EPI + grp;
-        const bool ok = e < np && fok;
-        float wv = __shfl(pv, (e < EPP ? e : 0) * HP + hid[0], kWave);
-        if (P.drop_p > 0.f && ok) {
-          const uint32_t r = hash3(P.drop_seed, b + e, P.head0 + hid[0]);
-          wv = (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f
-                                                                               : wv * P.drop_scale;
-        }
-        acc[0] += (ok ? wv : 0.f) * (ok ? xv[q] : vzero<VW>());  // a dead slot read row 0
-      }
-      np = np1;
-      erv = erv1;
-#pragma unroll
-      for (int q = 0; q < CE; ++q) xv[q] = xv1[q];
-    }
-  } else if constexpr (GNN_GAT_PIPE && J == 1 && NCH == 1 && CE <= 4) {
+  if constexpr (GNN_GAT_PIPE && J == 1 && NCH == 1 && CE <= 4) {
     // Pipelined chunk loop: the next chunk's column ids are loaded while this chunk is
     // processed, and this chunk's er entries and Wh rows are issued together, before the
     // softmax arithmetic -- one memory round trip per chunk instead of col -> er -> Wh.

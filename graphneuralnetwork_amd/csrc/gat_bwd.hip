@@ -69,6 +69,45 @@ __global__ __launch_bounds__(256) void gat_bwd_prep_kernel(const float* __restri
   D[r * heads + h] = acc;
 }
 
+// Vector form (fh % 4 == 0, fh / 4 a power of two, 16-B rows): a thread per 4 features, the
+// head's D summed over its G = fh / 4 lanes by xor shuffles. The scalar kernel above runs a
+// thread per (row, head) over fh scalar loads: 0.51 ms at cfg3 (1.6 TB/s).
+template <int G>
+__global__ __launch_bounds__(256) void gat_bwd_prep_vec_kernel(const float* __restrict__ dy,
+                                                               const float* __restrict__ y,
+                                                               int64_t ldo, int64_t n_rows,
+                                                               int64_t heads, int elu,
+                                                               float* __restrict__ dout,
+                                                               float* __restrict__ D) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t per_row = heads * G;  // float4s per row
+  const bool live = t < n_rows * per_row;
+  const int64_t r = live ? t / per_row : 0, c = live ? t % per_row : 0;
+  float4 yv = make_float4(0.f, 0.f, 0.f, 0.f), gv = yv;
+  if (live) {
+    yv = *reinterpret_cast<const float4*>(y + r * ldo + 4 * c);
+    gv = *reinterpret_cast<const float4*>(dy + r * ldo + 4 * c);
+  }
+  float yy[4] = {yv.x, yv.y, yv.z, yv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w}, dd[4];
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float d = gg[i], o = yy[i];
+    if (elu && yy[i] <= 0.f) {  // ELU'(x) = y + 1 for x <= 0, x = log1p(y) (saturated: 0)
+      const float tt = yy[i] + 1.f;
+      d = gg[i] * tt;
+      o = tt > 0.f ? log1pf(yy[i]) : 0.f;
+    }
+    dd[i] = d;
+    acc = fmaf(d, o, acc);
+  }
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
+  if (!live) return;
+  *reinterpret_cast<float4*>(dout + r * (heads * 4 * G) + 4 * c) = make_float4(dd[0], dd[1], dd[2], dd[3]);
+  if (c % G == 0) D[r * heads + c / G] = acc;
+}
+
 // ---------------------------------------------------------------- edges
 struct BwdEdgeParams {
   const int64_t* rowptr;
@@ -427,6 +466,23 @@ extern "C" int gnn_gat_backward_prep_f32(const float* dy, const float* y, int64_
   if (n_rows < 0 || heads < 1 || fh < 1 || ldo < heads * fh) return GNN_E_ARG;
   if (n_rows == 0) return GNN_OK;
   if (!dy || !y || !dout || !D) return GNN_E_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t g = fh / 4;
+  if (fh % 4 == 0 && (g & (g - 1)) == 0 && g <= 64 && ldo % 4 == 0 && aligned_to(dy, 16) &&
+      aligned_to(y, 16) && aligned_to(dout, 16)) {
+    const int64_t tv = n_rows * heads * g;
+    const dim3 grid(static_cast<unsigned>((tv + 255) / 256));
+    switch (g) {
+      case 1: hipLaunchKernelGGL(gat_bwd_prep_vec_kernel<1>, grid, dim3(256), 0, s, dy, y, ldo, n_rows, heads, elu, dout, D); break;
+      case 2: hipLaunchKernelGGL(gat_bwd_prep_vec_kernel<2>, grid, dim3(256), 0, s, dy, y, ldo, n_rows, heads, elu, dout, D); break;
+      case 4: hipLaunchKernelGGL(gat_bwd_prep_vec_kernel<4>, grid, dim3(256), 0, s, dy, y, ldo, n_rows, heads, elu, dout, D); break;
+      case 8: hipLaunchKernelGGL(gat_bwd_prep_vec_kernel<8>, grid, dim3(256), 0, s, dy, y, ldo, n_rows, heads, elu, dout, D); break;
+      case 16: hipLaunchKernelGGL(gat_bwd_prep_vec_kernel<16>, grid, dim3(256), 0, s, dy, y, ldo, n_rows, heads, elu, dout, D); break;
+      case 32: hipLaunchKernelGGL(gat_bwd_prep_vec_kernel<32>, grid, dim3(256), 0, s, dy, y, ldo, n_rows, heads, elu, dout, D); break;
+      default: hipLaunchKernelGGL(gat_bwd_prep_vec_kernel<64>, grid, dim3(256), 0, s, dy, y, ldo, n_rows, heads, elu, dout, D); break;
+    }
+    return launch_status();
+  }
   const int64_t t = n_rows * heads;
   hipLaunchKernelGGL(gat_bwd_prep_kernel, dim3(static_cast<unsigned>((t + 255) / 256)), dim3(256), 0,
                      static_cast<hipStream_t>(stream), dy, y, ldo, n_rows, heads, fh, elu, dout, D);

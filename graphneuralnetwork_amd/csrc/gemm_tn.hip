@@ -1,0 +1,237 @@
+// gemm_tn.hip -- the weight gradients of the training step: C = A^T B over a long row axis.
+//
+// Replaces the autograd GEMMs of nn.Linear inside the reference's training loops
+// (GCN/train_eval.py:43-48 through Graph_conv_layer's `self.dense`, GCN/GCN.py:42: dW = dS^T X;
+// GAT/train_eval.py:75-76 through `torch.mm(h, self.W)`, GAT/models/layers.py:23: dW = h^T dWh),
+// and the bias gradient db = column sums of dY (GCN/GCN.py:45). A [n, M], B [n, K] with n the
+// node count (1M-10M) and M, K <= 128: a tall-skinny reduction with a tiny output, where a
+// library GEMM parallelises badly (hipBLASLt: 1.81 ms for 1M x 128 x 128 at cfg2, 7 % of HBM).
+//
+// Each workgroup reduces a contiguous block of rows: 32-row tiles of A and B are staged in LDS
+// with coalesced 16-B loads (the next tile is loaded into registers while this one is
+// multiplied), and thread (tm, tk) accumulates its TM x TK patch of the outer products in fp32
+// registers, in row order. The per-workgroup partials go to a workspace and a second kernel sums
+// them in workgroup order: deterministic, no atomics. fp32 FMAs: on gfx950 the fp32 MFMA runs at
+// the fp32 vector rate, so there is nothing to gain from the matrix cores at fp32.
+// Optional: dsum[k] = sum_i D[i, k] (a third [n, K] operand, accumulated while its tiles pass).
+#include "common.hpp"
+
+namespace gnn {
+
+constexpr int kTnThreads = 256;
+constexpr int kTnRows = 32;  // rows per LDS tile
+
+template <int M, int K>
+struct TnShape {
+  // the 256 threads tile the M x K output as (M / TM) x (K / TK)
+  static constexpr int TM = M >= 128 ? 8 : (M >= 64 ? 4 : 1);
+  static constexpr int TK = (M / TM) * (K / 8) == kTnThreads ? 8
+                          : (M / TM) * (K / 4) == kTnThreads ? 4
+                          : (M / TM) * (K / 2) == kTnThreads ? 2 : 1;
+  static_assert((M / TM) * (K / TK) == kTnThreads, "unsupported (M, K)");
+  static constexpr int A4 = M / 4, B4 = K / 4;  // float4s per row
+};
+
+template <int M, int K, bool DSUM>
+__global__ __launch_bounds__(kTnThreads) void gemm_tn_partial_kernel(
+    const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb,
+    const float* __restrict__ d, int64_t ldd, int64_t n, int64_t rows_per_block,
+    float* __restrict__ part) {
+  using S = TnShape<M, K>;
+  constexpr int TM = S::TM, TK = S::TK, A4 = S::A4, B4 = S::B4;
+  constexpr int NA = (kTnRows * A4 + kTnThreads - 1) / kTnThreads;  // float4s per thread per tile
+  constexpr int NB = (kTnRows * B4 + kTnThreads - 1) / kTnThreads;
+  __shared__ float4 sa[kTnRows * A4];
+  __shared__ float4 sb[kTnRows * B4];
+  const int t = threadIdx.x;
+  const int tm = t / (K / TK), tk = t % (K / TK);
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  float acc[TM][TK];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TK; ++j) acc[i][j] = 0.f;
+  float4 ds[NB];  // DSUM: this thread's running sums of the D float4s it stages
+#pragma unroll
+  for (int q = 0; q < NB; ++q) ds[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  auto load = [&](int64_t row0, float4 (&va)[NA], float4 (&vb)[NB], float4 (&vd)[NB]) {
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int i = t + q * kTnThreads;
+      const int64_t row = row0 + i / A4;
+      va[q] = (i < kTnRows * A4 && row < r1)
+                  ? *reinterpret_cast<const float4*>(a + row * lda + 4 * (i % A4))
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int i = t + q * kTnThreads;
+      const int64_t row = row0 + i / B4;
+      const bool ok = i < kTnRows * B4 && row < r1;
+      vb[q] = ok ? *reinterpret_cast<const float4*>(b + row * ldb + 4 * (i % B4))
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (DSUM)
+        vd[q] = ok ? *reinterpret_cast<const float4*>(d + row * ldd + 4 * (i % B4))
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+
+  float4 va[NA], vb[NB], vd[NB];
+  load(r0, va, vb, vd);
+  for (int64_t row0 = r0; row0 < r1; row0 += kTnRows) {
+    __syncthreads();  // the previous tile's readers are done
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int i = t + q * kTnThreads;
+      if (i < kTnRows * A4) sa[i] = va[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int i = t + q * kTnThreads;
+      if (i < kTnRows * B4) sb[i] = vb[q];
+      if constexpr (DSUM) {
+        ds[q].x += vd[q].x;
+        ds[q].y += vd[q].y;
+        ds[q].z += vd[q].z;
+        ds[q].w += vd[q].w;
+      }
+    }
+    __syncthreads();
+    if (row0 + kTnRows < r1) load(row0 + kTnRows, va, vb, vd);  // next tile in flight
+    const int nr = static_cast<int>(min(static_cast<int64_t>(kTnRows), r1 - row0));
+    for (int r = 0; r < nr; ++r) {
+      float x[TM], y[TK];
+      const float* ar = reinterpret_cast<const float*>(sa + r * A4) + tm * TM;
+      const float* br = reinterpret_cast<const float*>(sb + r * B4) + tk * TK;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) x[i] = ar[i];
+#pragma unroll
+      for (int j = 0; j < TK; ++j) y[j] = br[j];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TK; ++j) acc[i][j] = fmaf(x[i], y[j], acc[i][j]);
+    }
+  }
+  float* pc = part + static_cast<int64_t>(blockIdx.x) * (M * K + (DSUM ? K : 0));
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TK; ++j) pc[(tm * TM + i) * K + tk * TK + j] = acc[i][j];
+  if constexpr (DSUM) {
+    // every thread stages the same float4 columns of D in every tile (i % B4 is fixed per q):
+    // the threads holding column group c are t = c + B4 * s; sum them in a fixed order via LDS
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int i = t + q * kTnThreads;
+      if (i < kTnRows * B4) sb[i] = ds[q];
+    }
+    __syncthreads();
+    if (t < B4) {
+      float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int i = t; i < kTnRows * B4; i += B4) {
+        s4.x += sb[i].x;
+        s4.y += sb[i].y;
+        s4.z += sb[i].z;
+        s4.w += sb[i].w;
+      }
+      pc[M * K + 4 * t] = s4.x;
+      pc[M * K + 4 * t + 1] = s4.y;
+      pc[M * K + 4 * t + 2] = s4.z;
+      pc[M * K + 4 * t + 3] = s4.w;
+    }
+  }
+}
+
+// out[e] (+)= sum over the blocks' partials, in block order (e < M*K: C, then dsum)
+__global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(const float* __restrict__ part,
+                                                             int64_t blocks, int64_t stride,
+                                                             int64_t mk, int64_t k,
+                                                             float* __restrict__ c, int64_t ldc,
+                                                             int trans_c,
+                                                             float* __restrict__ dsum) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (e >= stride) return;
+  float s = 0.f;
+  for (int64_t g = 0; g < blocks; ++g) s += part[g * stride + e];
+  if (e >= mk)
+    dsum[e - mk] = s;
+  else if (trans_c)
+    c[(e % k) * ldc + e / k] = s;  // C^T: [k, m]
+  else
+    c[(e / k) * ldc + e % k] = s;
+}
+
+constexpr int64_t kTnBlocks = 512;  // 2 workgroups per CU
+
+static int64_t tn_blocks(int64_t n) {
+  const int64_t by_rows = (n + 4 * kTnRows - 1) / (4 * kTnRows);  // >= 4 tiles per block
+  return by_rows < kTnBlocks ? (by_rows < 1 ? 1 : by_rows) : kTnBlocks;
+}
+
+template <int M, int K>
+static int launch_tn(const float* a, int64_t lda, const float* b, int64_t ldb, const float* d,
+                     int64_t ldd, int64_t n, float* c, int64_t ldc, int trans_c, float* dsum,
+                     float* part, hipStream_t s) {
+  const int64_t blocks = tn_blocks(n);
+  int64_t rpb = (n + blocks - 1) / blocks;
+  rpb = (rpb + kTnRows - 1) / kTnRows * kTnRows;
+  const int64_t stride = M * K + (d ? K : 0);
+  if (d)
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<M, K, true>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+  else
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<M, K, false>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3(static_cast<unsigned>((stride + 255) / 256)),
+                     dim3(256), 0, s, part, blocks, stride, static_cast<int64_t>(M * K),
+                     static_cast<int64_t>(K), c, ldc, trans_c, dsum);
+  return launch_status();
+}
+
+}  // namespace gnn
+
+using namespace gnn;
+
+extern "C" int gnn_gemm_tn_supported(int64_t m, int64_t k) {
+  return (m == 128 && k == 128) || (m == 64 && k == 64) || (m == 128 && k == 64) ||
+         (m == 64 && k == 128) || (m == 8 && k == 64);
+}
+
+extern "C" int64_t gnn_gemm_tn_workspace_bytes(int64_t n, int64_t m, int64_t k) {
+  if (n < 0 || m < 1 || k < 1) return GNN_E_ARG;
+  return tn_blocks(n) * (m * k + k) * static_cast<int64_t>(sizeof(float));
+}
+
+// C[m, k] = A^T B = sum_i A[i, :]^T B[i, :] (A [n, m], B [n, k], row strides lda / ldb), stored
+// as C (trans_c = 0, row stride ldc >= k) or as C^T [k, m] (trans_c = 1, ldc >= m); when
+// d != NULL also dsum[k] = sum_i D[i, :] (D [n, k]). fp32, deterministic. Shapes: (m, k) in
+// gnn_gemm_tn_supported; rows 16-B aligned (row strides multiples of 4 floats).
+extern "C" int gnn_gemm_tn_f32(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t n,
+                               int64_t m, int64_t k, float* c, int64_t ldc, int32_t trans_c,
+                               const float* d, int64_t ldd, float* dsum, void* workspace,
+                               int64_t workspace_bytes, void* stream) {
+  if (n < 0 || !a || !b || !c || !workspace || lda < m || ldb < k) return GNN_E_ARG;
+  if (trans_c ? ldc < m : ldc < k) return GNN_E_ARG;
+  if (d && (!dsum || ldd < k)) return GNN_E_ARG;
+  if (!gnn_gemm_tn_supported(m, k)) return GNN_E_UNSUPPORTED;
+  if (workspace_bytes < gnn_gemm_tn_workspace_bytes(n, m, k)) return GNN_E_ARG;
+  if (!aligned_to(a, 16) || !aligned_to(b, 16) || (d && !aligned_to(d, 16)) || lda % 4 ||
+      ldb % 4 || (d && ldd % 4))
+    return GNN_E_ALIGN;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(workspace);
+  const int tc = trans_c ? 1 : 0;
+  if (m == 128 && k == 128)
+    return launch_tn<128, 128>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
+  if (m == 64 && k == 64)
+    return launch_tn<64, 64>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
+  if (m == 128 && k == 64)
+    return launch_tn<128, 64>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
+  if (m == 64 && k == 128)
+    return launch_tn<64, 128>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
+  return launch_tn<8, 64>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
+}

@@ -39,7 +39,7 @@ from torch import nn
 
 from .graph import as_csr
 from .ops import (GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_backward, gat_column_order,
-                  gat_logits, gat_project)
+                  gat_logits, gat_project, gemm_tn)
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
@@ -67,14 +67,48 @@ class _GatLayerFn(torch.autograd.Function):
         dwh, dout, dl, der = gat_backward(g, Wh, el, er, stats, out, dy, a_src, a_dst, heads, fh,
                                           slope, mode, activation == "elu", drop_p, seed)
         n = Wh.shape[0]
-        W3 = Wh.detach().view(n, heads, fh)
-        da_src = (dl.unsqueeze(-1) * W3).sum(0).reshape(-1)   # el = a_src . Wh
-        da_dst = (der.unsqueeze(-1) * W3).sum(0).reshape(-1)  # er = a_dst . Wh
+        da_src, da_dst = _attention_vector_grads(Wh.detach(), dl, der, heads, fh)
         if mode == GAT_DENSE and g.has_empty_rows():
             # an edgeless row is the uniform average of every row (layers.py:29-32)
             empty = (g.rowptr[1:] - g.rowptr[:-1]) == 0
             dwh = dwh + dout[empty].sum(0) / n
         return dwh, da_src, da_dst, None, None, None, None, None, None, None, None
+
+
+def _attention_vector_grads(Wh, dl, der, heads, fh):
+    """d a_src[h, f] = sum_n dl[n, h] Wh[n, h, f] (el = a_src . Wh) and likewise d a_dst with der:
+    the diagonal [h, h*fh:(h+1)*fh] blocks of dl^T Wh, one pass over Wh each (gnn_gemm_tn_f32)
+    where the shape is covered, else the torch reduction."""
+    out = []
+    for g in (dl, der):
+        r = gemm_tn(g, Wh)
+        if r is None:
+            out.append((g.unsqueeze(-1) * Wh.view(-1, heads, fh)).sum(0).reshape(-1))
+        else:
+            c = r[0].view(heads, heads, fh)
+            out.append(c[torch.arange(heads), torch.arange(heads)].reshape(-1))
+    return out[0], out[1]
+
+
+class _ProjectFn(torch.autograd.Function):
+    """Wh = x W (layers.py:23 / :97, all heads side by side) with the weight gradient
+    dW = x^T dWh by gnn_gemm_tn_f32 (a K = N reduction; hipBLASLt parallelises it badly)."""
+
+    @staticmethod
+    def forward(ctx, x, W):
+        ctx.save_for_backward(x, W)
+        return torch.mm(x, W)
+
+    @staticmethod
+    def backward(ctx, dwh):
+        x, W = ctx.saved_tensors
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dwh, W.t())
+        if ctx.needs_input_grad[1]:
+            r = gemm_tn(x, dwh.contiguous())
+            dw = r[0] if r is not None else torch.mm(x.t(), dwh)
+        return dx, dw
 
 
 def _project(x, W, heads, fh, a_src, a_dst):
@@ -86,6 +120,9 @@ def _project(x, W, heads, fh, a_src, a_dst):
         r = gat_project(x, W, heads, fh, a_src, a_dst)
         if r is not None:
             return r[0], (r[1], r[2])
+    if x.is_cuda and x.dtype == torch.float32 and W.dtype == torch.float32 \
+            and torch.is_grad_enabled() and (x.requires_grad or W.requires_grad):
+        return _ProjectFn.apply(x, W), None
     return torch.mm(x, W), None
 
 

@@ -355,6 +355,37 @@ def spmm(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None) -> torc
     return spmm_forward(g, x, bias)
 
 
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, d: torch.Tensor | None = None,
+            trans: bool = False):
+    """(A^T B, column sums of D) over the row axis (gnn_gemm_tn_f32): the weight / bias
+    gradients of the training step. ``trans``: return (A^T B)^T = B^T A. None when the shape is
+    not covered (the caller uses torch.mm)."""
+    _require_device(a, b, d)
+    if (a.dtype != torch.float32 or b.dtype != torch.float32 or a.dim() != 2 or b.dim() != 2
+            or a.shape[0] != b.shape[0] or (d is not None and d.shape != b.shape)):
+        return None
+    n, m = a.shape
+    k = b.shape[1]
+    lib = _lib.load()
+    if not lib.gnn_gemm_tn_supported(m, k):
+        return None
+    ts = [a, b] + ([d] if d is not None else [])
+    ts = [t if (t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0)
+          else t.contiguous() for t in ts]
+    a, b = ts[0], ts[1]
+    d = ts[2] if d is not None else None
+    c = torch.empty((k, m) if trans else (m, k), dtype=torch.float32, device=a.device)
+    dsum = torch.empty(k, dtype=torch.float32, device=a.device) if d is not None else None
+    ws = torch.empty(int(lib.gnn_gemm_tn_workspace_bytes(n, m, k)), dtype=torch.uint8,
+                     device=a.device)
+    _lib.check(lib.gnn_gemm_tn_f32(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), n, m, k,
+                                   c.data_ptr(), c.stride(0), 1 if trans else 0, _lib.ptr(d),
+                                   d.stride(0) if d is not None else 0, _lib.ptr(dsum),
+                                   ws.data_ptr(), ws.numel(), _lib.stream_handle(a.device)),
+               "gnn_gemm_tn_f32")
+    return c, dsum
+
+
 def _transform_or_mm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """x @ w^T: the MFMA transform where it covers the shape, else torch.mm (hipBLASLt)."""
     y = gcn_transform(x, w)
@@ -370,7 +401,8 @@ class _GcnLayerFn(torch.autograd.Function):
               then Y = A S + b (the forward SpMM path, bias in its epilogue);
     backward  dS = A^T dY (the same SpMM kernels; A itself when it is symmetric, as the GCN
               normalisation is: no transposed copy), dX = dS W on the MFMA transform,
-              dW = dS^T X (torch.mm: a K = n_rows reduction, hipBLASLt), db = column sums of dY.
+              dW = dS^T X and db = the column sums of dY in one pass (gnn_gemm_tn_f32, a
+              K = n_rows reduction: 1.81 ms on hipBLASLt at cfg2).
     The support S is not kept for backward (dW needs X and dS only)."""
 
     @staticmethod
@@ -396,9 +428,15 @@ class _GcnLayerFn(torch.autograd.Function):
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
             gx = _transform_or_mm(ds, weight.t().contiguous())
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            gw = torch.mm(ds.t(), x)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+            # dW = dS^T X as (X^T dS)^T, with db = the column sums of dY read in the same pass
+            r = gemm_tn(x, ds, gy if want_b else None, trans=True)
+            if r is not None:
+                gw, gb = r
+            else:
+                gw = torch.mm(ds.t(), x)
+        if want_b and gb is None:
             gb = gy.sum(0)
         return gx, gw, gb, None
 
@@ -637,8 +675,12 @@ GAT_SHORT_MAX_DEG = 16  # rows with 2..16 edges take the short-row path (A/B at 
 # Packed row tasks for the rows of degree <= GAT_SHORT_MAX_DEG (gnn_gat_csr_tasks_f32,
 # gat.hip gat_packed_rows): runs of consecutive low-degree rows, edgeless and one-edge rows
 # included, cut at GAT_TASK_COST edges + rows, one wave per task -- in place of the packed
-# small rows and gat_short_kernel's four rows per wave
-GAT_TASKS = True
+# small rows and gat_short_kernel's four rows per wave. Built, tested, and slower at cfg3:
+# aggregation 0.943-0.976 ms (cost 64-256) against 0.779 ms for the row classes
+# (tools/gat_tasks_ab.py, profiles/r05b_gat_tasks_ab.log): the small-row path packs the 435K
+# edgeless / one-edge rows far more cheaply than a task's per-row flush and per-edge softmax
+# update. Opt-in.
+GAT_TASKS = False
 GAT_TASK_COST = 128
 
 

@@ -492,6 +492,23 @@ int gnn_gat_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, int64_t n_r
                           int64_t ldwh, const float* erh, int64_t ldeh);
 
 /*
+ * Weight gradients of the training step (GCN/train_eval.py:43-48 through GCN/GCN.py:42,
+ * GAT/train_eval.py:75-76 through GAT/models/layers.py:23): C = A^T B summed over the n rows
+ * (A [n, m], B [n, k], row strides lda / ldb), written as C [m, k] (trans_c = 0, row stride
+ * ldc >= k) or C^T [k, m] (trans_c = 1, ldc >= m); with d != NULL also dsum[k] = the column sums
+ * of D [n, k] (the bias gradient, read in the same pass). fp32 FMAs in row order per block of
+ * rows, the block partials summed in block order (deterministic). (m, k) as
+ * gnn_gemm_tn_supported; 16-B aligned rows (GNN_E_ALIGN). workspace:
+ * gnn_gemm_tn_workspace_bytes(n, m, k) bytes of device memory.
+ */
+int gnn_gemm_tn_supported(int64_t m, int64_t k);
+int64_t gnn_gemm_tn_workspace_bytes(int64_t n, int64_t m, int64_t k);
+int gnn_gemm_tn_f32(const float* a, int64_t lda, const float* b, int64_t ldb, int64_t n,
+                    int64_t m, int64_t k, float* c, int64_t ldc, int32_t trans_c, const float* d,
+                    int64_t ldd, float* dsum, void* workspace, int64_t workspace_bytes,
+                    void* stream);
+
+/*
  * Column mean of x[n_rows, feat] (double accumulation, deterministic): the dense
  * GAT layer's output for an edgeless row (uniform softmax over all N nodes,
  * GAT/models/layers.py:29-32). scratch: gnn_col_mean_scratch_bytes(n_rows, feat).

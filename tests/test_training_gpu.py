@@ -120,3 +120,72 @@ def test_gcn_layer_training_cfg2_full_size(dev):
     layer.zero_grad()
     layer(X, g).backward(gy)
     close(X.grad.cpu().numpy(), dS @ W)
+
+
+@pytest.mark.parametrize("m,k", [(128, 128), (64, 64), (128, 64), (64, 128), (8, 64)])
+@pytest.mark.parametrize("n", [1, 37, 20000, 300001])
+def test_gemm_tn_vs_float64(dev, m, k, n):
+    """gnn_gemm_tn_f32 (the weight / bias gradients): A^T B and the column sums of D against
+    float64, plain and transposed output, strided rows, an empty row range; deterministic."""
+    from graphneuralnetwork_amd.ops import gemm_tn
+    gen = torch.Generator(device=dev).manual_seed(m + k + n)
+    a = torch.randn(n, m + 4, device=dev, generator=gen)[:, :m]   # row stride m + 4
+    b = torch.randn(n, k, device=dev, generator=gen)
+    d = torch.randn(n, k, device=dev, generator=gen)
+    c, ds = gemm_tn(a, b, d)
+    ref = a.double().t() @ b.double()
+    close(c.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5)
+    close(ds.cpu().numpy(), d.double().sum(0).cpu().numpy(), rtol=1e-5)
+    ct, none = gemm_tn(a, b, trans=True)
+    assert none is None and ct.shape == (k, m)
+    assert torch.equal(ct, c.t())
+    c2, ds2 = gemm_tn(a, b, d)
+    assert torch.equal(c2, c) and torch.equal(ds2, ds)
+    assert gemm_tn(torch.randn(n, 96, device=dev), b) is None  # uncovered shape: caller's torch.mm
+
+
+def test_gat_training_grads_use_tn_kernel(dev):
+    """The GAT block's W / a gradients through _ProjectFn and _attention_vector_grads
+    (gnn_gemm_tn_f32) equal float64 autograd of the same layer math."""
+    from graphneuralnetwork_amd.gat import GAT
+    from graphneuralnetwork_amd.graph import CsrGraph
+    n = 3000
+    rng = np.random.default_rng(9)
+    r = np.concatenate([rng.integers(0, n, 30000), np.arange(n)])   # every row has an edge
+    c = np.concatenate([rng.integers(0, n, 30000), np.arange(n)])
+    order = np.lexsort((c, r))
+    r, col = r[order], c[order].astype(np.int32)
+    rowptr = np.zeros(n + 1, np.int64)
+    np.add.at(rowptr, r + 1, 1)
+    rowptr = np.cumsum(rowptr)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.ones(col.size, device=dev), n, n)
+    net = GAT(64, 8, 3, dropout=0.0, alpha=0.2, nheads=8).to(dev).train()
+    X = torch.randn(n, 64, device=dev)
+    gy = torch.randn(n, 64, device=dev)
+    net._heads(X, g).backward(gy)
+    # float64 reference of the same block
+    W = torch.cat([m.W for m in net.attentions], 1).detach().double().cpu().requires_grad_()
+    a_s = torch.cat([m._a_parts()[0] for m in net.attentions]).detach().double().cpu()
+    a_d = torch.cat([m._a_parts()[1] for m in net.attentions]).detach().double().cpu()
+    a_s.requires_grad_()
+    a_d.requires_grad_()
+    Xd = X.double().cpu()
+    rows = torch.from_numpy(np.repeat(np.arange(n), np.diff(rowptr)))
+    cols = torch.from_numpy(col.astype(np.int64))
+    Wh = (Xd @ W).view(n, 8, 8)
+    el = (Wh * a_s.view(8, 8)).sum(-1)
+    er = (Wh * a_d.view(8, 8)).sum(-1)
+    z = torch.nn.functional.leaky_relu(el[rows] + er[cols], 0.2)
+    mx = torch.full((n, 8), -torch.inf, dtype=torch.float64).index_reduce(0, rows, z, "amax")
+    p = torch.exp(z - mx[rows])
+    den = torch.zeros(n, 8, dtype=torch.float64).index_add(0, rows, p)
+    num = torch.zeros(n, 8, 8, dtype=torch.float64).index_add(0, rows, p.unsqueeze(-1) * Wh[cols])
+    out = torch.nn.functional.elu(num / den.unsqueeze(-1)).view(n, 64)
+    out.backward(gy.double().cpu())
+    gW = torch.cat([m.W.grad for m in net.attentions], 1).cpu().numpy()
+    close(gW, W.grad.numpy())
+    ga_s = torch.cat([m.a.grad.view(-1)[:8] for m in net.attentions]).cpu().numpy()
+    ga_d = torch.cat([m.a.grad.view(-1)[8:] for m in net.attentions]).cpu().numpy()
+    close(ga_s, a_s.grad.numpy())
+    close(ga_d, a_d.grad.numpy())

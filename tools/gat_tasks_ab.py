@@ -4,10 +4,11 @@ cost 64 / 128 / 256 edges + rows, degree threshold 16 / 32) against the row clas
 (packed small rows + gat_short_kernel), interleaved in one process, HIP events per launch;
 outputs compared with the row-class path.
 
-    python tools/gat_tasks_ab.py [--reps 30] [--libs gatpipe2]
+    python tools/gat_tasks_ab.py [--reps 30] [--libs <variant tags>]
 
 --libs: variant libraries (lib/variants/libgnn_<tag>.so, build.build_variant) timed with the
-default schedule beside the main library (e.g. gatpipe2 = GNN_GAT_PIPE=2: two chunks in flight).
+default schedule beside the main library (round 5: gatpipe2 = a depth-2 chunk pipeline, since
+removed: profiles/r05b_gat_tasks_ab.log).
 """
 from __future__ import annotations
 

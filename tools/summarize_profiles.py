@@ -29,7 +29,8 @@ ROOT = Path(__file__).resolve().parent.parent
 WORKLOADS = {
     "cfg2": (128, "spmm_csr_kernel+spmm_fixup_kernel", ("steps", 7)),
     "ns": (128, "spmm_csr_kernel+spmm_fixup_kernel", ("steps", 7)),
-    "cfg3": (64, "gat_csr_kernel+gat_short_kernel+gat_fixup_kernel", ("median", None)),
+    "cfg3": (64, "gat_csr_kernel+gat_short_kernel+gat_task_kernel+gat_fixup_kernel",
+             ("median", None)),
     "cfg4": (128, "sage_aggregate_kernel<4, 32, 1, 0, true, 8, false>", ("largest", None)),
 }
 SQ = ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VALU",
@@ -43,8 +44,9 @@ def rows(path):
 def counter(path, name, kernel, how):
     vals = [float(r["Counter_Value"]) for r in rows(path)
             if kernel in r["Kernel_Name"] and r["Counter_Name"] == name]
-    if not vals:
-        raise SystemExit(f"no {name} rows for {kernel!r} in {path}")
+    if not vals:  # a kernel of the list this schedule does not launch
+        print(f"  (no {name} rows for {kernel!r})")
+        return 0.0, 0
     mode, n = how
     if mode == "steps":
         return sum(vals) / n, len(vals)
