@@ -631,10 +631,10 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
     """One training step of the drop-in 8-head GAT attention block at cfg3 (GAT.py:16's heads
     through GATBase._heads: one X W GEMM for all heads, the fused edge-softmax aggregation with
     ELU; GAT/train_eval.py:75-76's loss.backward()): forward + backward with W, a_src, a_dst
-    requiring grad (X is the input features). The backward's three HIP passes
-    (csrc/gat_bwd.hip: prep, SDDMM edge pass, transposed node pass; replacing the autograd of
-    GAT/models/layers.py:22-37 and SpecialSpmmFunction.backward :54-64) are also timed alone,
-    each with a roofline on its compulsory bytes."""
+    requiring grad (X is the input features). The backward's HIP passes (csrc/gat_bwd.hip:
+    the row pass with the prep fused in, the recomputing node pass over A^T; replacing the
+    autograd of GAT/models/layers.py:22-37 and SpecialSpmmFunction.backward :54-64) are also
+    timed alone, each with a roofline on its compulsory bytes."""
     from graphneuralnetwork_amd.gat import GAT
     from graphneuralnetwork_amd.ops import GAT_DENSE, gat_aggregate, gat_backward, gat_logits
     gen = torch.Generator(device=dev).manual_seed(3)
@@ -669,14 +669,22 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
             for name, a, b in tl:
                 per.setdefault(name, []).append(a.elapsed_time(b))
     n, nnz, feat = g.n_rows, g.nnz, H * Fh
+    two_pass = "rows" in per
     comp = {"prep": n * 4 * (3 * feat + H),
             "edges": nnz * (4 + 8 * H) + n * (8 + 16 * H + 4 * feat) + g.n_cols * (4 * H + 4 * feat),
-            "nodes": nnz * (12 + 8 * H) + n * (8 + 8 * feat + 8 * H)}
+            "rows": nnz * 4 + n * (8 + 12 * feat + 28 * H) + g.n_cols * (4 * H + 4 * feat),
+            "nodes": (nnz * 4 + n * (8 + 12 * feat + 28 * H)) if two_pass else
+                     (nnz * (12 + 8 * H) + n * (8 + 8 * feat + 8 * H))}
     what = {"prep": "gat_bwd_prep_kernel: dout = dy ELU'(out), D = dout . out",
             "edges": "gat_bwd_edge_kernel (+ del fix-up): SDDMM g = dout_i . Wh_j, edge weights "
                      "w_ij and softmax/LeakyReLU gradients ds_ij written per (edge, head)",
-            "nodes": "gat_bwd_node_kernel (+ fix-up) over the transposed CSR: dWh_j = sum_i w_ij "
-                     "dout_i + der_j a_dst + del_j a_src"}
+            "rows": "gat_bwd_rows_kernel (+ del fix-up): prep fused (dout, D_i), SDDMM g = "
+                    "dout_i . Wh_j and ds_ij summed into del_i; per-row record {el, lse, D}",
+            "nodes": ("gat_bwd_node_r_kernel (+ fix-up) over A^T (A itself when symmetric): "
+                      "a_ij, g_ij, w_ij, ds_ij recomputed from the gathered dout_i and {el, lse, "
+                      "D}_i; dWh_j = sum_i w_ij dout_i + der_j a_dst + del_j a_src") if two_pass
+                     else ("gat_bwd_node_kernel (+ fix-up) over the transposed CSR: dWh_j = "
+                           "sum_i w_ij dout_i + der_j a_dst + del_j a_src")}
     kernels = {}
     for name, ms in per.items():
         t = statistics.mean(ms) / 1e3
@@ -693,10 +701,15 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
            "forward_path": "torch.mm (X W, autograd) + gat_logits + gat_aggregate with per-row "
                            "log-sum-exp stats (hub-staged Wh / er)",
            "backward_kernels": kernels,
-           "compulsory_bytes_model": {
+           "compulsory_bytes_model": ({
+               "rows": "4 nnz + N (8 + 12 H Fh + 28 H) + N (4 H + 4 H Fh): y, dy, el, lse, "
+                       "rowptr, col read, dout, {el, lse, D, 0}, del written, er / Wh gathered "
+                       "once",
+               "nodes": "4 nnz + N (8 + 12 H Fh + 28 H): rowptr, sources, dout + record "
+                        "gathered once, own Wh / er / del, dWh and der written"} if two_pass else {
                "prep": "4 N (3 H Fh + H)",
                "edges": "nnz (4 + 8 H) + N (8 + 16 H + 4 H Fh) + N (4 H + 4 H Fh)",
-               "nodes": "nnz (12 + 8 H) + N (8 + 8 H Fh + 8 H)"}}
+               "nodes": "nnz (12 + 8 H) + N (8 + 8 H Fh + 8 H)"})}
     if not args.no_cpu_baseline:
         try:
             res["cpu_reference_ops"] = cpu_gat_train_ops(g, X.cpu(), W.cpu(), a_s.cpu(),
@@ -1135,11 +1148,12 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
     GCN/train_eval.py:43-48's loss.backward()), as a hidden layer (dX needed too): forward =
     MFMA transform into the column-degree order + XCD-sliced SpMM with the bias epilogue;
     backward = SpMM over A^T (A itself: the normalised adjacency is symmetric) + MFMA transform
-    (dX = dS W) + hipBLASLt GEMM (dW = dS^T X) + column sums (db). Each backward component is
+    (dX = dS W) + the tall-skinny A^T B kernel (dW = dS^T X with db = column sums of dY in the
+    same pass; hipBLASLt's torch.mm timed beside it). Each backward component is
     also timed alone; the backward SpMM carries its own roofline (compulsory bytes, as the
     forward's)."""
     from graphneuralnetwork_amd.gcn import Graph_conv_layer
-    from graphneuralnetwork_amd.ops import gcn_transform, spmm_forward
+    from graphneuralnetwork_amd.ops import gcn_transform, gemm_tn, spmm_forward
     gen = torch.Generator(device=dev).manual_seed(1)
     layer = Graph_conv_layer(F, F).to(dev)
     X = torch.randn(g.n_cols, F, device=dev, generator=gen).requires_grad_(True)
@@ -1162,7 +1176,10 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
     Wt = layer.dense.weight.detach().t().contiguous()
     Xd = X.detach()
     dx_ms = time_steps(lambda: gcn_transform(ds, Wt), steps, 2, dev)[0]
-    dw_ms = time_steps(lambda: torch.mm(ds.t(), Xd), steps, 2, dev)[0]
+    tn = gemm_tn(Xd, ds, gy, trans=True) is not None
+    dw_ms = (time_steps(lambda: gemm_tn(Xd, ds, gy, trans=True), steps, 2, dev)[0] if tn else
+             time_steps(lambda: torch.mm(ds.t(), Xd), steps, 2, dev)[0])
+    mm_ms = time_steps(lambda: torch.mm(ds.t(), Xd), steps, 2, dev)[0]
     db_ms = time_steps(lambda: gy.sum(0), steps, 2, dev)[0]
     comp = compulsory_bytes(g.nnz, g.n_rows, g.n_cols, F)
     t_sp = statistics.mean(spmm_ms) / 1e3
@@ -1177,8 +1194,9 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
         "backward_components_ms": {
             "spmm_dS_AT_dY": statistics.median(spmm_ms),
             "transform_dX_dS_W": statistics.median(dx_ms),
-            "gemm_dW_dST_X_hipblaslt": statistics.median(dw_ms),
-            "colsum_db": statistics.median(db_ms)},
+            ("gemm_tn_dW_db" if tn else "gemm_dW_dST_X_hipblaslt"): statistics.median(dw_ms),
+            "colsum_db" + ("_in_gemm_tn" if tn else ""): (0.0 if tn else statistics.median(db_ms))},
+        "hipblaslt_mm_dW_for_comparison_ms": statistics.median(mm_ms),
         "backward_spmm_graph": "A itself (symmetric: no transposed copy)" if gt is g else
                                "transposed CSR",
         "roofline_backward_spmm": {
@@ -1192,6 +1210,8 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": 2 * nbytes_rows / (statistics.mean(dw_ms) / 1e3) / 1e9 / HBM_PEAK_GBPS,
             "bytes": 2 * nbytes_rows,
+            "kernel": ("gemm_tn_partial_kernel + gemm_tn_reduce_kernel (dW^T = X^T dS and "
+                       "db = colsum dY in one pass)") if tn else "hipBLASLt (torch.mm)",
             "note": "dS and X read once (K = n_rows reduction, %.1f GFLOP)"
                     % (2 * g.n_rows * F * F / 1e9)},
         "roofline_backward_transform_dX": {

@@ -156,6 +156,20 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _vp,                                   # dwh, der
         _i64, _vp, _vp, _i64, _vp, _vp, _i64,       # plan of the transposed graph
         _vp, _i64, _vp, _vp]),                      # rows, n_rows_list, part, stream
+    "gnn_gat_backward_rows_f32": (ctypes.c_int, [
+        _vp, _vp, _i64, _vp, _i64, _i64, _i64,      # rowptr, col, n_rows, wh, ldw, heads, fh
+        _vp, _vp, _vp, _vp, _vp, _i64, _i32,        # el, er, lse, dy, y, ldo, elu
+        ctypes.c_float, _i32, ctypes.c_float, ctypes.c_uint64,  # slope, mode, drop_p, seed
+        _vp, _vp, _vp,                              # dout, nstat, del
+        _i64, _vp, _vp, _i64, _vp, _vp, _i64,       # plan
+        _vp, _i64, _vp, _i64, _vp, _vp]),           # rows, n, short_rows, n, del_part, stream
+    "gnn_gat_backward_nodes_recompute_f32": (ctypes.c_int, [
+        _vp, _vp, _vp, _i64, _i64, _i64,            # rowptr_t, src_t, eid_t, n, heads, fh
+        _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,    # dout, nstat, wh, ldw, er, del, a_src, a_dst
+        ctypes.c_float, _i32, ctypes.c_float, ctypes.c_uint64,  # slope, mode, drop_p, seed
+        _vp, _vp,                                   # dwh, der
+        _i64, _vp, _vp, _i64, _vp, _vp, _i64,       # plan of the transposed graph
+        _vp, _i64, _vp, _i64, _vp, _vp]),           # rows, n, short_rows, n, part, stream
     "gnn_col_mean_scratch_bytes": (_i64, [_i64, _i64]),
     "gnn_col_mean_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _vp, _vp]),
     "gnn_sage_aggregate_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _i64,

@@ -456,6 +456,420 @@ static int dispatch_nodes(const BwdNodeParams& P, const int32_t* lr, const int32
   return launch_status();
 }
 
+// ---------------------------------------------------------------- rows + recomputing nodes
+// The two passes above hand 2 x 4 H bytes per (edge, head) from the edge pass to the node
+// pass (w_ij, ds_ij written in CSR order, then read through eid_t: two random 4 H-byte reads per
+// edge, each its own cache line) and the prep pass writes dout for the edge pass to re-read.
+// Here the row pass does the prep itself and writes, besides dout and del, only a per-row
+// record nstat_i = {el_i, lse_i, D_i, 0} (4 H floats: one 128-B line at H = 8); the node pass
+// gathers dout_i with nstat_i and recomputes a_ij, g_ij = dout_i . Wh_j (Wh_j is the node's
+// own row, held in registers), w_ij and ds_ij. Per edge the node pass reads 4 + 4 feat + 16 H
+// bytes (12 + 4 feat + 2 x 2 lines before) and the row pass writes nothing.
+constexpr int kRowLds = 1152;    // floats of LDS per wave (4.5 KB: 8 waves per SIMD stay)
+constexpr int kShortRowsW = 8;   // rows per wave of the short-row class (8 lanes each)
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float bwd_keep(float p, float scale, uint64_t seed, int64_t e, int64_t h) {
+  if (p <= 0.f) return 1.f;
+  const uint32_t r = bwd_hash3(seed, e, static_cast<int>(h));
+  return (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < p) ? 0.f : scale;
+}
+
+struct BwdRowParams {
+  const int64_t* rowptr;
+  const int32_t* col;
+  const float* wh;
+  int64_t ldw;
+  const float* el;
+  const float* er;
+  const float* lse;
+  const float* dy;
+  const float* y;
+  int64_t ldo;
+  int elu, sparse, hp;
+  int64_t H, fh, feat;
+  float slope, drop_p, drop_scale;
+  uint64_t drop_seed;
+  float* dout;      // [n, feat]
+  float* nstat;     // [n, 4 H]
+  float* del;       // [n, H]
+  float* del_part;  // [n_seg, H]
+  int64_t seg_len;
+  const int32_t* seg_row;
+  const int64_t* seg_begin;
+  int64_t n_seg, seg_waves;
+  const int32_t* rows;  // one wave per row
+  int64_t n_rows_list, row_waves;
+  const int32_t* short_rows;  // kShortRowsW rows per wave
+  int64_t n_short;
+};
+
+// Waves: [segments of long rows | rows | short rows, 8 per wave]. Prep (lanes = features):
+// dout_i = dy_i ELU'(out_i) into LDS (and HBM: by a long row's first segment only), the
+// products dout . out into LDS, D_i per head summed from them. Edges (lanes = (edge slot,
+// head), HP heads per pass): ds_ij as gat_bwd_edge_kernel, summed into del_i (segments: partials).
+template <int VW, int NFV>
+__global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
+  constexpr int U = 2;
+  __shared__ float lds[kBwWaves][kRowLds];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x >> 6;
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kBwWaves + wid;
+  int mode;  // 0 segment, 1 row, 2 short rows
+  int64_t row0 = -1, sbase = 0;
+  if (wave < P.seg_waves) {
+    if (wave >= P.n_seg) return;
+    mode = 0;
+    row0 = P.seg_row[wave];
+  } else if (wave < P.seg_waves + P.row_waves) {
+    const int64_t i = wave - P.seg_waves;
+    if (i >= P.n_rows_list) return;
+    mode = 1;
+    row0 = P.rows[i];
+  } else {
+    sbase = (wave - P.seg_waves - P.row_waves) * kShortRowsW;
+    if (sbase >= P.n_short) return;
+    mode = 2;
+  }
+  const int nr = mode == 2 ? kShortRowsW : 1;
+  const bool write = mode != 0 || P.seg_begin[wave] == P.rowptr[row0];
+  auto row_of = [&](int r) -> int64_t {
+    if (mode != 2) return row0;
+    return sbase + r < P.n_short ? P.short_rows[sbase + r] : -1;
+  };
+  float* dbuf = lds[wid];
+  float* pbuf = dbuf + nr * P.feat;
+  float* Dbuf = pbuf + nr * P.feat;
+  // ---- prep
+  for (int r = 0; r < nr; ++r) {
+    const int64_t i = row_of(r);
+    if (i < 0) break;  // short rows are listed first to last: the tail slots are empty
+    for (int64_t f = static_cast<int64_t>(lane) * VW; f < P.feat; f += kWave * VW) {
+      const typename Vec<VW>::T yv = vload<VW>(P.y + i * P.ldo + f);
+      const typename Vec<VW>::T gv = vload<VW>(P.dy + i * P.ldo + f);
+      typename Vec<VW>::T dv, pv;
+#pragma unroll
+      for (int k = 0; k < VW; ++k) {
+        const float yy = vget(yv, k), g = vget(gv, k);
+        float d = g, o = yy;
+        if (P.elu && yy <= 0.f) {  // ELU'(x) = y + 1 for x <= 0, x = log1p(y) (saturated: 0)
+          const float t = yy + 1.f;
+          d = g * t;
+          o = t > 0.f ? log1pf(yy) : 0.f;
+        }
+        vset(dv, k, d);
+        vset(pv, k, d * o);
+      }
+      vstore<VW>(dbuf + r * P.feat + f, dv);
+      vstore<VW>(pbuf + r * P.feat + f, pv);
+      if (write) vstore<VW>(P.dout + i * P.feat + f, dv);
+    }
+  }
+  wave_lds_sync();
+  for (int64_t t = lane; t < nr * P.H; t += kWave) {
+    const int r = static_cast<int>(t / P.H);
+    const int64_t h = t % P.H;
+    const int64_t i = row_of(r);
+    const float* pp = pbuf + r * P.feat + h * P.fh;
+    float s = 0.f;
+    for (int64_t k = 0; k < P.fh; ++k) s += pp[k];
+    Dbuf[t] = s;
+    if (i >= 0 && write) {
+      float* ns = P.nstat + i * 4 * P.H;
+      ns[h] = P.el[i * P.H + h];
+      ns[P.H + h] = P.lse[i * P.H + h];
+      ns[2 * P.H + h] = s;
+      ns[3 * P.H + h] = 0.f;
+    }
+  }
+  wave_lds_sync();
+  // ---- edges
+  const int LR = kWave / nr;         // lanes of one row
+  const int r = lane / LR, l = lane % LR;
+  const int HP = P.hp;
+  const int ah = l & (HP - 1), es = l / HP, ES = LR / HP;
+  const int64_t i = row_of(r);
+  int64_t beg = 0, end = 0;
+  if (i >= 0) {
+    if (mode == 0) {
+      beg = P.seg_begin[wave];
+      end = min(beg + P.seg_len, P.rowptr[i + 1]);
+    } else {
+      beg = P.rowptr[i];
+      end = P.rowptr[i + 1];
+    }
+  }
+  const int64_t ii = i >= 0 ? i : 0;
+  const float* drow = dbuf + r * P.feat;
+  const float sgn = P.sparse ? -1.f : 1.f;
+  for (int64_t h0 = 0; h0 < P.H; h0 += HP) {
+    const int64_t h = h0 + ah;
+    const bool hk = h < P.H && i >= 0;
+    const int64_t hh = h < P.H ? h : 0;
+    const float eli = P.el[ii * P.H + hh];
+    const float lsei = P.lse[ii * P.H + hh];
+    const float Di = Dbuf[r * P.H + hh];
+    const float* dh = drow + hh * P.fh;
+    float dsum = 0.f;
+    if (hk) {
+      for (int64_t b = beg + es; b < end; b += static_cast<int64_t>(ES) * U) {
+        int32_t c[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t e = b + static_cast<int64_t>(u) * ES;
+          ok[u] = e < end;
+          c[u] = ok[u] ? P.col[e] : 0;
+        }
+        float erv[U];
+        typename Vec<VW>::T wv[U][NFV > 0 ? NFV : 1];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          erv[u] = P.er[static_cast<int64_t>(c[u]) * P.H + h];
+          if constexpr (NFV > 0) {
+            const float* xr = P.wh + static_cast<int64_t>(c[u]) * P.ldw + h * P.fh;
+#pragma unroll
+            for (int v = 0; v < NFV; ++v) wv[u][v] = vload<VW>(xr + v * VW);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float g = 0.f;
+          if constexpr (NFV > 0) {
+#pragma unroll
+            for (int v = 0; v < NFV; ++v) {
+              const typename Vec<VW>::T dv = vload<VW>(dh + v * VW);
+#pragma unroll
+              for (int k = 0; k < VW; ++k) g = fmaf(vget(dv, k), vget(wv[u][v], k), g);
+            }
+          } else {
+            const float* xr = P.wh + static_cast<int64_t>(c[u]) * P.ldw + h * P.fh;
+            for (int64_t f = 0; f < P.fh; f += VW) {
+              const typename Vec<VW>::T dv = vload<VW>(dh + f);
+              const typename Vec<VW>::T xv = vload<VW>(xr + f);
+#pragma unroll
+              for (int k = 0; k < VW; ++k) g = fmaf(vget(dv, k), vget(xv, k), g);
+            }
+          }
+          const float sv = eli + erv[u];
+          const float x = sv > 0.f ? sv : P.slope * sv;
+          const float dzds = (sv > 0.f ? 1.f : P.slope) * sgn;
+          const float a = __expf(sgn * x - lsei);
+          const float m = bwd_keep(P.drop_p, P.drop_scale, P.drop_seed,
+                                   b + static_cast<int64_t>(u) * ES, h);
+          const float ds = a * (m * g - Di) * dzds;
+          if (ok[u]) dsum += ds;
+        }
+      }
+    }
+    for (int o = HP; o < LR; o <<= 1) dsum += __shfl_xor(dsum, o, kWave);
+    if (hk && es == 0) {
+      if (mode == 0)
+        P.del_part[wave * P.H + h] = dsum;
+      else
+        P.del[i * P.H + h] = dsum;
+    }
+  }
+}
+
+struct BwdNodeRParams {
+  const int64_t* rowptr_t;
+  const int32_t* src_t;
+  const int64_t* eid_t;  // read only with dropout (the mask hashes the CSR edge id)
+  const float* dout;
+  const float* nstat;
+  const float* wh;
+  int64_t ldw;
+  const float* er;
+  int sparse, G;  // G = lanes per head (fh / VW, a power of two)
+  float slope, drop_p, drop_scale;
+  uint64_t drop_seed;
+  int64_t row_waves;
+  const int32_t* short_rows;  // EPI rows per wave (one per lane group)
+  int64_t n_short;
+};
+
+// Lanes = features (LPR lanes x VW, NCH chunks), EPI = 64 / LPR lane groups; a segment or row
+// wave spreads its edges over the groups, a short-row wave gives each group a row of its own.
+template <int VW, int LPR, int NCH>
+__global__ __launch_bounds__(kBw) void gat_bwd_node_r_kernel(BwdNodeParams P, BwdNodeRParams R) {
+  constexpr int EPI = kWave / LPR;
+  constexpr int U = 4;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kBwWaves + (threadIdx.x >> 6);
+  const int sub = lane & (LPR - 1);
+  const int grp = lane / LPR;
+  int mode;
+  int64_t j = -1, beg = 0, end = 0;
+  if (wave < P.seg_waves) {
+    if (wave >= P.n_seg) return;
+    mode = 0;
+    j = P.seg_row[wave];
+    beg = P.seg_begin[wave];
+    end = min(beg + P.seg_len, P.rowptr_t[j + 1]);
+  } else if (wave < P.seg_waves + R.row_waves) {
+    const int64_t i = wave - P.seg_waves;
+    if (i >= P.n_rows_list) return;
+    mode = 1;
+    j = P.rows[i];
+    beg = P.rowptr_t[j];
+    end = P.rowptr_t[j + 1];
+  } else {
+    const int64_t s = (wave - P.seg_waves - R.row_waves) * EPI;
+    if (s >= R.n_short) return;
+    mode = 2;
+    if (s + grp < R.n_short) {
+      j = R.short_rows[s + grp];
+      beg = R.rowptr_t[j];
+      end = R.rowptr_t[j + 1];
+    }
+  }
+  const int eo = mode == 2 ? 0 : grp;
+  const int ES = mode == 2 ? 1 : EPI;
+  const int64_t jj = j >= 0 ? j : 0;
+  int hid[NCH];
+  typename Vec<VW>::T whj[NCH], acc[NCH];
+  float erj[NCH], dsa[NCH];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+    const bool okf = f < P.feat;
+    hid[ch] = okf ? static_cast<int>(f / P.fh) : 0;
+    whj[ch] = okf ? vload<VW>(R.wh + jj * R.ldw + f) : vzero<VW>();
+    erj[ch] = R.er[jj * P.H + hid[ch]];
+    acc[ch] = vzero<VW>();
+    dsa[ch] = 0.f;
+  }
+  const float sgn = R.sparse ? -1.f : 1.f;
+  for (int64_t b = beg + eo; b < end; b += static_cast<int64_t>(ES) * U) {
+    bool ok[U];
+    int64_t src[U], eid[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t e = b + static_cast<int64_t>(u) * ES;
+      ok[u] = e < end;
+      src[u] = ok[u] ? R.src_t[e] : 0;
+      eid[u] = (ok[u] && R.drop_p > 0.f) ? R.eid_t[e] : 0;
+    }
+    typename Vec<VW>::T xv[U][NCH];
+    float elv[U][NCH], lsv[U][NCH], Dv[U][NCH];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float* ns = R.nstat + src[u] * 4 * P.H;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+        xv[u][ch] = f < P.feat ? vload<VW>(R.dout + src[u] * P.feat + f) : vzero<VW>();
+        elv[u][ch] = ns[hid[ch]];
+        lsv[u][ch] = ns[P.H + hid[ch]];
+        Dv[u][ch] = ns[2 * P.H + hid[ch]];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        float g = 0.f;
+#pragma unroll
+        for (int k = 0; k < VW; ++k) g = fmaf(vget(xv[u][ch], k), vget(whj[ch], k), g);
+        for (int o = 1; o < R.G; o <<= 1) g += __shfl_xor(g, o, kWave);
+        const float sv = elv[u][ch] + erj[ch];
+        const float x = sv > 0.f ? sv : R.slope * sv;
+        const float dzds = (sv > 0.f ? 1.f : R.slope) * sgn;
+        const float a = __expf(sgn * x - lsv[u][ch]);
+        const float m = bwd_keep(R.drop_p, R.drop_scale, R.drop_seed, eid[u], hid[ch]);
+        const float w = ok[u] ? m * a : 0.f;
+        const float ds = ok[u] ? a * (m * g - Dv[u][ch]) * dzds : 0.f;
+        acc[ch] += w * xv[u][ch];
+        dsa[ch] += ds;
+      }
+    }
+  }
+  if (mode != 2) {
+#pragma unroll
+    for (int o = LPR; o < kWave; o <<= 1) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        acc[ch] += shfl_xor_f(acc[ch], o);
+        dsa[ch] += __shfl_xor(dsa[ch], o, kWave);
+      }
+    }
+  }
+  if (mode == 0) {
+    if (lane < LPR) {
+      float* pr = P.part + wave * P.ldp;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+        if (f < P.feat) {
+          vstore<VW>(pr + f, acc[ch]);
+          if (f % P.fh == 0) pr[P.feat + hid[ch]] = dsa[ch];
+        }
+      }
+    }
+    return;
+  }
+  if (j < 0 || (mode == 1 && lane >= LPR)) return;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
+    if (f < P.feat && f % P.fh == 0) P.der[j * P.H + hid[ch]] = dsa[ch];
+  }
+  node_epilogue<VW, LPR, NCH>(P, j, sub, hid, acc, dsa);
+}
+
+template <int VW, int LPR, int NCH>
+static void launch_nodes_r(const BwdNodeParams& P0, const BwdNodeRParams& R0, const int32_t* long_row,
+                           const int32_t* long_seg_ptr, int64_t n_long, hipStream_t s) {
+  constexpr int EPI = kWave / LPR;
+  BwdNodeParams P = P0;
+  BwdNodeRParams R = R0;
+  const int64_t seg_blocks = (P.n_seg + kBwWaves - 1) / kBwWaves;
+  const int64_t row_blocks = (P.n_rows_list + kBwWaves - 1) / kBwWaves;
+  const int64_t short_waves = (R.n_short + EPI - 1) / EPI;
+  const int64_t short_blocks = (short_waves + kBwWaves - 1) / kBwWaves;
+  P.seg_waves = seg_blocks * kBwWaves;
+  R.row_waves = row_blocks * kBwWaves;
+  const int64_t blocks = seg_blocks + row_blocks + short_blocks;
+  if (blocks > 0)
+    hipLaunchKernelGGL((gat_bwd_node_r_kernel<VW, LPR, NCH>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBw), 0, s, P, R);
+  if (n_long > 0)
+    hipLaunchKernelGGL((gat_bwd_node_fixup_kernel<VW, LPR, NCH>),
+                       dim3(static_cast<unsigned>((n_long + kBwWaves - 1) / kBwWaves)), dim3(kBw), 0,
+                       s, P, long_row, long_seg_ptr, n_long);
+}
+
+// lanes per row chunk for feat / VW vectors (0: feat above 256 vectors)
+static int node_r_lpr(int64_t nv) { return nv <= 64 ? next_pow2_le64(nv) : nv <= 256 ? 64 : 0; }
+
+template <int VW>
+static int dispatch_nodes_r(const BwdNodeParams& P, const BwdNodeRParams& R, const int32_t* lr,
+                            const int32_t* lsp, int64_t nl, hipStream_t s) {
+  const int64_t nv = (P.feat + VW - 1) / VW;
+  if (nv <= 64) {
+    switch (next_pow2_le64(nv)) {
+      case 1: launch_nodes_r<VW, 1, 1>(P, R, lr, lsp, nl, s); break;
+      case 2: launch_nodes_r<VW, 2, 1>(P, R, lr, lsp, nl, s); break;
+      case 4: launch_nodes_r<VW, 4, 1>(P, R, lr, lsp, nl, s); break;
+      case 8: launch_nodes_r<VW, 8, 1>(P, R, lr, lsp, nl, s); break;
+      case 16: launch_nodes_r<VW, 16, 1>(P, R, lr, lsp, nl, s); break;
+      case 32: launch_nodes_r<VW, 32, 1>(P, R, lr, lsp, nl, s); break;
+      default: launch_nodes_r<VW, 64, 1>(P, R, lr, lsp, nl, s); break;
+    }
+  } else if (nv <= 128) {
+    launch_nodes_r<VW, 64, 2>(P, R, lr, lsp, nl, s);
+  } else {
+    launch_nodes_r<VW, 64, 4>(P, R, lr, lsp, nl, s);
+  }
+  return launch_status();
+}
+
 }  // namespace gnn
 
 using namespace gnn;
@@ -632,4 +1046,170 @@ extern "C" int gnn_gat_backward_nodes_f32(
     default: GNN_NODES(1, 8);
   }
 #undef GNN_NODES
+}
+
+static int hp_for(int64_t heads) { return heads <= 1 ? 1 : heads <= 2 ? 2 : heads <= 4 ? 4 : 8; }
+
+extern "C" int gnn_gat_backward_rows_f32(
+    const int64_t* rowptr, const int32_t* col, int64_t n_rows, const float* wh, int64_t ldw,
+    int64_t heads, int64_t fh, const float* el, const float* er, const float* lse, const float* dy,
+    const float* y, int64_t ldo, int32_t elu, float negative_slope, int32_t mode, float dropout_p,
+    uint64_t dropout_seed, float* dout, float* nstat, float* del, int64_t seg_len,
+    const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
+    const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows, int64_t n_rows_list,
+    const int32_t* short_rows, int64_t n_short, float* del_part, void* stream) {
+  const int64_t feat = heads * fh;
+  if (n_rows < 0 || heads < 1 || fh < 1 || ldw < feat || ldo < feat || n_seg < 0 || n_long < 0 ||
+      n_rows_list < 0 || n_short < 0 || seg_len < 1 || (mode != 0 && mode != 1))
+    return GNN_E_ARG;
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return GNN_E_ARG;
+  if (n_rows == 0) return GNN_OK;
+  if (!rowptr || !wh || !el || !er || !lse || !dy || !y || !dout || !nstat || !del) return GNN_E_ARG;
+  if (n_seg > 0 && (!seg_row || !seg_begin || !long_row || !long_seg_ptr || !del_part))
+    return GNN_E_ARG;
+  if ((n_rows_list > 0 && !rows) || (n_short > 0 && !short_rows)) return GNN_E_ARG;
+  // the prep's LDS: dout and products of the wave's rows, D per (row, head)
+  if (2 * feat + heads > kRowLds || (n_short > 0 && kShortRowsW * (2 * feat + heads) > kRowLds))
+    return GNN_E_UNSUPPORTED;
+  BwdRowParams P{};
+  P.rowptr = rowptr;
+  P.col = col;
+  P.wh = wh;
+  P.ldw = ldw;
+  P.el = el;
+  P.er = er;
+  P.lse = lse;
+  P.dy = dy;
+  P.y = y;
+  P.ldo = ldo;
+  P.elu = elu != 0;
+  P.sparse = mode;
+  P.hp = hp_for(heads);
+  P.H = heads;
+  P.fh = fh;
+  P.feat = feat;
+  P.slope = negative_slope;
+  P.drop_p = dropout_p;
+  P.drop_scale = dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f;
+  P.drop_seed = dropout_seed;
+  P.dout = dout;
+  P.nstat = nstat;
+  P.del = del;
+  P.del_part = del_part;
+  P.seg_len = seg_len;
+  P.seg_row = seg_row;
+  P.seg_begin = seg_begin;
+  P.n_seg = n_seg;
+  P.rows = rows;
+  P.n_rows_list = n_rows_list;
+  P.short_rows = short_rows;
+  P.n_short = n_short;
+  const int64_t seg_blocks = (n_seg + kBwWaves - 1) / kBwWaves;
+  const int64_t row_blocks = (n_rows_list + kBwWaves - 1) / kBwWaves;
+  const int64_t short_waves = (n_short + kShortRowsW - 1) / kShortRowsW;
+  const int64_t blocks = seg_blocks + row_blocks + (short_waves + kBwWaves - 1) / kBwWaves;
+  P.seg_waves = seg_blocks * kBwWaves;
+  P.row_waves = row_blocks * kBwWaves;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool vec4 = fh % 4 == 0 && ldw % 4 == 0 && ldo % 4 == 0 && aligned_to(wh, 16) &&
+                    aligned_to(dy, 16) && aligned_to(y, 16) && aligned_to(dout, 16);
+  const int64_t nfv = vec4 ? fh / 4 : fh;
+  const dim3 grid(static_cast<unsigned>(blocks));
+  if (blocks > 0) {
+#define GNN_ROWS(VW, NFV) hipLaunchKernelGGL((gat_bwd_rows_kernel<VW, NFV>), grid, dim3(kBw), 0, s, P)
+    if (vec4) {
+      switch (nfv) {
+        case 1: GNN_ROWS(4, 1); break;
+        case 2: GNN_ROWS(4, 2); break;
+        case 4: GNN_ROWS(4, 4); break;
+        default: GNN_ROWS(4, 0); break;
+      }
+    } else {
+      switch (nfv) {
+        case 1: GNN_ROWS(1, 1); break;
+        case 2: GNN_ROWS(1, 2); break;
+        case 4: GNN_ROWS(1, 4); break;
+        default: GNN_ROWS(1, 0); break;
+      }
+    }
+#undef GNN_ROWS
+  }
+  if (n_long > 0) {
+    const int64_t t = n_long * heads;
+    hipLaunchKernelGGL(gat_bwd_del_fixup_kernel, dim3(static_cast<unsigned>((t + 255) / 256)),
+                       dim3(256), 0, s, long_row, long_seg_ptr, n_long, heads, heads,
+                       static_cast<int64_t>(0), del_part, del);
+  }
+  return launch_status();
+}
+
+extern "C" int gnn_gat_backward_nodes_recompute_f32(
+    const int64_t* rowptr_t, const int32_t* src_t, const int64_t* eid_t, int64_t n_nodes,
+    int64_t heads, int64_t fh, const float* dout, const float* nstat, const float* wh,
+    int64_t ldw, const float* er, const float* del, const float* a_src, const float* a_dst,
+    float negative_slope, int32_t mode, float dropout_p, uint64_t dropout_seed, float* dwh,
+    float* der, int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
+    const int32_t* long_row, const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows,
+    int64_t n_rows_list, const int32_t* short_rows, int64_t n_short, float* part, void* stream) {
+  const int64_t feat = heads * fh;
+  if (n_nodes < 0 || heads < 1 || fh < 1 || ldw < feat || n_seg < 0 || n_long < 0 ||
+      n_rows_list < 0 || n_short < 0 || seg_len < 1 || (mode != 0 && mode != 1))
+    return GNN_E_ARG;
+  if (!(dropout_p >= 0.f && dropout_p < 1.f)) return GNN_E_ARG;
+  if (n_nodes == 0) return GNN_OK;
+  if (!rowptr_t || !dout || !nstat || !wh || !er || !del || !a_src || !a_dst || !dwh || !der)
+    return GNN_E_ARG;
+  if (dropout_p > 0.f && !eid_t) return GNN_E_ARG;
+  if (n_seg > 0 && (!seg_row || !seg_begin || !long_row || !long_seg_ptr || !part))
+    return GNN_E_ARG;
+  if ((n_rows_list > 0 && !rows) || (n_short > 0 && !short_rows)) return GNN_E_ARG;
+  const int64_t ldp = feat + heads;
+  const bool vec4 = fh % 4 == 0 && ldw % 4 == 0 && aligned_to(dout, 16) && aligned_to(wh, 16) &&
+                    aligned_to(dwh, 16) && aligned_to(a_src, 16) && aligned_to(a_dst, 16) &&
+                    (part == nullptr || (aligned_to(part, 16) && ldp % 4 == 0));
+  const int VW = vec4 ? 4 : 1;
+  const int64_t G = fh / VW;  // lanes of one head: a power of two inside one lane row
+  const int lpr = node_r_lpr((feat + VW - 1) / VW);
+  if (fh % VW != 0 || (G & (G - 1)) != 0 || lpr == 0 || G > lpr) return GNN_E_UNSUPPORTED;
+  BwdNodeParams P{};
+  P.rowptr_t = rowptr_t;
+  P.src_t = src_t;
+  P.eid_t = eid_t;
+  P.n_nodes = n_nodes;
+  P.del = del;
+  P.a_src = a_src;
+  P.a_dst = a_dst;
+  P.H = heads;
+  P.fh = fh;
+  P.feat = feat;
+  P.dwh = dwh;
+  P.der = der;
+  P.part = part;
+  P.ldp = ldp;
+  P.seg_len = seg_len;
+  P.seg_row = seg_row;
+  P.seg_begin = seg_begin;
+  P.n_seg = n_seg;
+  P.rows = rows;
+  P.n_rows_list = n_rows_list;
+  BwdNodeRParams R{};
+  R.rowptr_t = rowptr_t;
+  R.src_t = src_t;
+  R.eid_t = eid_t;
+  R.dout = dout;
+  R.nstat = nstat;
+  R.wh = wh;
+  R.ldw = ldw;
+  R.er = er;
+  R.sparse = mode;
+  R.G = static_cast<int>(G);
+  R.slope = negative_slope;
+  R.drop_p = dropout_p;
+  R.drop_scale = dropout_p > 0.f ? 1.f / (1.f - dropout_p) : 1.f;
+  R.drop_seed = dropout_seed;
+  R.short_rows = short_rows;
+  R.n_short = n_short;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return vec4 ? dispatch_nodes_r<4>(P, R, long_row, long_seg_ptr, n_long, s)
+              : dispatch_nodes_r<1>(P, R, long_row, long_seg_ptr, n_long, s);
 }

@@ -1147,12 +1147,110 @@ def gather_rows(x: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = N
 
 
 # ---------------------------------------------------------------- GAT backward
+# The GAT backward as two passes (gnn_gat_backward_rows_f32: prep + del, per-row statistics;
+# gnn_gat_backward_nodes_recompute_f32: the transposed aggregation recomputing the edge
+# weights) instead of three (prep, edge pass writing w / ds per (edge, head), node pass reading
+# them back); the three-pass path serves the shapes the two-pass kernels refuse.
+GAT_BWD_RECOMPUTE = True
+GAT_BWD_SHORT_DEG = 8   # rows with <= 8 edges: several per wave in both passes
+
+
+def _short_split(plan, rowptr, max_deg):
+    """(rows of more than max_deg edges, rows of at most max_deg edges incl. the plan's
+    small rows) of a plan's non-segmented rows, cached on the plan."""
+    cache = plan.__dict__.setdefault("_bwd_short", {})
+    if max_deg not in cache:
+        mid, short = plan.gat_split(rowptr, max_deg)
+        cache[max_deg] = (mid, torch.cat([short, plan.small_row]).contiguous())
+    return cache[max_deg]
+
+
+def _bwd_recompute_ok(heads: int, fh: int, ldw: int) -> bool:
+    """The shapes gnn_gat_backward_rows_f32 / _nodes_recompute_f32 take (16-B aligned tensors):
+    the row pass's LDS (2 feat + heads <= 1152 floats) and the node pass's lane layout (fh / VW
+    lanes per head a power of two, feat <= 256 VW; VW = 4 when fh and the Wh pitch are
+    multiples of 4)."""
+    feat = heads * fh
+    vw = 4 if fh % 4 == 0 and ldw % 4 == 0 else 1
+    lanes = fh // vw
+    nv = -(-feat // vw)
+    lpr = 0 if nv > 256 else (64 if nv > 64 else 1 << max(0, (nv - 1).bit_length()))
+    return (2 * feat + heads <= 1152 and fh % vw == 0 and lanes & (lanes - 1) == 0
+            and 0 < lanes <= lpr)
+
+
+def _gat_backward_recompute(g, wh, el, er, stats, y, dy, a_src, a_dst, heads, fh,
+                            negative_slope, mode, elu, dropout_p, seed, seg_len, mark):
+    """The two-pass backward; None when the kernels refuse the shape (GNN_E_UNSUPPORTED)."""
+    n = g.n_rows
+    feat = heads * fh
+    if not _bwd_recompute_ok(heads, fh, wh.stride(0)):
+        return None
+    dev = wh.device
+    lib = _lib.load()
+    stream = _lib.stream_handle(dev)
+    f32 = dict(dtype=torch.float32, device=dev)
+    sl = seg_len if seg_len is not None else seg_len_for(feat, GAT_SEG_BYTES)
+    plan = g.plan(sl)
+    short_ok = 8 * (2 * feat + heads) <= 1152
+    rows, short = (_short_split(plan, g.rowptr, GAT_BWD_SHORT_DEG) if short_ok
+                   else (plan.row_list(), plan.small_row[:0]))
+    dout = torch.empty((n, feat), **f32)
+    nstat = torch.empty((n, 4 * heads), **f32)
+    dl = torch.empty((n, heads), **f32)
+    del_part = torch.empty((max(plan.n_seg, 1), heads), **f32)
+    seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
+    mark("rows")
+    rc = lib.gnn_gat_backward_rows_f32(
+        g.rowptr.data_ptr(), g.col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
+        el.data_ptr(), er.data_ptr(), stats.data_ptr(), dy.data_ptr(), y.data_ptr(), feat,
+        int(elu), float(negative_slope), int(mode), float(dropout_p), seed64,
+        dout.data_ptr(), nstat.data_ptr(), dl.data_ptr(), plan.seg_len,
+        _lib.ptr(plan.seg_row), _lib.ptr(plan.seg_begin), plan.n_seg, _lib.ptr(plan.long_row),
+        plan.long_seg_ptr.data_ptr(), plan.n_long, _lib.ptr(rows), rows.numel(),
+        _lib.ptr(short), short.numel(), del_part.data_ptr(), stream)
+    if rc == _lib.E_UNSUPPORTED:  # (_bwd_recompute_ok passed: an unaligned view)
+        mark(None)
+        return None
+    _lib.check(rc, "gnn_gat_backward_rows_f32")
+    if g.symmetric and dropout_p == 0.0:
+        # A^T = A: node j's in-edges are row j's (ascending sources); no edge ids needed
+        rowptr_t, src_t, eid_t, gt = g.rowptr, g.col, None, g
+    else:
+        rowptr_t, src_t, eid_t, gt = g.transpose_eid()
+    pt = gt.plan(sl)
+    rows_t, short_t = _short_split(pt, rowptr_t, GAT_BWD_SHORT_DEG)
+    dwh = torch.empty((n, feat), **f32)
+    der = torch.empty((n, heads), **f32)
+    part = torch.empty((max(pt.n_seg, 1), feat + heads), **f32)
+    a_src = a_src.contiguous().float()
+    a_dst = a_dst.contiguous().float()
+    mark("nodes")
+    rc = lib.gnn_gat_backward_nodes_recompute_f32(
+        rowptr_t.data_ptr(), src_t.data_ptr(), _lib.ptr(eid_t), n, heads, fh, dout.data_ptr(),
+        nstat.data_ptr(), wh.data_ptr(), wh.stride(0), er.data_ptr(), dl.data_ptr(),
+        a_src.data_ptr(), a_dst.data_ptr(), float(negative_slope), int(mode), float(dropout_p),
+        seed64, dwh.data_ptr(), der.data_ptr(), pt.seg_len, _lib.ptr(pt.seg_row),
+        _lib.ptr(pt.seg_begin), pt.n_seg, _lib.ptr(pt.long_row), pt.long_seg_ptr.data_ptr(),
+        pt.n_long, _lib.ptr(rows_t), rows_t.numel(), _lib.ptr(short_t), short_t.numel(),
+        part.data_ptr(), stream)
+    if rc == _lib.E_UNSUPPORTED:
+        # the row pass's outputs are the three-pass path's prep + edge outputs but for w / ds:
+        # start over there (a shape both refuse is one the three-pass kernels also cover)
+        mark(None)
+        return None
+    _lib.check(rc, "gnn_gat_backward_nodes_recompute_f32")
+    mark(None)
+    return dwh, dout, dl, der
+
+
 def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tensor,
                  stats: torch.Tensor, y: torch.Tensor, dy: torch.Tensor, a_src: torch.Tensor,
                  a_dst: torch.Tensor, heads: int, fh: int, negative_slope: float, mode: int,
                  elu: bool, dropout_p: float = 0.0, seed: int = 0,
                  seg_len: int | None = None, timings: list | None = None):
-    """dWh (incl. the el/er terms), del, der for one GAT layer (three HIP passes).
+    """dWh (incl. the el/er terms), del, der for one GAT layer: two HIP passes (row pass,
+    recomputing node pass; GAT_BWD_RECOMPUTE) or, for the shapes those refuse, three.
 
     Returns (dwh [N, H*fh], dout [N, H*fh], del [N, H], der [N, H]). ``timings`` (a list):
     (pass name, start event, end event) of each pass on the current stream is appended
@@ -1165,8 +1263,6 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
     stream = _lib.stream_handle(dev)
     dy = dy.contiguous()
     y = y.contiguous()
-    dout = torch.empty((n, feat), dtype=torch.float32, device=dev)
-    D = torch.empty((n, heads), dtype=torch.float32, device=dev)
 
     def mark(name):
         if timings is not None:
@@ -1177,6 +1273,13 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
             if name:
                 timings.append((name, ev, None))
 
+    if GAT_BWD_RECOMPUTE:
+        r = _gat_backward_recompute(g, wh, el, er, stats, y, dy, a_src, a_dst, heads, fh,
+                                    negative_slope, mode, elu, dropout_p, seed, seg_len, mark)
+        if r is not None:
+            return r
+    dout = torch.empty((n, feat), dtype=torch.float32, device=dev)
+    D = torch.empty((n, heads), dtype=torch.float32, device=dev)
     mark("prep")
     _lib.check(lib.gnn_gat_backward_prep_f32(dy.data_ptr(), y.data_ptr(), feat, n, heads, fh,
                                              int(elu), dout.data_ptr(), D.data_ptr(), stream),

@@ -20,6 +20,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import math
+
 import torch
 
 from . import _lib
@@ -197,6 +199,17 @@ class SampledBatch:
                 Gathered(table, self.frontier_nbrs, True), [trust_map(m) for m in self.neigh_maps])
 
 
+_STAT_HOST = {}
+
+
+def _stat_host(n: int) -> torch.Tensor:
+    """A pinned host buffer of n int64 (cached) for sample_batch's one readback."""
+    t = _STAT_HOST.get(n)
+    if t is None:
+        t = _STAT_HOST[n] = torch.empty(n, dtype=torch.int64, pin_memory=True)
+    return t
+
+
 def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int = 0,
                  gcn: bool = False) -> SampledBatch:
     """L = len(fanouts) layer frontier for ``seeds`` (get_layer_adj_nodes,
@@ -223,12 +236,22 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
     caps = [seeds.numel()]
     for i in range(L - 1):
         caps.append(min(adj.n_rows, caps[i] * (1 + widths[i])))
-    i64 = dict(dtype=torch.int64, device=dev)
-    layers = [seeds] + [torch.empty(caps[i], **i64) for i in range(1, L)]
-    nbrs = [torch.empty((caps[i], widths[i]), **i64) for i in range(L)]
-    cmaps = [torch.empty(caps[i], **i64) for i in range(L - 1)]
-    nmaps = [torch.empty((caps[i], widths[i]), **i64) for i in range(L - 1)]
-    stat = torch.empty(L + 1, **i64)
+    # every output in ONE allocation (views at 256-B boundaries): the call is host-bound at
+    # cfg4 size, where seven allocations cost more than the three kernels
+    shapes = ([(caps[i],) for i in range(1, L)] + [(caps[i], widths[i]) for i in range(L)] +
+              [(caps[i],) for i in range(L - 1)] + [(caps[i], widths[i]) for i in range(L - 1)] +
+              [(L + 1,)])
+    offs, tot = [], 0
+    for sh in shapes:
+        offs.append(tot)
+        tot += -(-math.prod(sh) // 32) * 32
+    buf = torch.empty(tot, dtype=torch.int64, device=dev)
+    views = [buf[o:o + math.prod(sh)].view(sh) for o, sh in zip(offs, shapes)]
+    layers = [seeds] + views[:L - 1]
+    nbrs = views[L - 1:2 * L - 1]
+    cmaps = views[2 * L - 1:3 * L - 2]
+    nmaps = views[3 * L - 2:4 * L - 3]
+    stat = views[-1]
     ws = _sample_ws(adj.n_rows, dev)
     import ctypes
     P = ctypes.c_void_p
@@ -243,7 +266,10 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
                                      1 if gcn else 0, arr([None] + layers[1:]), cap_a, arr(nbrs),
                                      arr(cmaps), arr(nmaps), stat.data_ptr(), ws.data_ptr(),
                                      ws.numel(), _lib.stream_handle(dev)), "gnn_sample_layers")
-    st = stat.cpu().tolist()  # the one host synchronisation: every layer size + the error bits
+    host = _stat_host(L + 1)
+    host.copy_(stat, non_blocking=True)  # pinned: no staging copy
+    torch.cuda.current_stream(dev).synchronize()  # the one host synchronisation
+    st = host.tolist()  # every layer size + the error bits
     sizes, e = st[:L], int(st[L]) & 0xFFFFFFFF
     _raise_sample_error(e & 3)  # the sampler's own errors first, as the step-by-step path
     if e & 8:

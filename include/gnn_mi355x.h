@@ -554,6 +554,38 @@ int gnn_gat_backward_nodes_f32(const int64_t* rowptr_t, const int32_t* src_t,
                                const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
                                const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows,
                                int64_t n_rows_list, float* part, void* stream);
+/*
+ * GAT backward, two passes with recomputation (what ops.gat_backward runs; the three passes
+ * above remain for the shapes these refuse with GNN_E_UNSUPPORTED):
+ * rows : over CSR rows, the prep fused in: dout (as prep), del (as edges), and per row
+ *        nstat[i] = {el_i[0..H), lse_i[0..H), D_i[0..H), 0[0..H)} ([n, 4 heads]); no per-edge
+ *        output. Rows: plan segments + `rows` (one wave each) + `short_rows` (8 per wave; the
+ *        low-degree rows), every row exactly once. Unsupported: 2 heads*fh + heads > 1152, or
+ *        short rows with 8 (2 heads*fh + heads) > 1152.
+ * nodes_recompute: over the transposed CSR: per edge (i -> j) a_ij, g_ij = dout_i . Wh_j, w_ij,
+ *        ds_ij recomputed from dout_i, nstat_i and node j's own Wh_j / er_j; dwh, der as nodes.
+ *        eid_t is read only when dropout_p > 0. Rows: plan segments + `rows` + `short_rows`
+ *        (one per lane group). Unsupported: fh / VW lanes per head not a power of two (VW = 4
+ *        when fh % 4 == 0 and 16-B aligned, else 1), heads*fh above 256 VW.
+ */
+int gnn_gat_backward_rows_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                              const float* wh, int64_t ldw, int64_t heads, int64_t fh,
+                              const float* el, const float* er, const float* lse, const float* dy,
+                              const float* y, int64_t ldo, int32_t elu, float negative_slope,
+                              int32_t mode, float dropout_p, uint64_t dropout_seed, float* dout,
+                              float* nstat, float* del, int64_t seg_len, const int32_t* seg_row,
+                              const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
+                              const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows,
+                              int64_t n_rows_list, const int32_t* short_rows, int64_t n_short,
+                              float* del_part, void* stream);
+int gnn_gat_backward_nodes_recompute_f32(
+    const int64_t* rowptr_t, const int32_t* src_t, const int64_t* eid_t, int64_t n_nodes,
+    int64_t heads, int64_t fh, const float* dout, const float* nstat, const float* wh,
+    int64_t ldw, const float* er, const float* del, const float* a_src, const float* a_dst,
+    float negative_slope, int32_t mode, float dropout_p, uint64_t dropout_seed, float* dwh,
+    float* der, int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
+    const int32_t* long_row, const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows,
+    int64_t n_rows_list, const int32_t* short_rows, int64_t n_short, float* part, void* stream);
 
 /* ---- GraphSAGE aggregation modes ---- */
 #define GNN_SAGE_MEAN 0   /* torch.mean(neigh_feat, dim=1)               -> fp32 out  */

@@ -305,20 +305,33 @@ def _torch_gat(Wh, a_src, a_dst, mask, H, fh, slope, sparse, elu):
 @pytest.mark.parametrize("heads,fh", [(8, 8), (1, 7), (3, 4), (2, 16), (12, 4), (17, 2)])
 @pytest.mark.parametrize("sparse", [False, True])
 @pytest.mark.parametrize("seg_len", [None, 16])
-def test_gat_backward_vs_torch(dev, heads, fh, sparse, seg_len):
+@pytest.mark.parametrize("path", ["two_pass", "two_pass_sym", "three_pass"])
+def test_gat_backward_vs_torch(dev, heads, fh, sparse, seg_len, path, monkeypatch):
     """Every head count trains: more than 8 heads run the edge pass in groups of 8 and
-    reduce der 8 heads per pass inside the node kernel (>8 heads used to raise)."""
+    reduce der 8 heads per pass inside the node kernel (>8 heads used to raise).
+    two_pass: the row pass + recomputing node pass (every shape but fh = 7, whose 7 lanes per
+    head take the three passes), over the transposed CSR or, for a graph marked symmetric, the
+    graph itself; three_pass: GAT_BWD_RECOMPUTE off. Row 4 holds 200 extra edges (a long row /
+    long column at seg_len 16); rows of <= 8 edges take the packed short-row waves."""
     from graphneuralnetwork_amd.gat import _GatLayerFn
     from graphneuralnetwork_amd.graph import CsrGraph
     from graphneuralnetwork_amd import graph as graph_mod
+    from graphneuralnetwork_amd import ops
     n = 300
     rng = np.random.default_rng(heads * 10 + fh)
     s = np.concatenate([rng.integers(0, n, 3000), np.arange(n), np.full(200, 4)])
     d = np.concatenate([rng.integers(0, n, 3000), np.arange(n), rng.integers(0, n, 200)])
+    if path == "two_pass_sym":
+        s, d = np.concatenate([s, d]), np.concatenate([d, s])
     key = np.unique(s * n + d)
     rowptr, col, _ = O.coo_to_csr(key // n, key % n, np.ones(key.size, np.float32), n)
     g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
-                 torch.ones(col.size, device=dev), n, n)
+                 torch.ones(col.size, device=dev), n, n, symmetric=path == "two_pass_sym")
+    monkeypatch.setattr(ops, "GAT_BWD_RECOMPUTE", path != "three_pass")
+    ran = []
+    inner = ops._gat_backward_recompute
+    monkeypatch.setattr(ops, "_gat_backward_recompute",
+                        lambda *a: ran.append(inner(*a)) or ran[-1])
     mask = torch.zeros(n, n, dtype=torch.bool)
     mask[key // n, key % n] = True
     feat = heads * fh
@@ -350,6 +363,10 @@ def test_gat_backward_vs_torch(dev, heads, fh, sparse, seg_len):
     close(Wh.grad.cpu().numpy(), Wt.grad.numpy(), rtol=2e-4)
     close(a_s.grad.cpu().numpy(), ast.grad.numpy(), rtol=2e-4)
     close(a_d.grad.cpu().numpy(), adt.grad.numpy(), rtol=2e-4)
+    if path == "three_pass":
+        assert not ran
+    else:  # the two-pass kernels ran unless the shape is one they refuse
+        assert len(ran) == 1 and (ran[0] is not None) == (fh != 7)
 
 
 @pytest.mark.parametrize("kind", ["dense", "sparse"])
@@ -377,12 +394,17 @@ def test_gat_model_trains(golden, dev, kind):
 
 
 @pytest.mark.parametrize("sparse", [False, True])
-def test_gat_dropout_backward_exact(dev, sparse):
+@pytest.mark.parametrize("recompute", [True, False])
+def test_gat_dropout_backward_exact(dev, sparse, recompute, monkeypatch):
     """With dropout the backward must use the forward's mask: recover the mask by running
-    the forward on an identity Wh (out = m * alpha), then check gradients against torch."""
+    the forward on an identity Wh (out = m * alpha), then check gradients against torch
+    (the two-pass backward hashes the CSR edge id read through eid_t, the three-pass one the
+    edge it walks)."""
+    from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.gat import _GatLayerFn
     from graphneuralnetwork_amd.graph import CsrGraph
     from graphneuralnetwork_amd.ops import GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_logits
+    monkeypatch.setattr(ops, "GAT_BWD_RECOMPUTE", recompute)
     n, p, seed = 64, 0.4, 1234
     rng = np.random.default_rng(3)
     s = np.concatenate([rng.integers(0, n, 600), np.arange(n)])
@@ -539,3 +561,33 @@ def test_gat_model_column_order(dev, kind, monkeypatch):
         monkeypatch.setattr(ops, "DEGREE_ORDER", False)
         y_nat = model(x, graph())
     assert torch.equal(y, y_nat)
+
+
+def test_gat_backward_two_pass_matches_three_pass_cfg3(dev, monkeypatch):
+    """At BASELINE cfg3 size (R-MAT 1M / 10M, symmetric normalised adjacency, 8 x 8 heads) the
+    two-pass backward (row pass + recomputing node pass over the graph itself) and the
+    three-pass one agree on dWh, dout, del and der within fp32 summation-order differences."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    s, d = rmat_edges(1_000_000, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), 1_000_000, device=dev)
+    H, Fh = 8, 8
+    gen = torch.Generator(device=dev).manual_seed(2)
+    wh = torch.randn(g.n_rows, H * Fh, device=dev, generator=gen)
+    a_s = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
+    a_d = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
+    el, er = ops.gat_logits(wh, H, Fh, a_s, a_d)
+    stats = torch.empty((g.n_rows, H), device=dev)
+    y = ops.gat_aggregate(g, wh, el, er, H, Fh, 0.2, ops.GAT_DENSE, "elu", stats=stats)
+    dy = torch.randn(g.n_rows, H * Fh, device=dev, generator=gen)
+    res = {}
+    for rc in (True, False):
+        monkeypatch.setattr(ops, "GAT_BWD_RECOMPUTE", rc)
+        tl = []
+        res[rc] = ops.gat_backward(g, wh, el, er, stats, y, dy, a_s, a_d, H, Fh, 0.2,
+                                   ops.GAT_DENSE, True, timings=tl)
+        assert [t[0] for t in tl] == (["rows", "nodes"] if rc else ["prep", "edges", "nodes"])
+    for a, b in zip(res[True], res[False]):
+        err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+        assert err < 1e-5, err

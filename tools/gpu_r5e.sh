@@ -1,0 +1,13 @@
+# round-5 GPU pass e: GAT backward probe (short-row bounds, three-pass beside) + its SQ / traffic
+# counters per kernel; a failing GPU step ends the script
+set -o pipefail
+mkdir -p gpurun_out/prof
+export TMPDIR=/tmp
+timeout -k 10 300 python3 -u tools/gat_bwd_probe.py --reps 15 --short 0,4,8,16 --three > gpurun_out/r5e_gat_bwd_probe.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/r5e_stats -o run -- python3 -u tools/gat_bwd_probe.py --reps 3 > gpurun_out/r5e_stats.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES --output-format csv -d gpurun_out/prof/r5e_sq -o run -- python3 -u tools/gat_bwd_probe.py --reps 3 > gpurun_out/r5e_sq.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/r5e_fetch -o run -- python3 -u tools/gat_bwd_probe.py --reps 3 > gpurun_out/r5e_fetch.log 2>&1 && \
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --output-format csv -d gpurun_out/prof/r5e_write -o run -- python3 -u tools/gat_bwd_probe.py --reps 3 > gpurun_out/r5e_write.log 2>&1
+rc=$?
+find gpurun_out/prof/r5e_* -type f ! -name '*kernel_stats.csv' ! -name '*counter_collection.csv' -delete 2>/dev/null
+exit $rc
