@@ -461,7 +461,7 @@ static int dispatch_nodes(const BwdNodeParams& P, const int32_t* lr, const int32
 // pass (w_ij, ds_ij written in CSR order, then read through eid_t: two random 4 H-byte reads per
 // edge, each its own cache line) and the prep pass writes dout for the edge pass to re-read.
 // Here the row pass does the prep itself and writes, besides dout and del, only a per-row
-// record nstat_i = {el_i, lse_i, D_i, 0} (4 H floats: one 128-B line at H = 8); the node pass
+// record nstat_i = {el, lse, D, 0} per head (4 H floats: one 128-B line at H = 8); the node pass
 // gathers dout_i with nstat_i and recomputes a_ij, g_ij = dout_i . Wh_j (Wh_j is the node's
 // own row, held in registers), w_ij and ds_ij. Per edge the node pass reads 4 + 4 feat + 16 H
 // bytes (12 + 4 feat + 2 x 2 lines before) and the row pass writes nothing.
@@ -545,47 +545,46 @@ __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
   float* dbuf = lds[wid];
   float* pbuf = dbuf + nr * P.feat;
   float* Dbuf = pbuf + nr * P.feat;
-  // ---- prep
-  for (int r = 0; r < nr; ++r) {
+  // ---- prep: the (row, feature vector) pairs of the wave's rows spread over the lanes (a
+  // short-row wave's 8 rows at 64 features take 2 lane passes, not 8)
+  const int nv = static_cast<int>(P.feat / VW);  // feat % VW == 0 when VW = 4
+  for (int t = lane; t < nr * nv; t += kWave) {
+    const int r = t / nv;
+    const int64_t f = static_cast<int64_t>(t - r * nv) * VW;
     const int64_t i = row_of(r);
-    if (i < 0) break;  // short rows are listed first to last: the tail slots are empty
-    for (int64_t f = static_cast<int64_t>(lane) * VW; f < P.feat; f += kWave * VW) {
-      const typename Vec<VW>::T yv = vload<VW>(P.y + i * P.ldo + f);
-      const typename Vec<VW>::T gv = vload<VW>(P.dy + i * P.ldo + f);
-      typename Vec<VW>::T dv, pv;
+    if (i < 0) continue;  // the tail slots of a short-row wave
+    const typename Vec<VW>::T yv = vload<VW>(P.y + i * P.ldo + f);
+    const typename Vec<VW>::T gv = vload<VW>(P.dy + i * P.ldo + f);
+    typename Vec<VW>::T dv, pv;
 #pragma unroll
-      for (int k = 0; k < VW; ++k) {
-        const float yy = vget(yv, k), g = vget(gv, k);
-        float d = g, o = yy;
-        if (P.elu && yy <= 0.f) {  // ELU'(x) = y + 1 for x <= 0, x = log1p(y) (saturated: 0)
-          const float t = yy + 1.f;
-          d = g * t;
-          o = t > 0.f ? log1pf(yy) : 0.f;
-        }
-        vset(dv, k, d);
-        vset(pv, k, d * o);
+    for (int k = 0; k < VW; ++k) {
+      const float yy = vget(yv, k), g = vget(gv, k);
+      float d = g, o = yy;
+      if (P.elu && yy <= 0.f) {  // ELU'(x) = y + 1 for x <= 0, x = log(y + 1) (saturated: 0)
+        const float tt = yy + 1.f;
+        d = g * tt;
+        o = tt > 0.f ? __logf(tt) : 0.f;
       }
-      vstore<VW>(dbuf + r * P.feat + f, dv);
-      vstore<VW>(pbuf + r * P.feat + f, pv);
-      if (write) vstore<VW>(P.dout + i * P.feat + f, dv);
+      vset(dv, k, d);
+      vset(pv, k, d * o);
     }
+    vstore<VW>(dbuf + r * P.feat + f, dv);
+    vstore<VW>(pbuf + r * P.feat + f, pv);
+    if (write) vstore<VW>(P.dout + i * P.feat + f, dv);
   }
   wave_lds_sync();
-  for (int64_t t = lane; t < nr * P.H; t += kWave) {
-    const int r = static_cast<int>(t / P.H);
-    const int64_t h = t % P.H;
+  const int H32 = static_cast<int>(P.H), fh32 = static_cast<int>(P.fh);
+  for (int t = lane; t < nr * H32; t += kWave) {
+    const int r = t / H32;
+    const int h = t - r * H32;
     const int64_t i = row_of(r);
-    const float* pp = pbuf + r * P.feat + h * P.fh;
+    const float* pp = pbuf + r * P.feat + h * fh32;
     float s = 0.f;
-    for (int64_t k = 0; k < P.fh; ++k) s += pp[k];
+    for (int k = 0; k < fh32; ++k) s += pp[k];
     Dbuf[t] = s;
-    if (i >= 0 && write) {
-      float* ns = P.nstat + i * 4 * P.H;
-      ns[h] = P.el[i * P.H + h];
-      ns[P.H + h] = P.lse[i * P.H + h];
-      ns[2 * P.H + h] = s;
-      ns[3 * P.H + h] = 0.f;
-    }
+    if (i >= 0 && write)
+      *reinterpret_cast<float4*>(P.nstat + (i * P.H + h) * 4) =
+          make_float4(P.el[i * P.H + h], P.lse[i * P.H + h], s, 0.f);
   }
   wave_lds_sync();
   // ---- edges
@@ -615,6 +614,11 @@ __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
     const float lsei = P.lse[ii * P.H + hh];
     const float Di = Dbuf[r * P.H + hh];
     const float* dh = drow + hh * P.fh;
+    typename Vec<VW>::T dreg[NFV > 0 ? NFV : 1];
+    if constexpr (NFV > 0) {
+#pragma unroll
+      for (int v = 0; v < NFV; ++v) dreg[v] = vload<VW>(dh + v * VW);
+    }
     float dsum = 0.f;
     if (hk) {
       for (int64_t b = beg + es; b < end; b += static_cast<int64_t>(ES) * U) {
@@ -643,9 +647,8 @@ __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
           if constexpr (NFV > 0) {
 #pragma unroll
             for (int v = 0; v < NFV; ++v) {
-              const typename Vec<VW>::T dv = vload<VW>(dh + v * VW);
 #pragma unroll
-              for (int k = 0; k < VW; ++k) g = fmaf(vget(dv, k), vget(wv[u][v], k), g);
+              for (int k = 0; k < VW; ++k) g = fmaf(vget(dreg[v], k), vget(wv[u][v], k), g);
             }
           } else {
             const float* xr = P.wh + static_cast<int64_t>(c[u]) * P.ldw + h * P.fh;
@@ -757,17 +760,15 @@ __global__ __launch_bounds__(kBw) void gat_bwd_node_r_kernel(BwdNodeParams P, Bw
       eid[u] = (ok[u] && R.drop_p > 0.f) ? R.eid_t[e] : 0;
     }
     typename Vec<VW>::T xv[U][NCH];
-    float elv[U][NCH], lsv[U][NCH], Dv[U][NCH];
+    float4 st[U][NCH];  // {el, lse, D, 0} of (source, head)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float* ns = R.nstat + src[u] * 4 * P.H;
+      const float4* ns = reinterpret_cast<const float4*>(R.nstat) + src[u] * P.H;
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
         xv[u][ch] = f < P.feat ? vload<VW>(R.dout + src[u] * P.feat + f) : vzero<VW>();
-        elv[u][ch] = ns[hid[ch]];
-        lsv[u][ch] = ns[P.H + hid[ch]];
-        Dv[u][ch] = ns[2 * P.H + hid[ch]];
+        st[u][ch] = ns[hid[ch]];
       }
     }
 #pragma unroll
@@ -778,13 +779,13 @@ __global__ __launch_bounds__(kBw) void gat_bwd_node_r_kernel(BwdNodeParams P, Bw
 #pragma unroll
         for (int k = 0; k < VW; ++k) g = fmaf(vget(xv[u][ch], k), vget(whj[ch], k), g);
         for (int o = 1; o < R.G; o <<= 1) g += __shfl_xor(g, o, kWave);
-        const float sv = elv[u][ch] + erj[ch];
+        const float sv = st[u][ch].x + erj[ch];
         const float x = sv > 0.f ? sv : R.slope * sv;
         const float dzds = (sv > 0.f ? 1.f : R.slope) * sgn;
-        const float a = __expf(sgn * x - lsv[u][ch]);
+        const float a = __expf(sgn * x - st[u][ch].y);
         const float m = bwd_keep(R.drop_p, R.drop_scale, R.drop_seed, eid[u], hid[ch]);
         const float w = ok[u] ? m * a : 0.f;
-        const float ds = ok[u] ? a * (m * g - Dv[u][ch]) * dzds : 0.f;
+        const float ds = ok[u] ? a * (m * g - st[u][ch].z) * dzds : 0.f;
         acc[ch] += w * xv[u][ch];
         dsa[ch] += ds;
       }
@@ -1065,6 +1066,7 @@ extern "C" int gnn_gat_backward_rows_f32(
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return GNN_E_ARG;
   if (n_rows == 0) return GNN_OK;
   if (!rowptr || !wh || !el || !er || !lse || !dy || !y || !dout || !nstat || !del) return GNN_E_ARG;
+  if (!aligned_to(nstat, 16)) return GNN_E_ALIGN;
   if (n_seg > 0 && (!seg_row || !seg_begin || !long_row || !long_seg_ptr || !del_part))
     return GNN_E_ARG;
   if ((n_rows_list > 0 && !rows) || (n_short > 0 && !short_rows)) return GNN_E_ARG;
@@ -1160,6 +1162,7 @@ extern "C" int gnn_gat_backward_nodes_recompute_f32(
   if (!rowptr_t || !dout || !nstat || !wh || !er || !del || !a_src || !a_dst || !dwh || !der)
     return GNN_E_ARG;
   if (dropout_p > 0.f && !eid_t) return GNN_E_ARG;
+  if (!aligned_to(nstat, 16)) return GNN_E_ALIGN;
   if (n_seg > 0 && (!seg_row || !seg_begin || !long_row || !long_seg_ptr || !part))
     return GNN_E_ARG;
   if ((n_rows_list > 0 && !rows) || (n_short > 0 && !short_rows)) return GNN_E_ARG;

@@ -11,8 +11,8 @@
 // with coalesced 16-B loads (the next tile is loaded into registers while this one is
 // multiplied), and thread (tm, tk) accumulates its TM x TK patch of the outer products in fp32
 // registers, in row order. The per-workgroup partials go to a workspace and a second kernel sums
-// them in workgroup order: deterministic, no atomics. fp32 FMAs: on gfx950 the fp32 MFMA runs at
-// the fp32 vector rate, so there is nothing to gain from the matrix cores at fp32.
+// them in workgroup order: deterministic, no atomics. That FMA kernel serves M = 8; M, K >= 64
+// run gemm_tn_mfma_kernel below (the same staging, fp32 MFMA products).
 // Optional: dsum[k] = sum_i D[i, k] (a third [n, K] operand, accumulated while its tiles pass).
 #include "common.hpp"
 
@@ -146,6 +146,144 @@ __global__ __launch_bounds__(kTnThreads) void gemm_tn_partial_kernel(
   }
 }
 
+// The same partials on the fp32 MFMA (v_mfma_f32_32x32x2_f32: exact fp32, a k-ordered fmaf
+// chain, 64 FLOP/clk/SIMD; the FMA kernel above is VALU-bound at ~53 TF/s). The tiles are
+// staged exactly as above (each element loaded once, coalesced, the next tile in flight); rows
+// are padded by 32 floats so that the two lane halves of an operand read (rows r, r + 1) hit
+// disjoint banks. For a row pair, lane l holds A[i = l & 31][k = l >> 5] and B[k][j = l & 31]
+// (cdna_hip_programming.md: the 32x32x2 f32 operand maps): wave (h, s) multiplies A's 32-column
+// block h into every 32-column block of B (K / 32 accumulator tiles) over the tile's row pairs
+// s, s + S, ... (S = 4 / (M / 32)); the S partials are summed in s order through LDS.
+typedef float f16x __attribute__((ext_vector_type(16)));
+
+template <int M, int K, bool DSUM>
+__global__ __launch_bounds__(kTnThreads) void gemm_tn_mfma_kernel(
+    const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb,
+    const float* __restrict__ d, int64_t ldd, int64_t n, int64_t rows_per_block,
+    float* __restrict__ part) {
+  constexpr int A4 = M / 4, B4 = K / 4;
+  constexpr int PA = M + 32, PB = K + 32;  // padded LDS row pitches (floats)
+  constexpr int NA = (kTnRows * A4 + kTnThreads - 1) / kTnThreads;
+  constexpr int NB = (kTnRows * B4 + kTnThreads - 1) / kTnThreads;
+  constexpr int QA = M / 32, QB = K / 32;
+  constexpr int S = 4 / QA;  // row-pair streams per tile
+  __shared__ float4 sa[kTnRows * PA / 4];
+  __shared__ float4 sb[kTnRows * PB / 4];
+  __shared__ float red[S > 1 ? M * K : 1];
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int h = w % QA, s = w / QA;
+  const int i = lane & 31, kk = lane >> 5;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  f16x acc[QB];
+#pragma unroll
+  for (int q = 0; q < QB; ++q) acc[q] = f16x(0.f);
+  float4 ds[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) ds[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  auto load = [&](int64_t row0, float4 (&va)[NA], float4 (&vb)[NB], float4 (&vd)[NB]) {
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int e = t + q * kTnThreads;
+      const int64_t row = row0 + e / A4;
+      va[q] = (e < kTnRows * A4 && row < r1)
+                  ? *reinterpret_cast<const float4*>(a + row * lda + 4 * (e % A4))
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int e = t + q * kTnThreads;
+      const int64_t row = row0 + e / B4;
+      const bool ok = e < kTnRows * B4 && row < r1;
+      vb[q] = ok ? *reinterpret_cast<const float4*>(b + row * ldb + 4 * (e % B4))
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (DSUM)
+        vd[q] = ok ? *reinterpret_cast<const float4*>(d + row * ldd + 4 * (e % B4))
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+
+  // one register set: tile k + 1's loads in flight during tile k's MFMAs (two sets, tile k + 2
+  // in flight as well, took 184 VGPRs + 128 AGPRs at 128 x 128: one wave per SIMD)
+  float4 va[NA], vb[NB], vd[NB];
+  load(r0, va, vb, vd);
+  const float* saf = reinterpret_cast<const float*>(sa);
+  const float* sbf = reinterpret_cast<const float*>(sb);
+  for (int64_t row0 = r0; row0 < r1; row0 += kTnRows) {
+    __syncthreads();  // the previous tile's readers are done
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int e = t + q * kTnThreads;
+      if (e < kTnRows * A4) sa[(e / A4) * (PA / 4) + e % A4] = va[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int e = t + q * kTnThreads;
+      if (e < kTnRows * B4) sb[(e / B4) * (PB / 4) + e % B4] = vb[q];
+      if constexpr (DSUM) {
+        ds[q].x += vd[q].x;
+        ds[q].y += vd[q].y;
+        ds[q].z += vd[q].z;
+        ds[q].w += vd[q].w;
+      }
+    }
+    __syncthreads();
+    if (row0 + kTnRows < r1) load(row0 + kTnRows, va, vb, vd);  // next tile in flight
+    const int np = static_cast<int>((min(static_cast<int64_t>(kTnRows), r1 - row0) + 1) / 2);
+    for (int p = s; p < np; p += S) {  // rows past r1 were staged as zeros
+      const int r = 2 * p + kk;
+      const float av = saf[r * PA + 32 * h + i];
+#pragma unroll
+      for (int q = 0; q < QB; ++q)
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, sbf[r * PB + 32 * q + i], acc[q], 0, 0, 0);
+    }
+  }
+  float* pc = part + static_cast<int64_t>(blockIdx.x) * (M * K + (DSUM ? K : 0));
+  // the S row-pair streams' partials, summed in s order: s = S - 1 stores, ..., s = 0 writes
+  for (int tt = S - 1; tt >= 0; --tt) {
+    if (s == tt) {
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+#pragma unroll
+        for (int rg = 0; rg < 16; ++rg) {
+          const int m = 32 * h + (rg & 3) + 8 * (rg >> 2) + 4 * kk, nn = 32 * q + i;
+          float v = acc[q][rg];
+          if (tt < S - 1) v += red[m * K + nn];
+          if (tt > 0)
+            red[m * K + nn] = v;
+          else
+            pc[m * K + nn] = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (DSUM) {
+    // as the FMA kernel: the threads holding column group c (t = c + B4 * j) summed in order
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int e = t + q * kTnThreads;
+      if (e < kTnRows * B4) sb[e] = ds[q];
+    }
+    __syncthreads();
+    if (t < B4) {
+      float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int e = t; e < kTnRows * B4; e += B4) {
+        s4.x += sb[e].x;
+        s4.y += sb[e].y;
+        s4.z += sb[e].z;
+        s4.w += sb[e].w;
+      }
+      pc[M * K + 4 * t] = s4.x;
+      pc[M * K + 4 * t + 1] = s4.y;
+      pc[M * K + 4 * t + 2] = s4.z;
+      pc[M * K + 4 * t + 3] = s4.w;
+    }
+  }
+}
+
 // out[e] (+)= sum over the blocks' partials, in block order (e < M*K: C, then dsum)
 __global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(const float* __restrict__ part,
                                                              int64_t blocks, int64_t stride,
@@ -180,12 +318,25 @@ static int launch_tn(const float* a, int64_t lda, const float* b, int64_t ldb, c
   int64_t rpb = (n + blocks - 1) / blocks;
   rpb = (rpb + kTnRows - 1) / kTnRows * kTnRows;
   const int64_t stride = M * K + (d ? K : 0);
-  if (d)
+#ifndef GNN_TN_FMA  // A/B: the FMA kernel at every shape
+  constexpr bool mfma = M >= 64 && K >= 32;
+#else
+  constexpr bool mfma = false;
+#endif
+  if constexpr (mfma) {
+    if (d)
+      hipLaunchKernelGGL((gemm_tn_mfma_kernel<M, K, true>), dim3(static_cast<unsigned>(blocks)),
+                         dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+    else
+      hipLaunchKernelGGL((gemm_tn_mfma_kernel<M, K, false>), dim3(static_cast<unsigned>(blocks)),
+                         dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+  } else if (d) {
     hipLaunchKernelGGL((gemm_tn_partial_kernel<M, K, true>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
-  else
+  } else {
     hipLaunchKernelGGL((gemm_tn_partial_kernel<M, K, false>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+  }
   hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3(static_cast<unsigned>((stride + 255) / 256)),
                      dim3(256), 0, s, part, blocks, stride, static_cast<int64_t>(M * K),
                      static_cast<int64_t>(K), c, ldc, trans_c, dsum);

@@ -1196,7 +1196,7 @@ def _gat_backward_recompute(g, wh, el, er, stats, y, dy, a_src, a_dst, heads, fh
     rows, short = (_short_split(plan, g.rowptr, GAT_BWD_SHORT_DEG) if short_ok
                    else (plan.row_list(), plan.small_row[:0]))
     dout = torch.empty((n, feat), **f32)
-    nstat = torch.empty((n, 4 * heads), **f32)
+    nstat = torch.empty((n, heads, 4), **f32)  # {el, lse, D, 0} per (row, head)
     dl = torch.empty((n, heads), **f32)
     del_part = torch.empty((max(plan.n_seg, 1), heads), **f32)
     seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
-import math
+import ctypes
 
 import torch
 
@@ -232,42 +232,28 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
         return sample_batch_stepwise(adj, seeds, fanouts, seed, gcn)
     dev = adj.device
     L = len(fanouts)
-    widths = [k + (1 if gcn else 0) for k in fanouts]
-    caps = [seeds.numel()]
-    for i in range(L - 1):
-        caps.append(min(adj.n_rows, caps[i] * (1 + widths[i])))
-    # every output in ONE allocation (views at 256-B boundaries): the call is host-bound at
-    # cfg4 size, where seven allocations cost more than the three kernels
-    shapes = ([(caps[i],) for i in range(1, L)] + [(caps[i], widths[i]) for i in range(L)] +
-              [(caps[i],) for i in range(L - 1)] + [(caps[i], widths[i]) for i in range(L - 1)] +
-              [(L + 1,)])
-    offs, tot = [], 0
-    for sh in shapes:
-        offs.append(tot)
-        tot += -(-math.prod(sh) // 32) * 32
+    plan = _batch_plan(adj.n_rows, seeds.numel(), fanouts, gcn)
+    caps, offs, tot, fan_a, cap_a = plan
+    # every output in ONE allocation at 256-B boundaries, its pieces addressed by offset and
+    # viewed once, at their final sizes, after the readback: the call is host-bound at cfg4
+    # size (three ~15 us kernels), so host work is what there is to cut
     buf = torch.empty(tot, dtype=torch.int64, device=dev)
-    views = [buf[o:o + math.prod(sh)].view(sh) for o, sh in zip(offs, shapes)]
-    layers = [seeds] + views[:L - 1]
-    nbrs = views[L - 1:2 * L - 1]
-    cmaps = views[2 * L - 1:3 * L - 2]
-    nmaps = views[3 * L - 2:4 * L - 3]
-    stat = views[-1]
+    base = buf.data_ptr()
+    ptr = [base + 8 * o for o in offs]  # layers 1.., nbrs 0.., cmaps, nmaps, stat
     ws = _sample_ws(adj.n_rows, dev)
-    import ctypes
     P = ctypes.c_void_p
-    arr = lambda ts: (P * max(1, len(ts)))(*[t.data_ptr() if t is not None else None  # noqa: E731
-                                              for t in ts])
-    fan_a = (ctypes.c_int64 * L)(*fanouts)
     seed_a = (ctypes.c_uint64 * L)(*[stream_seed(seed, i) for i in range(L)])
-    cap_a = (ctypes.c_int64 * L)(*caps)
     lib = _lib.load()
     _lib.check(lib.gnn_sample_layers(adj.rowptr.data_ptr(), adj.col.data_ptr(), adj.n_rows,
                                      seeds.data_ptr(), seeds.numel(), L, fan_a, seed_a,
-                                     1 if gcn else 0, arr([None] + layers[1:]), cap_a, arr(nbrs),
-                                     arr(cmaps), arr(nmaps), stat.data_ptr(), ws.data_ptr(),
-                                     ws.numel(), _lib.stream_handle(dev)), "gnn_sample_layers")
+                                     1 if gcn else 0, (P * L)(None, *ptr[:L - 1]), cap_a,
+                                     (P * L)(*ptr[L - 1:2 * L - 1]),
+                                     (P * max(1, L - 1))(*ptr[2 * L - 1:3 * L - 2]),
+                                     (P * max(1, L - 1))(*ptr[3 * L - 2:4 * L - 3]), ptr[-1],
+                                     ws.data_ptr(), ws.numel(), _lib.stream_handle(dev)),
+               "gnn_sample_layers")
     host = _stat_host(L + 1)
-    host.copy_(stat, non_blocking=True)  # pinned: no staging copy
+    host.copy_(buf[offs[-1]:offs[-1] + L + 1], non_blocking=True)  # pinned: no staging copy
     torch.cuda.current_stream(dev).synchronize()  # the one host synchronisation
     st = host.tolist()  # every layer size + the error bits
     sizes, e = st[:L], int(st[L]) & 0xFFFFFFFF
@@ -279,11 +265,46 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
     if e & 16:
         raise RuntimeError("sample_batch: the frontier scan's look-back did not complete "
                            "(internal error)")
-    layers = [seeds] + [layers[i][:sizes[i]] for i in range(1, L)]
-    cmaps = [cmaps[i][:sizes[i]] for i in range(L - 1)]
-    nmaps = [nmaps[i][:sizes[i]] for i in range(L - 1)]
-    return SampledBatch(seeds, layers[-1], nbrs[L - 1][:sizes[L - 1]], cmaps[::-1], nmaps[::-1],
-                        tuple(layers))
+    widths = [k + (1 if gcn else 0) for k in fanouts]
+
+    def view(o, rows, w=0):
+        return buf.as_strided((rows, w) if w else (rows,), (w, 1) if w else (1,), o)
+
+    layers = [seeds] + [view(offs[i - 1], sizes[i]) for i in range(1, L)]
+    nbrs_last = view(offs[2 * L - 2], sizes[L - 1], widths[L - 1])
+    cmaps = [view(offs[2 * L - 1 + i], sizes[i]) for i in range(L - 1)]
+    nmaps = [view(offs[3 * L - 2 + i], sizes[i], widths[i]) for i in range(L - 1)]
+    return SampledBatch(seeds, layers[-1], nbrs_last, cmaps[::-1], nmaps[::-1], tuple(layers))
+
+
+_BATCH_PLAN = {}
+
+
+def _batch_plan(n_rows: int, n_seeds: int, fanouts: tuple, gcn: bool):
+    """(caps, buffer offsets, total int64 count, fanout / cap ctypes arrays) of sample_batch's
+    one output buffer, cached per (graph size, batch size, fanouts, gcn). Pieces, in order:
+    layers 1..L-1 [cap_i], neighbour lists 0..L-1 [cap_i, w_i], centre maps 0..L-2 [cap_i],
+    neighbour maps 0..L-2 [cap_i, w_i], the L + 1 status words."""
+    key = (n_rows, n_seeds, fanouts, gcn)
+    p = _BATCH_PLAN.get(key)
+    if p is None:
+        L = len(fanouts)
+        widths = [k + (1 if gcn else 0) for k in fanouts]
+        caps = [n_seeds]
+        for i in range(L - 1):
+            caps.append(min(n_rows, caps[i] * (1 + widths[i])))
+        sizes = ([caps[i] for i in range(1, L)] + [caps[i] * widths[i] for i in range(L)] +
+                 [caps[i] for i in range(L - 1)] + [caps[i] * widths[i] for i in range(L - 1)] +
+                 [L + 1])
+        offs, tot = [], 0
+        for n in sizes:
+            offs.append(tot)
+            tot += -(-n // 32) * 32
+        p = (caps, offs, tot, (ctypes.c_int64 * L)(*fanouts), (ctypes.c_int64 * L)(*caps))
+        if len(_BATCH_PLAN) > 64:
+            _BATCH_PLAN.clear()
+        _BATCH_PLAN[key] = p
+    return p
 
 
 def sample_batch_stepwise(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int = 0,

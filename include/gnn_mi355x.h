@@ -558,7 +558,7 @@ int gnn_gat_backward_nodes_f32(const int64_t* rowptr_t, const int32_t* src_t,
  * GAT backward, two passes with recomputation (what ops.gat_backward runs; the three passes
  * above remain for the shapes these refuse with GNN_E_UNSUPPORTED):
  * rows : over CSR rows, the prep fused in: dout (as prep), del (as edges), and per row
- *        nstat[i] = {el_i[0..H), lse_i[0..H), D_i[0..H), 0[0..H)} ([n, 4 heads]); no per-edge
+ *        nstat[i][h] = {el_ih, lse_ih, D_ih, 0} ([n, heads, 4], 16-B aligned); no per-edge
  *        output. Rows: plan segments + `rows` (one wave each) + `short_rows` (8 per wave; the
  *        low-degree rows), every row exactly once. Unsupported: 2 heads*fh + heads > 1152, or
  *        short rows with 8 (2 heads*fh + heads) > 1152.
