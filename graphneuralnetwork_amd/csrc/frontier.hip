@@ -192,15 +192,20 @@ __global__ void batch_init_kernel(int64_t* __restrict__ stat, int n_layers, int6
 // ---- the 3-launch L-hop batch (gnn_sample_layers) -------------------------------------------
 // The frontier marks are byte flags (flags[v] = 1, plain stores: idempotent, no atomics), set by
 // the hop's sampling kernel itself. One scan kernel per hop transition turns them into the
-// frontier: a workgroup per tile of 1024 words (32 flags per word), the tile prefixes chained
-// by a decoupled look-back (each tile publishes its count, then its inclusive prefix, in ONE
-// 8-byte agent-scope atomic word {tag, kind, value}); it writes the frontier ids, the word
+// frontier: a workgroup per tile of 1024 words (32 flags per word); each tile publishes its
+// count in ONE 8-byte agent-scope atomic word {tag, kind, value} and takes as its prefix the
+// sum of every earlier tile's count (independent loads, no chain); it writes the frontier ids, the word
 // prefixes / bitmaps the position lookups need, and clears the flags it read (the workspace
 // is left all-zero for the next call: no memset). The next hop's sampling kernel also ranks the
 // previous hop's lists (its extra workgroups) and derives the previous hop's sampler errors.
 // For L = 2 ([25, 10]): sample + mark, scan + emit, sample + rank = 3 launches.
-constexpr int kScanTileWords = 1024;  // 256 threads x 4 words
-constexpr uint64_t kTileAgg = 1, kTileInc = 2;
+// 256 threads x 4 words (1024 x 8, 39 tiles at 10M nodes, was slower: 0.107 vs 0.083 ms per
+// cfg4 batch -- the dense hub tiles' emission on few workgroups)
+constexpr int kScanThreads = 256;
+constexpr int kScanWpt = 4;  // words per thread
+constexpr int kScanWaves = kScanThreads / 64;
+constexpr int kScanTileWords = kScanThreads * kScanWpt;
+constexpr uint64_t kTileAgg = 1;  // kind of a published tile count
 
 struct SampleWs {
   uint8_t* flags;   // [32 * n_words] (zero between calls)
@@ -326,7 +331,7 @@ __device__ __forceinline__ uint64_t tile_word(uint64_t tag, uint64_t kind, uint3
 // prefixes and bitmaps of the flagged words, flags cleared; one workgroup per tile, tiles taken
 // by ticket (ctl[1], reset by the launch before) so that a tile waits only on tiles that an
 // earlier-started workgroup holds
-__global__ __launch_bounds__(256) void batch_scan_kernel(uint8_t* __restrict__ flags,
+__global__ __launch_bounds__(kScanThreads) void batch_scan_kernel(uint8_t* __restrict__ flags,
                                                          int64_t n_words, uint32_t* __restrict__ bits,
                                                          uint32_t* __restrict__ pre,
                                                          uint64_t* __restrict__ tile_st,
@@ -335,7 +340,7 @@ __global__ __launch_bounds__(256) void batch_scan_kernel(uint8_t* __restrict__ f
                                                          int64_t* __restrict__ count,
                                                          int32_t* __restrict__ err) {
   __shared__ int64_t s_tile;
-  __shared__ uint32_t s_wave[4];
+  __shared__ uint32_t s_wave[kScanWaves];
   __shared__ uint32_t s_prefix;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (tid == 0)
@@ -348,11 +353,11 @@ __global__ __launch_bounds__(256) void batch_scan_kernel(uint8_t* __restrict__ f
     return;
   }
   const uint64_t tag = (ctl[0] + static_cast<uint64_t>(static_cast<int64_t>(tag_off))) & 0x3fffffffull;
-  const int64_t w0 = tile * kScanTileWords + tid * 4;
-  uint32_t mask[4];
+  const int64_t w0 = tile * kScanTileWords + tid * kScanWpt;
+  uint32_t mask[kScanWpt];
   uint32_t cnt = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < kScanWpt; ++q) {
     const int64_t w = w0 + q;
     mask[q] = 0;
     if (w < n_words) {
@@ -381,48 +386,51 @@ __global__ __launch_bounds__(256) void batch_scan_kernel(uint8_t* __restrict__ f
   __syncthreads();
   uint32_t wave_off = 0, agg = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < kScanWaves; ++q) {
     wave_off += q < wid ? s_wave[q] : 0;
     agg += s_wave[q];
   }
   const uint32_t excl = wave_off + incl - cnt;
-  // publish the tile's count, look back for the prefix of the tiles before it
+  // publish the tile's count; the prefix is the sum of EVERY earlier tile's count, loaded 8
+  // windows of 64 at a time (independent loads: one round trip, not one per window as a
+  // nearest-inclusive-prefix look-back takes -- 306 tiles at 10M nodes made that a chain of
+  // up to 5 dependent agent-scope loads, 20 us per scan)
   if (wid == 0) {
     if (lane == 0)
-      __hip_atomic_store(tile_st + tile, tile_word(tag, tile == 0 ? kTileInc : kTileAgg, agg),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t prefix = 0;
-    int64_t look = tile - 1;  // the nearest tile not yet summed
-    uint32_t polls = 0;       // every wave leaves: a tile that never publishes is an error
-    while (look >= 0) {
-      const int64_t j = look - lane;
-      uint64_t sw = tile_word(tag, kTileInc, 0);  // before tile 0: an inclusive prefix of 0
-      bool ready = true;
-      if (j >= 0) {
-        sw = __hip_atomic_load(tile_st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ready = (sw >> 34) == tag && ((sw >> 32) & 3) != 0;
-      }
-      if (__ballot(!ready)) {  // a tile of this window has not published yet
-        if (++polls > (1u << 22)) {
-          if (lane == 0) atomicOr(err, kBatchErrInternal);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      const uint64_t inc = __ballot(((sw >> 32) & 3) == kTileInc);
-      const int stop = inc ? __ffsll(static_cast<unsigned long long>(inc)) - 1 : 63;
-      uint32_t v = lane <= stop ? static_cast<uint32_t>(sw) : 0;
+      __hip_atomic_store(tile_st + tile, tile_word(tag, kTileAgg, agg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t part = 0;
+    uint32_t polls = 0;  // every wave leaves: a tile that never publishes is an error
+    bool failed = false;
+    for (int64_t j0 = 0; j0 < tile && !failed; j0 += 64 * 8) {
+      uint64_t sw[8];
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      prefix += v;
-      if (inc) break;
-      look -= 64;
+      for (int q = 0; q < 8; ++q) {
+        const int64_t j = j0 + q * 64 + lane;
+        sw[q] = j < tile ? __hip_atomic_load(tile_st + j, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)
+                         : tile_word(tag, kTileAgg, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t j = j0 + q * 64 + lane;
+        while (__ballot((sw[q] >> 34) != tag)) {  // a tile of this window has not published
+          if (++polls > (1u << 22)) {
+            failed = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          if ((sw[q] >> 34) != tag)
+            sw[q] = __hip_atomic_load(tile_st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        part += static_cast<uint32_t>(sw[q]);
+      }
     }
+    if (failed && lane == 0) atomicOr(err, kBatchErrInternal);
+    uint32_t prefix = part;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) prefix += __shfl_xor(prefix, o, 64);
     if (lane == 0) {
-      if (tile > 0)
-        __hip_atomic_store(tile_st + tile, tile_word(tag, kTileInc, prefix + agg),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_prefix = prefix;
       if ((tile + 1) * kScanTileWords >= n_words) {  // the last tile: the frontier size
         const int64_t total = static_cast<int64_t>(prefix) + agg;
@@ -434,7 +442,7 @@ __global__ __launch_bounds__(256) void batch_scan_kernel(uint8_t* __restrict__ f
   __syncthreads();
   uint32_t o = s_prefix + excl;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < kScanWpt; ++q) {
     uint32_t m = mask[q];
     if (m == 0) continue;
     const int64_t w = w0 + q;
@@ -653,7 +661,8 @@ extern "C" int gnn_sample_layers(const int64_t* rowptr, const int32_t* col, int6
     launch_hop_k(A, i > 0 ? rank_blocks : 0, s);
     if (i + 1 == n_layers) break;
     // S_{i+1} = the flagged ids of S_i and nbrs[i] (tag i of this call's L)
-    hipLaunchKernelGGL(batch_scan_kernel, dim3(static_cast<unsigned>(sw_tiles(n_words))), dim3(256),
+    hipLaunchKernelGGL(batch_scan_kernel, dim3(static_cast<unsigned>(sw_tiles(n_words))),
+                       dim3(kScanThreads),
                        0, s, w.flags, n_words, w.bits, w.pre, w.tile, w.ctl, i + 1 - n_layers,
                        caps[i + 1], layers[i + 1], stat + i + 1, err);
   }

@@ -634,11 +634,11 @@ __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
         typename Vec<VW>::T wv[U][NFV > 0 ? NFV : 1];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          erv[u] = P.er[static_cast<int64_t>(c[u]) * P.H + h];
+          erv[u] = ok[u] ? P.er[static_cast<int64_t>(c[u]) * P.H + h] : 0.f;
           if constexpr (NFV > 0) {
             const float* xr = P.wh + static_cast<int64_t>(c[u]) * P.ldw + h * P.fh;
 #pragma unroll
-            for (int v = 0; v < NFV; ++v) wv[u][v] = vload<VW>(xr + v * VW);
+            for (int v = 0; v < NFV; ++v) wv[u][v] = ok[u] ? vload<VW>(xr + v * VW) : vzero<VW>();
           }
         }
 #pragma unroll
@@ -767,8 +767,9 @@ __global__ __launch_bounds__(kBw) void gat_bwd_node_r_kernel(BwdNodeParams P, Bw
 #pragma unroll
       for (int ch = 0; ch < NCH; ++ch) {
         const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
-        xv[u][ch] = f < P.feat ? vload<VW>(R.dout + src[u] * P.feat + f) : vzero<VW>();
-        st[u][ch] = ns[hid[ch]];
+        // masked slots (past the row's end) issue no loads
+        xv[u][ch] = (ok[u] && f < P.feat) ? vload<VW>(R.dout + src[u] * P.feat + f) : vzero<VW>();
+        st[u][ch] = ok[u] ? ns[hid[ch]] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
 #pragma unroll

@@ -284,17 +284,38 @@ __global__ __launch_bounds__(kTnThreads) void gemm_tn_mfma_kernel(
   }
 }
 
-// out[e] (+)= sum over the blocks' partials, in block order (e < M*K: C, then dsum)
+// out[e] = the sum over the blocks' partials in a fixed order (e < M*K: C, then dsum). A
+// workgroup takes 64 consecutive elements; its 4 waves sum the partials g, g + 4, g + 8, ...
+// (coalesced 256-B rows of the partial array, 8 loads in flight per lane) and the 4 wave sums
+// are added in wave order. (One thread per element walking all 512 partials took 127 us.)
+constexpr int kTnRedGroups = 4;
 __global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(const float* __restrict__ part,
                                                              int64_t blocks, int64_t stride,
                                                              int64_t mk, int64_t k,
                                                              float* __restrict__ c, int64_t ldc,
                                                              int trans_c,
                                                              float* __restrict__ dsum) {
-  const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (e >= stride) return;
+  __shared__ float sred[kTnRedGroups][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * 64 + lane;
   float s = 0.f;
-  for (int64_t g = 0; g < blocks; ++g) s += part[g * stride + e];
+  if (e < stride) {
+    int64_t j = g;
+    for (; j + 7 * kTnRedGroups < blocks; j += 8 * kTnRedGroups) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(j + u * kTnRedGroups) * stride + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; j < blocks; j += kTnRedGroups) s += part[j * stride + e];
+  }
+  sred[g][lane] = s;
+  __syncthreads();
+  if (g != 0 || e >= stride) return;
+  s = sred[0][lane];
+#pragma unroll
+  for (int q = 1; q < kTnRedGroups; ++q) s += sred[q][lane];
   if (e >= mk)
     dsum[e - mk] = s;
   else if (trans_c)
@@ -337,7 +358,7 @@ static int launch_tn(const float* a, int64_t lda, const float* b, int64_t ldb, c
     hipLaunchKernelGGL((gemm_tn_partial_kernel<M, K, false>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
   }
-  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3(static_cast<unsigned>((stride + 255) / 256)),
+  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3(static_cast<unsigned>((stride + 63) / 64)),
                      dim3(256), 0, s, part, blocks, stride, static_cast<int64_t>(M * K),
                      static_cast<int64_t>(K), c, ldc, trans_c, dsum);
   return launch_status();

@@ -38,8 +38,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
-from .ops import (GAT_DENSE, GAT_SPARSE, gat_aggregate, gat_backward, gat_column_order,
-                  gat_logits, gat_project, gemm_tn)
+from .ops import (GAT_DENSE, GAT_SPARSE, _transform_or_mm, gat_aggregate, gat_backward,
+                  gat_column_order, gat_logits, gat_project, gemm_tn)
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
@@ -91,20 +91,21 @@ def _attention_vector_grads(Wh, dl, der, heads, fh):
 
 
 class _ProjectFn(torch.autograd.Function):
-    """Wh = x W (layers.py:23 / :97, all heads side by side) with the weight gradient
-    dW = x^T dWh by gnn_gemm_tn_f32 (a K = N reduction; hipBLASLt parallelises it badly)."""
+    """Wh = x W (layers.py:23 / :97, all heads side by side) on the MFMA transform (torch.mm where
+    it does not cover the shape) with the weight gradient dW = x^T dWh by gnn_gemm_tn_f32 (a
+    K = N reduction; hipBLASLt parallelises it badly)."""
 
     @staticmethod
     def forward(ctx, x, W):
         ctx.save_for_backward(x, W)
-        return torch.mm(x, W)
+        return _transform_or_mm(x, W.t())  # the MFMA transform (x W = x (W^T)^T)
 
     @staticmethod
     def backward(ctx, dwh):
         x, W = ctx.saved_tensors
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dwh, W.t())
+            dx = _transform_or_mm(dwh, W)
         if ctx.needs_input_grad[1]:
             r = gemm_tn(x, dwh.contiguous())
             dw = r[0] if r is not None else torch.mm(x.t(), dwh)

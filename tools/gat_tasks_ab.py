@@ -7,8 +7,9 @@ outputs compared with the row-class path.
     python tools/gat_tasks_ab.py [--reps 30] [--libs <variant tags>]
 
 --libs: variant libraries (lib/variants/libgnn_<tag>.so, build.build_variant) timed with the
-default schedule beside the main library (round 5: gatpipe2 = a depth-2 chunk pipeline, since
-removed: profiles/r05b_gat_tasks_ab.log).
+row-class schedule beside the main library (round 5: gatpipe2 = a depth-2 chunk pipeline, since
+removed, profiles/r05b_gat_tasks_ab.log; noer = -DGNN_GAT_PROBE_NO_ER, the aggregation without
+its er gathers -- a traffic probe, wrong results).
 """
 from __future__ import annotations
 
@@ -50,7 +51,7 @@ def main():
     variants = [("rowclass", False, 128, 16, None), ("tasks_c64", True, 64, 16, None),
                 ("tasks_c128", True, 128, 16, None), ("tasks_c256", True, 256, 16, None),
                 ("tasks_c128_d32", True, 128, 32, None)]
-    variants += [(f"tasks_c128_{t}", True, 128, 16, LIB_DIR / "variants" / f"libgnn_{t}.so")
+    variants += [(f"rowclass_{t}", False, 128, 16, LIB_DIR / "variants" / f"libgnn_{t}.so")
                  for t in a.libs.split(",") if t]
 
     current = {"lib": "unset"}
