@@ -129,6 +129,21 @@ SIGNATURES: dict[str, tuple] = {
         _vp, _vp,                       # partial, stats
         _u32, _vp,                      # flags, stream
         _vp, _i64, _vp, _i64]),
+    "gnn_gat_csr_ex_f32": (ctypes.c_int, [
+        _vp, _vp, _i64,                 # rowptr, col_hub, n_rows
+        _vp, _i64, _i64, _i64,          # wh, ldw, heads, fh
+        _vp, _vp, _i64,                 # el, er, lde
+        ctypes.c_float, _i32, _vp,      # negative_slope, mode, empty_row_fill
+        ctypes.c_float, ctypes.c_uint64,  # dropout_p, dropout_seed
+        _vp, _i64,                      # out, ldo
+        _i64, _vp, _vp, _i64,           # seg_len, seg_row, seg_begin, n_seg
+        _vp, _vp, _i64,                 # long_row, long_seg_ptr, n_long
+        _vp, _vp, _i64,                 # small_row, small_col, n_small
+        _vp, _i64, _vp, _i64,           # mid_row, n_mid, short_row, n_short
+        _vp, _vp,                       # partial, stats
+        _u32, _vp,                      # flags, stream
+        _vp, _i64, _vp, _i64,           # whh, ldwh, erh, ldeh (NULL: no staged tables)
+        _vp]),                          # a_dst (NULL: er gathered)
     "gnn_gat_csr_tasks_f32": (ctypes.c_int, [
         _vp, _vp, _i64,                 # rowptr, col (hub ranks -1-k when staged), n_rows
         _vp, _i64, _i64, _i64,          # wh, ldw, heads, fh
@@ -162,7 +177,8 @@ SIGNATURES: dict[str, tuple] = {
         ctypes.c_float, _i32, ctypes.c_float, ctypes.c_uint64,  # slope, mode, drop_p, seed
         _vp, _vp, _vp,                              # dout, nstat, del
         _i64, _vp, _vp, _i64, _vp, _vp, _i64,       # plan
-        _vp, _i64, _vp, _i64, _vp, _vp]),           # rows, n, short_rows, n, del_part, stream
+        _vp, _i64, _vp, _i64, _vp, _vp, _vp]),      # rows, n, short_rows, n, del_part, a_dst,
+                                                    # stream
     "gnn_gat_backward_nodes_recompute_f32": (ctypes.c_int, [
         _vp, _vp, _vp, _i64, _i64, _i64,            # rowptr_t, src_t, eid_t, n, heads, fh
         _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,    # dout, nstat, wh, ldw, er, del, a_src, a_dst

@@ -112,7 +112,26 @@ struct GatParams {
   // at most kGatTaskRows consecutive rows of low degree (edgeless and one-edge rows included)
   const int32_t* task_row;
   int64_t n_task;
+  // er recomputed from the gathered Wh rows (gnn_gat_csr_ex_f32 with a_dst): er_j[h] =
+  // a_dst[h] . Wh_j[h], the lane's VW-feature partial dot summed over the er_g lanes of its
+  // head -- no er gather in the one-chunk loop, the short rows and the small rows (the er gather
+  // was 0.17 of 0.78 ms at cfg3, tools/gat_tasks_ab.py --libs noer). NULL: er gathered.
+  const float* a_dst;
+  int er_g;
 };
+
+template <int VW>
+__device__ __forceinline__ float er_partial(typename Vec<VW>::T x, typename Vec<VW>::T a) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < VW; ++k) s = fmaf(vget(x, k), vget(a, k), s);
+  return s;
+}
+// sum over the er_g lanes of a head (aligned lane groups, all active)
+__device__ __forceinline__ float er_reduce(float v, int g) {
+  for (int o = 1; o < g; o <<= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
 
 // Wh row / er entry of column c (hub-staged when c < 0). Without staging no column id is
 // negative and the select never picks the hub tables.
@@ -181,6 +200,13 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
       xv[u][ch] = (c >= 0 && f < P.feat) ? vload<VW>(xr + f) : vzero<VW>();
     }
   }
+  float erx[SU];  // er of (slot's column, lane's head) from the gathered row (NCH == 1)
+  if (P.a_dst != nullptr && NCH == 1) {
+    const int64_t f = static_cast<int64_t>(sub) * VW;
+    const typename Vec<VW>::T ad = f < P.feat ? vload<VW>(P.a_dst + f) : vzero<VW>();
+#pragma unroll
+    for (int u = 0; u < SU; ++u) erx[u] = er_reduce(er_partial<VW>(xv[u][0], ad), P.er_g);
+  }
 #pragma unroll
   for (int u = 0; u < SU; ++u) {
     if (rows[u] < 0) continue;
@@ -194,7 +220,9 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
         const int h = static_cast<int>(f / P.fh);
         float lse = -INFINITY;
         if (cols[u] >= 0) {
-          const float sv = P.el[rows[u] * P.lde + h] + P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
+          const float erv = (P.a_dst != nullptr && NCH == 1)
+                                ? erx[u] : P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
+          const float sv = P.el[rows[u] * P.lde + h] + erv;
           const float x = sv > 0.f ? sv : P.slope * sv;
           lse = SPARSE ? -x : x;
         }
@@ -204,7 +232,9 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
         r = (!SPARSE && P.empty_fill) ? vload<VW>(P.empty_fill + f) : typename Vec<VW>::T(NAN);
       } else if (SPARSE) {
         const int h = static_cast<int>(f / P.fh);
-        const float sv = P.el[rows[u] * P.lde + h] + P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
+        const float erv = (P.a_dst != nullptr && NCH == 1)
+                              ? erx[u] : P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
+        const float sv = P.el[rows[u] * P.lde + h] + erv;
         const float p = __expf(-(sv > 0.f ? sv : P.slope * sv));
         float wv = p;
         if (P.drop_p > 0.f) {
@@ -252,6 +282,7 @@ __device__ __forceinline__ void gat_short_rows(const GatParams& P, int64_t wave,
   const int64_t beg = P.rowptr[row], end = P.rowptr[row + 1];
   const int h = static_cast<int>(f / P.fh);
   const float eli = P.el[row * P.lde + h];
+  const typename Vec<VW>::T adst = P.a_dst != nullptr ? vload<VW>(P.a_dst + f) : vzero<VW>();
   float m = SPARSE ? 0.f : -INFINITY, l = 0.f;
   typename Vec<VW>::T acc = vzero<VW>();
   for (int64_t b = beg; b < end; b += K) {
@@ -261,15 +292,30 @@ __device__ __forceinline__ void gat_short_rows(const GatParams& P, int64_t wave,
     typename Vec<VW>::T xv[K];
 #pragma unroll
     for (int e = 0; e < K; ++e) c[e] = e < n ? P.col[b + e] : 0;
+    if (P.a_dst != nullptr) {  // er from the gathered rows: one round trip, no er loads
 #pragma unroll
-    for (int e = 0; e < K; ++e) {
-      z[e] = -INFINITY;
-      if (e < n) {
-        const float sv = eli + er_at(P, c[e], h);
-        const float x = sv > 0.f ? sv : P.slope * sv;
-        z[e] = SPARSE ? -x : x;
+      for (int e = 0; e < K; ++e) xv[e] = e < n ? vload<VW>(wh_row(P, c[e]) + f) : vzero<VW>();
+#pragma unroll
+      for (int e = 0; e < K; ++e) {
+        const float erv = er_reduce(er_partial<VW>(xv[e], adst), P.er_g);
+        z[e] = -INFINITY;
+        if (e < n) {
+          const float sv = eli + erv;
+          const float x = sv > 0.f ? sv : P.slope * sv;
+          z[e] = SPARSE ? -x : x;
+        }
       }
-      xv[e] = e < n ? vload<VW>(wh_row(P, c[e]) + f) : vzero<VW>();
+    } else {
+#pragma unroll
+      for (int e = 0; e < K; ++e) {
+        z[e] = -INFINITY;
+        if (e < n) {
+          const float sv = eli + er_at(P, c[e], h);
+          const float x = sv > 0.f ? sv : P.slope * sv;
+          z[e] = SPARSE ? -x : x;
+        }
+        xv[e] = e < n ? vload<VW>(wh_row(P, c[e]) + f) : vzero<VW>();
+      }
     }
     if (!SPARSE) {
       float cm = z[0];
@@ -531,19 +577,30 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
     // softmax arithmetic -- one memory round trip per chunk instead of col -> er -> Wh.
     // Same arithmetic in the same order as the loop below (bit-identical results).
     int c_next = ae < end - beg ? P.col[beg + ae] : 0;
-    for (int64_t b = beg; b < end; b += C) {
-      const int np = static_cast<int>(min(static_cast<int64_t>(C), end - b));
-      const int cj = c_next;
-      if (b + C < end) c_next = b + C + ae < end ? P.col[b + C + ae] : 0;
-      const bool live = ae < np && head_ok;
-      const float erv = live ? er_at(P, cj, ah) : 0.f;
-      const int64_t f0 = static_cast<int64_t>(sub) * VW;
-      typename Vec<VW>::T xv[CE];
+    const bool rec = P.a_dst != nullptr;
+    const int64_t f0 = static_cast<int64_t>(sub) * VW;
+    const typename Vec<VW>::T adst = (rec && f0 < P.feat) ? vload<VW>(P.a_dst + f0) : vzero<VW>();
+    // phase-A lane (ae, ah) reads the er of edge ae = q EPI + (ae % EPI) from the first lane
+    // of head ah in lane group ae % EPI
+    const int er_src = (ae % EPI) * LPR + ah * P.er_g;
+    // this chunk's Wh rows: CE gather slots, EPI edges per slot
+    auto load_rows = [&](int cj, int np, typename Vec<VW>::T (&xv)[CE]) {
 #pragma unroll
       for (int q = 0; q < CE; ++q) {
         const int e = q * EPI + grp;
         const int ce = __shfl(cj, (e < EPP ? e : 0) * HP, kWave);
         xv[q] = (e < np && f0 < P.feat) ? vload<VW>(wh_row(P, ce) + f0) : vzero<VW>();
+      }
+    };
+    // softmax update and accumulation of one chunk (erv: the gathered er, unless rec)
+    auto consume = [&](int64_t b, int np, float erv, const typename Vec<VW>::T (&xv)[CE]) {
+      const bool live = ae < np && head_ok;
+      if (rec) {
+#pragma unroll
+        for (int q = 0; q < CE; ++q) {
+          const float v = __shfl(er_reduce(er_partial<VW>(xv[q], adst), P.er_g), er_src, kWave);
+          if (ae / EPI == q) erv = v;
+        }
       }
       float z = -INFINITY;
       if (live) {
@@ -577,6 +634,96 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
                                                                                : wv * P.drop_scale;
         }
         acc[0] += (ok ? wv : 0.f) * xv[q];
+      }
+    };
+    auto chunk_np = [&](int64_t b) {
+      return b < end ? static_cast<int>(min(static_cast<int64_t>(C), end - b)) : 0;
+    };
+    auto next_col = [&](int64_t b) { return (b < end && b + ae < end) ? P.col[b + ae] : 0; };
+    if (rec) {
+      // er comes with the rows: the whole chunk runs in the feature layout -- lane (sub, grp)
+      // holds edge q EPI + grp of slot q for its head hid[0]: er and z per slot from its own
+      // row slice (xor-summed over the head's er_g lanes), the chunk max over the slots and
+      // lane groups (xor shuffles), a lane-partial denominator. No phase-A layout, so none of
+      // the per-slot column-id / weight / scale lane permutes; one permute at the end hands
+      // the denominator and max to the epilogue's phase-A lanes.
+      const float elh = P.el[row * P.lde + hid[0]];
+      const bool fok = f0 < P.feat;
+      float mh = SPARSE ? 0.f : -INFINITY;
+      float lh = 0.f;
+      int cn[CE];
+#pragma unroll
+      for (int q = 0; q < CE; ++q) {
+        const int64_t e = beg + q * EPI + grp;
+        cn[q] = e < end ? P.col[e] : 0;
+      }
+      for (int64_t b = beg; b < end; b += C) {
+        const int np = chunk_np(b);
+        int cc[CE];
+#pragma unroll
+        for (int q = 0; q < CE; ++q) cc[q] = cn[q];
+        if (b + C < end) {
+#pragma unroll
+          for (int q = 0; q < CE; ++q) {
+            const int64_t e = b + C + q * EPI + grp;
+            cn[q] = e < end ? P.col[e] : 0;
+          }
+        }
+        typename Vec<VW>::T xv[CE];
+#pragma unroll
+        for (int q = 0; q < CE; ++q)
+          xv[q] = (q * EPI + grp < np && fok) ? vload<VW>(wh_row(P, cc[q]) + f0) : vzero<VW>();
+        float z[CE];
+#pragma unroll
+        for (int q = 0; q < CE; ++q) {
+          const float sv = elh + er_reduce(er_partial<VW>(xv[q], adst), P.er_g);
+          const float x = sv > 0.f ? sv : P.slope * sv;
+          z[q] = q * EPI + grp < np ? (SPARSE ? -x : x) : -INFINITY;
+        }
+        if (!SPARSE) {
+          float cm = z[0];
+#pragma unroll
+          for (int q = 1; q < CE; ++q) cm = fmaxf(cm, z[q]);
+#pragma unroll
+          for (int o = LPR; o < kWave; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, kWave));
+          const float mn = fmaxf(mh, cm);
+          const float scale = __expf(mh - mn);  // 0 on the first chunk (mh = -inf)
+          mh = mn;
+          lh *= scale;
+          acc[0] *= scale;
+        }
+#pragma unroll
+        for (int q = 0; q < CE; ++q) {
+          const int e = q * EPI + grp;
+          const float p = z[q] == -INFINITY ? 0.f : (SPARSE ? __expf(z[q]) : __expf(z[q] - mh));
+          lh += p;
+          float wv = p;
+          if (P.drop_p > 0.f && e < np) {
+            const uint32_t r = hash3(P.drop_seed, b + e, P.head0 + hid[0]);
+            wv = (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f
+                                                                                 : wv * P.drop_scale;
+          }
+          acc[0] += (e < np && fok ? wv : 0.f) * xv[q];
+        }
+      }
+      // the head's denominator over every lane group, then into the epilogue's layout: phase-A
+      // lane (0, ah) holds it (the epilogue sums the edge slots), every lane the head's max
+#pragma unroll
+      for (int o = LPR; o < kWave; o <<= 1) lh += __shfl_xor(lh, o, kWave);
+      const int src = (ah * P.er_g) & (kWave - 1);
+      const float lA = __shfl(lh, src, kWave);
+      const float mA = __shfl(mh, src, kWave);
+      lsum = ae == 0 ? lA : 0.f;
+      if (!SPARSE) m = mA;
+    } else {
+      for (int64_t b = beg; b < end; b += C) {
+        const int np = chunk_np(b);
+        const int cj = c_next;
+        if (b + C < end) c_next = next_col(b + C);
+        const float erv = (ae < np && head_ok) ? er_at(P, cj, ah) : 0.f;
+        typename Vec<VW>::T xv[CE];
+        load_rows(cj, np, xv);
+        consume(b, np, erv, xv);
       }
     }
   } else
@@ -1034,7 +1181,8 @@ static int gat_entry(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
                      const int32_t* short_row, int64_t n_short,
                      float* partial, float* stats, uint32_t flags, void* stream,
                      const float* whh, int64_t ldwh, const float* erh, int64_t ldeh,
-                     const int32_t* task_row = nullptr, int64_t n_task = 0) {
+                     const int32_t* task_row = nullptr, int64_t n_task = 0,
+                     const float* a_dst = nullptr) {
   if (n_rows < 0 || heads < 1 || fh < 1 || seg_len < 1 || n_seg < 0 || n_long < 0 || n_small < 0)
     return GNN_E_ARG;
   if (n_task < 0 || (n_task > 0 && (task_row == nullptr || mid_row == nullptr))) return GNN_E_ARG;
@@ -1115,7 +1263,15 @@ static int gat_entry(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
                       (P.whh == nullptr || (aligned_to(P.whh, 16) && ldwh % 4 == 0)) &&
                       aligned_to(P.out, 16) &&
                       (P.empty_fill == nullptr || aligned_to(P.empty_fill, 16)) &&
-                      (P.partial == nullptr || (aligned_to(P.partial, 16) && ldp % 4 == 0));
+                      (P.partial == nullptr || (aligned_to(P.partial, 16) && ldp % 4 == 0)) &&
+                      (a_dst == nullptr || aligned_to(a_dst + h0 * fh, 16));
+    // er from the gathered rows: the lanes of a head a power of two, one lane chunk per row
+    {
+      const int64_t vw = vec4 ? 4 : 1, g = fh / vw;
+      const bool rec = a_dst != nullptr && fh % vw == 0 && (g & (g - 1)) == 0 && P.feat <= 64 * vw;
+      P.a_dst = rec ? a_dst + h0 * fh : nullptr;
+      P.er_g = static_cast<int>(g);
+    }
     // tasks run in the one-chunk geometry only (NCH == 1: <= 64 lanes x VW features per row)
     if (P.n_task > 0 && P.feat > 64 * (vec4 ? 4 : 1)) return GNN_E_UNSUPPORTED;
     int rc;
@@ -1197,4 +1353,33 @@ extern "C" int gnn_gat_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, 
                    n_seg, long_row, long_seg_ptr, n_long, nullptr, nullptr, 0, mid_row, n_mid,
                    nullptr, 0, partial, stats, flags, stream, whh, ldwh, erh, ldeh, task_row,
                    n_task);
+}
+
+// gnn_gat_csr_hub_f32 with optional hub tables (whh / erh both NULL: none) and optional a_dst
+// [heads * fh]: the attention vector er = Wh . a_dst came from (GAT/models/layers.py:26-27 /
+// :106), with which the kernels recompute er_j from the Wh_j rows they gather instead of
+// loading er (the one-chunk loop, the short and the small rows; er is still read by the other
+// row paths and must be given). Same values up to the rounding of er's dot products.
+extern "C" int gnn_gat_csr_ex_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                                  const float* wh, int64_t ldw, int64_t heads, int64_t fh,
+                                  const float* el, const float* er, int64_t lde,
+                                  float negative_slope, int32_t mode,
+                                  const float* empty_row_fill, float dropout_p,
+                                  uint64_t dropout_seed, float* out, int64_t ldo, int64_t seg_len,
+                                  const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg,
+                                  const int32_t* long_row, const int32_t* long_seg_ptr,
+                                  int64_t n_long, const int32_t* small_row,
+                                  const int32_t* small_col, int64_t n_small,
+                                  const int32_t* mid_row, int64_t n_mid,
+                                  const int32_t* short_row, int64_t n_short, float* partial,
+                                  float* stats, uint32_t flags, void* stream, const float* whh,
+                                  int64_t ldwh, const float* erh, int64_t ldeh,
+                                  const float* a_dst) {
+  if ((whh == nullptr) != (erh == nullptr)) return GNN_E_ARG;
+  if (whh == nullptr) ldwh = ldeh = 0;
+  return gat_entry(rowptr, col, n_rows, wh, ldw, heads, fh, el, er, lde, negative_slope, mode,
+                   empty_row_fill, dropout_p, dropout_seed, out, ldo, seg_len, seg_row, seg_begin,
+                   n_seg, long_row, long_seg_ptr, n_long, small_row, small_col, n_small, mid_row,
+                   n_mid, short_row, n_short, partial, stats, flags, stream, whh, ldwh, erh, ldeh,
+                   nullptr, 0, a_dst);
 }

@@ -507,6 +507,7 @@ struct BwdRowParams {
   int64_t n_rows_list, row_waves;
   const int32_t* short_rows;  // kShortRowsW rows per wave
   int64_t n_short;
+  const float* a_dst;  // non-NULL (and NFV > 0): er_j = a_dst . Wh_j from the gathered row
 };
 
 // Waves: [segments of long rows | rows | short rows, 8 per wave]. Prep (lanes = features):
@@ -614,10 +615,14 @@ __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
     const float lsei = P.lse[ii * P.H + hh];
     const float Di = Dbuf[r * P.H + hh];
     const float* dh = drow + hh * P.fh;
-    typename Vec<VW>::T dreg[NFV > 0 ? NFV : 1];
+    typename Vec<VW>::T dreg[NFV > 0 ? NFV : 1], areg[NFV > 0 ? NFV : 1];
+    const bool rec = NFV > 0 && P.a_dst != nullptr;  // er_j from the gathered Wh_j (no er loads)
     if constexpr (NFV > 0) {
 #pragma unroll
-      for (int v = 0; v < NFV; ++v) dreg[v] = vload<VW>(dh + v * VW);
+      for (int v = 0; v < NFV; ++v) {
+        dreg[v] = vload<VW>(dh + v * VW);
+        areg[v] = rec ? vload<VW>(P.a_dst + hh * P.fh + v * VW) : vzero<VW>();
+      }
     }
     float dsum = 0.f;
     if (hk) {
@@ -634,11 +639,25 @@ __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
         typename Vec<VW>::T wv[U][NFV > 0 ? NFV : 1];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          erv[u] = ok[u] ? P.er[static_cast<int64_t>(c[u]) * P.H + h] : 0.f;
+          erv[u] = (ok[u] && !rec) ? P.er[static_cast<int64_t>(c[u]) * P.H + h] : 0.f;
           if constexpr (NFV > 0) {
             const float* xr = P.wh + static_cast<int64_t>(c[u]) * P.ldw + h * P.fh;
 #pragma unroll
             for (int v = 0; v < NFV; ++v) wv[u][v] = ok[u] ? vload<VW>(xr + v * VW) : vzero<VW>();
+          }
+        }
+        if constexpr (NFV > 0) {
+          if (rec) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              float e = 0.f;
+#pragma unroll
+              for (int v = 0; v < NFV; ++v) {
+#pragma unroll
+                for (int k = 0; k < VW; ++k) e = fmaf(vget(wv[u][v], k), vget(areg[v], k), e);
+              }
+              erv[u] = e;
+            }
           }
         }
 #pragma unroll
@@ -1059,7 +1078,8 @@ extern "C" int gnn_gat_backward_rows_f32(
     uint64_t dropout_seed, float* dout, float* nstat, float* del, int64_t seg_len,
     const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
     const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows, int64_t n_rows_list,
-    const int32_t* short_rows, int64_t n_short, float* del_part, void* stream) {
+    const int32_t* short_rows, int64_t n_short, float* del_part, const float* a_dst,
+    void* stream) {
   const int64_t feat = heads * fh;
   if (n_rows < 0 || heads < 1 || fh < 1 || ldw < feat || ldo < feat || n_seg < 0 || n_long < 0 ||
       n_rows_list < 0 || n_short < 0 || seg_len < 1 || (mode != 0 && mode != 1))
@@ -1115,8 +1135,10 @@ extern "C" int gnn_gat_backward_rows_f32(
   P.row_waves = row_blocks * kBwWaves;
   hipStream_t s = static_cast<hipStream_t>(stream);
   const bool vec4 = fh % 4 == 0 && ldw % 4 == 0 && ldo % 4 == 0 && aligned_to(wh, 16) &&
-                    aligned_to(dy, 16) && aligned_to(y, 16) && aligned_to(dout, 16);
+                    aligned_to(dy, 16) && aligned_to(y, 16) && aligned_to(dout, 16) &&
+                    (a_dst == nullptr || aligned_to(a_dst, 16));
   const int64_t nfv = vec4 ? fh / 4 : fh;
+  P.a_dst = a_dst;
   const dim3 grid(static_cast<unsigned>(blocks));
   if (blocks > 0) {
 #define GNN_ROWS(VW, NFV) hipLaunchKernelGGL((gat_bwd_rows_kernel<VW, NFV>), grid, dim3(kBw), 0, s, P)

@@ -55,7 +55,7 @@ class _GatLayerFn(torch.autograd.Function):
         el, er = gat_logits(Wh, heads, fh, a_src, a_dst)
         stats = torch.empty((g.n_rows, heads), dtype=torch.float32, device=Wh.device)
         out = gat_aggregate(g, Wh, el, er, heads, fh, slope, mode, activation,
-                            dropout_p=drop_p, seed=seed, stats=stats)
+                            dropout_p=drop_p, seed=seed, stats=stats, a_dst=a_dst)
         ctx.save_for_backward(Wh, a_src, a_dst, el, er, stats, out)
         ctx.cfg = (g, heads, fh, slope, mode, activation, drop_p, seed)
         return out
@@ -156,7 +156,7 @@ class _AttentionBase(nn.Module):
         else:
             el, er = logits if logits is not None else gat_logits(Wh, heads, fh, a_src, a_dst)
             out = gat_aggregate(g, Wh, el, er, heads, fh, self.alpha, self.MODE, activation,
-                                dropout_p=p, seed=seed)
+                                dropout_p=p, seed=seed, a_dst=a_dst)
         if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
             assert not torch.isnan(out).any()
         return out
@@ -180,7 +180,8 @@ class _AttentionBase(nn.Module):
         Wh, el, er = r
         if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
             assert not torch.isnan(Wh).any()
-        out = gat_aggregate(order.graph, Wh, el, er, heads, fh, self.alpha, self.MODE, activation)
+        out = gat_aggregate(order.graph, Wh, el, er, heads, fh, self.alpha, self.MODE, activation,
+                            a_dst=a_dst)
         if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
             assert not torch.isnan(out).any()
         return out

@@ -681,6 +681,9 @@ GAT_SHORT_MAX_DEG = 16  # rows with 2..16 edges take the short-row path (A/B at 
 # edgeless / one-edge rows far more cheaply than a task's per-row flush and per-edge softmax
 # update. Opt-in.
 GAT_TASKS = False
+# er_j recomputed from the gathered Wh_j rows when gat_aggregate is given a_dst (no er gather:
+# cfg3 aggregation without the er loads 0.605 vs 0.777 ms, profiles/r05j_gat_noer_ab.log)
+GAT_ER_RECOMPUTE = True
 GAT_TASK_COST = 128
 
 
@@ -815,8 +818,12 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
                   dropout_p: float = 0.0, seed: int = 0, seg_len: int | None = None,
                   out: torch.Tensor | None = None,
                   stats: torch.Tensor | None = None, hubs: int | None = None,
-                  xcd: bool | None = None) -> torch.Tensor:
+                  xcd: bool | None = None, a_dst: torch.Tensor | None = None) -> torch.Tensor:
     """Fused edge-softmax + neighbour aggregation for all heads (one HIP launch + fix-up).
+
+    ``a_dst`` ([heads * fh], the vector er = Wh . a_dst came from): the kernels recompute er_j
+    from the Wh rows they gather instead of loading it (gnn_gat_csr_ex_f32; GAT_ER_RECOMPUTE);
+    the same values up to the rounding of er's dot products.
 
     ``hubs``: Wh / er rows of the highest-degree columns staged into compact tables first
     (gnn_gat_csr_hub_f32; 0 = none, default ``hub_rows_for``); same output bits.
@@ -913,6 +920,15 @@ def gat_aggregate(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Ten
             _lib.check(rc, "gnn_gat_csr_tasks_f32")
             return out
         # the row-class launch below (same plan, same partial buffer) covers the shape
+    if a_dst is not None and GAT_ER_RECOMPUTE:
+        a_dst = a_dst.detach().reshape(-1).contiguous().float()
+        if a_dst.numel() != feat:
+            raise ValueError("a_dst must hold heads * fh values")
+        _require_device(a_dst)
+        rc = lib.gnn_gat_csr_ex_f32(g.rowptr.data_ptr(), col.data_ptr(), *args, _lib.ptr(whh),
+                                    ldwh, _lib.ptr(erh), lderh, a_dst.data_ptr())
+        _lib.check(rc, "gnn_gat_csr_ex_f32")
+        return out
     if hp is not None:
         rc = lib.gnn_gat_csr_hub_f32(g.rowptr.data_ptr(), hp.col_hub.data_ptr(), *args,
                                      whh.data_ptr(), ldwh, erh.data_ptr(), lderh)
@@ -1195,6 +1211,8 @@ def _gat_backward_recompute(g, wh, el, er, stats, y, dy, a_src, a_dst, heads, fh
     short_ok = 8 * (2 * feat + heads) <= 1152
     rows, short = (_short_split(plan, g.rowptr, GAT_BWD_SHORT_DEG) if short_ok
                    else (plan.row_list(), plan.small_row[:0]))
+    a_src = a_src.detach().reshape(-1).contiguous().float()
+    a_dst = a_dst.detach().reshape(-1).contiguous().float()
     dout = torch.empty((n, feat), **f32)
     nstat = torch.empty((n, heads, 4), **f32)  # {el, lse, D, 0} per (row, head)
     dl = torch.empty((n, heads), **f32)
@@ -1208,7 +1226,8 @@ def _gat_backward_recompute(g, wh, el, er, stats, y, dy, a_src, a_dst, heads, fh
         dout.data_ptr(), nstat.data_ptr(), dl.data_ptr(), plan.seg_len,
         _lib.ptr(plan.seg_row), _lib.ptr(plan.seg_begin), plan.n_seg, _lib.ptr(plan.long_row),
         plan.long_seg_ptr.data_ptr(), plan.n_long, _lib.ptr(rows), rows.numel(),
-        _lib.ptr(short), short.numel(), del_part.data_ptr(), stream)
+        _lib.ptr(short), short.numel(), del_part.data_ptr(),
+        a_dst.data_ptr() if GAT_ER_RECOMPUTE else None, stream)
     if rc == _lib.E_UNSUPPORTED:  # (_bwd_recompute_ok passed: an unaligned view)
         mark(None)
         return None
@@ -1223,8 +1242,6 @@ def _gat_backward_recompute(g, wh, el, er, stats, y, dy, a_src, a_dst, heads, fh
     dwh = torch.empty((n, feat), **f32)
     der = torch.empty((n, heads), **f32)
     part = torch.empty((max(pt.n_seg, 1), feat + heads), **f32)
-    a_src = a_src.contiguous().float()
-    a_dst = a_dst.contiguous().float()
     mark("nodes")
     rc = lib.gnn_gat_backward_nodes_recompute_f32(
         rowptr_t.data_ptr(), src_t.data_ptr(), _lib.ptr(eid_t), n, heads, fh, dout.data_ptr(),

@@ -471,6 +471,26 @@ int gnn_gat_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub, int64_t n
                         int64_t ldwh, const float* erh, int64_t ldeh);
 
 /*
+ * gnn_gat_csr_hub_f32 with the hub tables optional (whh / erh both NULL: no staging, col plain)
+ * and an optional a_dst [heads * fh] (the vector er = Wh . a_dst was computed with,
+ * GAT/models/layers.py:26-27 / :106): with it the kernels recompute er_j from the Wh_j rows they
+ * gather (one-chunk rows, short rows, one-edge rows) instead of loading er -- the er gathers were
+ * 0.17 of 0.78 ms at cfg3. er must still be given (the other row paths read it). Outputs equal
+ * to the er-gathering form up to the rounding of er's dot products.
+ */
+int gnn_gat_csr_ex_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                       const float* wh, int64_t ldw, int64_t heads, int64_t fh, const float* el,
+                       const float* er, int64_t lde, float negative_slope, int32_t mode,
+                       const float* empty_row_fill, float dropout_p, uint64_t dropout_seed,
+                       float* out, int64_t ldo, int64_t seg_len, const int32_t* seg_row,
+                       const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
+                       const int32_t* long_seg_ptr, int64_t n_long, const int32_t* small_row,
+                       const int32_t* small_col, int64_t n_small, const int32_t* mid_row,
+                       int64_t n_mid, const int32_t* short_row, int64_t n_short, float* partial,
+                       float* stats, uint32_t flags, void* stream, const float* whh,
+                       int64_t ldwh, const float* erh, int64_t ldeh, const float* a_dst);
+
+/*
  * The same layer with the low-degree rows as packed row tasks (the package's default at fh % 4
  * == 0): task_row [2 n_task] = [begin, end) ranges of <= 63 consecutive rows of degree <= the
  * plan's threshold (edgeless and one-edge rows included; gnn_spmm_tasks_build builds them),
@@ -560,7 +580,9 @@ int gnn_gat_backward_nodes_f32(const int64_t* rowptr_t, const int32_t* src_t,
  * rows : over CSR rows, the prep fused in: dout (as prep), del (as edges), and per row
  *        nstat[i][h] = {el_ih, lse_ih, D_ih, 0} ([n, heads, 4], 16-B aligned); no per-edge
  *        output. Rows: plan segments + `rows` (one wave each) + `short_rows` (8 per wave; the
- *        low-degree rows), every row exactly once. Unsupported: 2 heads*fh + heads > 1152, or
+ *        low-degree rows), every row exactly once. a_dst (nullable, [heads * fh]): er_j
+ *        recomputed from the gathered Wh_j row (fh / VW <= 4) instead of loaded from er.
+ *        Unsupported: 2 heads*fh + heads > 1152, or
  *        short rows with 8 (2 heads*fh + heads) > 1152.
  * nodes_recompute: over the transposed CSR: per edge (i -> j) a_ij, g_ij = dout_i . Wh_j, w_ij,
  *        ds_ij recomputed from dout_i, nstat_i and node j's own Wh_j / er_j; dwh, der as nodes.
@@ -577,7 +599,7 @@ int gnn_gat_backward_rows_f32(const int64_t* rowptr, const int32_t* col, int64_t
                               const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
                               const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows,
                               int64_t n_rows_list, const int32_t* short_rows, int64_t n_short,
-                              float* del_part, void* stream);
+                              float* del_part, const float* a_dst, void* stream);
 int gnn_gat_backward_nodes_recompute_f32(
     const int64_t* rowptr_t, const int32_t* src_t, const int64_t* eid_t, int64_t n_nodes,
     int64_t heads, int64_t fh, const float* dout, const float* nstat, const float* wh,

@@ -591,3 +591,43 @@ def test_gat_backward_two_pass_matches_three_pass_cfg3(dev, monkeypatch):
     for a, b in zip(res[True], res[False]):
         err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
         assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("heads,fh", [(8, 8), (1, 16), (4, 4), (2, 32), (3, 8), (1, 7), (16, 4)])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("hubs", [0, 64])
+def test_gat_er_recomputed_from_rows(dev, heads, fh, mode, hubs):
+    """gnn_gat_csr_ex_f32 with a_dst (er_j recomputed from the gathered Wh_j rows: one-chunk
+    rows, short rows, one-edge rows) against the er-gathering launch: outputs and per-row LSE
+    stats within fp32 rounding of er's dot product, dropout masks identical; rows of every class
+    (edgeless, one edge, short, mid, a long row split into segments), hub tables on and off.
+    Shapes whose head lanes are not a power of two (fh = 7) fall back to gathering er."""
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.ops import gat_aggregate, gat_logits
+    n = 700
+    rng = np.random.default_rng(heads * 100 + fh)
+    deg = rng.choice([0, 1, 2, 5, 12, 40], n)
+    deg[3] = 900  # a long row
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    col = np.concatenate([np.sort(rng.choice(n, d, replace=d > n)) for d in deg]).astype(np.int32)
+    g = CsrGraph(torch.from_numpy(rowptr).to(dev), torch.from_numpy(col).to(dev),
+                 torch.ones(col.size, device=dev), n, n)
+    feat = heads * fh
+    gen = torch.Generator(device=dev).manual_seed(7)
+    wh = torch.randn(n, feat, device=dev, generator=gen)
+    a_s = torch.randn(feat, device=dev, generator=gen) * 0.3
+    a_d = torch.randn(feat, device=dev, generator=gen) * 0.3
+    el, er = gat_logits(wh, heads, fh, a_s, a_d)
+    for drop in (0.0, 0.3):
+        s0 = torch.empty(n, heads, device=dev)
+        s1 = torch.empty(n, heads, device=dev)
+        y0 = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, "elu", dropout_p=drop, seed=5,
+                           stats=s0, hubs=hubs)
+        y1 = gat_aggregate(g, wh, el, er, heads, fh, 0.2, mode, "elu", dropout_p=drop, seed=5,
+                           stats=s1, hubs=hubs, a_dst=a_d)
+        fin = torch.isfinite(y0)
+        assert torch.equal(fin, torch.isfinite(y1))
+        close(y1[fin].cpu().numpy(), y0[fin].cpu().numpy(), rtol=1e-5)
+        sf = torch.isfinite(s0)
+        assert torch.equal(sf, torch.isfinite(s1))
+        close(s1[sf].cpu().numpy(), s0[sf].cpu().numpy(), rtol=1e-5)

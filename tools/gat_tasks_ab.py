@@ -1,10 +1,11 @@
-"""A/B of the GAT low-degree row schedule at cfg3 (8 x 8 heads over the 1M / 10M R-MAT graph in
-the column-degree order, as bench.py run_gat): packed row tasks (gnn_gat_csr_tasks_f32, task
-cost 64 / 128 / 256 edges + rows, degree threshold 16 / 32) against the row classes they replace
-(packed small rows + gat_short_kernel), interleaved in one process, HIP events per launch;
-outputs compared with the row-class path.
+"""A/B of the GAT aggregation at cfg3 (8 x 8 heads over the 1M / 10M R-MAT graph in the
+column-degree order, as bench.py run_gat): the row classes (packed small rows + gat_short_kernel)
+with er gathered or recomputed from the gathered Wh rows (a_dst, gnn_gat_csr_ex_f32), and with
+--tasks the packed row tasks (gnn_gat_csr_tasks_f32, task cost 64 / 128 / 256 edges + rows,
+degree threshold 16 / 32), interleaved in one process, HIP events per launch; outputs compared
+with the row-class path.
 
-    python tools/gat_tasks_ab.py [--reps 30] [--libs <variant tags>]
+    python tools/gat_tasks_ab.py [--reps 30] [--tasks] [--libs <variant tags>]
 
 --libs: variant libraries (lib/variants/libgnn_<tag>.so, build.build_variant) timed with the
 row-class schedule beside the main library (round 5: gatpipe2 = a depth-2 chunk pipeline, since
@@ -29,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--libs", default="")
+    ap.add_argument("--tasks", action="store_true", help="also the packed-task schedules")
     a = ap.parse_args()
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
@@ -48,16 +50,20 @@ def main():
     out = torch.empty_like(wh)
     from graphneuralnetwork_amd import _lib
     from graphneuralnetwork_amd.build import LIB_DIR
-    variants = [("rowclass", False, 128, 16, None), ("tasks_c64", True, 64, 16, None),
-                ("tasks_c128", True, 128, 16, None), ("tasks_c256", True, 256, 16, None),
-                ("tasks_c128_d32", True, 128, 32, None)]
-    variants += [(f"rowclass_{t}", False, 128, 16, LIB_DIR / "variants" / f"libgnn_{t}.so")
+    variants = [("rowclass", False, 128, 16, None, False),
+                ("rowclass_er_from_rows", False, 128, 16, None, True)]
+    if a.tasks:
+        variants += [("tasks_c64", True, 64, 16, None, False),
+                     ("tasks_c128", True, 128, 16, None, False),
+                     ("tasks_c256", True, 256, 16, None, False),
+                     ("tasks_c128_d32", True, 128, 32, None, False)]
+    variants += [(f"rowclass_{t}", False, 128, 16, LIB_DIR / "variants" / f"libgnn_{t}.so", False)
                  for t in a.libs.split(",") if t]
 
     current = {"lib": "unset"}
 
     def prep(v):  # outside the timed region: a library switch rebinds every symbol
-        _, tasks, cost, deg, lib = v
+        _, tasks, cost, deg, lib, _rec = v
         ops.GAT_TASKS, ops.GAT_TASK_COST, ops.GAT_SHORT_MAX_DEG = tasks, cost, deg
         if current["lib"] != lib:
             _lib.use_variant(lib)
@@ -65,7 +71,8 @@ def main():
 
     def run(v):
         prep(v)
-        return ops.gat_aggregate(ga, wh, el, er, H, Fh, 0.2, ops.GAT_DENSE, "elu", out=out)
+        return ops.gat_aggregate(ga, wh, el, er, H, Fh, 0.2, ops.GAT_DENSE, "elu", out=out,
+                                 a_dst=a_d if v[5] else None)
 
     ref = run(variants[0]).clone()
     times = {v[0]: [] for v in variants}

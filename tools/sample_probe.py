@@ -3,7 +3,7 @@ degree order, as bench.py run_sage): the fused sample_batch and the hop-by-hop p
 around each call, plus the host wall time per call. Run under rocprofv3 --kernel-trace --stats
 for the per-kernel split.
 
-    python tools/sample_probe.py [--reps 20]
+    python tools/sample_probe.py [--reps 20] [--libs noticket,noemit]
 """
 from __future__ import annotations
 
@@ -23,7 +23,11 @@ sys.path.insert(0, str(ROOT))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--libs", default="", help="variant library tags timed beside the main "
+                    "library (fused path only; lib/variants/libgnn_<tag>.so)")
     a = ap.parse_args()
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd.build import LIB_DIR
     from graphneuralnetwork_amd.rmat import rmat_edges
     from graphneuralnetwork_amd.sampler import (degree_ordered, sample_batch,
                                                 sample_batch_stepwise, symmetric_adjacency)
@@ -37,7 +41,11 @@ def main():
     cand = torch.nonzero(adj.rowptr[1:] > adj.rowptr[:-1]).view(-1)
     seeds = cand[torch.randperm(cand.numel(), device=dev, generator=gen)[:8192]]
     out = {}
-    for name, fn in (("fused", sample_batch), ("stepwise", sample_batch_stepwise)):
+    runs = [("fused", sample_batch, None), ("stepwise", sample_batch_stepwise, None)]
+    runs += [(f"fused_{t}", sample_batch, LIB_DIR / "variants" / f"libgnn_{t}.so")
+             for t in a.libs.split(",") if t]
+    for name, fn, lib in runs:
+        _lib.use_variant(lib)
         for _ in range(3):
             fn(adj, seeds, (25, 10), seed=0)
         torch.cuda.synchronize()
@@ -53,6 +61,7 @@ def main():
             ev.append(e0.elapsed_time(e1))
         out[name] = {"event_ms": round(statistics.median(ev), 4),
                      "wall_ms": round(statistics.median(wall), 4)}
+    _lib.use_variant(None)
     print(json.dumps(out), flush=True)
 
 

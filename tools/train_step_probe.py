@@ -3,7 +3,7 @@ the cfg2 Graph_conv_layer(128, 128) step (X requiring grad) or the cfg3 8 x 8-he
 step (W, a_src, a_dst requiring grad), as bench.py's gcn_train_step / gat_train_step; prints the
 HIP-event median step time.
 
-    python tools/train_step_probe.py --model gcn|gat [--steps 10]
+    python tools/train_step_probe.py --model gcn|gat [--steps 10] [--er-gather]
 """
 from __future__ import annotations
 
@@ -22,7 +22,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", choices=("gcn", "gat"), default="gcn")
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--er-gather", action="store_true",
+                    help="GAT: er loaded, not recomputed from the gathered rows")
     a = ap.parse_args()
+    if a.er_gather:
+        from graphneuralnetwork_amd import ops
+        ops.GAT_ER_RECOMPUTE = False
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     from graphneuralnetwork_amd.rmat import rmat_edges
     dev = torch.device("cuda:0")
