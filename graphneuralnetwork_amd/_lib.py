@@ -273,7 +273,10 @@ def use_variant(path) -> ctypes.CDLL:
         return load()
     lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_LOCAL)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:  # an older build may lack entries added since (A/B of a previous tree)
+            fn = getattr(lib, name)
+        except AttributeError:
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib

@@ -176,7 +176,7 @@ constexpr int gat_small_unroll() {
 // so out = Wh_j exactly; sparse computes (p * Wh_j) / p with p = exp(-LeakyReLU)
 // like the reference (inf/0 -> NaN preserved). No edge: dense -> empty_fill,
 // sparse -> 0/0 = NaN.
-template <int VW, int LPR, int NCH, bool SPARSE>
+template <int VW, int LPR, int NCH, bool SPARSE, bool REC>
 __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave, int lane) {
   constexpr int EPI = kWave / LPR;
   const int sub = lane & (LPR - 1);
@@ -201,7 +201,7 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
     }
   }
   float erx[SU];  // er of (slot's column, lane's head) from the gathered row (NCH == 1)
-  if (P.a_dst != nullptr && NCH == 1) {
+  if constexpr (REC) {
     const int64_t f = static_cast<int64_t>(sub) * VW;
     const typename Vec<VW>::T ad = f < P.feat ? vload<VW>(P.a_dst + f) : vzero<VW>();
 #pragma unroll
@@ -220,8 +220,7 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
         const int h = static_cast<int>(f / P.fh);
         float lse = -INFINITY;
         if (cols[u] >= 0) {
-          const float erv = (P.a_dst != nullptr && NCH == 1)
-                                ? erx[u] : P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
+          const float erv = REC ? erx[u] : P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
           const float sv = P.el[rows[u] * P.lde + h] + erv;
           const float x = sv > 0.f ? sv : P.slope * sv;
           lse = SPARSE ? -x : x;
@@ -232,8 +231,7 @@ __device__ __forceinline__ void gat_small_rows(const GatParams& P, int64_t wave,
         r = (!SPARSE && P.empty_fill) ? vload<VW>(P.empty_fill + f) : typename Vec<VW>::T(NAN);
       } else if (SPARSE) {
         const int h = static_cast<int>(f / P.fh);
-        const float erv = (P.a_dst != nullptr && NCH == 1)
-                              ? erx[u] : P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
+        const float erv = REC ? erx[u] : P.er[static_cast<int64_t>(cols[u]) * P.lde + h];
         const float sv = P.el[rows[u] * P.lde + h] + erv;
         const float p = __expf(-(sv > 0.f ? sv : P.slope * sv));
         float wv = p;
@@ -271,7 +269,7 @@ constexpr int kGatShortChunk = GNN_GAT_SHORT_CHUNK;  // edges whose loads one la
 // (chunks of kGatShortChunk edges, online max across chunks). Same arithmetic per
 // edge as gat_csr_kernel (dense: exp(z - max), sparse: exp(z)); requires fh % VW == 0
 // and NCH == 1 (the launcher routes other shapes through the one-row-per-wave path).
-template <int VW, int LPR, bool SPARSE>
+template <int VW, int LPR, bool SPARSE, bool REC>
 __device__ __forceinline__ void gat_short_rows(const GatParams& P, int64_t wave, int lane) {
   constexpr int RPW = kWave / LPR;
   constexpr int K = kGatShortChunk;
@@ -282,7 +280,7 @@ __device__ __forceinline__ void gat_short_rows(const GatParams& P, int64_t wave,
   const int64_t beg = P.rowptr[row], end = P.rowptr[row + 1];
   const int h = static_cast<int>(f / P.fh);
   const float eli = P.el[row * P.lde + h];
-  const typename Vec<VW>::T adst = P.a_dst != nullptr ? vload<VW>(P.a_dst + f) : vzero<VW>();
+  const typename Vec<VW>::T adst = REC ? vload<VW>(P.a_dst + f) : vzero<VW>();
   float m = SPARSE ? 0.f : -INFINITY, l = 0.f;
   typename Vec<VW>::T acc = vzero<VW>();
   for (int64_t b = beg; b < end; b += K) {
@@ -292,7 +290,7 @@ __device__ __forceinline__ void gat_short_rows(const GatParams& P, int64_t wave,
     typename Vec<VW>::T xv[K];
 #pragma unroll
     for (int e = 0; e < K; ++e) c[e] = e < n ? P.col[b + e] : 0;
-    if (P.a_dst != nullptr) {  // er from the gathered rows: one round trip, no er loads
+    if constexpr (REC) {  // er from the gathered rows: one round trip, no er loads
 #pragma unroll
       for (int e = 0; e < K; ++e) xv[e] = e < n ? vload<VW>(wh_row(P, c[e]) + f) : vzero<VW>();
 #pragma unroll
@@ -347,9 +345,9 @@ __device__ __forceinline__ void gat_short_rows(const GatParams& P, int64_t wave,
   vstore<VW>(P.out + row * P.ldo + f, r);
 }
 
-template <int VW, int LPR, bool SPARSE>
+template <int VW, int LPR, bool SPARSE, bool REC>
 __global__ __launch_bounds__(kGatBlock) void gat_short_kernel(GatParams P) {
-  gat_short_rows<VW, LPR, SPARSE>(P, static_cast<int64_t>(blockIdx.x) * kGatWaves + (threadIdx.x >> 6),
+  gat_short_rows<VW, LPR, SPARSE, REC>(P, static_cast<int64_t>(blockIdx.x) * kGatWaves + (threadIdx.x >> 6),
                                   threadIdx.x & (kWave - 1));
 }
 
@@ -517,7 +515,7 @@ __global__ __launch_bounds__(kGatBlock) void gat_task_kernel(GatParams P) {
 #define GNN_GAT_OCC
 #endif
 
-template <int VW, int LPR, int NCH, int HP, bool SPARSE, int U, int J>
+template <int VW, int LPR, int NCH, int HP, bool SPARSE, int U, int J, bool REC>
 __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParams P) {
   constexpr int EPI = kWave / LPR;  // phase B: edges per gather instruction
   constexpr int EPP = kWave / HP;   // phase A: edges per pass (lane = edge x head)
@@ -553,7 +551,7 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
     beg = P.rowptr[row];
     end = P.rowptr[row + 1];
   } else {
-    gat_small_rows<VW, LPR, NCH, SPARSE>(
+    gat_small_rows<VW, LPR, NCH, SPARSE, REC>(
         P, wave - P.seg_waves - P.mid_waves - P.short_waves, lane);
     return;
   }
@@ -577,12 +575,9 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
     // softmax arithmetic -- one memory round trip per chunk instead of col -> er -> Wh.
     // Same arithmetic in the same order as the loop below (bit-identical results).
     int c_next = ae < end - beg ? P.col[beg + ae] : 0;
-    const bool rec = P.a_dst != nullptr;
+    constexpr bool rec = REC;
     const int64_t f0 = static_cast<int64_t>(sub) * VW;
     const typename Vec<VW>::T adst = (rec && f0 < P.feat) ? vload<VW>(P.a_dst + f0) : vzero<VW>();
-    // phase-A lane (ae, ah) reads the er of edge ae = q EPI + (ae % EPI) from the first lane
-    // of head ah in lane group ae % EPI
-    const int er_src = (ae % EPI) * LPR + ah * P.er_g;
     // this chunk's Wh rows: CE gather slots, EPI edges per slot
     auto load_rows = [&](int cj, int np, typename Vec<VW>::T (&xv)[CE]) {
 #pragma unroll
@@ -592,16 +587,9 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
         xv[q] = (e < np && f0 < P.feat) ? vload<VW>(wh_row(P, ce) + f0) : vzero<VW>();
       }
     };
-    // softmax update and accumulation of one chunk (erv: the gathered er, unless rec)
+    // softmax update and accumulation of one chunk with its gathered er values
     auto consume = [&](int64_t b, int np, float erv, const typename Vec<VW>::T (&xv)[CE]) {
       const bool live = ae < np && head_ok;
-      if (rec) {
-#pragma unroll
-        for (int q = 0; q < CE; ++q) {
-          const float v = __shfl(er_reduce(er_partial<VW>(xv[q], adst), P.er_g), er_src, kWave);
-          if (ae / EPI == q) erv = v;
-        }
-      }
       float z = -INFINITY;
       if (live) {
         const float sv = eli + erv;
@@ -640,50 +628,45 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
       return b < end ? static_cast<int>(min(static_cast<int64_t>(C), end - b)) : 0;
     };
     auto next_col = [&](int64_t b) { return (b < end && b + ae < end) ? P.col[b + ae] : 0; };
-    if (rec) {
+    if constexpr (rec) {
       // er comes with the rows: the whole chunk runs in the feature layout -- lane (sub, grp)
       // holds edge q EPI + grp of slot q for its head hid[0]: er and z per slot from its own
       // row slice (xor-summed over the head's er_g lanes), the chunk max over the slots and
       // lane groups (xor shuffles), a lane-partial denominator. No phase-A layout, so none of
       // the per-slot column-id / weight / scale lane permutes; one permute at the end hands
-      // the denominator and max to the epilogue's phase-A lanes.
+      // the denominator and max to the epilogue's phase-A lanes. (4 slots per chunk: 0.93 ms,
+      // the next chunk's rows kept in flight: 1.02 ms, against 0.79 for this form at cfg3 --
+      // register-bound occupancy, profiles/r05p_gat_ab.log.)
+      constexpr int RS = CE;
+      constexpr int CR = RS * EPI;
       const float elh = P.el[row * P.lde + hid[0]];
       const bool fok = f0 < P.feat;
       float mh = SPARSE ? 0.f : -INFINITY;
       float lh = 0.f;
-      int cn[CE];
+      auto cols = [&](int64_t b, int (&c)[RS]) {
 #pragma unroll
-      for (int q = 0; q < CE; ++q) {
-        const int64_t e = beg + q * EPI + grp;
-        cn[q] = e < end ? P.col[e] : 0;
-      }
-      for (int64_t b = beg; b < end; b += C) {
-        const int np = chunk_np(b);
-        int cc[CE];
-#pragma unroll
-        for (int q = 0; q < CE; ++q) cc[q] = cn[q];
-        if (b + C < end) {
-#pragma unroll
-          for (int q = 0; q < CE; ++q) {
-            const int64_t e = b + C + q * EPI + grp;
-            cn[q] = e < end ? P.col[e] : 0;
-          }
+        for (int q = 0; q < RS; ++q) {
+          const int64_t e = b + q * EPI + grp;
+          c[q] = e < end ? P.col[e] : 0;
         }
-        typename Vec<VW>::T xv[CE];
+      };
+      auto rows = [&](int64_t b, const int (&c)[RS], typename Vec<VW>::T (&xv)[RS]) {
 #pragma unroll
-        for (int q = 0; q < CE; ++q)
-          xv[q] = (q * EPI + grp < np && fok) ? vload<VW>(wh_row(P, cc[q]) + f0) : vzero<VW>();
-        float z[CE];
+        for (int q = 0; q < RS; ++q)
+          xv[q] = (b + q * EPI + grp < end && fok) ? vload<VW>(wh_row(P, c[q]) + f0) : vzero<VW>();
+      };
+      auto use = [&](int64_t b, const typename Vec<VW>::T (&xv)[RS]) {
+        float z[RS];
 #pragma unroll
-        for (int q = 0; q < CE; ++q) {
+        for (int q = 0; q < RS; ++q) {
           const float sv = elh + er_reduce(er_partial<VW>(xv[q], adst), P.er_g);
           const float x = sv > 0.f ? sv : P.slope * sv;
-          z[q] = q * EPI + grp < np ? (SPARSE ? -x : x) : -INFINITY;
+          z[q] = b + q * EPI + grp < end ? (SPARSE ? -x : x) : -INFINITY;
         }
         if (!SPARSE) {
           float cm = z[0];
 #pragma unroll
-          for (int q = 1; q < CE; ++q) cm = fmaxf(cm, z[q]);
+          for (int q = 1; q < RS; ++q) cm = fmaxf(cm, z[q]);
 #pragma unroll
           for (int o = LPR; o < kWave; o <<= 1) cm = fmaxf(cm, __shfl_xor(cm, o, kWave));
           const float mn = fmaxf(mh, cm);
@@ -693,18 +676,26 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
           acc[0] *= scale;
         }
 #pragma unroll
-        for (int q = 0; q < CE; ++q) {
-          const int e = q * EPI + grp;
+        for (int q = 0; q < RS; ++q) {
+          const int64_t e = b + q * EPI + grp;
           const float p = z[q] == -INFINITY ? 0.f : (SPARSE ? __expf(z[q]) : __expf(z[q] - mh));
           lh += p;
           float wv = p;
-          if (P.drop_p > 0.f && e < np) {
-            const uint32_t r = hash3(P.drop_seed, b + e, P.head0 + hid[0]);
+          if (P.drop_p > 0.f && e < end) {
+            const uint32_t r = hash3(P.drop_seed, e, P.head0 + hid[0]);
             wv = (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f
                                                                                  : wv * P.drop_scale;
           }
-          acc[0] += (e < np && fok ? wv : 0.f) * xv[q];
+          acc[0] += (e < end && fok ? wv : 0.f) * xv[q];
         }
+      };
+      int cn[RS];
+      cols(beg, cn);
+      for (int64_t b = beg; b < end; b += CR) {
+        typename Vec<VW>::T xv[RS];
+        rows(b, cn, xv);
+        cols(b + CR, cn);  // the next chunk's column ids while this chunk's rows are in flight
+        use(b, xv);
       }
       // the head's denominator over every lane group, then into the epilogue's layout: phase-A
       // lane (0, ah) holds it (the epilogue sums the edge slots), every lane the head's max
@@ -993,9 +984,26 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
   Q.mid_waves = mid_blocks * kGatWaves;
   Q.short_waves = short_blocks * kGatWaves;
   const int64_t blocks = seg_blocks + mid_blocks + short_blocks + small_blocks;
-  if (blocks > 0)
-    hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U, J>),
-                       dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), GNN_GAT_LDS_PAD, s, Q);
+  // er recomputed from the gathered rows: separate instances (the gathering loop's registers
+  // do not weigh on the recomputing one), only where the one-chunk loop runs
+  constexpr bool kRec = GNN_GAT_PIPE && J == 1 && NCH == 1 && CE <= 4;
+  if (blocks > 0) {
+    if constexpr (kRec) {
+      if (P.a_dst != nullptr) {
+        hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U, J, true>),
+                           dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), GNN_GAT_LDS_PAD,
+                           s, Q);
+      } else {
+        hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U, J, false>),
+                           dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), GNN_GAT_LDS_PAD,
+                           s, Q);
+      }
+    } else {
+      hipLaunchKernelGGL((gat_csr_kernel<VW, LPR, NCH, HP, SPARSE, U, J, false>),
+                         dim3(static_cast<unsigned>(blocks)), dim3(kGatBlock), GNN_GAT_LDS_PAD, s,
+                         Q);
+    }
+  }
   if constexpr (NCH == 1) {
     if (P.n_task > 0) {
       hipLaunchKernelGGL((gat_task_kernel<VW, LPR, SPARSE>),
@@ -1004,9 +1012,11 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
     }
     if (P.n_short > 0) {
       const int64_t sw = (P.n_short + EPI - 1) / EPI;
-      hipLaunchKernelGGL((gat_short_kernel<VW, LPR, SPARSE>),
-                         dim3(static_cast<unsigned>((sw + kGatWaves - 1) / kGatWaves)),
-                         dim3(kGatBlock), 0, s, Q);
+      const dim3 grid(static_cast<unsigned>((sw + kGatWaves - 1) / kGatWaves));
+      if (P.a_dst != nullptr)
+        hipLaunchKernelGGL((gat_short_kernel<VW, LPR, SPARSE, true>), grid, dim3(kGatBlock), 0, s, Q);
+      else
+        hipLaunchKernelGGL((gat_short_kernel<VW, LPR, SPARSE, false>), grid, dim3(kGatBlock), 0, s, Q);
     }
   }
   if (P.n_long > 0)

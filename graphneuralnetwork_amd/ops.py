@@ -681,9 +681,12 @@ GAT_SHORT_MAX_DEG = 16  # rows with 2..16 edges take the short-row path (A/B at 
 # edgeless / one-edge rows far more cheaply than a task's per-row flush and per-edge softmax
 # update. Opt-in.
 GAT_TASKS = False
-# er_j recomputed from the gathered Wh_j rows when gat_aggregate is given a_dst (no er gather:
-# cfg3 aggregation without the er loads 0.605 vs 0.777 ms, profiles/r05j_gat_noer_ab.log)
-GAT_ER_RECOMPUTE = True
+# er_j recomputed from the gathered Wh_j rows when gat_aggregate is given a_dst, instead of an
+# er load per (edge, head group). Built and measured, not the default: a probe that dropped the
+# er loads ran the cfg3 aggregation in 0.605 vs 0.777 ms (profiles/r05j_gat_noer_ab.log), but
+# with er taken from the rows the whole chunk waits on them -- 0.793 vs 0.783 ms
+# (r05p_gat_ab.log); the backward row pass: 1.163 vs 1.17 ms (r05n_gat_bwd_probe.log).
+GAT_ER_RECOMPUTE = False
 GAT_TASK_COST = 128
 
 

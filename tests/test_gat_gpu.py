@@ -563,10 +563,12 @@ def test_gat_model_column_order(dev, kind, monkeypatch):
     assert torch.equal(y, y_nat)
 
 
-def test_gat_backward_two_pass_matches_three_pass_cfg3(dev, monkeypatch):
+@pytest.mark.parametrize("er_rec", [False, True])
+def test_gat_backward_two_pass_matches_three_pass_cfg3(dev, monkeypatch, er_rec):
     """At BASELINE cfg3 size (R-MAT 1M / 10M, symmetric normalised adjacency, 8 x 8 heads) the
-    two-pass backward (row pass + recomputing node pass over the graph itself) and the
-    three-pass one agree on dWh, dout, del and der within fp32 summation-order differences."""
+    two-pass backward (row pass + recomputing node pass over the graph itself; er_rec: the row
+    pass takes er_j from the gathered rows) and the three-pass one agree on dWh, dout, del and
+    der within fp32 summation-order differences."""
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     from graphneuralnetwork_amd.rmat import rmat_edges
@@ -581,6 +583,7 @@ def test_gat_backward_two_pass_matches_three_pass_cfg3(dev, monkeypatch):
     stats = torch.empty((g.n_rows, H), device=dev)
     y = ops.gat_aggregate(g, wh, el, er, H, Fh, 0.2, ops.GAT_DENSE, "elu", stats=stats)
     dy = torch.randn(g.n_rows, H * Fh, device=dev, generator=gen)
+    monkeypatch.setattr(ops, "GAT_ER_RECOMPUTE", er_rec)
     res = {}
     for rc in (True, False):
         monkeypatch.setattr(ops, "GAT_BWD_RECOMPUTE", rc)
@@ -596,14 +599,16 @@ def test_gat_backward_two_pass_matches_three_pass_cfg3(dev, monkeypatch):
 @pytest.mark.parametrize("heads,fh", [(8, 8), (1, 16), (4, 4), (2, 32), (3, 8), (1, 7), (16, 4)])
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("hubs", [0, 64])
-def test_gat_er_recomputed_from_rows(dev, heads, fh, mode, hubs):
+def test_gat_er_recomputed_from_rows(dev, heads, fh, mode, hubs, monkeypatch):
     """gnn_gat_csr_ex_f32 with a_dst (er_j recomputed from the gathered Wh_j rows: one-chunk
     rows, short rows, one-edge rows) against the er-gathering launch: outputs and per-row LSE
     stats within fp32 rounding of er's dot product, dropout masks identical; rows of every class
     (edgeless, one edge, short, mid, a long row split into segments), hub tables on and off.
     Shapes whose head lanes are not a power of two (fh = 7) fall back to gathering er."""
+    from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.graph import CsrGraph
     from graphneuralnetwork_amd.ops import gat_aggregate, gat_logits
+    monkeypatch.setattr(ops, "GAT_ER_RECOMPUTE", True)  # built, off by default (slower)
     n = 700
     rng = np.random.default_rng(heads * 100 + fh)
     deg = rng.choice([0, 1, 2, 5, 12, 40], n)

@@ -57,8 +57,11 @@ def main():
                      ("tasks_c128", True, 128, 16, None, False),
                      ("tasks_c256", True, 256, 16, None, False),
                      ("tasks_c128_d32", True, 128, 32, None, False)]
-    variants += [(f"rowclass_{t}", False, 128, 16, LIB_DIR / "variants" / f"libgnn_{t}.so", False)
-                 for t in a.libs.split(",") if t]
+    for t in a.libs.split(","):  # "<tag>" or "<tag>+rec" (with a_dst: er from the rows)
+        if t:
+            tag, rec = t.split("+")[0], t.endswith("+rec")
+            variants.append((f"rowclass_{t}", False, 128, 16,
+                             LIB_DIR / "variants" / f"libgnn_{tag}.so", rec))
 
     current = {"lib": "unset"}
 
