@@ -528,9 +528,10 @@ def run_gat(args, dev, rank: int = 0, world: int = 1):
 
     def layer():  # GAT inference layer: fused MFMA transform + logits, then aggregation
         wh, e_l, e_r = gat_project(X, W, H, Fh, a_s, a_d, col_rows=inv)
-        return gat_aggregate(ga, wh, e_l, e_r, H, Fh, 0.2, GAT_DENSE, "elu", out=out)
+        return gat_aggregate(ga, wh, e_l, e_r, H, Fh, 0.2, GAT_DENSE, "elu", out=out, a_dst=a_d)
 
-    agg = {m: (lambda m=m: gat_aggregate(ga, Wh_o, el_o, er_o, H, Fh, 0.2, m, "elu", out=out))
+    agg = {m: (lambda m=m: gat_aggregate(ga, Wh_o, el_o, er_o, H, Fh, 0.2, m, "elu", out=out,
+                                         a_dst=a_d))
            for m in (GAT_DENSE, GAT_SPARSE)}
     layer_ms, wall = time_steps(layer, args.steps, args.warmup, dev)
     agg_ms = {m: time_steps(f, args.steps, args.warmup, dev)[0] for m, f in agg.items()}

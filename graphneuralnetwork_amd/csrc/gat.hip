@@ -707,14 +707,24 @@ __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParam
       lsum = ae == 0 ? lA : 0.f;
       if (!SPARSE) m = mA;
     } else {
+      // er runs one chunk ahead of the rows: chunk k + 1's er (and chunk k + 2's column ids)
+      // load while chunk k's rows are in flight, so chunk k's softmax arithmetic needs only
+      // values already in registers and runs under its rows' latency; only the weighted sum
+      // waits for them. (er issued beside the rows, the softmax waited for both: a probe
+      // without er loads ran 0.605 against 0.777 ms, profiles/r05j_gat_noer_ab.log.)
+      int cj = c_next;
+      float erv = (ae < chunk_np(beg) && head_ok) ? er_at(P, cj, ah) : 0.f;
+      c_next = next_col(beg + C);
       for (int64_t b = beg; b < end; b += C) {
         const int np = chunk_np(b);
-        const int cj = c_next;
-        if (b + C < end) c_next = next_col(b + C);
-        const float erv = (ae < np && head_ok) ? er_at(P, cj, ah) : 0.f;
         typename Vec<VW>::T xv[CE];
         load_rows(cj, np, xv);
+        const float er_n = (ae < chunk_np(b + C) && head_ok) ? er_at(P, c_next, ah) : 0.f;
+        const int c_n2 = next_col(b + 2 * C);
         consume(b, np, erv, xv);
+        cj = c_next;
+        erv = er_n;
+        c_next = c_n2;
       }
     }
   } else
