@@ -584,12 +584,13 @@ def run_gat(args, dev, rank: int = 0, world: int = 1):
                         "gather_model_frac": gm / t / 1e9 / HBM_PEAK_GBPS,
                         "traffic_GBps": traffic / t / 1e9 if traffic else None,
                         "traffic_frac": traffic / t / 1e9 / HBM_PEAK_GBPS if traffic else None,
-                        "kernel": (("gat_csr_kernel<dense, hub> reading the Wh / er rows of "
-                                    "the %d highest-degree columns in place (the first rows in "
-                                    "the column-degree order) + " % hub_k) if order is not None
+                        "kernel": (("gat_eh_kernel<dense, er from the rows> (segments, mid "
+                                    "and one-edge rows; the Wh rows of the %d highest-degree "
+                                    "columns read in place, the first rows in the column-degree "
+                                    "order) + " % hub_k) if order is not None
                                    else ("gather_rows_kernel x2 (hub staging: Wh / er rows of "
-                                         "the %d highest-degree columns) + gat_csr_kernel<dense, "
-                                         "hub> + " % hub_k) if hub_k else "gat_csr_kernel<dense> + ")
+                                         "the %d highest-degree columns) + gat_eh_kernel<dense> + "
+                                         % hub_k) if hub_k else "gat_eh_kernel<dense> + ")
                                   + "gat_short_kernel + gat_fixup_kernel",
                         "avg_launch_ms": k_ms,
                         "median_launch_ms": statistics.median(agg_ms[GAT_DENSE])}}

@@ -167,6 +167,9 @@ constexpr int gat_small_unroll() {
 #define GNN_GAT_PIPE 1  // pipelined chunk loop in gat_csr_kernel (0: plain loop; a depth-2 form,
                         // two chunks in flight, was slower: profiles/r05b_gat_tasks_ab.log)
 #endif
+#ifndef GNN_GAT_EH
+#define GNN_GAT_EH 1  // segments and mid rows in the edge-head layout (gat_eh_kernel)
+#endif
 #ifndef GNN_GAT_CHUNK
 #define GNN_GAT_CHUNK 8  // edges per phase-A chunk (A/B at cfg3 with the short-row path: 8 > 16 > 32 > 64)
 #endif
@@ -514,6 +517,150 @@ __global__ __launch_bounds__(kGatBlock) void gat_task_kernel(GatParams P) {
 #else
 #define GNN_GAT_OCC
 #endif
+
+// Edge-head layout (heads <= 8 per group, fh = 4 NF): lane (ae, ah) = (edge slot, head) holds
+// head ah's fh features of edge ae's Wh row (NF float4 loads: 8 lanes read a 256-B row at fh = 8),
+// so the score, the online softmax and the weighted sum all run lane-locally: no per-chunk lane
+// permutes of column ids or weights (gat_csr_kernel moves both between its edge x head and
+// feature layouts every chunk), one xor-butterfly over the edge slots per row at the end. With
+// REC, er_j[ah] = a_dst[ah] . Wh_j[ah] comes from the lane's own slice (no er gather: 1.2 of
+// the 4.1 GB the one-chunk kernel fetched at cfg3, profiles/r05r_*); U chunks of EPP edges are
+// loaded before any is used. Segments and mid rows here, edgeless / one-edge rows as in
+// gat_csr_kernel (gat_small_rows), short rows in gat_short_kernel.
+template <int NF, int HP, bool SPARSE, bool REC, int LPR>
+__global__ __launch_bounds__(kGatBlock) void gat_eh_kernel(GatParams P) {
+  constexpr int EPP = kWave / HP;  // edges per chunk
+  constexpr int U = 2;             // chunks loaded together
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wave = static_cast<int64_t>(blockIdx.x) * kGatWaves + (threadIdx.x >> 6);
+  const int ah = lane & (HP - 1);
+  const int ae = lane / HP;
+  int64_t row, beg, end;
+  bool is_seg = false;
+  if (wave < P.seg_waves) {
+    if (wave >= P.n_seg) return;
+    row = P.seg_row[wave];
+    beg = P.seg_begin[wave];
+    end = min(beg + P.seg_len, P.rowptr[row + 1]);
+    is_seg = true;
+  } else if (wave < P.seg_waves + P.mid_waves) {
+    const int64_t i = wave - P.seg_waves;
+    if (i >= P.n_mid) return;
+    row = P.mid_row ? P.mid_row[i] : i;
+    beg = P.rowptr[row];
+    end = P.rowptr[row + 1];
+  } else {
+    gat_small_rows<4, LPR, 1, SPARSE, REC>(P, wave - P.seg_waves - P.mid_waves, lane);
+    return;
+  }
+  const bool head_ok = ah < P.heads;
+  const int64_t hoff = head_ok ? ah : 0;
+  const int64_t fo = hoff * P.fh;  // the head's first feature
+  const float eli = P.el[row * P.lde + hoff];
+  f4 ad[NF];
+#pragma unroll
+  for (int v = 0; v < NF; ++v) ad[v] = REC ? vload<4>(P.a_dst + fo + 4 * v) : f4(0.f);
+  float m = SPARSE ? 0.f : -INFINITY;
+  float l = 0.f;
+  f4 acc[NF];
+#pragma unroll
+  for (int v = 0; v < NF; ++v) acc[v] = f4(0.f);
+  const float sgn = SPARSE ? -1.f : 1.f;
+  int cn[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) cn[u] = beg + u * EPP + ae < end ? P.col[beg + u * EPP + ae] : 0;
+  for (int64_t b = beg; b < end; b += U * EPP) {
+    f4 x[U][NF];
+    float erv[U];
+    bool live[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      live[u] = b + u * EPP + ae < end && head_ok;
+      const float* xr = wh_row(P, cn[u]) + fo;
+#pragma unroll
+      for (int v = 0; v < NF; ++v) x[u][v] = live[u] ? vload<4>(xr + 4 * v) : f4(0.f);
+      if constexpr (!REC) erv[u] = live[u] ? er_at(P, cn[u], ah) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // the next U chunks' column ids while these rows land
+      const int64_t e = b + (U + u) * EPP + ae;
+      cn[u] = e < end ? P.col[e] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (b + u * EPP >= end) break;  // uniform
+      if constexpr (REC) {
+        float s = 0.f;
+#pragma unroll
+        for (int v = 0; v < NF; ++v) {
+          s = fmaf(x[u][v].x, ad[v].x, s);
+          s = fmaf(x[u][v].y, ad[v].y, s);
+          s = fmaf(x[u][v].z, ad[v].z, s);
+          s = fmaf(x[u][v].w, ad[v].w, s);
+        }
+        erv[u] = s;
+      }
+      float z = -INFINITY;
+      if (live[u]) {
+        const float sv = eli + erv[u];
+        z = sgn * (sv > 0.f ? sv : P.slope * sv);
+      }
+      float p;
+      if (!SPARSE) {
+        float pm = z;
+#pragma unroll
+        for (int o = HP; o < kWave; o <<= 1) pm = fmaxf(pm, __shfl_xor(pm, o, kWave));
+        const float mn = fmaxf(m, pm);
+        const float scale = __expf(m - mn);  // 0 on the first chunk (m = -inf)
+        m = mn;
+        p = z == -INFINITY ? 0.f : __expf(z - mn);
+        l = l * scale + p;
+#pragma unroll
+        for (int v = 0; v < NF; ++v) acc[v] *= scale;
+      } else {
+        p = z == -INFINITY ? 0.f : __expf(z);  // exp(-LeakyReLU), no max subtraction
+        l += p;
+      }
+      float w = p;
+      if (P.drop_p > 0.f && live[u]) {
+        const uint32_t r = hash3(P.drop_seed, b + u * EPP + ae, P.head0 + ah);
+        w = (static_cast<float>(r >> 8) * (1.0f / 16777216.0f) < P.drop_p) ? 0.f : w * P.drop_scale;
+      }
+#pragma unroll
+      for (int v = 0; v < NF; ++v) acc[v] += w * x[u][v];
+    }
+  }
+  // the head's sums over the edge slots (every lane of the head ends with them)
+#pragma unroll
+  for (int o = HP; o < kWave; o <<= 1) {
+    l += __shfl_xor(l, o, kWave);
+#pragma unroll
+    for (int v = 0; v < NF; ++v) acc[v] += shfl_xor_f(acc[v], o);
+  }
+  if (lane >= HP || !head_ok) return;
+  if (is_seg) {
+    float* pr = P.partial + wave * P.ldp;
+#pragma unroll
+    for (int v = 0; v < NF; ++v) vstore<4>(pr + fo + 4 * v, acc[v]);
+    pr[P.feat + ah] = l;
+    pr[P.feat + P.heads + ah] = m;
+    return;
+  }
+  const bool empty = end == beg;
+  if (P.stats) P.stats[row * P.lds + ah] = empty ? -INFINITY : (SPARSE ? 0.f : m) + __logf(l);
+  float* orow = P.out + row * P.ldo + fo;
+#pragma unroll
+  for (int v = 0; v < NF; ++v) {
+    f4 r;
+    if (!SPARSE && empty)
+      r = P.empty_fill ? vload<4>(P.empty_fill + fo + 4 * v) : f4(NAN);
+    else
+      r = acc[v] / l;  // sparse, no edge: 0/0 = NaN like the reference
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = act_apply(r[k], P.flags);
+    vstore<4>(orow + 4 * v, r);
+  }
+}
 
 template <int VW, int LPR, int NCH, int HP, bool SPARSE, int U, int J, bool REC>
 __global__ __launch_bounds__(kGatBlock) GNN_GAT_OCC void gat_csr_kernel(GatParams P) {
@@ -994,6 +1141,32 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
   Q.mid_waves = mid_blocks * kGatWaves;
   Q.short_waves = short_blocks * kGatWaves;
   const int64_t blocks = seg_blocks + mid_blocks + short_blocks + small_blocks;
+  // the edge-head layout kernel when a head's features are 1, 2 or 4 float4 (GNN_GAT_EH)
+  if constexpr (VW == 4 && NCH == 1 && HP <= 8) {
+    const int nf = static_cast<int>(P.fh / 4);
+    if (GNN_GAT_EH && P.fh % 4 == 0 && (nf == 1 || nf == 2 || nf == 4) && blocks - short_blocks > 0 &&
+        short_blocks == 0) {
+      const dim3 grid(static_cast<unsigned>(blocks));
+#define GNN_EH(NFV)                                                                         \
+  do {                                                                                      \
+    if (P.a_dst != nullptr)                                                                 \
+      hipLaunchKernelGGL((gat_eh_kernel<NFV, HP, SPARSE, true, LPR>), grid, dim3(kGatBlock), \
+                         0, s, Q);                                                          \
+    else                                                                                    \
+      hipLaunchKernelGGL((gat_eh_kernel<NFV, HP, SPARSE, false, LPR>), grid, dim3(kGatBlock),\
+                         0, s, Q);                                                          \
+  } while (0)
+      if (nf == 1)
+        GNN_EH(1);
+      else if (nf == 2)
+        GNN_EH(2);
+      else
+        GNN_EH(4);
+#undef GNN_EH
+      goto after_main;
+    }
+  }
+  {
   // er recomputed from the gathered rows: separate instances (the gathering loop's registers
   // do not weigh on the recomputing one), only where the one-chunk loop runs
   constexpr bool kRec = GNN_GAT_PIPE && J == 1 && NCH == 1 && CE <= 4;
@@ -1014,6 +1187,8 @@ static void launch_gat(const GatParams& P, hipStream_t s) {
                          Q);
     }
   }
+  }
+after_main:
   if constexpr (NCH == 1) {
     if (P.n_task > 0) {
       hipLaunchKernelGGL((gat_task_kernel<VW, LPR, SPARSE>),

@@ -682,11 +682,12 @@ GAT_SHORT_MAX_DEG = 16  # rows with 2..16 edges take the short-row path (A/B at 
 # update. Opt-in.
 GAT_TASKS = False
 # er_j recomputed from the gathered Wh_j rows when gat_aggregate is given a_dst, instead of an
-# er load per (edge, head group). Built and measured, not the default: a probe that dropped the
-# er loads ran the cfg3 aggregation in 0.605 vs 0.777 ms (profiles/r05j_gat_noer_ab.log), but
-# with er taken from the rows the whole chunk waits on them -- 0.793 vs 0.783 ms
-# (r05p_gat_ab.log); the backward row pass: 1.163 vs 1.17 ms (r05n_gat_bwd_probe.log).
-GAT_ER_RECOMPUTE = False
+# er load per (edge, head group): 1.2 of the 4.1 GB the aggregation fetched at cfg3
+# (profiles/r05r_*). In gat_csr_kernel's layouts the recomputation cost what the loads saved
+# (0.793 vs 0.783 ms, r05p_gat_ab.log); in the edge-head layout (gat_eh_kernel: each lane holds
+# its head's slice of the row) it is a lane-local dot product: 0.631 vs 0.772 ms
+# (r05t_gat_ab.log). The backward row pass takes er_j the same way.
+GAT_ER_RECOMPUTE = True
 GAT_TASK_COST = 128
 
 

@@ -608,7 +608,7 @@ def test_gat_er_recomputed_from_rows(dev, heads, fh, mode, hubs, monkeypatch):
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.graph import CsrGraph
     from graphneuralnetwork_amd.ops import gat_aggregate, gat_logits
-    monkeypatch.setattr(ops, "GAT_ER_RECOMPUTE", True)  # built, off by default (slower)
+    monkeypatch.setattr(ops, "GAT_ER_RECOMPUTE", True)
     n = 700
     rng = np.random.default_rng(heads * 100 + fh)
     deg = rng.choice([0, 1, 2, 5, 12, 40], n)

@@ -66,8 +66,9 @@ def main():
     current = {"lib": "unset"}
 
     def prep(v):  # outside the timed region: a library switch rebinds every symbol
-        _, tasks, cost, deg, lib, _rec = v
+        _, tasks, cost, deg, lib, rec = v
         ops.GAT_TASKS, ops.GAT_TASK_COST, ops.GAT_SHORT_MAX_DEG = tasks, cost, deg
+        ops.GAT_ER_RECOMPUTE = rec
         if current["lib"] != lib:
             _lib.use_variant(lib)
             current["lib"] = lib

@@ -29,7 +29,7 @@ ROOT = Path(__file__).resolve().parent.parent
 WORKLOADS = {
     "cfg2": (128, "spmm_csr_kernel+spmm_fixup_kernel", ("steps", 7)),
     "ns": (128, "spmm_csr_kernel+spmm_fixup_kernel", ("steps", 7)),
-    "cfg3": (64, "gat_csr_kernel+gat_short_kernel+gat_task_kernel+gat_fixup_kernel",
+    "cfg3": (64, "gat_eh_kernel+gat_csr_kernel+gat_short_kernel+gat_task_kernel+gat_fixup_kernel",
              ("median", None)),
     "cfg4": (128, "sage_aggregate_kernel<4, 32, 1, 0, true, 8, false>", ("largest", None)),
 }
