@@ -65,6 +65,9 @@ VARIANTS = {
     "su8": ["GNN_SAGE_U=8"],
     "su16": ["GNN_SAGE_U=16"],
     "su4": ["GNN_SAGE_U=4"],
+    # edge (col, val) moved to the edge slots by v_readlane + select instead of ds_bpermute:
+    # slower (cfg2 0.946 vs 0.870 ms, ns 11.87 vs 11.79 ms, profiles/r05u_readlane_*.log)
+    "readlane": ["GNN_SPMM_READLANE=1"],
 }
 
 
