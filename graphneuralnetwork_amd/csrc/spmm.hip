@@ -104,6 +104,27 @@ struct SpmmParams {
 // rows per packed task: the task's rowptr values (rows + 1) live in one VGPR (lane = row)
 constexpr int kTaskRows = kWave - 1;
 
+#ifndef GNN_SPMM_READLANE
+#define GNN_SPMM_READLANE 0  // A/B: edge (col, val) moved to the slots by v_readlane + select
+#endif
+// v of lane (base + s * stride) & 63 for the calling lane's slot s = lane / LPR (base wave-
+// uniform): EPI scalar lane reads and selects instead of one ds_bpermute round trip through LDS
+template <int LPR>
+__device__ __forceinline__ int slot_lane_i(int v, int base, int stride, int grp) {
+  constexpr int EPI = kWave / LPR;
+  int r = __builtin_amdgcn_readlane(v, base & (kWave - 1));
+#pragma unroll
+  for (int s = 1; s < EPI; ++s) {
+    const int t = __builtin_amdgcn_readlane(v, (base + s * stride) & (kWave - 1));
+    r = grp == s ? t : r;
+  }
+  return r;
+}
+template <int LPR>
+__device__ __forceinline__ float slot_lane_f(float v, int base, int stride, int grp) {
+  return __int_as_float(slot_lane_i<LPR>(__float_as_int(v), base, stride, grp));
+}
+
 // acc[ch] += sum_{e in [beg, end)} val[e] * x[col[e]][(ch*LPR + sub)*VW .. +VW)
 //
 // HUB: a column id c < 0 names row -1-c of the staged hub table xh (the highest-degree
@@ -133,9 +154,14 @@ __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ col,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = k + u * EPI + grp;
+#if GNN_SPMM_READLANE
+        const int ce = slot_lane_i<LPR>(c, k + u * EPI, 1, grp);
+        const float we = slot_lane_f<LPR>(v, k + u * EPI, 1, grp);
+#else
         const int src = e & (kWave - 1);
         const int ce = __shfl(c, src, kWave);
         const float we = __shfl(v, src, kWave);
+#endif
         w[u] = e < n ? we : 0.f;
         const float* xr = (HUB && ce < 0) ? xh + static_cast<int64_t>(-1 - ce) * ldh
                                           : x + static_cast<int64_t>(ce) * ldx;
@@ -361,9 +387,14 @@ __device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int 
       float w[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+#if GNN_SPMM_READLANE
+        const int ce = slot_lane_i<LPR>(c, (k + u) & (LPR - 1), LPR, grp);
+        const float we = slot_lane_f<LPR>(v, (k + u) & (LPR - 1), LPR, grp);
+#else
         const int src = grp * LPR + ((k + u) & (LPR - 1));
         const int ce = __shfl(c, src, kWave);
         const float we = __shfl(v, src, kWave);
+#endif
         const bool ok = cb + k + u < ee;
         w[u] = ok ? we : 0.f;
         const float* xr = (HUB && ce < 0) ? P.xh + static_cast<int64_t>(-1 - ce) * P.ldh
