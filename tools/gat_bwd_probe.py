@@ -3,7 +3,7 @@ adjacency, natural order as bench.py's gat_train_step): per-pass HIP-event media
 backward (row pass, recomputing node pass) for short-row degree bounds, and of the three-pass
 backward, interleaved in one process.
 
-    python tools/gat_bwd_probe.py [--reps 20] [--short 0,4,8,16] [--three]
+    python tools/gat_bwd_probe.py [--reps 20] [--short 0,4,8,16] [--three] [--libs tags]
 """
 from __future__ import annotations
 
@@ -24,7 +24,11 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--short", default="8")
     ap.add_argument("--three", action="store_true")
+    ap.add_argument("--libs", default="", help="variant library tags (lib/variants/libgnn_<tag>"
+                    ".so) timed with the two-pass backward beside the main library")
     a = ap.parse_args()
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd.build import LIB_DIR
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     from graphneuralnetwork_amd.rmat import rmat_edges
@@ -40,12 +44,15 @@ def main():
     stats = torch.empty((g.n_rows, H), device=dev)
     y = ops.gat_aggregate(g, wh, el, er, H, Fh, 0.2, ops.GAT_DENSE, "elu", stats=stats)
     dy = torch.randn(g.n_rows, H * Fh, device=dev, generator=gen)
-    variants = [(f"two_pass_short{k}", True, int(k)) for k in a.short.split(",") if k != ""]
+    variants = [(f"two_pass_short{k}", True, int(k), None) for k in a.short.split(",") if k != ""]
     if a.three:
-        variants.append(("three_pass", False, 8))
+        variants.append(("three_pass", False, 8, None))
+    variants += [(f"two_pass_{t}", True, 8, LIB_DIR / "variants" / f"libgnn_{t}.so")
+                 for t in a.libs.split(",") if t]
 
     def run(v, tl=None):
-        _, rc, k = v
+        _, rc, k, lib = v
+        _lib.use_variant(lib)
         ops.GAT_BWD_RECOMPUTE, ops.GAT_BWD_SHORT_DEG = rc, k
         return ops.gat_backward(g, wh, el, er, stats, y, dy, a_s, a_d, H, Fh, 0.2,
                                 ops.GAT_DENSE, True, timings=tl)
