@@ -108,6 +108,50 @@ __global__ __launch_bounds__(256) void gat_bwd_prep_vec_kernel(const float* __re
   if (c % G == 0) D[r * heads + c / G] = acc;
 }
 
+// The same with the row pass's per-(row, head) record: nstat[r][h] = {el, lse, D, 0} (the row
+// pass then reads dout and the record from HBM instead of computing them per row in LDS).
+template <int G>
+__global__ __launch_bounds__(256) void gat_bwd_prep_rec_kernel(const float* __restrict__ dy,
+                                                               const float* __restrict__ y,
+                                                               int64_t ldo, int64_t n_rows,
+                                                               int64_t heads, int elu,
+                                                               const float* __restrict__ el,
+                                                               const float* __restrict__ lse,
+                                                               float* __restrict__ dout,
+                                                               float* __restrict__ nstat) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t per_row = heads * G;  // float4s per row
+  const bool live = t < n_rows * per_row;
+  const int64_t r = live ? t / per_row : 0, c = live ? t % per_row : 0;
+  float4 yv = make_float4(0.f, 0.f, 0.f, 0.f), gv = yv;
+  if (live) {
+    yv = *reinterpret_cast<const float4*>(y + r * ldo + 4 * c);
+    gv = *reinterpret_cast<const float4*>(dy + r * ldo + 4 * c);
+  }
+  float yy[4] = {yv.x, yv.y, yv.z, yv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w}, dd[4];
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float d = gg[i], o = yy[i];
+    if (elu && yy[i] <= 0.f) {  // ELU'(x) = y + 1 for x <= 0, x = log(y + 1) (saturated: 0)
+      const float tt = yy[i] + 1.f;
+      d = gg[i] * tt;
+      o = tt > 0.f ? __logf(tt) : 0.f;
+    }
+    dd[i] = d;
+    acc = fmaf(d, o, acc);
+  }
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) acc += __shfl_xor(acc, o, 64);
+  if (!live) return;
+  *reinterpret_cast<float4*>(dout + r * (heads * 4 * G) + 4 * c) = make_float4(dd[0], dd[1], dd[2], dd[3]);
+  if (c % G == 0) {
+    const int64_t h = c / G;
+    *reinterpret_cast<float4*>(nstat + (r * heads + h) * 4) =
+        make_float4(el[r * heads + h], lse[r * heads + h], acc, 0.f);
+  }
+}
+
 // ---------------------------------------------------------------- edges
 struct BwdEdgeParams {
   const int64_t* rowptr;
@@ -466,6 +510,9 @@ static int dispatch_nodes(const BwdNodeParams& P, const int32_t* lr, const int32
 // own row, held in registers), w_ij and ds_ij. Per edge the node pass reads 4 + 4 feat + 16 H
 // bytes (12 + 4 feat + 2 x 2 lines before) and the row pass writes nothing.
 constexpr int kRowLds = 1152;    // floats of LDS per wave (4.5 KB: 8 waves per SIMD stay)
+#ifndef GNN_BWD_SPLIT_PREP
+#define GNN_BWD_SPLIT_PREP 1  // prep in its own coalesced kernel (0: fused into the row pass)
+#endif
 constexpr int kShortRowsW = 8;   // rows per wave of the short-row class (8 lanes each)
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -514,10 +561,11 @@ struct BwdRowParams {
 // dout_i = dy_i ELU'(out_i) into LDS (and HBM: by a long row's first segment only), the
 // products dout . out into LDS, D_i per head summed from them. Edges (lanes = (edge slot,
 // head), HP heads per pass): ds_ij as gat_bwd_edge_kernel, summed into del_i (segments: partials).
-template <int VW, int NFV>
+template <int VW, int NFV, bool PREP, bool REC>
 __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
   constexpr int U = 2;
-  __shared__ float lds[kBwWaves][kRowLds];
+  // PREP = false: dout and the {el, lse, D} records came from gat_bwd_prep_rec_kernel
+  __shared__ float lds[kBwWaves][PREP ? kRowLds : 1];
   const int lane = threadIdx.x & (kWave - 1);
   const int wid = threadIdx.x >> 6;
   const int64_t wave = static_cast<int64_t>(blockIdx.x) * kBwWaves + wid;
@@ -549,6 +597,7 @@ __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
   // ---- prep: the (row, feature vector) pairs of the wave's rows spread over the lanes (a
   // short-row wave's 8 rows at 64 features take 2 lane passes, not 8)
   const int nv = static_cast<int>(P.feat / VW);  // feat % VW == 0 when VW = 4
+  if constexpr (PREP) {
   for (int t = lane; t < nr * nv; t += kWave) {
     const int r = t / nv;
     const int64_t f = static_cast<int64_t>(t - r * nv) * VW;
@@ -588,6 +637,7 @@ __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
           make_float4(P.el[i * P.H + h], P.lse[i * P.H + h], s, 0.f);
   }
   wave_lds_sync();
+  }
   // ---- edges
   const int LR = kWave / nr;         // lanes of one row
   const int r = lane / LR, l = lane % LR;
@@ -611,12 +661,22 @@ __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
     const int64_t h = h0 + ah;
     const bool hk = h < P.H && i >= 0;
     const int64_t hh = h < P.H ? h : 0;
-    const float eli = P.el[ii * P.H + hh];
-    const float lsei = P.lse[ii * P.H + hh];
-    const float Di = Dbuf[r * P.H + hh];
-    const float* dh = drow + hh * P.fh;
+    float eli, lsei, Di;
+    const float* dh;
+    if constexpr (PREP) {
+      eli = P.el[ii * P.H + hh];
+      lsei = P.lse[ii * P.H + hh];
+      Di = Dbuf[r * P.H + hh];
+      dh = drow + hh * P.fh;
+    } else {  // the row's own record and dout slice, from the prep kernel
+      const float4 ns = *reinterpret_cast<const float4*>(P.nstat + (ii * P.H + hh) * 4);
+      eli = ns.x;
+      lsei = ns.y;
+      Di = ns.z;
+      dh = P.dout + ii * P.feat + hh * P.fh;
+    }
     typename Vec<VW>::T dreg[NFV > 0 ? NFV : 1], areg[NFV > 0 ? NFV : 1];
-    const bool rec = NFV > 0 && P.a_dst != nullptr;  // er_j from the gathered Wh_j (no er loads)
+    constexpr bool rec = NFV > 0 && REC;  // er_j from the gathered Wh_j (no er loads)
     if constexpr (NFV > 0) {
 #pragma unroll
       for (int v = 0; v < NFV; ++v) {
@@ -1140,8 +1200,41 @@ extern "C" int gnn_gat_backward_rows_f32(
   const int64_t nfv = vec4 ? fh / 4 : fh;
   P.a_dst = a_dst;
   const dim3 grid(static_cast<unsigned>(blocks));
+  // the prep as its own coalesced pass (a float4 per thread, D summed over the head's lanes)
+  // when the head's features are whole float4s, 2^k of them; else fused into the row pass
+  const bool rec = a_dst != nullptr;
+  const int64_t g4 = fh / 4;
+  const bool split = GNN_BWD_SPLIT_PREP && vec4 && (g4 & (g4 - 1)) == 0 && g4 <= 64 &&
+                     aligned_to(nstat, 16);
+  if (split) {
+    const int64_t tv = n_rows * heads * g4;
+    const dim3 pg(static_cast<unsigned>((tv + 255) / 256));
+#define GNN_PREP(G) hipLaunchKernelGGL(gat_bwd_prep_rec_kernel<G>, pg, dim3(256), 0, s, dy, y, ldo, n_rows, heads, static_cast<int>(elu != 0), el, lse, dout, nstat)
+    switch (g4) {
+      case 1: GNN_PREP(1); break;
+      case 2: GNN_PREP(2); break;
+      case 4: GNN_PREP(4); break;
+      case 8: GNN_PREP(8); break;
+      case 16: GNN_PREP(16); break;
+      case 32: GNN_PREP(32); break;
+      default: GNN_PREP(64); break;
+    }
+#undef GNN_PREP
+  }
   if (blocks > 0) {
-#define GNN_ROWS(VW, NFV) hipLaunchKernelGGL((gat_bwd_rows_kernel<VW, NFV>), grid, dim3(kBw), 0, s, P)
+#define GNN_ROWS(VW, NFV)                                                                       \
+  do {                                                                                          \
+    if (split && rec)                                                                           \
+      hipLaunchKernelGGL((gat_bwd_rows_kernel<VW, NFV, false, NFV != 0>), grid, dim3(kBw), 0, s, \
+                         P);                                                                    \
+    else if (split)                                                                             \
+      hipLaunchKernelGGL((gat_bwd_rows_kernel<VW, NFV, false, false>), grid, dim3(kBw), 0, s, P); \
+    else if (rec)                                                                               \
+      hipLaunchKernelGGL((gat_bwd_rows_kernel<VW, NFV, true, NFV != 0>), grid, dim3(kBw), 0, s,  \
+                         P);                                                                    \
+    else                                                                                        \
+      hipLaunchKernelGGL((gat_bwd_rows_kernel<VW, NFV, true, false>), grid, dim3(kBw), 0, s, P); \
+  } while (0)
     if (vec4) {
       switch (nfv) {
         case 1: GNN_ROWS(4, 1); break;
