@@ -778,7 +778,7 @@ struct BwdNodeRParams {
 
 // Lanes = features (LPR lanes x VW, NCH chunks), EPI = 64 / LPR lane groups; a segment or row
 // wave spreads its edges over the groups, a short-row wave gives each group a row of its own.
-template <int VW, int LPR, int NCH>
+template <int VW, int LPR, int NCH, bool DROP>
 __global__ __launch_bounds__(kBw) void gat_bwd_node_r_kernel(BwdNodeParams P, BwdNodeRParams R) {
   constexpr int EPI = kWave / LPR;
   constexpr int U = 4;
@@ -836,7 +836,7 @@ __global__ __launch_bounds__(kBw) void gat_bwd_node_r_kernel(BwdNodeParams P, Bw
       const int64_t e = b + static_cast<int64_t>(u) * ES;
       ok[u] = e < end;
       src[u] = ok[u] ? R.src_t[e] : 0;
-      eid[u] = (ok[u] && R.drop_p > 0.f) ? R.eid_t[e] : 0;
+      eid[u] = (DROP && ok[u]) ? R.eid_t[e] : 0;  // the mask hashes the CSR edge id
     }
     typename Vec<VW>::T xv[U][NCH];
     float4 st[U][NCH];  // {el, lse, D, 0} of (source, head)
@@ -863,7 +863,7 @@ __global__ __launch_bounds__(kBw) void gat_bwd_node_r_kernel(BwdNodeParams P, Bw
         const float x = sv > 0.f ? sv : R.slope * sv;
         const float dzds = (sv > 0.f ? 1.f : R.slope) * sgn;
         const float a = __expf(sgn * x - st[u][ch].y);
-        const float m = bwd_keep(R.drop_p, R.drop_scale, R.drop_seed, eid[u], hid[ch]);
+        const float m = DROP ? bwd_keep(R.drop_p, R.drop_scale, R.drop_seed, eid[u], hid[ch]) : 1.f;
         const float w = ok[u] ? m * a : 0.f;
         const float ds = ok[u] ? a * (m * g - st[u][ch].z) * dzds : 0.f;
         acc[ch] += w * xv[u][ch];
@@ -917,9 +917,14 @@ static void launch_nodes_r(const BwdNodeParams& P0, const BwdNodeRParams& R0, co
   P.seg_waves = seg_blocks * kBwWaves;
   R.row_waves = row_blocks * kBwWaves;
   const int64_t blocks = seg_blocks + row_blocks + short_blocks;
-  if (blocks > 0)
-    hipLaunchKernelGGL((gat_bwd_node_r_kernel<VW, LPR, NCH>), dim3(static_cast<unsigned>(blocks)),
-                       dim3(kBw), 0, s, P, R);
+  if (blocks > 0) {  // dropout as a template flag: its edge ids stay out of the common path
+    if (R.drop_p > 0.f)
+      hipLaunchKernelGGL((gat_bwd_node_r_kernel<VW, LPR, NCH, true>),
+                         dim3(static_cast<unsigned>(blocks)), dim3(kBw), 0, s, P, R);
+    else
+      hipLaunchKernelGGL((gat_bwd_node_r_kernel<VW, LPR, NCH, false>),
+                         dim3(static_cast<unsigned>(blocks)), dim3(kBw), 0, s, P, R);
+  }
   if (n_long > 0)
     hipLaunchKernelGGL((gat_bwd_node_fixup_kernel<VW, LPR, NCH>),
                        dim3(static_cast<unsigned>((n_long + kBwWaves - 1) / kBwWaves)), dim3(kBw), 0,
