@@ -57,6 +57,9 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_spmm_tasks_check": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp]),
     "gnn_sage_gather_concat_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _i64, _i64, _i64,
                                                    _i64, _i32, _vp, _i64, _vp, _i64, _vp, _vp]),
+    "gnn_sage_gather_concat_live_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _i64, _i64, _vp,
+                                                        _i64, _i64, _i32, _vp, _i64, _vp, _i64,
+                                                        _vp, _vp]),
     "gnn_halo_alltoallv_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp]),
     "gnn_halo_rccl_path": (ctypes.c_int, [ctypes.c_char_p, _i64]),
     "gnn_spmm_plan_scratch_bytes": (_i64, [_i64]),
@@ -93,6 +96,8 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_transform_get_precision": (ctypes.c_int, []),
     "gnn_gcn_transform_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnn_linear_relu_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "gnn_linear_relu_live_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
+                                                _vp]),
     "gnn_linear_relu_cls_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64,
                                                _vp, _vp, _i64, _vp, _i64, _vp]),
     "gnn_gcn_transform_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64,

@@ -64,11 +64,11 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
     const int64_t* __restrict__ idx, int64_t ldi, int64_t M, int64_t k, int64_t feat,
     void* __restrict__ out, int64_t ldo, int32_t* __restrict__ err,
     const int64_t* __restrict__ self_idx = nullptr, float* __restrict__ self_out = nullptr,
-    int64_t ld_self = 0) {
+    int64_t ld_self = 0, const int64_t* __restrict__ live = nullptr) {
   constexpr int EPI = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t m = static_cast<int64_t>(blockIdx.x) * kSageWaves + (threadIdx.x >> 6);
-  if (m >= M) return;
+  if (m >= M || (live != nullptr && m >= *live)) return;  // live: a device row count
   const int sub = lane & (LPR - 1);
   const int grp = lane / LPR;
 
@@ -223,6 +223,7 @@ struct SageArgs {
   const int64_t* self_idx = nullptr;  // gather form: also copy table[self_idx[m]] ...
   float* self_out = nullptr;          // ... into self_out[m] (one launch for cat[self, agg])
   int64_t ld_self = 0;
+  const int64_t* live = nullptr;      // rows [0, min(*live, M)) only (device row count)
 };
 
 template <int VW, int LPR, int NCH, int MODE, bool GATHER>
@@ -234,12 +235,12 @@ static int launch_sage(const SageArgs& a) {
     hipLaunchKernelGGL((sage_aggregate_kernel<VW, LPR, NCH, MODE, GATHER, U, GATHER>),
                        dim3(static_cast<unsigned>(blocks)), dim3(kSageBlock), GNN_SAGE_LDS_PAD, a.s,
                        a.src, a.ld_row, a.ld_m, a.n_table, a.idx, a.ldi, a.M, a.k, a.feat, a.out,
-                       a.ldo, a.err, a.self_idx, a.self_out, a.ld_self);
+                       a.ldo, a.err, a.self_idx, a.self_out, a.ld_self, a.live);
   else
     hipLaunchKernelGGL((sage_aggregate_kernel<VW, LPR, NCH, MODE, GATHER, U>),
                        dim3(static_cast<unsigned>(blocks)), dim3(kSageBlock), GNN_SAGE_LDS_PAD, a.s,
                        a.src, a.ld_row, a.ld_m, a.n_table, a.idx, a.ldi, a.M, a.k, a.feat, a.out,
-                       a.ldo, a.err, nullptr, nullptr, 0);
+                       a.ldo, a.err, nullptr, nullptr, 0, a.live);
   return launch_status();
 }
 
@@ -345,11 +346,28 @@ extern "C" int gnn_gather_rows_f32(const float* x, int64_t ldx, int64_t n_x, con
   return launch_status();
 }
 
+extern "C" int gnn_sage_gather_concat_live_f32(const float* table, int64_t ldt, int64_t n_table,
+                                               const int64_t* self_idx, const int64_t* idx,
+                                               int64_t ldi, int64_t M, const int64_t* live,
+                                               int64_t k, int64_t feat, int32_t mode,
+                                               float* self_out, int64_t ld_self, float* out,
+                                               int64_t ldo, int32_t* err_flag, void* stream);
+
 extern "C" int gnn_sage_gather_concat_f32(const float* table, int64_t ldt, int64_t n_table,
                                           const int64_t* self_idx, const int64_t* idx, int64_t ldi,
                                           int64_t M, int64_t k, int64_t feat, int32_t mode,
                                           float* self_out, int64_t ld_self, float* out, int64_t ldo,
                                           int32_t* err_flag, void* stream) {
+  return gnn_sage_gather_concat_live_f32(table, ldt, n_table, self_idx, idx, ldi, M, nullptr, k,
+                                         feat, mode, self_out, ld_self, out, ldo, err_flag, stream);
+}
+
+extern "C" int gnn_sage_gather_concat_live_f32(const float* table, int64_t ldt, int64_t n_table,
+                                               const int64_t* self_idx, const int64_t* idx,
+                                               int64_t ldi, int64_t M, const int64_t* live,
+                                               int64_t k, int64_t feat, int32_t mode,
+                                               float* self_out, int64_t ld_self, float* out,
+                                               int64_t ldo, int32_t* err_flag, void* stream) {
   if (M < 0 || k < 0 || feat < 0 || n_table < 0 || !(mode == kMean || mode == kSum || mode == kMaxPool))
     return GNN_E_ARG;
   if (M == 0 || feat == 0) return GNN_OK;
@@ -360,6 +378,6 @@ extern "C" int gnn_sage_gather_concat_f32(const float* table, int64_t ldt, int64
   const bool vec4 = feat % 4 == 0 && ldt % 4 == 0 && ldo % 4 == 0 && ld_self % 4 == 0 &&
                     aligned_to(table, 16) && aligned_to(out, 16) && aligned_to(self_out, 16);
   SageArgs a{table, ldt, 0, n_table, idx, ldi, M, k, feat, out, ldo, err_flag,
-             static_cast<hipStream_t>(stream), self_idx, self_out, ld_self};
+             static_cast<hipStream_t>(stream), self_idx, self_out, ld_self, live};
   return run_sage<true>(a, mode, vec4);
 }

@@ -29,6 +29,9 @@ struct RowIdx {  // the optional output-row scatter (gcn_transform_kernel y_row)
   const int64_t* row;
   int64_t n_y;
   int32_t* err;
+  // optional device row count: rows [0, min(*live, n_rows)) are computed (a sampled batch's
+  // frontier size, never read back to the host; n_rows is then the buffer's capacity)
+  const int64_t* live = nullptr;
 };
 // the optional classifier epilogue (gnn_linear_relu_cls_f32): logits = y wd^T + bd
 constexpr int kMaxCls = 4;
@@ -81,7 +84,11 @@ template <int K, int CB, int NW, bool RELU, int TR, int MODE, bool X6 = false>
 __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
     float* __restrict__ y, int64_t ldy, const int64_t* __restrict__ y_row, int64_t n_y,
-    int32_t* __restrict__ err, Classifier cls) {
+    int32_t* __restrict__ err, Classifier cls, const int64_t* __restrict__ live) {
+  if (live != nullptr) {  // uniform: every wave reads the same count
+    const int64_t l = *live;
+    n_rows = l < n_rows ? (l > 0 ? l : 0) : n_rows;
+  }
   constexpr bool SCATTER = MODE == kTfScatter;
   constexpr bool CLS = MODE == kTfClassify;
   constexpr int kTfBlock = NW * kWave;
@@ -407,16 +414,16 @@ static void launch_transform_kernel(dim3 grid, const float* x, int64_t ldx, int6
   if (ri.row != nullptr)  // a template flag: no index loads in the in-order kernel
     hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfScatter, X6>), grid,
                        dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err,
-                       cls);
+                       cls, ri.live);
   else if (RELU && cls.logits != nullptr)  // the classifier epilogue: SageLayer GEMMs only
     hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, RELU ? kTfClassify : kTfPlain,
                                              X6>),
                        grid, dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y,
-                       ri.err, cls);
+                       ri.err, cls, ri.live);
   else
     hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfPlain, X6>), grid,
                        dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err,
-                       cls);
+                       cls, ri.live);
 }
 
 template <int K, int CB, int NW, bool RELU, int TR>
@@ -575,6 +582,15 @@ extern "C" int gnn_linear_relu_f32(const float* x, int64_t ldx, int64_t n_rows, 
                                    const float* w, int64_t fout, float* y, int64_t ldy,
                                    void* stream) {
   return transform_entry<true>(x, ldx, n_rows, k, w, fout, y, ldy, stream);
+}
+
+extern "C" int gnn_linear_relu_live_f32(const float* x, int64_t ldx, int64_t n_rows,
+                                        const int64_t* live, int64_t k, const float* w,
+                                        int64_t fout, float* y, int64_t ldy, void* stream) {
+  if (n_rows > 0 && !live) return GNN_E_ARG;
+  RowIdx ri{nullptr, 0, nullptr};
+  ri.live = live;
+  return transform_entry<true>(x, ldx, n_rows, k, w, fout, y, ldy, stream, ri);
 }
 
 extern "C" int gnn_linear_relu_cls_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,

@@ -54,10 +54,22 @@ class Gathered(NamedTuple):
     (GraphSAGE/data_utils.py:161-162); see ``sampler.sample_batch``.
     ``trusted``: the indices are known to be in range (built by the device
     sampler), so the gather skips its index check and the host sync it costs.
+    ``live``: a device int64 scalar -- only ``index[:live]`` is real (a batch from
+    ``sample_batch(..., sync=False)``, whose sizes the host never read; ``index`` is then
+    the buffer at its capacity). The fused inference layer runs on it as it is; any other
+    path reads the count back and slices.
     """
     table: torch.Tensor
     index: torch.Tensor
     trusted: bool = False
+    live: torch.Tensor | None = None
+
+
+def _trim(g):
+    """A Gathered with a device row count as an ordinary one (one host read)."""
+    if not isinstance(g, Gathered) or g.live is None:
+        return g
+    return Gathered(g.table, g.index[:int(g.live.item())], g.trusted)
 
 
 def trust_map(t: torch.Tensor) -> torch.Tensor:
@@ -250,18 +262,39 @@ def _fused_sage_layer(block, center, neigh: Gathered, dense: nn.Linear | None = 
     ``dense`` (the last layer of a supervised net): the classifier of GraphSAGE.py:51-52 runs in
     the GEMM's epilogue when the MFMA kernel takes the shape (``ops.linear_relu_classify``);
     the return value is then ``(y, logits)``, else ``y`` alone."""
+    live = neigh.live
+    if live is not None:
+        # a device row count: the concat gather + MFMA GEMM run on the buffers' capacity and
+        # read the count themselves (no host round trip); other shapes / the classifier
+        # epilogue read it back and slice
+        W = block.weight.weight
+        if (dense is not None or not isinstance(center, Gathered) or center.table is not neigh.table
+                or center.live is None or not _sage_gemm_on_mfma(neigh.index.shape[0])
+                or W.dtype != torch.float32):
+            center, neigh, live = _trim(center), _trim(neigh), None
     if isinstance(center, Gathered):
         self_src, self_idx, trusted = center.table, center.index, center.trusted
     else:
         self_src, self_idx, trusted = center, None, True
-    y = sage_layer(neigh.table, neigh.index, block.weight.weight, self_src, self_idx,
-                   check=not (trusted and neigh.trusted))
+    y = None
+    if live is None:
+        y = sage_layer(neigh.table, neigh.index, block.weight.weight, self_src, self_idx,
+                       check=not (trusted and neigh.trusted))
     if y is not None:
         return y
     M, n = neigh.index.shape[0], block.input_size
     dev = neigh.table.device
     buf = torch.empty((M, 2 * n), dtype=torch.float32, device=dev)
-    if isinstance(center, Gathered) and center.table is neigh.table:
+    if live is not None:
+        sage_gather_concat(neigh.table, center.index, neigh.index, "MEAN",
+                           check=not (center.trusted and neigh.trusted), out=buf, live=live)
+        y = gcn_transform(buf, block.weight.weight, relu=True, live=live)
+        if y is not None:
+            return y
+        # the transform does not take the shape: the rows past the count are never read
+        buf = buf[:int(live.item())]
+        M = buf.shape[0]
+    elif isinstance(center, Gathered) and center.table is neigh.table:
         # both halves of cat[self, agg] in one launch (gnn_sage_gather_concat_f32)
         sage_gather_concat(neigh.table, center.index, neigh.index, "MEAN",
                            check=not (center.trusted and neigh.trusted), out=buf)
@@ -327,6 +360,7 @@ class GraphSAGE(nn.Module):
                     if isinstance(feats_data, tuple):  # the classifier ran in the epilogue
                         feats_data, classes = feats_data
                 else:
+                    center, neigh = _trim(center), _trim(neigh)
                     if isinstance(center, Gathered):
                         center = _gather(center.table, center.index, center.trusted)
                     feats_data = block(center, Aggregator(neigh, self.agg_func))
@@ -334,8 +368,9 @@ class GraphSAGE(nn.Module):
                     cm = center_nodes_map[i]
                     nm = center_neigh_nodes_map[i]
                     if _trusted(cm) and _trusted(nm):  # device-sampler maps: no -1, in range
-                        center = Gathered(feats_data, cm, True)
-                        neigh = Gathered(feats_data, nm, True)
+                        lv = getattr(cm, "_gnn_live", None)  # sync=False batch: device size
+                        center = Gathered(feats_data, cm, True, lv)
+                        neigh = Gathered(feats_data, nm, True, lv)
                     else:                              # GraphSAGE.py:56-57 (-1 padding dropped)
                         center = Gathered(feats_data, cm[cm != -1], False)
                         neigh = Gathered(feats_data, nm[nm[:, 0] != -1, :], False)

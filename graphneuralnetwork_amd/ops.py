@@ -560,7 +560,7 @@ def set_transform_precision(mode: str) -> str:
 
 def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
                   out: torch.Tensor | None = None, out_rows: torch.Tensor | None = None,
-                  check_rows: bool = True) -> torch.Tensor | None:
+                  check_rows: bool = True, live: torch.Tensor | None = None) -> torch.Tensor | None:
     """support = x @ weight^T on fp32 MFMA (gnn_gcn_transform_f32), the dense half of
     Graph_conv_layer.forward (GCN/GCN.py:42); ``relu=True``: max(x @ weight^T, 0)
     (gnn_linear_relu_f32, the SageLayer at GraphSAGE/GraphSAGE.py:18-20). Inference only
@@ -572,7 +572,11 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
     degree-ordered graph's column order; ``out`` (or a new [rows of x, fout] tensor) receives
     it; the ids must not repeat (two rows stored to one support row leave either).
     ``check_rows=False`` skips the host read of the range-check flag (trusted ids, e.g. a
-    ``DegreeOrder``'s; the kernel still skips the store of a bad id)."""
+    ``DegreeOrder``'s; the kernel still skips the store of a bad id).
+
+    ``live`` (with ``relu=True``): a device int64 scalar; only rows [0, min(live, rows of x))
+    are computed (gnn_linear_relu_live_f32) -- a sampled batch's frontier whose size the host
+    never read; the other output rows are left as they were."""
     _require_device(x, weight)
     if (x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 2
             or weight.dim() != 2 or x.shape[1] != weight.shape[1]):
@@ -585,6 +589,12 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
         return None
     if out_rows is not None and relu:
         raise ValueError("out_rows= is supported without the ReLU epilogue only")
+    if live is not None:
+        _require_device(live)
+        if not relu or out_rows is not None:
+            raise ValueError("live= is supported with the ReLU epilogue (the SageLayer) only")
+        if live.dtype != torch.int64 or live.numel() != 1:
+            raise TypeError("live must be a one-element int64 device tensor")
     if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
         x = x.contiguous()
     w = weight.contiguous()
@@ -609,6 +619,12 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
             "gnn_gcn_transform_rows_f32")
         if check_rows and int(err.item()):
             raise IndexError("gcn_transform: an output row id is out of range")
+        return out
+    if live is not None:
+        _lib.check(lib.gnn_linear_relu_live_f32(
+            x.data_ptr(), x.stride(0), x.shape[0], live.data_ptr(), k, w.data_ptr(), fout,
+            out.data_ptr(), out.stride(0), _lib.stream_handle(x.device)),
+            "gnn_linear_relu_live_f32")
         return out
     fn, name = ((lib.gnn_linear_relu_f32, "gnn_linear_relu_f32") if relu else
                 (lib.gnn_gcn_transform_f32, "gnn_gcn_transform_f32"))
@@ -1050,10 +1066,13 @@ def sage_gather_aggregate(table: torch.Tensor, idx: torch.Tensor, agg_func: str 
 
 def sage_gather_concat(table: torch.Tensor, self_idx: torch.Tensor, idx: torch.Tensor,
                        agg_func: str = "MEAN", check: bool = True,
-                       out: torch.Tensor | None = None) -> torch.Tensor:
+                       out: torch.Tensor | None = None,
+                       live: torch.Tensor | None = None) -> torch.Tensor:
     """[M, 2F] = cat[table[self_idx], Aggregator(table[idx])] in one launch
     (gnn_sage_gather_concat_f32): the SageLayer input of GraphSAGE/GraphSAGE.py:17 with the
-    gathers of :47-49. ``out`` may be any [M, 2F] float32 view with unit column stride."""
+    gathers of :47-49. ``out`` may be any [M, 2F] float32 view with unit column stride.
+    ``live``: a device int64 scalar; rows [0, min(live, M)) only (gnn_sage_gather_concat_live_f32,
+    M = the capacity of a sampled batch whose frontier size the host never read)."""
     if agg_func not in ("MEAN", "SUM", "MAXPOOL"):
         raise RuntimeError(f"agg_func {agg_func!r} has no concat form")
     _require_device(table, self_idx, idx, out)
@@ -1079,13 +1098,17 @@ def sage_gather_concat(table: torch.Tensor, self_idx: torch.Tensor, idx: torch.T
         out[:, :F].copy_(gather_rows(table, self_idx, check=check))
         out[:, F:].fill_(_EMPTY_FILL[SAGE_KINDS[agg_func]])
         return out
+    if live is not None:
+        _require_device(live)
+        if live.dtype != torch.int64 or live.numel() != 1:
+            raise TypeError("live must be a one-element int64 device tensor")
     err = _err_flag(table.device, check)
     lib = _lib.load()
-    _lib.check(lib.gnn_sage_gather_concat_f32(
+    _lib.check(lib.gnn_sage_gather_concat_live_f32(
         table.data_ptr(), table.stride(0), table.shape[0], self_idx.data_ptr(), idx.data_ptr(),
-        idx.stride(0), M, k, F, SAGE_KINDS[agg_func], out.data_ptr(), out.stride(0),
-        out[:, F:].data_ptr(), out.stride(0), err.data_ptr(), _lib.stream_handle(table.device)),
-        "gnn_sage_gather_concat_f32")
+        idx.stride(0), M, _lib.ptr(live), k, F, SAGE_KINDS[agg_func], out.data_ptr(),
+        out.stride(0), out[:, F:].data_ptr(), out.stride(0), err.data_ptr(),
+        _lib.stream_handle(table.device)), "gnn_sage_gather_concat_live_f32")
     if check:
         _check_err(err, "sage_gather_concat")
     return out

@@ -174,10 +174,29 @@ class SampledBatch:
     center_maps: list          # L-1 tensors, forward order (see above)
     neigh_maps: list           # L-1 tensors [|S_{L-2-i}|, k_{L-2-i}], forward order
     layers: tuple = ()         # S_0 (the seeds), ..., S_{L-1} (= frontier)
+    # sample_batch(..., sync=False): the tensors above are the buffers at their capacity,
+    # live[i] = |S_i| as a device int64 scalar (None for the seeds), and _finish() reads the
+    # sizes and error bits back and returns the batch at its real sizes
+    live: tuple = ()
+    _finish: object = None
+
+    @property
+    def pending(self) -> bool:
+        """True for a sync=False batch whose sizes and error bits the host has not read."""
+        return self._finish is not None
+
+    def sync(self) -> "SampledBatch":
+        """This batch at its real sizes (one host read for a pending batch; raises the
+        sampler's errors exactly as sample_batch(..., sync=True) does)."""
+        return self._finish() if self._finish is not None else self
+
+    def check(self) -> None:
+        """Raise the sampler's error, if any (a pending batch's one host read)."""
+        self.sync()
 
     @property
     def layer_sizes(self) -> tuple:
-        return tuple(int(t.numel()) for t in self.layers)
+        return tuple(int(t.numel()) for t in self.sync().layers)
 
     @property
     def center_map(self) -> torch.Tensor:
@@ -191,12 +210,17 @@ class SampledBatch:
 
     @property
     def sampled_edges(self) -> int:
-        return int(self.frontier_nbrs.numel() + sum(m.numel() for m in self.neigh_maps))
+        b = self.sync()
+        return int(b.frontier_nbrs.numel() + sum(m.numel() for m in b.neigh_maps))
 
     def forward_args(self, table: torch.Tensor):
-        """The 4 leading arguments of GraphSAGE.forward (supervised branch)."""
-        return (Gathered(table, self.frontier, True), [trust_map(m) for m in self.center_maps],
-                Gathered(table, self.frontier_nbrs, True), [trust_map(m) for m in self.neigh_maps])
+        """The 4 leading arguments of GraphSAGE.forward (supervised branch). A pending batch's
+        arguments carry the device sizes (``Gathered.live``, the maps' ``_gnn_live``): the
+        inference forward then runs without a host round trip."""
+        lv = self.live[-1] if self.live else None
+        return (Gathered(table, self.frontier, True, lv), [trust_map(m) for m in self.center_maps],
+                Gathered(table, self.frontier_nbrs, True, lv),
+                [trust_map(m) for m in self.neigh_maps])
 
 
 _STAT_HOST = {}
@@ -211,7 +235,7 @@ def _stat_host(n: int) -> torch.Tensor:
 
 
 def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int = 0,
-                 gcn: bool = False) -> SampledBatch:
+                 gcn: bool = False, sync: bool = True) -> SampledBatch:
     """L = len(fanouts) layer frontier for ``seeds`` (get_layer_adj_nodes,
     GraphSAGE/data_utils.py:82-103, with a fanout per layer like GraphSAGE_Pytorch's
     multihop_sampling): fanouts[i] neighbours for every node of S_i, chained per hop.
@@ -220,7 +244,14 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
     on the device -- for [25, 10] three launches: draw + frontier marks, the frontier scan,
     draw + the maps -- and ONE host read at the end fetches the layer sizes and the error bits:
     the same tensors as ``sample_batch_stepwise`` (which reads each frontier size back before
-    the next hop), bit for bit."""
+    the next hop), bit for bit.
+
+    ``sync=False``: no host read at all -- the batch comes back pending (``SampledBatch.live``
+    holds the layer sizes on the device, the tensors are the buffers at their capacity), so
+    the inference forward is enqueued right behind the sampler; ``batch.check()`` /
+    ``batch.sync()`` later read the sizes and error bits (the sampler's errors are raised
+    there, after a forward that ran on the flawed lists -- its gathers are range-checked, so
+    it reads nothing outside the tables)."""
     fanouts = tuple(int(k) for k in fanouts)
     if not fanouts or min(fanouts) < 1:
         raise ValueError("fanouts must hold at least one positive neighbour count")
@@ -252,29 +283,44 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
                                      (P * max(1, L - 1))(*ptr[3 * L - 2:4 * L - 3]), ptr[-1],
                                      ws.data_ptr(), ws.numel(), _lib.stream_handle(dev)),
                "gnn_sample_layers")
-    host = _stat_host(L + 1)
-    host.copy_(buf[offs[-1]:offs[-1] + L + 1], non_blocking=True)  # pinned: no staging copy
-    torch.cuda.current_stream(dev).synchronize()  # the one host synchronisation
-    st = host.tolist()  # every layer size + the error bits
-    sizes, e = st[:L], int(st[L]) & 0xFFFFFFFF
-    _raise_sample_error(e & 3)  # the sampler's own errors first, as the step-by-step path
-    if e & 8:
-        raise IndexError("sample_batch: a sampled id outside the graph reached the frontier")
-    if e & 4:
-        raise RuntimeError("sample_batch: a frontier outgrew its buffer (internal bound error)")
-    if e & 16:
-        raise RuntimeError("sample_batch: the frontier scan's look-back did not complete "
-                           "(internal error)")
     widths = [k + (1 if gcn else 0) for k in fanouts]
 
     def view(o, rows, w=0):
         return buf.as_strided((rows, w) if w else (rows,), (w, 1) if w else (1,), o)
 
-    layers = [seeds] + [view(offs[i - 1], sizes[i]) for i in range(1, L)]
-    nbrs_last = view(offs[2 * L - 2], sizes[L - 1], widths[L - 1])
-    cmaps = [view(offs[2 * L - 1 + i], sizes[i]) for i in range(L - 1)]
-    nmaps = [view(offs[3 * L - 2 + i], sizes[i], widths[i]) for i in range(L - 1)]
-    return SampledBatch(seeds, layers[-1], nbrs_last, cmaps[::-1], nmaps[::-1], tuple(layers))
+    def build(sizes, live=(), finish=None):
+        layers = [seeds] + [view(offs[i - 1], sizes[i]) for i in range(1, L)]
+        nbrs_last = view(offs[2 * L - 2], sizes[L - 1], widths[L - 1])
+        cmaps = [view(offs[2 * L - 1 + i], sizes[i]) for i in range(L - 1)]
+        nmaps = [view(offs[3 * L - 2 + i], sizes[i], widths[i]) for i in range(L - 1)]
+        for i in range(1, L - 1) if live else ():  # rows of map i = |S_i| (i = 0: the seeds)
+            cmaps[i]._gnn_live = live[i]
+            nmaps[i]._gnn_live = live[i]
+        return SampledBatch(seeds, layers[-1], nbrs_last, cmaps[::-1], nmaps[::-1],
+                            tuple(layers), tuple(live), finish)
+
+    def finish():
+        host = _stat_host(L + 1)
+        host.copy_(buf[offs[-1]:offs[-1] + L + 1], non_blocking=True)  # pinned: no staging
+        torch.cuda.current_stream(dev).synchronize()  # the one host synchronisation
+        st = host.tolist()  # every layer size + the error bits
+        sizes, e = st[:L], int(st[L]) & 0xFFFFFFFF
+        _raise_sample_error(e & 3)  # the sampler's own errors first, as the step-by-step path
+        if e & 8:
+            raise IndexError("sample_batch: a sampled id outside the graph reached the frontier")
+        if e & 4:
+            raise RuntimeError("sample_batch: a frontier outgrew its buffer (internal bound "
+                               "error)")
+        if e & 16:
+            raise RuntimeError("sample_batch: the frontier scan's look-back did not complete "
+                               "(internal error)")
+        return build(sizes)
+
+    if sync:
+        return finish()
+    stat = offs[-1]
+    live = [None] + [buf[stat + i:stat + i + 1] for i in range(1, L)]
+    return build(caps, live, finish)
 
 
 _BATCH_PLAN = {}

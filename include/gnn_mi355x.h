@@ -372,6 +372,15 @@ int gnn_linear_relu_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, 
                         int64_t fout, float* y, int64_t ldy, void* stream);
 
 /*
+ * gnn_linear_relu_f32 over rows [0, min(*live, n_rows)) only: *live is a DEVICE int64 (a
+ * frontier size written by gnn_sample_layers, never read back by the host), n_rows the
+ * capacity of x / y. Rows from *live on are neither read nor written. live must not be NULL.
+ */
+int gnn_linear_relu_live_f32(const float* x, int64_t ldx, int64_t n_rows, const int64_t* live,
+                             int64_t k, const float* w, int64_t fout, float* y, int64_t ldy,
+                             void* stream);
+
+/*
  * The last SageLayer with the GraphSAGE classifier fused into its epilogue:
  *   y = max(x @ w^T, 0)                      GraphSAGE/GraphSAGE.py:18-20 (the embedding)
  *   logits[n, c] = y[n, :] . wd[c, :] + bd[c]  GraphSAGE.py:51-52 (self.dense, nn.Linear)
@@ -656,6 +665,17 @@ int gnn_sage_gather_concat_f32(const float* table, int64_t ldt, int64_t n_table,
                                int64_t M, int64_t k, int64_t feat, int32_t mode, float* self_out,
                                int64_t ld_self, float* out, int64_t ldo, int32_t* err_flag,
                                void* stream);
+
+/*
+ * gnn_sage_gather_concat_f32 over rows [0, min(*live, M)) (live: a DEVICE int64 row count,
+ * NULL = M): a sampled batch's layer runs on its buffers' capacity M without the host reading
+ * the frontier size first. Rows from *live on are neither read nor written.
+ */
+int gnn_sage_gather_concat_live_f32(const float* table, int64_t ldt, int64_t n_table,
+                                    const int64_t* self_idx, const int64_t* idx, int64_t ldi,
+                                    int64_t M, const int64_t* live, int64_t k, int64_t feat,
+                                    int32_t mode, float* self_out, int64_t ld_self, float* out,
+                                    int64_t ldo, int32_t* err_flag, void* stream);
 
 /*
  * One fused GraphSAGE inference layer (MEAN, not gcn):

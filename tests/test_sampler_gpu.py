@@ -377,3 +377,67 @@ def test_degree_ordered_keeps_edge_values(dev):
     assert sorted(zip(rows2.tolist(), c2.tolist(), v2.tolist())) == want
     for r in range(0, adj.n_rows, 97):                               # ascending neighbours
         assert np.all(np.diff(c2[rp2[r]:rp2[r + 1]]) > 0)
+
+
+@pytest.mark.parametrize("fanouts,F,H", [((25, 10), 128, 128), ((10, 5, 3), 64, 128),
+                                         ((25, 10), 32, 16)])
+def test_pending_batch_forward_equals_synced(dev, fanouts, F, H):
+    """sample_batch(..., sync=False): no host read between the sampler and the forward (the
+    layer sizes stay on the device, the fused concat gather and MFMA GEMM read them); the
+    embeddings and logits equal the synced batch's bit for bit, for the fused shapes
+    (F = 128 / 64 -> H = 128) and for a shape the live path hands back to the host (F = 32),
+    and sync() returns the synced batch's tensors."""
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    from graphneuralnetwork_amd.sampler import sample_batch
+    adj = _adj(dev, n=40000, e=300000, seed=4)
+    deg = (adj.rowptr[1:] - adj.rowptr[:-1]).cpu().numpy()
+    seeds = torch.from_numpy(np.nonzero(deg > 0)[0][:700]).to(dev)
+    table = torch.randn(adj.n_rows, F, device=dev)
+    net = GraphSAGE(len(fanouts), F, H, False, agg_func="MEAN", Unsupervised=False,
+                    class_size=3).to(dev).eval()
+    a = sample_batch(adj, seeds, fanouts, seed=11)
+    p = sample_batch(adj, seeds, fanouts, seed=11, sync=False)
+    assert p.pending and not a.pending
+    assert p.frontier.numel() >= a.frontier.numel()  # the buffer at its capacity
+    with torch.no_grad():
+        e1, c1 = net(*a.forward_args(table), None, None, None, None, None)
+        e2, c2 = net(*p.forward_args(table), None, None, None, None, None)
+    assert torch.equal(e1, e2) and torch.equal(c1, c2)
+    s = p.sync()
+    assert not s.pending and s.layer_sizes == a.layer_sizes
+    assert torch.equal(s.frontier, a.frontier) and torch.equal(s.frontier_nbrs, a.frontier_nbrs)
+    for xs, ys in ((s.center_maps, a.center_maps), (s.neigh_maps, a.neigh_maps)):
+        for x, y in zip(xs, ys):
+            assert torch.equal(x, y)
+    assert p.sampled_edges == a.sampled_edges
+    # the non-fused paths (autograd, MAX) read the sizes back and slice: same results
+    net.agg_func = "MAX"
+    with torch.no_grad():
+        e3, _ = net(*a.forward_args(table), None, None, None, None, None)
+        e4, _ = net(*sample_batch(adj, seeds, fanouts, seed=11, sync=False).forward_args(table),
+                    None, None, None, None, None)
+    assert torch.equal(e3, e4)
+
+
+def test_pending_batch_errors_raise_at_check(dev):
+    """A pending batch with a sampler error (a seed without neighbours, an id out of range):
+    the forward runs on the flawed lists without faulting (its gathers are range-checked) and
+    check() raises the error sample_batch(..., sync=True) raises."""
+    from graphneuralnetwork_amd.graph import CsrGraph
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    from graphneuralnetwork_amd.sampler import sample_batch
+    rowptr = torch.tensor([0, 2, 3, 3], dtype=torch.int64, device=dev)
+    col = torch.tensor([1, 0, 0], dtype=torch.int32, device=dev)
+    g = CsrGraph(rowptr, col, torch.ones(3, device=dev), 3, 3)
+    table = torch.randn(3, 64, device=dev)
+    net = GraphSAGE(2, 64, 128, False, agg_func="MEAN", Unsupervised=False,
+                    class_size=3).to(dev).eval()
+    for seeds, match in (([0, 2], "empty sequence"), ([7, 0], "out of range")):
+        p = sample_batch(g, torch.tensor(seeds, device=dev), (4, 2), sync=False)
+        with torch.no_grad():
+            net(*p.forward_args(table), None, None, None, None, None)
+        with pytest.raises(IndexError, match=match):
+            p.check()
+    torch.cuda.synchronize()
+    ok = sample_batch(g, torch.tensor([0, 1], device=dev), (4, 2), sync=False)
+    ok.check()
