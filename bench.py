@@ -923,6 +923,15 @@ def run_sage(args, dev, rank: int = 0, world: int = 1, edges_np=None):
             log(f"[bench] graph capture of the aggregation failed: {e!r}")
         smp_ms, _ = time_steps(lambda: sample_batch(adj, seeds, (25, 10), seed=sample_seed),
                                args.steps, args.warmup, dev)
+        # the same call with the sizes left on the device (the batch path below): its three
+        # kernels and their enqueue, without the host read
+        smp_pending = []
+        smp_pending_ms, _ = time_steps(
+            lambda: smp_pending.append(sample_batch(adj, seeds, (25, 10), seed=sample_seed,
+                                                    sync=False)), args.steps, args.warmup, dev)
+        for b in smp_pending:
+            b.check()
+        del smp_pending
 
         def batch_step_synced():  # sampling (sizes read back) + the forward
             b = sample_batch(adj, seeds, (25, 10), seed=sample_seed)
@@ -988,6 +997,7 @@ def run_sage(args, dev, rank: int = 0, world: int = 1, edges_np=None):
            "batch_ms_note": "sample_batch(sync=False) + forward: the layer sizes stay on the "
                             "device, every batch's error word is read after the timed steps",
            "batch_synced_ms": statistics.median(batch_synced_ms),
+           "sample_pending_ms": statistics.median(smp_pending_ms),
            "median_step_ms": statistics.median(fwd_ms),
            "forward_hipgraph_ms": graph_ms,
            "first_sample_s": t_sample,
@@ -1592,8 +1602,8 @@ def _sub(res: dict) -> dict:
             "cache_cold_median_step_ms", "dtype",
             "config", "roofline", "cpu_baseline", "cpu_reference_ops",
             "first_step_s", "graph_build_s", "gcn_layer_ms", "layer_ms", "aggregate_ms",
-            "forward_ms", "forward_hipgraph_ms", "sample_ms", "batch_ms", "batch_ms_note",
-            "batch_synced_ms", "project_ms",
+            "forward_ms", "forward_hipgraph_ms", "sample_ms", "sample_pending_ms", "batch_ms",
+            "batch_ms_note", "batch_synced_ms", "project_ms",
             "project_tflops", "project_arithmetic", "train_step", "gcn_model_forward",
             "aggregators")
     return {k: res[k] for k in keep if k in res}

@@ -192,17 +192,22 @@ __global__ void batch_init_kernel(int64_t* __restrict__ stat, int n_layers, int6
 // ---- the 3-launch L-hop batch (gnn_sample_layers) -------------------------------------------
 // The frontier marks are byte flags (flags[v] = 1, plain stores: idempotent, no atomics), set by
 // the hop's sampling kernel itself. One scan kernel per hop transition turns them into the
-// frontier: a workgroup per tile of 1024 words (32 flags per word); each tile publishes its
+// frontier: a workgroup per tile of 512 words (32 flags per word); each tile publishes its
 // count in ONE 8-byte agent-scope atomic word {tag, kind, value} and takes as its prefix the
 // sum of every earlier tile's count (independent loads, no chain); it writes the frontier ids, the word
 // prefixes / bitmaps the position lookups need, and clears the flags it read (the workspace
 // is left all-zero for the next call: no memset). The next hop's sampling kernel also ranks the
 // previous hop's lists (its extra workgroups) and derives the previous hop's sampler errors.
 // For L = 2 ([25, 10]): sample + mark, scan + emit, sample + rank = 3 launches.
-// 256 threads x 4 words (1024 x 8, 39 tiles at 10M nodes, was slower: 0.107 vs 0.083 ms per
-// cfg4 batch -- the dense hub tiles' emission on few workgroups)
+// 8192-word tiles (1024 threads x 8 words, 39 tiles at 10M nodes) were slower: 0.107 vs 0.083 ms per
+// cfg4 batch (the dense hub tiles' emission on few workgroups)
+#ifndef GNN_SCAN_WPT
+// words per thread: 512-word tiles (611 at 10M nodes); in one process 4 / 2 / 1 words gave
+// 57.1 / 55.4 / 61.8 us per pending cfg4 batch (profiles/r05s_scan_wpt_ab.log)
+#define GNN_SCAN_WPT 2
+#endif
 constexpr int kScanThreads = 256;
-constexpr int kScanWpt = 4;  // words per thread
+constexpr int kScanWpt = GNN_SCAN_WPT;  // words per thread
 constexpr int kScanWaves = kScanThreads / 64;
 constexpr int kScanTileWords = kScanThreads * kScanWpt;
 constexpr uint64_t kTileAgg = 1;  // kind of a published tile count

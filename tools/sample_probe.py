@@ -3,7 +3,7 @@ degree order, as bench.py run_sage): the fused sample_batch and the hop-by-hop p
 around each call, plus the host wall time per call. Run under rocprofv3 --kernel-trace --stats
 for the per-kernel split.
 
-    python tools/sample_probe.py [--reps 20] [--libs noticket,noemit]
+    python tools/sample_probe.py [--reps 20] [--libs wpt1,wpt2]
 """
 from __future__ import annotations
 
@@ -41,11 +41,23 @@ def main():
     cand = torch.nonzero(adj.rowptr[1:] > adj.rowptr[:-1]).view(-1)
     seeds = cand[torch.randperm(cand.numel(), device=dev, generator=gen)[:8192]]
     out = {}
-    runs = [("fused", sample_batch, None), ("stepwise", sample_batch_stepwise, None)]
-    runs += [(f"fused_{t}", sample_batch, LIB_DIR / "variants" / f"libgnn_{t}.so")
-             for t in a.libs.split(",") if t]
+    from graphneuralnetwork_amd import sampler as S
+
+    def pending(*args, **kw):  # the sizes left on the device: the kernels' own time
+        return sample_batch(*args, sync=False, **kw)
+
+    runs = [("fused", sample_batch, None), ("stepwise", sample_batch_stepwise, None),
+            ("fused_pending", pending, None)]
+    for t in a.libs.split(","):
+        if t:
+            lib = LIB_DIR / "variants" / f"libgnn_{t}.so"
+            runs += [(f"fused_{t}", sample_batch, lib), (f"fused_pending_{t}", pending, lib)]
+    ref = sample_batch(adj, seeds, (25, 10), seed=0)
     for name, fn, lib in runs:
         _lib.use_variant(lib)
+        S._SAMPLE_WS.clear()  # a variant's scan may size its workspace differently
+        b = fn(adj, seeds, (25, 10), seed=0).sync()
+        assert torch.equal(b.frontier, ref.frontier) and torch.equal(b.neigh_map, ref.neigh_map)
         for _ in range(3):
             fn(adj, seeds, (25, 10), seed=0)
         torch.cuda.synchronize()
@@ -62,6 +74,7 @@ def main():
         out[name] = {"event_ms": round(statistics.median(ev), 4),
                      "wall_ms": round(statistics.median(wall), 4)}
     _lib.use_variant(None)
+    S._SAMPLE_WS.clear()
     print(json.dumps(out), flush=True)
 
 
