@@ -634,7 +634,7 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
     through GATBase._heads: one X W GEMM for all heads, the fused edge-softmax aggregation with
     ELU; GAT/train_eval.py:75-76's loss.backward()): forward + backward with W, a_src, a_dst
     requiring grad (X is the input features). The backward's HIP passes (csrc/gat_bwd.hip:
-    the row pass with the prep fused in, the recomputing node pass over A^T; replacing the
+    the coalesced prep + the row pass, the recomputing node pass over A^T; replacing the
     autograd of GAT/models/layers.py:22-37 and SpecialSpmmFunction.backward :54-64) are also
     timed alone, each with a roofline on its compulsory bytes."""
     from graphneuralnetwork_amd.gat import GAT
@@ -680,8 +680,9 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
     what = {"prep": "gat_bwd_prep_kernel: dout = dy ELU'(out), D = dout . out",
             "edges": "gat_bwd_edge_kernel (+ del fix-up): SDDMM g = dout_i . Wh_j, edge weights "
                      "w_ij and softmax/LeakyReLU gradients ds_ij written per (edge, head)",
-            "rows": "gat_bwd_rows_kernel (+ del fix-up): prep fused (dout, D_i), SDDMM g = "
-                    "dout_i . Wh_j and ds_ij summed into del_i; per-row record {el, lse, D}",
+            "rows": "gat_bwd_prep_rec_kernel (dout, D_i and the per-(row, head) record {el, "
+                    "lse, D}, coalesced) + gat_bwd_rows_kernel (+ del fix-up): SDDMM g = "
+                    "dout_i . Wh_j and ds_ij summed into del_i",
             "nodes": ("gat_bwd_node_r_kernel (+ fix-up) over A^T (A itself when symmetric): "
                       "a_ij, g_ij, w_ij, ds_ij recomputed from the gathered dout_i and {el, lse, "
                       "D}_i; dWh_j = sum_i w_ij dout_i + der_j a_dst + del_j a_src") if two_pass
@@ -700,8 +701,9 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
            "step_ms": statistics.median(step_ms), "forward_ms": statistics.median(fwd_ms),
            "backward_ms": statistics.median(bwd_ms),
            "edges_per_s": nnz / (statistics.median(step_ms) / 1e3),
-           "forward_path": "torch.mm (X W, autograd) + gat_logits + gat_aggregate with per-row "
-                           "log-sum-exp stats (hub-staged Wh / er)",
+           "forward_path": "X W on the MFMA transform (_ProjectFn) + gat_logits + the edge-head "
+                           "gat_aggregate (er from the gathered rows) with per-row log-sum-exp "
+                           "stats",
            "backward_kernels": kernels,
            "compulsory_bytes_model": ({
                "rows": "4 nnz + N (8 + 12 H Fh + 28 H) + N (4 H + 4 H Fh): y, dy, el, lse, "

@@ -561,9 +561,18 @@ struct BwdRowParams {
 // dout_i = dy_i ELU'(out_i) into LDS (and HBM: by a long row's first segment only), the
 // products dout . out into LDS, D_i per head summed from them. Edges (lanes = (edge slot,
 // head), HP heads per pass): ds_ij as gat_bwd_edge_kernel, summed into del_i (segments: partials).
+// Edges in flight per lane: row pass 2 (4: 1.18 vs 0.85 ms at cfg3), node pass 2 (4 / 8:
+// 1.097 / 1.397 vs 1.047 ms), profiles/r05r2_gat_bwd_u_drop_ab.log. A row-pass instance
+// without the dropout-mask code took 88 instead of 78 VGPRs and was slower (0.928 vs 0.847 ms).
+#ifndef GNN_BWD_ROW_U
+#define GNN_BWD_ROW_U 2
+#endif
+#ifndef GNN_BWD_NODE_U
+#define GNN_BWD_NODE_U 2
+#endif
 template <int VW, int NFV, bool PREP, bool REC>
 __global__ __launch_bounds__(kBw) void gat_bwd_rows_kernel(BwdRowParams P) {
-  constexpr int U = 2;
+  constexpr int U = GNN_BWD_ROW_U;
   // PREP = false: dout and the {el, lse, D} records came from gat_bwd_prep_rec_kernel
   __shared__ float lds[kBwWaves][PREP ? kRowLds : 1];
   const int lane = threadIdx.x & (kWave - 1);
@@ -781,7 +790,7 @@ struct BwdNodeRParams {
 template <int VW, int LPR, int NCH, bool DROP>
 __global__ __launch_bounds__(kBw) void gat_bwd_node_r_kernel(BwdNodeParams P, BwdNodeRParams R) {
   constexpr int EPI = kWave / LPR;
-  constexpr int U = 4;
+  constexpr int U = GNN_BWD_NODE_U;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = static_cast<int64_t>(blockIdx.x) * kBwWaves + (threadIdx.x >> 6);
   const int sub = lane & (LPR - 1);
