@@ -36,7 +36,9 @@ constexpr int kSageBlock = 256;
 #endif
 constexpr int kSageWaves = kSageBlock / kWave;
 
-enum SageMode : int32_t { kMean = 0, kArgmax = 1, kSum = 2, kMaxPool = 3 };
+// kArgmaxF: the argmax index stored as fp32 (exact below 2^24) -- what the SageLayer's
+// torch.cat([self_feats, argmax]) promotes it to (GraphSAGE/GraphSAGE.py:17, graph_utils.py:8)
+enum SageMode : int32_t { kMean = 0, kArgmax = 1, kSum = 2, kMaxPool = 3, kArgmaxF = 4 };
 
 // torch.max's value rule: a NaN on either side wins, else the larger value
 __device__ __forceinline__ float nanmax(float a, float b) { return (a > b || a != a) ? a : b; }
@@ -178,7 +180,13 @@ __global__ __launch_bounds__(kSageBlock) void sage_aggregate_kernel(
   for (int ch = 0; ch < NCH; ++ch) {
     const int64_t f = static_cast<int64_t>(ch * LPR + sub) * VW;
     if (f >= feat) continue;
-    if (MODE != kArgmax) {
+    if (MODE == kArgmaxF) {
+      typename Vec<VW>::T r;
+#pragma unroll
+      for (int i = 0; i < VW; ++i)
+        vset(r, i, arg[ch][i] == 0x7fffffff ? 0.f : static_cast<float>(arg[ch][i]));
+      vstore<VW>(static_cast<float*>(out) + m * ldo + f, r);
+    } else if (MODE != kArgmax) {
       // torch.mean: sum / k;  torch.sum: the sum;  torch.max(...).values: the max
       typename Vec<VW>::T r = MODE == kMean ? acc[ch] / static_cast<float>(k) : acc[ch];
       vstore<VW>(static_cast<float*>(out) + m * ldo + f, r);
@@ -285,6 +293,8 @@ static int run_sage(SageArgs a, int32_t mode, bool vec4) {
       rc = vec4 ? dispatch_sage<4, kSum, GATHER>(a) : dispatch_sage<1, kSum, GATHER>(a);
     else if (mode == kMaxPool)
       rc = vec4 ? dispatch_sage<4, kMaxPool, GATHER>(a) : dispatch_sage<1, kMaxPool, GATHER>(a);
+    else if (mode == kArgmaxF)
+      rc = vec4 ? dispatch_sage<4, kArgmaxF, GATHER>(a) : dispatch_sage<1, kArgmaxF, GATHER>(a);
     else
       rc = vec4 ? dispatch_sage<4, kArgmax, GATHER>(a) : dispatch_sage<1, kArgmax, GATHER>(a);
     if (rc != GNN_OK) return rc;
@@ -315,7 +325,7 @@ extern "C" int gnn_sage_gather_aggregate_f32(const float* table, int64_t ldt, in
                                              int64_t feat, int32_t mode, void* out, int64_t ldo,
                                              int32_t* err_flag, void* stream) {
   if (M < 0 || k < 0 || feat < 0 || n_table < 0 || (mode < kMean || mode > kMaxPool))
-    return GNN_E_ARG;
+    return GNN_E_ARG;  // GNN_SAGE_ARGMAX_F32: the concat entries only
   if (M == 0 || feat == 0) return GNN_OK;
   if (!table || !idx || !out || !err_flag || ldt < feat || ldo < feat || ldi < k) return GNN_E_ARG;
   if (k == 0) return GNN_E_UNSUPPORTED;
@@ -368,7 +378,8 @@ extern "C" int gnn_sage_gather_concat_live_f32(const float* table, int64_t ldt, 
                                                int64_t k, int64_t feat, int32_t mode,
                                                float* self_out, int64_t ld_self, float* out,
                                                int64_t ldo, int32_t* err_flag, void* stream) {
-  if (M < 0 || k < 0 || feat < 0 || n_table < 0 || !(mode == kMean || mode == kSum || mode == kMaxPool))
+  if (M < 0 || k < 0 || feat < 0 || n_table < 0 ||
+      !(mode == kMean || mode == kSum || mode == kMaxPool || mode == kArgmaxF))
     return GNN_E_ARG;
   if (M == 0 || feat == 0) return GNN_OK;
   if (!table || !self_idx || !idx || !self_out || !out || !err_flag || ldt < feat ||

@@ -247,8 +247,13 @@ class SageLayer(nn.Module):
         return torch._addmm_activation(part, aggregate_feats, W[:, n:].t())
 
 
-def _fused_sage_layer(block, center, neigh: Gathered, dense: nn.Linear | None = None):
+def _fused_sage_layer(block, center, neigh: Gathered, dense: nn.Linear | None = None,
+                      agg: str = 'MEAN'):
     """Inference SageLayer on a (table, index map) aggregate.
+
+    ``agg`` 'MAX' / 'MAXPOOL' (centre and neighbours Gathered from one table): the concat
+    launch writes the argmax index as fp32 (the value torch.cat([self, argmax]) promotes it
+    to) / the value max-pool into the [self | agg] buffer, then the same GEMM.
 
     Covered shapes (``ops.sage_layer``): ONE launch gathers the centre rows and the
     neighbour mean into an LDS tile and multiplies it by W on the matrix cores, ReLU fused.
@@ -277,7 +282,7 @@ def _fused_sage_layer(block, center, neigh: Gathered, dense: nn.Linear | None = 
     else:
         self_src, self_idx, trusted = center, None, True
     y = None
-    if live is None:
+    if live is None and agg == 'MEAN':
         y = sage_layer(neigh.table, neigh.index, block.weight.weight, self_src, self_idx,
                        check=not (trusted and neigh.trusted))
     if y is not None:
@@ -286,7 +291,7 @@ def _fused_sage_layer(block, center, neigh: Gathered, dense: nn.Linear | None = 
     dev = neigh.table.device
     buf = torch.empty((M, 2 * n), dtype=torch.float32, device=dev)
     if live is not None:
-        sage_gather_concat(neigh.table, center.index, neigh.index, "MEAN",
+        sage_gather_concat(neigh.table, center.index, neigh.index, agg,
                            check=not (center.trusted and neigh.trusted), out=buf, live=live)
         y = gcn_transform(buf, block.weight.weight, relu=True, live=live)
         if y is not None:
@@ -296,7 +301,7 @@ def _fused_sage_layer(block, center, neigh: Gathered, dense: nn.Linear | None = 
         M = buf.shape[0]
     elif isinstance(center, Gathered) and center.table is neigh.table:
         # both halves of cat[self, agg] in one launch (gnn_sage_gather_concat_f32)
-        sage_gather_concat(neigh.table, center.index, neigh.index, "MEAN",
+        sage_gather_concat(neigh.table, center.index, neigh.index, agg,
                            check=not (center.trusted and neigh.trusted), out=buf)
     else:
         if isinstance(center, Gathered):
@@ -342,8 +347,14 @@ class GraphSAGE(nn.Module):
         if not Unsupervised:
             self.dense = nn.Linear(out_size, class_size)
 
-    def _fused_ok(self, block) -> bool:
-        return not torch.is_grad_enabled() and self.agg_func == 'MEAN' and not block.gcn
+    def _fused_ok(self, block, center, neigh) -> bool:
+        if torch.is_grad_enabled() or block.gcn or not isinstance(neigh, Gathered):
+            return False
+        if self.agg_func == 'MEAN':
+            return True
+        # MAX / MAXPOOL: the one-launch concat form (centre and neighbours from one table)
+        return (self.agg_func in ('MAX', 'MAXPOOL') and isinstance(center, Gathered)
+                and center.table is neigh.table and neigh.table.dtype == torch.float32)
 
     def forward(self, center_feats_data, center_nodes_map, center_neigh_feats_data, center_neigh_nodes_map,
                 contexts_negatives_feats_data, contexts_negatives_nodes_map, contexts_negatives_neigh_feats_data,
@@ -353,10 +364,10 @@ class GraphSAGE(nn.Module):
             neigh = center_neigh_feats_data    # [M, k, F] tensor, or Gathered (table, [M, k] index)
             feats_data = classes = None
             for i, block in enumerate(self.sage_blocks):
-                if isinstance(neigh, Gathered) and self._fused_ok(block):
+                if self._fused_ok(block, center, neigh):
                     last = i == self.num_layers - 1 and not self.Unsupervised
                     feats_data = _fused_sage_layer(block, center, neigh,
-                                                   self.dense if last else None)
+                                                   self.dense if last else None, self.agg_func)
                     if isinstance(feats_data, tuple):  # the classifier ran in the epilogue
                         feats_data, classes = feats_data
                 else:

@@ -1072,9 +1072,12 @@ def sage_gather_concat(table: torch.Tensor, self_idx: torch.Tensor, idx: torch.T
     (gnn_sage_gather_concat_f32): the SageLayer input of GraphSAGE/GraphSAGE.py:17 with the
     gathers of :47-49. ``out`` may be any [M, 2F] float32 view with unit column stride.
     ``live``: a device int64 scalar; rows [0, min(live, M)) only (gnn_sage_gather_concat_live_f32,
-    M = the capacity of a sampled batch whose frontier size the host never read)."""
-    if agg_func not in ("MEAN", "SUM", "MAXPOOL"):
+    M = the capacity of a sampled batch whose frontier size the host never read).
+    'MAX' (torch.argmax over the neighbours, graph_utils.py:8): the index written as fp32, the
+    value torch.cat([self, argmax]) promotes it to (GNN_SAGE_ARGMAX_F32)."""
+    if agg_func not in ("MEAN", "SUM", "MAXPOOL", "MAX"):
         raise RuntimeError(f"agg_func {agg_func!r} has no concat form")
+    mode = 4 if agg_func == "MAX" else SAGE_KINDS[agg_func]
     _require_device(table, self_idx, idx, out)
     table = _rows_f32(table, "table")
     if idx.dim() != 2:
@@ -1106,7 +1109,7 @@ def sage_gather_concat(table: torch.Tensor, self_idx: torch.Tensor, idx: torch.T
     lib = _lib.load()
     _lib.check(lib.gnn_sage_gather_concat_live_f32(
         table.data_ptr(), table.stride(0), table.shape[0], self_idx.data_ptr(), idx.data_ptr(),
-        idx.stride(0), M, _lib.ptr(live), k, F, SAGE_KINDS[agg_func], out.data_ptr(),
+        idx.stride(0), M, _lib.ptr(live), k, F, mode, out.data_ptr(),
         out.stride(0), out[:, F:].data_ptr(), out.stride(0), err.data_ptr(),
         _lib.stream_handle(table.device)), "gnn_sage_gather_concat_live_f32")
     if check:

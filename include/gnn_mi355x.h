@@ -629,6 +629,9 @@ int gnn_gat_backward_nodes_recompute_f32(
                              GraphSAGE_Pytorch/models/Aggregator.py:23-24 reaches for
                              (there it gets the namedtuple and fails). A NaN in the
                              slice propagates.                                       */
+#define GNN_SAGE_ARGMAX_F32 4 /* the GNN_SAGE_ARGMAX index stored as fp32 (exact below
+                             2^24): the SageLayer's torch.cat([self, argmax]) promotion,
+                             GraphSAGE/GraphSAGE.py:17 -- gnn_sage_gather_concat_* only */
 
 /*
  * GraphSAGE Aggregator over a pre-gathered neighbour tensor
@@ -659,6 +662,7 @@ int gnn_sage_gather_aggregate_f32(const float* table, int64_t ldt, int64_t n_tab
  *   out[m, :]      = reduce_j table[idx[m * ldi + j], :]   (mode GNN_SAGE_MEAN / SUM / MAXPOOL)
  * self_out and out may be the two column halves of one [M, 2F] buffer. An index outside
  * [0, n_table) sets *err_flag |= 1 and reads nothing. k == 0 -> GNN_E_UNSUPPORTED.
+ * mode GNN_SAGE_ARGMAX_F32: out holds the argmax index as fp32 (the cat's promotion).
  */
 int gnn_sage_gather_concat_f32(const float* table, int64_t ldt, int64_t n_table,
                                const int64_t* self_idx, const int64_t* idx, int64_t ldi,

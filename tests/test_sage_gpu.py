@@ -408,3 +408,57 @@ def test_gather_concat_matches_separate_launches(dev, F, agg):
     bad[17] = n
     with pytest.raises(IndexError):
         sage_gather_concat(T, bad, I, agg)
+
+
+@pytest.mark.parametrize("F", [64, 128, 600])
+def test_gather_concat_argmax_as_float(dev, F):
+    """GNN_SAGE_ARGMAX_F32: the concat launch's second half is torch.argmax's int64 index
+    (graph_utils.py:8) as fp32 -- what torch.cat([self_feats, argmax]) promotes it to
+    (GraphSAGE.py:17) -- bit for bit, incl. NaN-first and first-of-equal ties."""
+    from graphneuralnetwork_amd.ops import gather_rows, sage_gather_aggregate, sage_gather_concat
+    rng = np.random.default_rng(F + 1)
+    n, M, k = 3000, 1200, 10
+    table = rng.standard_normal((n, F)).astype(np.float32)
+    table[5, :] = np.nan
+    table[6, :] = table[7, :]
+    idx = rng.integers(0, n, (M, k))
+    idx[0, 3] = 5
+    idx[1, 2], idx[1, 6] = 6, 7
+    sid = rng.integers(0, n, M)
+    T, I, S = (torch.from_numpy(a).to(dev) for a in (table, idx, sid))
+    got = sage_gather_concat(T, S, I, "MAX")
+    same = dict(rtol=0, atol=0, equal_nan=True)  # bit for bit; the NaN row may be a centre
+    torch.testing.assert_close(got[:, :F], gather_rows(T, S), **same)
+    arg = sage_gather_aggregate(T, I, "MAX")
+    assert arg.dtype == torch.int64
+    assert torch.equal(got[:, F:], arg.to(torch.float32))
+    assert torch.equal(arg[0], torch.full_like(arg[0], 3))  # NaN first
+    ref = torch.cat([T[S], torch.argmax(T[I], dim=1)], dim=1)  # the reference's promotion
+    torch.testing.assert_close(got, ref, **same)
+
+
+@pytest.mark.parametrize("agg", ["MAX", "MAXPOOL"])
+def test_fused_max_layers_vs_oracle(dev, agg):
+    """MAX / MAXPOOL inference on Gathered maps runs the one-launch concat + MFMA GEMM (with
+    the classifier epilogue); one layer on a sampled batch against the numpy oracle
+    (GraphSAGE/GraphSAGE.py:38-53, graph_utils.py:7-8; one layer: the argmax decisions are
+    over the table's own values, so the oracle's float64 and the device's fp32 agree)."""
+    from graphneuralnetwork_amd.graphsage import GraphSAGE
+    from graphneuralnetwork_amd.sampler import sample_batch
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    from graphneuralnetwork_amd.sampler import symmetric_adjacency
+    n, F, H = 20000, 128, 128
+    s, d = rmat_edges(n, 200000, 4)
+    adj = symmetric_adjacency(s, d, n, device=dev)
+    deg = (adj.rowptr[1:] - adj.rowptr[:-1]).cpu().numpy()
+    seeds = torch.from_numpy(np.flatnonzero(deg > 0)[:2048]).to(dev)
+    batch = sample_batch(adj, seeds, (10,), seed=5)
+    table = torch.randn(n, F, device=dev, generator=torch.Generator(dev).manual_seed(6))
+    torch.manual_seed(1)
+    net = GraphSAGE(1, F, H, False, agg_func=agg, Unsupervised=False, class_size=3).to(dev).eval()
+    with torch.no_grad():
+        assert net._fused_ok(net.sage_blocks[0], *batch.forward_args(table)[::2])
+        emb, logits = net(*batch.forward_args(table), None, None, None, None, None)
+    ref_emb, ref_logits = _sage_net_oracle(net, table, batch, agg)
+    close(emb.cpu().numpy(), ref_emb)
+    close(logits.cpu().numpy(), ref_logits)

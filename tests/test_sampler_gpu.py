@@ -410,13 +410,15 @@ def test_pending_batch_forward_equals_synced(dev, fanouts, F, H):
         for x, y in zip(xs, ys):
             assert torch.equal(x, y)
     assert p.sampled_edges == a.sampled_edges
-    # the non-fused paths (autograd, MAX) read the sizes back and slice: same results
-    net.agg_func = "MAX"
-    with torch.no_grad():
-        e3, _ = net(*a.forward_args(table), None, None, None, None, None)
-        e4, _ = net(*sample_batch(adj, seeds, fanouts, seed=11, sync=False).forward_args(table),
-                    None, None, None, None, None)
-    assert torch.equal(e3, e4)
+    # the fused MAX / MAXPOOL layers run on the device sizes too; the non-fused path
+    # (autograd) reads the sizes back and slices: same results as the synced batch
+    for agg, grad in (("MAX", False), ("MAXPOOL", False), ("MEAN", True)):
+        net.agg_func = agg
+        with torch.set_grad_enabled(grad):
+            e3, _ = net(*a.forward_args(table), None, None, None, None, None)
+            e4, _ = net(*sample_batch(adj, seeds, fanouts, seed=11, sync=False).forward_args(table),
+                        None, None, None, None, None)
+        assert torch.equal(e3, e4)
 
 
 def test_pending_batch_errors_raise_at_check(dev):
