@@ -462,3 +462,33 @@ def test_fused_max_layers_vs_oracle(dev, agg):
     ref_emb, ref_logits = _sage_net_oracle(net, table, batch, agg)
     close(emb.cpu().numpy(), ref_emb)
     close(logits.cpu().numpy(), ref_logits)
+
+
+def test_live_entries_touch_only_live_rows(dev):
+    """gnn_sage_gather_concat_live_f32 / gnn_linear_relu_live_f32: with a device row count
+    below the buffers' capacity, rows [0, live) equal the exact-size call bit for bit and the
+    rows past it are neither read (garbage indices there raise no error) nor written."""
+    from graphneuralnetwork_amd.ops import gcn_transform, sage_gather_concat
+    g = torch.Generator(device=dev).manual_seed(8)
+    n, F, H, cap, live, k = 5000, 128, 128, 3000, 1234, 10
+    table = torch.randn(n, F, device=dev, generator=g)
+    idx = torch.randint(0, n, (cap, k), device=dev, generator=g)
+    sid = torch.randint(0, n, (cap,), device=dev, generator=g)
+    idx[live:] = -7   # out of range past the count: must not be read
+    sid[live:] = n + 3
+    cnt = torch.tensor([live], dtype=torch.int64, device=dev)
+    for agg in ("MEAN", "MAX", "MAXPOOL"):
+        buf = torch.full((cap, 2 * F), 5.0, device=dev)
+        sage_gather_concat(table, sid, idx, agg, check=True, out=buf, live=cnt)  # no IndexError
+        ref = sage_gather_concat(table, sid[:live], idx[:live], agg)
+        assert torch.equal(buf[:live], ref)
+        assert bool((buf[live:] == 5.0).all())
+        W = torch.randn(H, 2 * F, device=dev, generator=g) * 0.05
+        y = torch.full((cap, H), -1.0, device=dev)
+        gcn_transform(buf, W, relu=True, out=y, live=cnt)
+        assert torch.equal(y[:live], gcn_transform(ref, W, relu=True))
+        assert bool((y[live:] == -1.0).all())
+    zero = torch.zeros(1, dtype=torch.int64, device=dev)
+    y = torch.full((cap, H), -1.0, device=dev)
+    gcn_transform(torch.randn(cap, 2 * F, device=dev), W, relu=True, out=y, live=zero)
+    assert bool((y == -1.0).all())

@@ -1,7 +1,8 @@
 """Runs the cfg4 GraphSAGE forward (degree-ordered dataset, 8192 seeds, [25, 10]) REPS times
-after warm-up, for a rocprofv3 --kernel-trace of its kernels:
+after warm-up, for a rocprofv3 --kernel-trace of its kernels; ``--batch``: whole batches
+instead (sample_batch(..., sync=False) + the forward, no host read inside a batch):
 
-    rocprofv3 --kernel-trace -d gpurun_out/sage_trace -o run --output-format csv -- python3 tools/sage_forward_trace.py
+    rocprofv3 --kernel-trace -d gpurun_out/sage_trace -o run --output-format csv -- python3 tools/sage_forward_trace.py [--batch]
     python3 tools/sage_forward_trace.py --summarize gpurun_out/sage_trace/.../run_kernel_trace.csv
 """
 import sys
@@ -12,7 +13,7 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 
-def main():
+def main(batch: bool = False):
     from graphneuralnetwork_amd.graphsage import GraphSAGE
     from graphneuralnetwork_amd.rmat import rmat_edges
     from graphneuralnetwork_amd.sampler import degree_ordered, sample_batch, symmetric_adjacency
@@ -30,20 +31,30 @@ def main():
     net = GraphSAGE(2, F, F, False, agg_func="MEAN", Unsupervised=False, class_size=3).to(dev).eval()
     fa = b.forward_args(table)
     import time
+    if batch:
+        def one():
+            p = sample_batch(adj, seeds, (25, 10), seed=0, sync=False)
+            net(*p.forward_args(table), None, None, None, None, None)
+            return p
+    else:
+        def one():
+            return net(*fa, None, None, None, None, None)
     with torch.no_grad():
         for _ in range(10):
-            net(*fa, None, None, None, None, None)
+            one()
         torch.cuda.synchronize()
         # host enqueue time per forward (no sync inside) vs the wall time until the GPU is done:
         # equal = the eager forward is paced by the host, not by its kernels
         t0 = time.perf_counter()
-        for _ in range(50):
-            net(*fa, None, None, None, None, None)
+        kept = [one() for _ in range(50)]
         t1 = time.perf_counter()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
+        for p in kept if batch else ():
+            p.check()
+    what = "batch" if batch else "forward"
     print(f"done frontier {b.frontier.numel()}: host enqueue {(t1 - t0) / 50 * 1e6:.1f} us per "
-          f"forward, wall {(t2 - t0) / 50 * 1e6:.1f} us per forward", flush=True)
+          f"{what}, wall {(t2 - t0) / 50 * 1e6:.1f} us per {what}", flush=True)
 
 
 def summarize(csv_path: str, per: int = 0, last: int = 50) -> None:
@@ -51,7 +62,9 @@ def summarize(csv_path: str, per: int = 0, last: int = 50) -> None:
     default: inferred from the repeating kernel-name cycle) and the median gap before it."""
     import csv
     import statistics
-    rows = sorted(csv.DictReader(open(csv_path)), key=lambda r: int(r["Start_Timestamp"]))
+    rows = sorted((r for r in csv.DictReader(open(csv_path))
+                   if not r["Kernel_Name"].startswith("__amd_rocclr")),  # the checks' readbacks
+                  key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in rows]
     if not per:
         for p in range(1, 20):
@@ -78,4 +91,4 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--summarize":
         summarize(sys.argv[2])
     else:
-        main()
+        main(batch="--batch" in sys.argv)
