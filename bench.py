@@ -1300,7 +1300,8 @@ def cpu_gcn_train_ops(g, F: int, max_nnz: int = 2_000_000, budget_s: float = 10.
 def gcn_model_forward(g, F: int, args, dev) -> dict:
     """The drop-in two-layer GCN_Model(F, F, F, 2) forward at the north star (GCN/GCN.py:21-27:
     Graph_conv_layer -> ReLU -> Dropout (eval: identity) -> Graph_conv_layer), each layer the
-    MFMA transform into the column order + the XCD-sliced SpMM."""
+    MFMA transform into the column order + the XCD-sliced SpMM, the ReLU in the first SpMM's
+    store epilogue."""
     from graphneuralnetwork_amd.gcn import GCN_Model
     gen = torch.Generator(device=dev).manual_seed(2)
     net = GCN_Model(F, F, F, 2, 0.5).to(dev).eval()

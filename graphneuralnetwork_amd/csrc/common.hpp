@@ -46,7 +46,7 @@ __device__ __forceinline__ f4 shfl_xor_f(f4 v, int m) {
 }
 
 __device__ __forceinline__ float act_apply(float v, uint32_t flags) {
-  if (flags & GNN_EPI_RELU) v = v > 0.f ? v : 0.f;
+  if (flags & GNN_EPI_RELU) v = (v > 0.f || v != v) ? v : 0.f;  // torch.relu: NaN stays NaN
   if (flags & GNN_EPI_ELU) v = v > 0.f ? v : expm1f(v);
   return v;
 }

@@ -24,10 +24,11 @@ rows in that order and the SpMM reads the hub rows in place, with no per-call st
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
-from .ops import column_order, gcn_layer, gcn_transform, spmm
+from .ops import column_order, gcn_layer, gcn_transform, spmm, spmm_forward
 
 
 class GCN_Model(nn.Module):
@@ -49,12 +50,32 @@ class GCN_Model(nn.Module):
                 self.gcn_blocks.add_module(f'dropout{i}', nn.Dropout(dropout))
 
     def forward(self, X, adj):
-        for gcn_block in self.gcn_blocks:
+        blocks = list(self.gcn_blocks)
+        i = 0
+        while i < len(blocks):
+            gcn_block = blocks[i]
             if gcn_block._get_name() == 'Graph_conv_layer':
+                nxt = blocks[i + 1] if i + 1 < len(blocks) else None
+                if _fuse_relu(gcn_block, nxt, X):
+                    # the ReLU in the SpMM's store epilogue (GNN_EPI_RELU): one pass over the
+                    # [n, hidden] activations fewer at inference
+                    X = gcn_block._forward(X, adj, 'relu')
+                    i += 2
+                    continue
                 X = gcn_block(X, adj)
             else:
                 X = gcn_block(X)
+            i += 1
         return X
+
+
+def _fuse_relu(block, nxt, X) -> bool:
+    """Graph_conv_layer followed by nn.ReLU (GCN/GCN.py:12-13) at inference, no hooks on
+    either module: the pair runs as one layer with the ReLU epilogue."""
+    return (isinstance(block, Graph_conv_layer) and type(nxt) is nn.ReLU and isinstance(X, torch.Tensor)
+            and X.is_cuda and not torch.is_grad_enabled()
+            and not (block._forward_hooks or block._forward_pre_hooks or nxt._forward_hooks
+                     or nxt._forward_pre_hooks))
 
 
 class Graph_conv_layer(nn.Module):
@@ -71,6 +92,10 @@ class Graph_conv_layer(nn.Module):
             self.register_parameter('bias', None)
 
     def forward(self, X_input, adj):
+        return self._forward(X_input, adj, None)
+
+    def _forward(self, X_input, adj, activation):
+        """forward, with ``activation`` ('relu' or None) in the SpMM's epilogue at inference."""
         g = as_csr(adj)
         support = None
         training = torch.is_grad_enabled() and (
@@ -80,7 +105,8 @@ class Graph_conv_layer(nn.Module):
                 and X_input.shape[0] == g.n_cols:
             # one differentiable op: MFMA transform + SpMM forward, SpMM + MFMA transform +
             # dW GEMM backward (ops._GcnLayerFn)
-            return gcn_layer(g, X_input, self.dense.weight, self.bias)
+            y = gcn_layer(g, X_input, self.dense.weight, self.bias)
+            return F.relu(y) if activation == 'relu' else y
         if X_input.is_cuda and not training:
             order = column_order(g, self.out_features)
             if order is not None and X_input.shape[0] == g.n_cols:
@@ -89,11 +115,14 @@ class Graph_conv_layer(nn.Module):
                 support = gcn_transform(X_input, self.dense.weight, out_rows=order.inv,
                                         check_rows=False)
                 if support is not None:
-                    return spmm(order.graph, support, self.bias)
+                    return spmm_forward(order.graph, support, self.bias, activation=activation)
             support = gcn_transform(X_input, self.dense.weight)  # MFMA kernel (inference)
+            if support is not None:
+                return spmm_forward(g, support, self.bias, activation=activation)
         if support is None:
             support = self.dense(X_input)
-        return spmm(g, support, self.bias)
+        y = spmm(g, support, self.bias)
+        return F.relu(y) if activation == 'relu' else y
 
     def __repr__(self):
         return self.__class__.__name__ + ' (' \
