@@ -280,6 +280,15 @@ def source_stamp(root: Path = ROOT) -> str:
     return h.hexdigest()[:16]
 
 
+def library_stamps() -> dict:
+    """The loaded library's embedded source stamp beside the tree's;
+    _lib.load() already refused a mismatch, the line records both."""
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd import build as B
+    lib_stamp, tree = _lib.build_stamp(), B.lib_source_stamp()
+    return {"lib_stamp": lib_stamp, "lib_tree_stamp": tree, "lib_stamp_ok": lib_stamp == tree}
+
+
 def traffic_record(path: Path):
     """(traffic bytes, source note, stamp, stale) of a profiles/traffic_*.json, or Nones."""
     try:
@@ -1167,6 +1176,11 @@ def gcn_roofline(nnz: int, n_rows: int, n_cols: int, feat: int, step_ms: list, t
             "min_launch_ms": min(step_ms)}
 
 
+def tn_kernel_name(m: int, k: int) -> str:
+    """The gemm_tn kernel launch_tn picks for an (M, K) shape (csrc/gemm_tn.hip)."""
+    return "gemm_tn_mfma_kernel" if m >= 64 and k >= 32 else "gemm_tn_partial_kernel"
+
+
 def _ms_stats(ms: list) -> dict:
     return {"median_ms": statistics.median(ms), "mean_ms": statistics.mean(ms)}
 
@@ -1212,6 +1226,7 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
     comp = compulsory_bytes(g.nnz, g.n_rows, g.n_cols, F)
     t_sp = statistics.mean(spmm_ms) / 1e3
     nbytes_rows = g.n_rows * 4 * F
+    dw_bytes = (3 if tn else 2) * nbytes_rows  # X, dS (+ dY, the db operand, in gemm_tn)
     res = {
         "what": "Graph_conv_layer(%d, %d) forward + loss.backward() at cfg2, X requiring grad "
                 "(a hidden layer: dX, dW, db)" % (F, F),
@@ -1234,14 +1249,15 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
             "kernel": "spmm_csr_kernel pass 1 + pass 2 (XCD-sliced hub staging of the natural-"
                       "order graph: dY is not in the column order) + fix-up"},
         "roofline_backward_gemm_dW": {
-            "bound": "hbm", "achieved": 2 * nbytes_rows / (statistics.mean(dw_ms) / 1e3) / 1e9,
+            "bound": "hbm", "achieved": dw_bytes / (statistics.mean(dw_ms) / 1e3) / 1e9,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": 2 * nbytes_rows / (statistics.mean(dw_ms) / 1e3) / 1e9 / HBM_PEAK_GBPS,
-            "bytes": 2 * nbytes_rows,
-            "kernel": ("gemm_tn_partial_kernel + gemm_tn_reduce_kernel (dW^T = X^T dS and "
-                       "db = colsum dY in one pass)") if tn else "hipBLASLt (torch.mm)",
-            "note": "dS and X read once (K = n_rows reduction, %.1f GFLOP)"
-                    % (2 * g.n_rows * F * F / 1e9)},
+            "frac": dw_bytes / (statistics.mean(dw_ms) / 1e3) / 1e9 / HBM_PEAK_GBPS,
+            "bytes": dw_bytes,
+            "kernel": ("%s + gemm_tn_reduce_kernel (dW^T = X^T dS and db = colsum dY in one "
+                       "pass)" % tn_kernel_name(F, F)) if tn else "hipBLASLt (torch.mm)",
+            "note": "X, dS and dY (the db operand) read once (K = n_rows reduction, %.1f GFLOP)"
+                    % (2 * g.n_rows * F * F / 1e9) if tn else
+                    "X and dS read once (%.1f GFLOP)" % (2 * g.n_rows * F * F / 1e9)},
         "roofline_backward_transform_dX": {
             "bound": "hbm", "achieved": 2 * nbytes_rows / (statistics.mean(dx_ms) / 1e3) / 1e9,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -1612,6 +1628,150 @@ def _sub(res: dict) -> dict:
     return {k: res[k] for k in keep if k in res}
 
 
+# The driver parses the ONE stdout line; a 20.9 KB line went unparsed in round 5 (VERDICT r5
+# weak #1). The line keeps the contract's keys and one-level summaries, the full result goes
+# to a sidecar JSON the line names.
+LINE_MAX_BYTES = 8000
+REQUIRED_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                 "roofline", "cpu_baseline")
+ROOFLINE_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_stale",
+                 "compulsory_bytes", "traffic_over_compulsory", "avg_launch_ms")
+CPU_KEYS = ("value", "unit", "cores", "kind", "sample", "seconds_per_step")
+CONFIG_KEYS = ("workload", "nodes", "directed_edges", "nnz", "feat_dim", "global_batch",
+               "parallelism", "exchange", "heads", "head_dim", "in_dim", "seeds", "fanout",
+               "frontier", "sampled_edges")
+
+
+def _rnd(v, sig: int = 5):
+    """Floats to `sig` significant digits (the line's numbers are measurements, not ids)."""
+    if isinstance(v, float):
+        return float(f"{v:.{sig}g}")
+    if isinstance(v, dict):
+        return {k: _rnd(x, sig) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_rnd(x, sig) for x in v]
+    return v
+
+
+def _short(text, n: int = 160):
+    return text if not isinstance(text, str) or len(text) <= n else text[:n - 3] + "..."
+
+
+def _pick(d, keys) -> dict:
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def _roof(r) -> dict | None:
+    if not isinstance(r, dict):
+        return None
+    out = _pick(r, ROOFLINE_KEYS)
+    if r.get("kernel"):
+        out["kernel"] = _short(r["kernel"], 120)
+    if r.get("traffic_source"):
+        out["traffic_source"] = r["traffic_source"].split(":")[0]
+    return out
+
+
+def _cpu(c) -> dict | None:
+    if not isinstance(c, dict):
+        return None
+    out = _pick(c, CPU_KEYS)
+    if "sample" in out:
+        out["sample"] = _short(out["sample"], 200)
+    if "error" in c:
+        out["error"] = _short(c["error"], 120)
+    return out
+
+
+def _summary(sub: dict) -> dict:
+    """A sub-workload (north star, cfg3, cfg4) as value / ms / frac and its few headline
+    times; everything else stays in the sidecar."""
+    roof = sub.get("roofline") or {}
+    out = {"value": sub.get("value"), "unit": sub.get("unit"),
+           "ms": sub.get("median_step_ms", sub.get("ms_per_step")),
+           "frac": roof.get("frac"), "traffic": roof.get("traffic"),
+           "avg_launch_ms": roof.get("avg_launch_ms"),
+           "cpu_baseline_value": (sub.get("cpu_baseline") or {}).get("value")}
+    for k in ("gcn_layer_ms", "layer_ms", "forward_ms", "sample_ms", "sample_pending_ms",
+              "batch_ms", "batch_synced_ms", "project_ms"):
+        if k in sub:
+            out[k] = sub[k]
+    if isinstance(sub.get("aggregate_ms"), dict):
+        out["aggregate_ms"] = sub["aggregate_ms"]
+    if isinstance(sub.get("config"), dict):
+        out["workload"] = _short(sub["config"].get("workload"), 100)
+    for k in ("train_step", "gcn_model_forward"):
+        t = sub.get(k)
+        if isinstance(t, dict):
+            out[k + "_ms"] = t.get("step_ms", t.get("forward_ms"))
+    if "target" in sub:
+        out["target_met"] = bool(roof.get("frac") is not None and roof["frac"] >= 0.6)
+    if isinstance(sub.get("aggregators"), dict):
+        out["aggregators_forward_ms"] = {k: v.get("forward_ms") for k, v in
+                                         sub["aggregators"].items() if isinstance(v, dict)}
+    return {k: v for k, v in out.items() if v is not None}
+
+
+def compact_line(res: dict, detail: str | None = None) -> dict:
+    """The driver's line: the contract's keys, the headline roofline and CPU baseline, the
+    library / tree stamps, one-level summaries of the other workloads and training steps, and
+    the path of the sidecar holding the full result. Never longer than LINE_MAX_BYTES."""
+    line = {k: res[k] for k in REQUIRED_KEYS[:12] if k in res}
+    line["config"] = _pick(res.get("config", {}), CONFIG_KEYS)
+    for k in ("median_step_ms", "cache_cold_median_step_ms", "gcn_layer_ms", "first_step_s",
+              "graph_build_s", "partition_build_s", "lib_stamp", "lib_tree_stamp",
+              "lib_stamp_ok", "bench_wall_s"):
+        if k in res:
+            line[k] = res[k]
+    line["roofline"] = _roof(res.get("roofline"))
+    line["cpu_baseline"] = _cpu(res.get("cpu_baseline"))
+    if isinstance(res.get("train_step"), dict):
+        t = res["train_step"]
+        line["train_gcn_cfg2"] = {"step_ms": t.get("step_ms"), "forward_ms": t.get("forward_ms"),
+                                  "backward_ms": t.get("backward_ms"),
+                                  "edges_per_s": t.get("edges_per_s")}
+    if isinstance(res.get("phases_ms"), dict):  # N > 1: the per-phase max over ranks
+        line["phases_ms_max"] = res["phases_ms"].get("max_over_ranks")
+        line["exchange_MB_rank0"] = res["phases_ms"].get("exchange_MB_rank0")
+    for k in ("north_star", "cfg3", "cfg4"):
+        if isinstance(res.get(k), dict):
+            line[k] = _summary(res[k])
+            if k == "cfg3" and isinstance(res[k].get("train_step"), dict):
+                t = res[k]["train_step"]
+                line["train_gat_cfg3"] = {"step_ms": t.get("step_ms"),
+                                          "forward_ms": t.get("forward_ms"),
+                                          "backward_ms": t.get("backward_ms")}
+    if detail:
+        line["detail"] = detail
+    line = _rnd(line)
+    for k in ("value", "ms_per_step"):  # the headline numbers at full precision
+        if k in res:
+            line[k] = res[k]
+    # last resort (never expected): drop the summaries, then the optional extras
+    for k in ("north_star", "cfg4", "cfg3", "train_gat_cfg3", "train_gcn_cfg2", "phases_ms_max",
+              "exchange_MB_rank0"):
+        if len(json.dumps(line)) <= LINE_MAX_BYTES:
+            break
+        line.pop(k, None)
+    assert len(json.dumps(line)) <= LINE_MAX_BYTES
+    return line
+
+
+def write_detail(res: dict, world: int) -> str | None:
+    """The full result beside the line: $GNN_BENCH_DETAIL or gpurun_out/bench_detail_n<N>.json
+    (relative to the repo root); the line names it. A failed write leaves the line intact."""
+    path = Path(os.environ.get("GNN_BENCH_DETAIL") or
+                ROOT / "gpurun_out" / f"bench_detail_n{world}.json")
+    try:
+        path.parent.mkdir(parents=True, exist_ok=True)
+        path.write_text(json.dumps(res, indent=1) + "\n")
+    except OSError as e:
+        log(f"[bench] detail file not written: {e!r}")
+        return None
+    return str(path.relative_to(ROOT)) if path.is_relative_to(ROOT) else str(path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1711,8 +1871,10 @@ def main():
     phase("report", 120)
     if rank == 0:
         res["bench_wall_s"] = time.perf_counter() - t_all
+        res.update(library_stamps())
+        line = compact_line(res, write_detail(res, world))
         sys.stdout.flush()
-        os.write(json_fd, (json.dumps(res) + "\n").encode())
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
     phase("done", None)

@@ -28,6 +28,8 @@ _vp = ctypes.c_void_p
 SIGNATURES: dict[str, tuple] = {
     "gnn_version": (ctypes.c_int, []),
     "gnn_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "gnn_build_stamp": (ctypes.c_char_p, []),
+    "gnn_build_defines": (ctypes.c_char_p, []),
     "gnn_spmm_csr_f32": (ctypes.c_int, [
         _vp, _vp, _vp, _i64,            # rowptr, col, val, n_rows
         _vp, _i64, _i64,                # x, ldx, feat
@@ -265,8 +267,27 @@ def load(build_if_missing: bool = False) -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        check_stamp(lib)
         _lib = lib
         return lib
+
+
+def build_stamp(lib=None) -> str:
+    """The source stamp embedded in the loaded library (``gnn_build_stamp()``)."""
+    return (lib or load()).gnn_build_stamp().decode()
+
+
+def check_stamp(lib) -> None:
+    """Refuse a library not built from this tree's sources: a stale
+    prebuilt .so would otherwise run silently under a newer tree's tests and bench."""
+    built, tree = lib.gnn_build_stamp().decode(), _build.lib_source_stamp()
+    if built != tree:
+        raise RuntimeError(
+            f"{library_path()} was built from sources with stamp {built}, but this tree's are "
+            f"{tree}: rebuild with `python -m graphneuralnetwork_amd.build`")
+    if lib.gnn_build_defines().decode():
+        raise RuntimeError(f"{library_path()} is a tuning-variant build "
+                           f"({lib.gnn_build_defines().decode()}), not the product library")
 
 
 def use_variant(path) -> ctypes.CDLL:
@@ -277,6 +298,8 @@ def use_variant(path) -> ctypes.CDLL:
         _lib = None
         return load()
     lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_LOCAL)
+    if not hasattr(lib, "gnn_build_stamp"):
+        raise RuntimeError(f"{path}: no gnn_build_stamp (built before round 6); rebuild it")
     for name, (res, args) in SIGNATURES.items():
         try:  # an older build may lack entries added since (A/B of a previous tree)
             fn = getattr(lib, name)

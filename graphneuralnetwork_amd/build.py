@@ -8,6 +8,7 @@ the GPU box; it is git-ignored.  hipcc cross-compiles without a GPU.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -74,38 +75,95 @@ def _stale(target: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile (if stale) and return the path of libgnn_mi355x.so."""
-    srcs = sources()
-    headers = sorted(CSRC_DIR.glob("*.hpp")) + [HEADER]
-    OBJ_DIR.mkdir(parents=True, exist_ok=True)
-    hipcc = _hipcc()
+def _headers() -> list[Path]:
+    return sorted(CSRC_DIR.glob("*.hpp")) + [HEADER]
+
+
+def lib_source_stamp(defines=()) -> str:
+    """sha256 (16 hex) of what the library is built from: every csrc source and header, the
+    export map, include/gnn_mi355x.h, the compile flags and the -D defines. ``build()`` embeds
+    it in the library (``gnn_build_stamp()``); ``_lib.load()`` refuses a library whose stamp
+    differs from the tree it is loaded from (VERDICT r5 next #6: the binary tied to the tree)."""
+    h = hashlib.sha256()
+    h.update(" ".join([*HIPCC_FLAGS, *defines]).encode() + b"\0")
+    for f in sources() + _headers() + [EXPORT_MAP]:
+        h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def _object_digest(src: Path, extra=()) -> str:
+    """Content hash of one object's inputs (its source, every header, its flags): objects are
+    rebuilt when this changes, not by mtime (a snapshot copy resets mtimes)."""
+    h = hashlib.sha256(" ".join([*HIPCC_FLAGS, *extra]).encode())
+    for f in [src] + _headers():
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def _needs_compile(src: Path, obj: Path, extra=()) -> bool:
+    sig = obj.with_suffix(".o.sha256")
+    return not (obj.exists() and sig.exists() and sig.read_text() == _object_digest(src, extra))
+
+
+def _compile_all(hipcc: str, jobs, verbose: bool = False) -> None:
+    """jobs: (src, obj, extra defines). Compiles in parallel, records each object's digest."""
     procs = []
-    objs = []
-    for src in srcs:
-        obj = OBJ_DIR / (src.stem + ".o")
-        objs.append(obj)
-        if force or _stale(obj, [src] + headers):
-            cmd = _compile_cmd(hipcc, src, obj)
-            if verbose:
-                print(" ".join(cmd), file=sys.stderr)
-            procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE,
-                                                stderr=subprocess.STDOUT, text=True)))
+    for src, obj, extra in jobs:
+        cmd = _compile_cmd(hipcc, src, obj, extra)
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((src, obj, extra, subprocess.Popen(cmd, stdout=subprocess.PIPE,
+                                                        stderr=subprocess.STDOUT, text=True)))
     failed = []
-    for src, p in procs:
+    for src, obj, extra, p in procs:
         out, _ = p.communicate()
         if p.returncode != 0:
             failed.append(f"--- {src.name} ---\n{out}")
-        elif verbose and out.strip():
+            continue
+        obj.with_suffix(".o.sha256").write_text(_object_digest(src, extra))
+        if verbose and out.strip():
             print(out, file=sys.stderr)
     if failed:
         raise RuntimeError("hipcc failed:\n" + "\n".join(failed))
-    if force or procs or _stale(LIB_PATH, objs + [EXPORT_MAP]):
+
+
+def _stamp_object(odir: Path, stamp: str, defines=()) -> Path:
+    """build_stamp.o: ``const char* gnn_build_stamp(void)`` returning the source stamp (and,
+    for a variant build, its defines), compiled by the system C compiler."""
+    src = odir / "build_stamp.c"
+    obj = odir / "build_stamp.o"
+    text = ("/* generated by graphneuralnetwork_amd/build.py */\n"
+            f"const char* gnn_build_stamp(void) {{ return \"{stamp}\"; }}\n"
+            f"const char* gnn_build_defines(void) {{ return \"{' '.join(defines)}\"; }}\n")
+    if not (src.exists() and obj.exists() and src.read_text() == text):
+        src.write_text(text)
+        r = subprocess.run(["gcc", "-O2", "-fPIC", "-c", str(src), "-o", str(obj)],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("build_stamp.c failed:\n" + r.stdout + r.stderr)
+    return obj
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile (what changed) and return the path of libgnn_mi355x.so, whose embedded
+    ``gnn_build_stamp()`` is ``lib_source_stamp()`` of this tree."""
+    srcs = sources()
+    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    hipcc = _hipcc()
+    objs = [OBJ_DIR / (src.stem + ".o") for src in srcs]
+    jobs = [(src, obj, ()) for src, obj in zip(srcs, objs) if force or _needs_compile(src, obj)]
+    _compile_all(hipcc, jobs, verbose)
+    stamp = lib_source_stamp()
+    stamp_file = LIB_PATH.with_suffix(".stamp")
+    objs.append(_stamp_object(OBJ_DIR, stamp))
+    if (force or jobs or not LIB_PATH.exists() or not stamp_file.exists()
+            or stamp_file.read_text() != stamp):
         tmp = LIB_PATH.with_suffix(".so.tmp")
         r = subprocess.run(_link_cmd(hipcc, tmp, objs), capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
         os.replace(tmp, LIB_PATH)
+        stamp_file.write_text(stamp)
     # the plain-C example is optional: a missing C compiler or a failing example build warns
     # and leaves the library usable (ADVICE r4); tests/test_capi.py builds it explicitly
     try:
@@ -152,21 +210,13 @@ def build_variant(tag: str, defines: list[str], only: list[str] | None = None) -
     out = LIB_DIR / "variants" / f"libgnn_{tag}.so"
     out.parent.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
-    headers = sorted(CSRC_DIR.glob("*.hpp")) + [HEADER]
-    stamp = odir / "defines.txt"
-    same = stamp.exists() and stamp.read_text() == "\n".join(defines)
-    procs = [(src, subprocess.Popen(_compile_cmd(hipcc, src, odir / (src.stem + ".o"),
-                                                 [f"-D{d}" for d in defines]),
-                                    stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
-             for src in sources()
-             if (not only or src.name in only)
-             and (not same or _stale(odir / (src.stem + ".o"), [src] + headers))]
-    failed = [f"--- {src.name} ---\n{p.communicate()[0]}" for src, p in procs if p.wait() != 0]
-    if failed:
-        raise RuntimeError("hipcc failed:\n" + "\n".join(failed))
-    stamp.write_text("\n".join(defines))
+    extra = tuple(f"-D{d}" for d in defines)
+    _compile_all(hipcc, [(src, odir / (src.stem + ".o"), extra) for src in sources()
+                         if (not only or src.name in only)
+                         and _needs_compile(src, odir / (src.stem + ".o"), extra)])
     objs = [(odir if not only or src.name in only else OBJ_DIR) / (src.stem + ".o")
             for src in sources()]
+    objs.append(_stamp_object(odir, lib_source_stamp(extra), extra))
     r = subprocess.run(_link_cmd(hipcc, out, objs), capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stdout + r.stderr)

@@ -348,13 +348,9 @@ __global__ __launch_bounds__(kScanThreads) void batch_scan_kernel(uint8_t* __res
   __shared__ uint32_t s_wave[kScanWaves];
   __shared__ uint32_t s_prefix;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-#ifdef GNN_SCAN_PROBE_NO_TICKET  // A/B probe: tile = workgroup id (no ticket atomic)
-  if (tid == 0) s_tile = blockIdx.x;
-#else
   if (tid == 0)
     s_tile = static_cast<int64_t>(__hip_atomic_fetch_add(ctl + 1, uint64_t(1), __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT));
-#endif
   __syncthreads();
   const int64_t tile = s_tile;
   if (tile >= (n_words + kScanTileWords - 1) / kScanTileWords) {  // tickets not reset: never
@@ -460,14 +456,12 @@ __global__ __launch_bounds__(kScanThreads) void batch_scan_kernel(uint8_t* __res
     uint4* f = reinterpret_cast<uint4*>(flags + 32 * w);
     f[0] = make_uint4(0, 0, 0, 0);
     f[1] = make_uint4(0, 0, 0, 0);
-#ifndef GNN_SCAN_PROBE_NO_EMIT  // A/B probe (wrong results): the scan without its id stores
     while (m) {
       const int t = __ffs(m) - 1;
       if (o < cap) out[o] = w * 32 + t;
       ++o;
       m &= m - 1;
     }
-#endif
   }
 }
 

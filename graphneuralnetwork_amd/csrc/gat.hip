@@ -140,12 +140,8 @@ __device__ __forceinline__ const float* wh_row(const GatParams& P, int c) {
                : P.wh + static_cast<int64_t>(c) * P.ldw;
 }
 __device__ __forceinline__ float er_at(const GatParams& P, int c, int h) {
-#ifdef GNN_GAT_PROBE_NO_ER  // traffic probe only (wrong results): er without its gather
-  return static_cast<float>((c ^ h) & 7) * 0.01f;
-#else
   return c < 0 ? P.erh[static_cast<int64_t>(-1 - c) * P.ldeh + h]
                : P.er[static_cast<int64_t>(c) * P.lde + h];
-#endif
 }
 
 #ifndef GNN_GAT_SMALL_UNROLL

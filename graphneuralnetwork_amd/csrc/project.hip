@@ -260,18 +260,6 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
           const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(xp);
           const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(xp + PLANE);
           const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(xp + 2 * PLANE);
-#ifdef GNN_PROJ_NO_MFMA  // A/B only: the tile's LDS reads without its MFMAs
-#pragma unroll
-          for (int t = 0; t <= NT; ++t) {
-            const f32x4 c = f32x4{static_cast<float>(x0[t & 7]), static_cast<float>(x1[t & 7]),
-                                  static_cast<float>(x2[t & 7]), static_cast<float>(s6)};
-            if (t < NT)
-              acc[j][t] += c;
-            else
-              acc2[j] += c;
-          }
-          continue;
-#endif
 #pragma unroll
           for (int t = 0; t <= NT; ++t) {  // smallest terms first; t == NT: the logit tile
             f32x4 c = t < NT ? acc[j][t] : acc2[j];
@@ -288,17 +276,7 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
           }
         }
       }
-    } else
-#ifdef GNN_PROJ_NO_MFMA
-    {
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[j][t] = f32x4{a[j][t], a[j][t + 1], a[j][t + 2], a[j][t + 3]};
-      acc2[j] = f32x4{a[j][4], a[j][5], a[j][6], a[j][7]};
-    }
-    }
-#else
+    } else {
 #pragma unroll
     for (int s = 0; s < S; ++s) {
 #pragma unroll
@@ -318,7 +296,7 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
 #endif
       }
     }
-#endif
+    }
     // Operands are swapped (D = W^T X^T), so acc[j][t][i] is Wh[row0 + 16j + r][16t + 4q + i]:
     // one 16-B store per tile, 4 lanes = 64 contiguous bytes of a row; acc2[j][i] is column
     // 4q + i of [el | er] for row 16j + r
@@ -338,13 +316,11 @@ __global__ __launch_bounds__(kProjBlock) void gat_project_kernel(
         crow = cok ? crow : 0;
       }
       if (orow < n_rows) {
-#ifndef GNN_PROJ_NO_WH
 #pragma unroll
         for (int t = 0; t < NT; ++t)
           if (cok)
             *reinterpret_cast<float4*>(wh + crow * ldwh + 16 * t + 4 * q) =
                 make_float4(acc[j][t][0], acc[j][t][1], acc[j][t][2], acc[j][t][3]);
-#endif
         if (vec_logits) {  // heads % 4 == 0: quarter q holds 4 whole logits of el or er
           const int c = 4 * q;
           if (c < 2 * heads && (c < heads || cok))

@@ -369,9 +369,15 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, d: torch.Tensor | None = None,
     lib = _lib.load()
     if not lib.gnn_gemm_tn_supported(m, k):
         return None
-    ts = [a, b] + ([d] if d is not None else [])
-    ts = [t if (t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0)
-          else t.contiguous() for t in ts]
+    def fits(t):
+        return t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+
+    # a copy for an operand the kernel cannot read in place: clone, not .contiguous(), which
+    # hands back a contiguous view at a misaligned storage offset unchanged
+    ts = [t if fits(t) else t.clone(memory_format=torch.contiguous_format)
+          for t in [a, b] + ([d] if d is not None else [])]
+    if not all(fits(t) for t in ts):  # rows of a length the 16-B loads cannot take
+        return None
     a, b = ts[0], ts[1]
     d = ts[2] if d is not None else None
     c = torch.empty((k, m) if trans else (m, k), dtype=torch.float32, device=a.device)

@@ -100,15 +100,21 @@ def _frontier_ws(n_nodes: int, dev) -> torch.Tensor:
 _SAMPLE_WS = {}
 
 
-def _sample_ws(n_nodes: int, dev) -> torch.Tensor:
+def _sample_ws(n_nodes: int, dev, stream=None) -> torch.Tensor:
     """gnn_sample_layers' workspace for an n_nodes graph: zero-filled once here; every call
-    leaves it zero-filled again (the frontier flags are cleared by the scan that reads them)."""
-    key = (dev, n_nodes)
+    leaves it zero-filled again (the frontier flags are cleared by the scan that reads them).
+    One workspace per (device, graph size, stream), as the header requires: two streams
+    sampling at once never share the flags / tile tags. Allocated on ``stream``
+    (the sampler's), so the caching allocator reuses it only in that stream's order."""
+    stream = stream if stream is not None else torch.cuda.current_stream(dev)
+    key = (dev, n_nodes, stream.cuda_stream)
     ws = _SAMPLE_WS.get(key)
     if ws is None:
-        ws = torch.zeros(int(_lib.load().gnn_sample_layers_workspace_bytes(n_nodes)),
-                         dtype=torch.uint8, device=dev)
-        _SAMPLE_WS.clear()  # one graph at a time
+        for k in [k for k in _SAMPLE_WS if k[1] != n_nodes]:  # one graph size at a time
+            del _SAMPLE_WS[k]
+        with torch.cuda.stream(stream):
+            ws = torch.zeros(int(_lib.load().gnn_sample_layers_workspace_bytes(n_nodes)),
+                             dtype=torch.uint8, device=dev)
         _SAMPLE_WS[key] = ws
     return ws
 
@@ -271,7 +277,8 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
     buf = torch.empty(tot, dtype=torch.int64, device=dev)
     base = buf.data_ptr()
     ptr = [base + 8 * o for o in offs]  # layers 1.., nbrs 0.., cmaps, nmaps, stat
-    ws = _sample_ws(adj.n_rows, dev)
+    stream = torch.cuda.current_stream(dev)  # the sampler's kernels and its readback
+    ws = _sample_ws(adj.n_rows, dev, stream)
     P = ctypes.c_void_p
     seed_a = (ctypes.c_uint64 * L)(*[stream_seed(seed, i) for i in range(L)])
     lib = _lib.load()
@@ -281,7 +288,7 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
                                      (P * L)(*ptr[L - 1:2 * L - 1]),
                                      (P * max(1, L - 1))(*ptr[2 * L - 1:3 * L - 2]),
                                      (P * max(1, L - 1))(*ptr[3 * L - 2:4 * L - 3]), ptr[-1],
-                                     ws.data_ptr(), ws.numel(), _lib.stream_handle(dev)),
+                                     ws.data_ptr(), ws.numel(), stream.cuda_stream),
                "gnn_sample_layers")
     widths = [k + (1 if gcn else 0) for k in fanouts]
 
@@ -300,9 +307,12 @@ def sample_batch(adj: CsrGraph, seeds: torch.Tensor, fanouts=(25, 10), seed: int
                             tuple(layers), tuple(live), finish)
 
     def finish():
+        # on the stream the sampler ran on, whatever stream is current when a pending batch is
+        # synced: the copy waits for the scan kernels that wrote the sizes
         host = _stat_host(L + 1)
-        host.copy_(buf[offs[-1]:offs[-1] + L + 1], non_blocking=True)  # pinned: no staging
-        torch.cuda.current_stream(dev).synchronize()  # the one host synchronisation
+        with torch.cuda.stream(stream):
+            host.copy_(buf[offs[-1]:offs[-1] + L + 1], non_blocking=True)  # pinned: no staging
+        stream.synchronize()  # the one host synchronisation
         st = host.tolist()  # every layer size + the error bits
         sizes, e = st[:L], int(st[L]) & 0xFFFFFFFF
         _raise_sample_error(e & 3)  # the sampler's own errors first, as the step-by-step path

@@ -59,6 +59,14 @@ int gnn_version(void);
 /* Human-readable text for a return code of this library (GNN_E_* or hipError_t). */
 const char* gnn_error_string(int code);
 
+/* Build provenance: sha256 (16 hex) of the sources, headers, export map and compile flags the
+ * library was built from (graphneuralnetwork_amd/build.py lib_source_stamp). The Python loader
+ * refuses a library whose stamp differs from the tree it is loaded from. */
+const char* gnn_build_stamp(void);
+
+/* The -D defines of a tuning-variant build (build.build_variant); "" for the product library. */
+const char* gnn_build_defines(void);
+
 /*
  * GCN aggregation: Y[r, :] = sum_{e in row r} val[e] * X[col[e], :] (+ bias) (epilogue)
  *

@@ -112,3 +112,17 @@ def test_c_program_links_and_checks_usage():
     B.build_examples()  # build() only warns when the example fails to build; here it must not
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "usage" in r.stderr
+
+
+def test_build_stamp_ties_library_to_tree(lib, monkeypatch):
+    """The library carries the stamp of the sources it was built from (build.lib_source_stamp,
+    embedded as gnn_build_stamp()); load() refuses one whose stamp differs from this tree."""
+    from graphneuralnetwork_amd import _lib
+    from graphneuralnetwork_amd import build as B
+    assert _lib.build_stamp(lib) == B.lib_source_stamp()
+    assert lib.gnn_build_defines().decode() == ""
+    assert B.lib_source_stamp(("-DX=1",)) != B.lib_source_stamp()
+    _lib.check_stamp(lib)
+    monkeypatch.setattr(B, "lib_source_stamp", lambda defines=(): "0" * 16)
+    with pytest.raises(RuntimeError, match="rebuild"):
+        _lib.check_stamp(lib)

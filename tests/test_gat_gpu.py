@@ -146,7 +146,8 @@ def test_gat_hub_staging_bitexact(dev, heads, fh, sparse):
 @pytest.mark.parametrize("heads,fh", [(8, 8), (12, 4), (1, 64), (2, 128)])
 @pytest.mark.parametrize("sparse", [False, True])
 def test_gat_packed_tasks_vs_short_rows(dev, heads, fh, sparse, monkeypatch):
-    """gnn_gat_csr_tasks_f32 (low-degree rows as packed tasks, the default at fh % 4 == 0)
+    """gnn_gat_csr_tasks_f32 (low-degree rows as packed tasks; opt-in through ops.GAT_TASKS,
+    measured slower than the row classes at cfg3)
     against the row-class path it replaces (packed small rows + gat_short_kernel) and the
     oracle: edgeless rows (dense: column mean; sparse: NaN), one-edge rows, runs longer than a
     task, long-row segments, two head groups (12 heads), hub staging, dropout (the same

@@ -443,3 +443,26 @@ def test_pending_batch_errors_raise_at_check(dev):
     torch.cuda.synchronize()
     ok = sample_batch(g, torch.tensor([0, 1], device=dev), (4, 2), sync=False)
     ok.check()
+
+
+@pytest.mark.gpu
+def test_pending_batch_synced_off_its_stream(dev):
+    """a batch sampled pending under a side stream and synced on another reads its
+    sizes on the sampler's stream (the copy waits for the scan), and each stream keeps its own
+    workspace. Equal to the batch sampled and synced on the default stream."""
+    from graphneuralnetwork_amd import sampler as S
+    adj = _adj(dev, n=40000, e=300000, seed=4)
+    deg = (adj.rowptr[1:] - adj.rowptr[:-1]).cpu().numpy()
+    seeds = torch.from_numpy(np.nonzero(deg > 0)[0][:700]).to(dev)
+    a = S.sample_batch(adj, seeds, (25, 10), seed=5)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(2_000_000)  # keep the side stream busy ahead of the sampler
+        p = S.sample_batch(adj, seeds, (25, 10), seed=5, sync=False)
+    s = p.sync()  # on the default stream: must still wait for the side stream's kernels
+    assert s.layer_sizes == a.layer_sizes
+    torch.cuda.current_stream(dev).wait_stream(side)
+    assert torch.equal(s.frontier, a.frontier) and torch.equal(s.neigh_map, a.neigh_map)
+    keys = [k for k in S._SAMPLE_WS if k[1] == adj.n_rows]
+    assert len({k[2] for k in keys}) == 2

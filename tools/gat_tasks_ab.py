@@ -9,8 +9,8 @@ with the row-class path.
 
 --libs: variant libraries (lib/variants/libgnn_<tag>.so, build.build_variant) timed with the
 row-class schedule beside the main library (round 5: gatpipe2 = a depth-2 chunk pipeline, since
-removed, profiles/r05b_gat_tasks_ab.log; noer = -DGNN_GAT_PROBE_NO_ER, the aggregation without
-its er gathers -- a traffic probe, wrong results).
+removed, profiles/r05b_gat_tasks_ab.log; the round-5 "noer" traffic probe, a wrong-result
+switch, was removed from the product sources in round 6).
 """
 from __future__ import annotations
 
