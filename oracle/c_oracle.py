@@ -41,6 +41,11 @@ def load():
         lib.oracle_sage_gather.restype = None
         lib.oracle_sage_argmax.argtypes = [vp, i64, vp, i64, i64, i64, i64, vp, i64]
         lib.oracle_sage_argmax.restype = None
+        lib.oracle_gat_block_grad.argtypes = [vp, vp, i64, vp, vp, vp, vp, vp, i64, i64,
+                                              ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_double, ctypes.c_uint64, vp, vp, vp, vp,
+                                              vp, vp]
+        lib.oracle_gat_block_grad.restype = ctypes.c_int
         _lib = lib
     return _lib
 
@@ -124,3 +129,54 @@ def sage_gather(table, idx, mode: str = "MEAN"):
     lib.oracle_sage_gather(table.ctypes.data, F, idx.ctypes.data, k, M, k, F, _SAGE_MODES[mode],
                            out.ctypes.data, F)
     return out
+
+
+def gat_block_grad(rowptr, col, x, W, a_src, a_dst, gy, heads: int, fh: int, slope: float,
+                   sparse: bool, elu: bool = True, drop_p: float = 0.0, drop_seed: int = 0):
+    """float64 forward + backward of the H-head GAT attention block (GAT/models/GAT.py:16 over
+    GAT/models/layers.py:22-37 / :94-131, all heads concatenated) for the loss sum(out * gy):
+    Wh = x W in float64, the C restatement of the aggregation and its gradients
+    (oracle_gat_block_grad), then dW = x^T dWh, d a_src / d a_dst per head and dx = dWh W^T.
+    Dropout masks re-derived from the HIP kernels' (seed, edge, head) hash. Returns a dict of
+    float64 arrays: out, dW, da_src, da_dst, dx, dwh, del, der, and ``slack_*`` for dwh, dW,
+    da_src, da_dst, dx: the per-element bound on how far an fp32 implementation may move from
+    these values by taking the other LeakyReLU' branch on edges whose t_ij is within rounding
+    of the kink at 0 (oracle_gat_block_grad's kink_del / kink_der, propagated with absolute
+    values); zero where no such edge contributes."""
+    lib = load()
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    x64 = np.asarray(x, dtype=np.float64)
+    W64 = np.asarray(W, dtype=np.float64)
+    n, F = x64.shape[0], heads * fh
+    wh = np.ascontiguousarray(x64 @ W64)
+    wh_abs = np.ascontiguousarray(np.abs(x64) @ np.abs(W64))
+    a_s = np.ascontiguousarray(a_src, dtype=np.float32)
+    a_d = np.ascontiguousarray(a_dst, dtype=np.float32)
+    g = np.ascontiguousarray(gy, dtype=np.float32)
+    out = np.empty((n, F))
+    dwh = np.empty((n, F))
+    dl = np.empty((n, heads))
+    der = np.empty((n, heads))
+    kdl = np.empty((n, heads))
+    kdr = np.empty((n, heads))
+    rc = lib.oracle_gat_block_grad(rowptr.ctypes.data, col.ctypes.data, n, wh.ctypes.data,
+                                   wh_abs.ctypes.data, a_s.ctypes.data, a_d.ctypes.data, g.ctypes.data, heads, fh,
+                                   float(slope), int(bool(sparse)), int(bool(elu)), float(drop_p),
+                                   int(drop_seed), out.ctypes.data, dwh.ctypes.data,
+                                   dl.ctypes.data, der.ctypes.data, kdl.ctypes.data,
+                                   kdr.ctypes.data)
+    if rc != 0:
+        raise ValueError(f"oracle_gat_block_grad failed ({rc}: -1 edgeless row, -2 memory)")
+    whh = wh.reshape(n, heads, fh)
+    r = {"out": out, "dwh": dwh, "del": dl, "der": der, "dW": x64.T @ dwh,
+         "da_src": np.einsum("nh,nhf->hf", dl, whh).reshape(-1),
+         "da_dst": np.einsum("nh,nhf->hf", der, whh).reshape(-1), "dx": dwh @ W64.T,
+         "kink_del": kdl, "kink_der": kdr}
+    sdwh = (np.repeat(kdr, fh, axis=1) * np.abs(a_d.astype(np.float64)) +
+            np.repeat(kdl, fh, axis=1) * np.abs(a_s.astype(np.float64)))
+    awh = np.abs(whh)
+    r.update(slack_dwh=sdwh, slack_dW=np.abs(x64).T @ sdwh, slack_dx=sdwh @ np.abs(W64).T,
+             slack_da_src=np.einsum("nh,nhf->hf", kdl, awh).reshape(-1),
+             slack_da_dst=np.einsum("nh,nhf->hf", kdr, awh).reshape(-1))
+    return r

@@ -234,6 +234,55 @@ def part_gat():
     np.savez_compressed(HERE / "gat.npz", **out)
 
 
+# ------------------------------------------------------------- GAT gradients
+def part_gatgrad():
+    """Gradients of the 8-head attention block (GAT/models/GAT.py:16: the heads of
+    layers.py:22-37 / :94-131 concatenated) under autograd -- the reference's own backward,
+    SpecialSpmmFunction.backward (layers.py:54-64) for the sparse heads -- for the loss
+    sum(block(h, adj) * gy): pins the float64 C restatement (oracle_gat_block_grad) that the
+    full-size training test checks the HIP backward against. Dropout 0 (torch's RNG stream is
+    not the HIP kernels' hash; the hash is restated and checked separately)."""
+    import importlib.util
+    import torch
+    spec = importlib.util.spec_from_file_location("ref_gat_layers", REF / "GAT/models/layers.py")
+    L = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(L)
+    torch.manual_seed(0)
+    rng = np.random.default_rng(11)
+    N, Fin, H, Fh, alpha = 384, 64, 8, 8, 0.2
+    s = rng.integers(0, N, 2500)
+    t = rng.integers(0, N, 2500)
+    A = np.zeros((N, N), np.float32)
+    A[s, t] = 1
+    A[t, s] = 1
+    A[np.arange(N), np.arange(N)] = 1
+    A[11, :] = 0
+    A[11, 11] = 1                          # a degree-1 row
+    A[:60, 3] = 1                          # a hub column
+    A[3, :60] = 1
+    h = _q(rng, (N, Fin), 32, 32)
+    gy = _q(rng, (N, H * Fh), 16, 16)
+    out = {"adj_row": np.nonzero(A)[0].astype(np.int32), "adj_col": np.nonzero(A)[1].astype(np.int32),
+           "h": h, "gy": gy, "n": np.int64(N), "alpha": np.float64(alpha), "heads": np.int64(H),
+           "fh": np.int64(Fh)}
+    for kind, cls in (("dense", L.GraphAttentionLayer), ("sparse", L.SpGraphAttentionLayer)):
+        heads = [cls(Fin, Fh, dropout=0.0, alpha=alpha, concat=True) for _ in range(H)]
+        for m in heads:
+            _set_params(m, rng, 64, 40)
+            m.train()
+        ht = torch.from_numpy(h).requires_grad_(True)
+        x = torch.cat([m(ht, torch.from_numpy(A)) for m in heads], dim=1)   # GAT/models/GAT.py:16
+        (x * torch.from_numpy(gy)).sum().backward()
+        out[f"{kind}_W"] = np.stack([m.W.detach().numpy() for m in heads])
+        out[f"{kind}_a"] = np.stack([m.a.detach().numpy().reshape(-1) for m in heads])
+        out[f"{kind}_out"] = x.detach().numpy()
+        out[f"{kind}_dW"] = np.stack([m.W.grad.numpy() for m in heads])
+        out[f"{kind}_da"] = np.stack([m.a.grad.numpy().reshape(-1) for m in heads])
+        out[f"{kind}_dh"] = ht.grad.numpy()
+        print("gatgrad", kind, x.shape)
+    np.savez_compressed(HERE / "gatgrad.npz", **out)
+
+
 # ----------------------------------------------------------------- GraphSAGE
 def part_sage():
     sys.path.insert(0, str(REF / "GraphSAGE"))
@@ -488,7 +537,8 @@ def part_features():
     print("gcn_features.npz", {k: v.shape for k, v in out.items()})
 
 
-PARTS = {"gcn": part_gcn, "features": part_features, "gat": part_gat, "sage": part_sage, "han": part_han,
+PARTS = {"gcn": part_gcn, "features": part_features, "gat": part_gat, "gatgrad": part_gatgrad,
+         "sage": part_sage, "han": part_han,
          "sagepy": part_sagepy, "pysampler": part_pysampler}
 
 if __name__ == "__main__":

@@ -245,3 +245,92 @@ def test_graphsage_tree_oracle_matches_reference(golden):
     y3 = O.neighbor_aggregator(nb, d["biasmean_sd_weight"], d["biasmean_sd_bias"], "mean")
     np.testing.assert_allclose(y3, d["biasmean_y"], rtol=1e-4, atol=1e-5)
     assert int(d["max_raises"]) == 1
+
+
+# ------------------------------------------------------- GAT block gradients
+def _gatgrad_inputs(g, kind):
+    n, H, fh = int(g["n"]), int(g["heads"]), int(g["fh"])
+    row, col = g["adj_row"].astype(np.int64), g["adj_col"].astype(np.int32)
+    order = np.lexsort((col, row))
+    row, col = row[order], col[order]
+    rowptr = np.concatenate([[0], np.cumsum(np.bincount(row, minlength=n))]).astype(np.int64)
+    W = np.concatenate(list(g[f"{kind}_W"]), axis=1)                      # [in, H fh]
+    a = g[f"{kind}_a"]                                                    # [H, 2 fh]
+    return n, H, fh, rowptr, col, W, a[:, :fh].reshape(-1), a[:, fh:].reshape(-1)
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse"])
+def test_gat_block_grad_oracle_matches_reference_autograd(golden, kind):
+    """oracle_gat_block_grad (the float64 checker of the full-size GAT training test) against
+    the reference's own autograd of the 8-head block (layers.py:22-37 dense, :94-131 with
+    SpecialSpmmFunction.backward :54-64 sparse; GAT.py:16 concatenation): the block output,
+    every head's dW and da, and dh, for the loss sum(block * gy)."""
+    g = golden("gatgrad")
+    n, H, fh, rowptr, col, W, a_s, a_d = _gatgrad_inputs(g, kind)
+    r = c_oracle.gat_block_grad(rowptr, col, g["h"], W, a_s, a_d, g["gy"], H, fh,
+                                float(g["alpha"]), kind == "sparse")
+    close(r["out"], g[f"{kind}_out"])
+    close(r["dW"], np.concatenate(list(g[f"{kind}_dW"]), axis=1))
+    da = np.concatenate([r["da_src"].reshape(H, fh), r["da_dst"].reshape(H, fh)], axis=1)
+    close(da, g[f"{kind}_da"])
+    close(r["dx"], g[f"{kind}_dh"])
+
+
+def _hash3(seed: int, edge: np.ndarray, head: int) -> np.ndarray:
+    """csrc/gat.hip hash3 in numpy uint32 arithmetic (the dropout stream)."""
+    M = np.uint64(0xFFFFFFFF)
+    e = edge.astype(np.uint64)
+    h = np.uint64(seed & 0xFFFFFFFF) ^ ((np.uint64(seed >> 32) * np.uint64(0x27d4eb2f)) & M)
+    h = h ^ ((e & M) * np.uint64(0x9e3779b9) & M)
+    h = h ^ (((e >> np.uint64(32)) * np.uint64(0x85ebca6b)) & M)
+    h = h ^ ((np.uint64(head) * np.uint64(0xc2b2ae35)) & M)
+    h = h ^ (h >> np.uint64(16))
+    h = (h * np.uint64(0x85ebca6b)) & M
+    h = h ^ (h >> np.uint64(13))
+    h = (h * np.uint64(0xc2b2ae35)) & M
+    h = h ^ (h >> np.uint64(16))
+    return h
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+def test_gat_block_grad_oracle_dropout(golden, sparse):
+    """With dropout the oracle re-derives the HIP kernels' (seed, CSR edge, head) masks: checked
+    against torch float64 autograd of the same block with the mask applied where the reference
+    applies F.dropout (after the softmax, layers.py:30 / after the rowsum, :115; inverted,
+    scale 1 / (1 - p))."""
+    import torch
+    g = golden("gatgrad")
+    kind = "sparse" if sparse else "dense"
+    n, H, fh, rowptr, col, W, a_s, a_d = _gatgrad_inputs(g, kind)
+    p, seed, slope = 0.35, 0x1234_5678_9abc, float(g["alpha"])
+    r = c_oracle.gat_block_grad(rowptr, col, g["h"], W, a_s, a_d, g["gy"], H, fh, slope, sparse,
+                                drop_p=p, drop_seed=seed)
+    row = np.repeat(np.arange(n), np.diff(rowptr))
+    eid = np.arange(col.size)
+    x = torch.tensor(g["h"], dtype=torch.float64, requires_grad=True)
+    Wt = torch.tensor(W, dtype=torch.float64, requires_grad=True)
+    ast = torch.tensor(a_s, dtype=torch.float64, requires_grad=True)
+    adt = torch.tensor(a_d, dtype=torch.float64, requires_grad=True)
+    wh = (x @ Wt).view(n, H, fh)
+    el = (wh * ast.view(H, fh)).sum(-1)
+    er = (wh * adt.view(H, fh)).sum(-1)
+    outs = []
+    for h in range(H):
+        t = el[row, h] + er[col, h]
+        z = torch.nn.functional.leaky_relu(t, slope)
+        z = -z if sparse else z
+        dense = torch.full((n, n), float("-inf"), dtype=torch.float64)
+        dense = dense.index_put((torch.from_numpy(row), torch.from_numpy(col.astype(np.int64))), z)
+        att = torch.softmax(dense, dim=1)
+        keep = (_hash3(seed, eid, h) >> np.uint64(8)).astype(np.float64) / 16777216.0 >= p
+        m = torch.zeros((n, n), dtype=torch.float64)
+        m[torch.from_numpy(row), torch.from_numpy(col.astype(np.int64))] = \
+            torch.from_numpy(keep.astype(np.float64) / (1 - p))
+        outs.append(torch.nn.functional.elu((att * m) @ wh[:, h, :]))
+    out = torch.cat(outs, dim=1)
+    (out * torch.tensor(g["gy"], dtype=torch.float64)).sum().backward()
+    close(r["out"], out.detach().numpy(), rtol=1e-9, atol_frac=1e-9)
+    close(r["dW"], Wt.grad.numpy(), rtol=1e-9, atol_frac=1e-9)
+    close(r["da_src"], ast.grad.numpy(), rtol=1e-9, atol_frac=1e-9)
+    close(r["da_dst"], adt.grad.numpy(), rtol=1e-9, atol_frac=1e-9)
+    close(r["dx"], x.grad.numpy(), rtol=1e-9, atol_frac=1e-9)

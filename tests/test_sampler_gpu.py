@@ -283,7 +283,7 @@ def test_fused_batch_leaves_workspace_clean(dev):
         assert torch.equal(a.frontier, b.frontier) and torch.equal(a.neigh_map, b.neigh_map)
         for x, y in zip(a.center_maps, b.center_maps):
             assert torch.equal(x, y)
-        ws = S._SAMPLE_WS[(adj.device, adj.n_rows)]
+        ws = S._SAMPLE_WS[(adj.device, adj.n_rows, torch.cuda.current_stream(dev).cuda_stream)]
         assert int(ws[:32 * n_words].count_nonzero()) == 0
         if empty.size and it == 1:
             with pytest.raises(IndexError):
