@@ -647,11 +647,21 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
     autograd of GAT/models/layers.py:22-37 and SpecialSpmmFunction.backward :54-64) are also
     timed alone, each with a roofline on its compulsory bytes."""
     from graphneuralnetwork_amd.gat import GAT
-    from graphneuralnetwork_amd.ops import GAT_DENSE, gat_aggregate, gat_backward, gat_logits
+    from graphneuralnetwork_amd.ops import (GAT_DENSE, gat_aggregate, gat_backward, gat_logits,
+                                            gat_train_order)
     gen = torch.Generator(device=dev).manual_seed(3)
     net = GAT(X.shape[1], Fh, 3, dropout=0.0, alpha=0.2, nheads=H).to(dev).train()
     gy = torch.randn(g.n_rows, H * Fh, device=dev, generator=gen)
     steps = max(3, min(args.steps, 10))
+    # the block runs over the graph GATBase.forward trains on: P A P^T (nodes in degree order,
+    # gat_train_order; x permuted once per model forward, on entry) -- X, gy in that order
+    t0 = time.perf_counter()
+    order = gat_train_order(g, H, Fh)
+    torch.cuda.synchronize(dev)
+    order_s = time.perf_counter() - t0
+    g_nat, X_nat, gy_nat = g, X, gy
+    if order is not None:
+        g, X, gy = order.graph, order.permute_rows(X), order.permute_rows(gy)
 
     def step():
         net.zero_grad(set_to_none=True)
@@ -662,6 +672,23 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
     keep = {"y": net._heads(X, g)}
     bwd_ms = time_steps(lambda: keep["y"].backward(gy, retain_graph=True), steps, 2, dev)[0]
     del keep
+
+    def step_nat():
+        net.zero_grad(set_to_none=True)
+        net._heads(X_nat, g_nat).backward(gy_nat)
+
+    nat_ms = time_steps(step_nat, steps, 2, dev)[0] if order is not None else step_ms
+    # the whole GAT model (8 heads, ELU, out_att 64 -> 3, ELU; GAT/train_eval.py:75-76 with a
+    # NLL loss on log_softmax of the logits), x entering and the logits leaving in the
+    # original order (GATBase.forward's two permutes inside the step)
+    labels = torch.randint(0, 3, (g.n_rows,), device=dev, generator=gen)
+
+    def model_step():
+        net.zero_grad(set_to_none=True)
+        torch.nn.functional.nll_loss(torch.nn.functional.log_softmax(net(X_nat, g_nat), 1),
+                                     labels).backward()
+
+    model_ms = time_steps(model_step, steps, 2, dev)[0]
     # the three backward passes alone (the tensors the autograd Function saves)
     W = torch.cat([m.W for m in net.attentions], 1).detach()
     a_s = torch.cat([m._a_parts()[0] for m in net.attentions]).detach()
@@ -710,6 +737,15 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
            "step_ms": statistics.median(step_ms), "forward_ms": statistics.median(fwd_ms),
            "backward_ms": statistics.median(bwd_ms),
            "edges_per_s": nnz / (statistics.median(step_ms) / 1e3),
+           "node_order": ("P A P^T (gat_train_order: nodes relabelled by degree once per graph, "
+                          "%.2f s outside the timed region; X, dy in that order as "
+                          "GATBase.forward hands them to the block)" % order_s)
+                         if order is not None else "natural",
+           "natural_order_step_ms": statistics.median(nat_ms),
+           "model_step_ms": statistics.median(model_ms),
+           "model_step_what": "GAT(%d, %d, 3, dropout=0, nheads=%d) forward + NLL loss backward "
+                              "(both attention layers; x in and logits out in the original "
+                              "order)" % (X.shape[1], Fh, H),
            "forward_path": "X W on the MFMA transform (_ProjectFn) + gat_logits + the edge-head "
                            "gat_aggregate (er from the gathered rows) with per-row log-sum-exp "
                            "stats",
@@ -729,7 +765,7 @@ def gat_train_step(g, X, H: int, Fh: int, args, dev) -> dict:
                                                          a_d.cpu(), H, Fh)
         except Exception as e:
             res["cpu_reference_ops"] = {"error": repr(e)}
-    del net, gy, Wh, out, stats
+    del net, gy, Wh, out, stats, X_nat, gy_nat, g_nat
     torch.cuda.empty_cache()
     return res
 
@@ -1741,7 +1777,10 @@ def compact_line(res: dict, detail: str | None = None) -> dict:
                 t = res[k]["train_step"]
                 line["train_gat_cfg3"] = {"step_ms": t.get("step_ms"),
                                           "forward_ms": t.get("forward_ms"),
-                                          "backward_ms": t.get("backward_ms")}
+                                          "backward_ms": t.get("backward_ms"),
+                                          "natural_order_step_ms":
+                                              t.get("natural_order_step_ms"),
+                                          "model_step_ms": t.get("model_step_ms")}
     if detail:
         line["detail"] = detail
     line = _rnd(line)

@@ -284,6 +284,163 @@ __global__ __launch_bounds__(kTnThreads) void gemm_tn_mfma_kernel(
   }
 }
 
+// The same partials from bf16 MFMAs on three-piece splits (common.hpp split3: each fp32 operand
+// = v0 + v1 + v2 in bf16, the six piece products down to order 2^-16 summed in fp32 -- the
+// transforms' "X6" arithmetic, error per product at fp32 rounding). v_mfma_f32_32x32x16_bf16
+// takes 16 node rows per instruction: lane l holds A[rows 16 s + 8 (l >> 5) + j][column l & 31]
+// for j = 0..7 (cdna_hip_programming.md, the bf16 A / B lane maps), so each lane reads a
+// column strip of the staged tile: 8 ds_read_b32 down the rows, which the row pitch M + 4
+// (8 rows apart = 32 banks apart) keeps conflict-free for the two lane halves; the strips are
+// split in registers. 6 x 32 cycles per 16 rows x 32 x 32 outputs against 8 x 64 on the f32
+// MFMA: the kernel is left paced by its HBM reads. C/D lane map as the f32 form's.
+template <int M, int K, bool DSUM>
+__global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
+    const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb,
+    const float* __restrict__ d, int64_t ldd, int64_t n, int64_t rows_per_block,
+    float* __restrict__ part) {
+  constexpr int A4 = M / 4, B4 = K / 4;
+  constexpr int PA = M + 4, PB = K + 4;  // padded LDS row pitches (floats)
+  constexpr int NA = (kTnRows * A4 + kTnThreads - 1) / kTnThreads;
+  constexpr int NB = (kTnRows * B4 + kTnThreads - 1) / kTnThreads;
+  constexpr int QA = M / 32, QB = K / 32;
+  constexpr int S = 4 / QA;  // k-step streams per tile
+  __shared__ float4 sa[kTnRows * PA / 4];
+  __shared__ float4 sb[kTnRows * PB / 4];
+  __shared__ float red[S > 1 ? M * K : 1];
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int h = w % QA, s = w / QA;
+  const int i = lane & 31, kh = lane >> 5;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  f16x acc[QB];
+#pragma unroll
+  for (int q = 0; q < QB; ++q) acc[q] = f16x(0.f);
+  float4 ds[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) ds[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  auto load = [&](int64_t row0, float4 (&va)[NA], float4 (&vb)[NB], float4 (&vd)[NB]) {
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int e = t + q * kTnThreads;
+      const int64_t row = row0 + e / A4;
+      va[q] = (e < kTnRows * A4 && row < r1)
+                  ? *reinterpret_cast<const float4*>(a + row * lda + 4 * (e % A4))
+                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int e = t + q * kTnThreads;
+      const int64_t row = row0 + e / B4;
+      const bool ok = e < kTnRows * B4 && row < r1;
+      vb[q] = ok ? *reinterpret_cast<const float4*>(b + row * ldb + 4 * (e % B4))
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (DSUM)
+        vd[q] = ok ? *reinterpret_cast<const float4*>(d + row * ldd + 4 * (e % B4))
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+
+  float4 va[NA], vb[NB], vd[NB];
+  load(r0, va, vb, vd);
+  const float* saf = reinterpret_cast<const float*>(sa);
+  const float* sbf = reinterpret_cast<const float*>(sb);
+  for (int64_t row0 = r0; row0 < r1; row0 += kTnRows) {
+    __syncthreads();  // the previous tile's readers are done
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int e = t + q * kTnThreads;
+      if (e < kTnRows * A4) sa[(e / A4) * (PA / 4) + e % A4] = va[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int e = t + q * kTnThreads;
+      if (e < kTnRows * B4) sb[(e / B4) * (PB / 4) + e % B4] = vb[q];
+      if constexpr (DSUM) {
+        ds[q].x += vd[q].x;
+        ds[q].y += vd[q].y;
+        ds[q].z += vd[q].z;
+        ds[q].w += vd[q].w;
+      }
+    }
+    __syncthreads();
+    if (row0 + kTnRows < r1) load(row0 + kTnRows, va, vb, vd);  // next tile in flight
+    const int nsteps = static_cast<int>((min(static_cast<int64_t>(kTnRows), r1 - row0) + 15) / 16);
+    for (int st = s; st < nsteps; st += S) {  // rows past r1 were staged as zeros
+      const int rb = 16 * st + 8 * kh;
+      bf16x8 a0, a1, a2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __bf16 x0, x1, x2;
+        split3(saf[(rb + j) * PA + 32 * h + i], x0, x1, x2);
+        a0[j] = x0;
+        a1[j] = x1;
+        a2[j] = x2;
+      }
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        bf16x8 b0, b1, b2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          __bf16 y0, y1, y2;
+          split3(sbf[(rb + j) * PB + 32 * q + i], y0, y1, y2);
+          b0[j] = y0;
+          b1[j] = y1;
+          b2[j] = y2;
+        }
+        f16x c = acc[q];  // smallest terms first
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
+        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c, 0, 0, 0);
+      }
+    }
+  }
+  float* pc = part + static_cast<int64_t>(blockIdx.x) * (M * K + (DSUM ? K : 0));
+  for (int tt = S - 1; tt >= 0; --tt) {  // the S streams' partials, summed in s order
+    if (s == tt) {
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+#pragma unroll
+        for (int rg = 0; rg < 16; ++rg) {
+          const int m = 32 * h + (rg & 3) + 8 * (rg >> 2) + 4 * kh, nn = 32 * q + i;
+          float v = acc[q][rg];
+          if (tt < S - 1) v += red[m * K + nn];
+          if (tt > 0)
+            red[m * K + nn] = v;
+          else
+            pc[m * K + nn] = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (DSUM) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int e = t + q * kTnThreads;
+      if (e < kTnRows * B4) sb[e] = ds[q];
+    }
+    __syncthreads();
+    if (t < B4) {
+      float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int e = t; e < kTnRows * B4; e += B4) {
+        s4.x += sb[e].x;
+        s4.y += sb[e].y;
+        s4.z += sb[e].z;
+        s4.w += sb[e].w;
+      }
+      pc[M * K + 4 * t] = s4.x;
+      pc[M * K + 4 * t + 1] = s4.y;
+      pc[M * K + 4 * t + 2] = s4.z;
+      pc[M * K + 4 * t + 3] = s4.w;
+    }
+  }
+}
+
 // out[e] = the sum over the blocks' partials in a fixed order (e < M*K: C, then dsum). A
 // workgroup takes 64 consecutive elements; its 4 waves sum the partials g, g + 4, g + 8, ...
 // (coalesced 256-B rows of the partial array, 8 loads in flight per lane) and the 4 wave sums
@@ -325,6 +482,9 @@ __global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(const float* __rest
 }
 
 constexpr int64_t kTnBlocks = 512;  // 2 workgroups per CU
+#ifndef GNN_TN_X6  // A/B: 0 = the f32 MFMA kernel in either arithmetic mode
+#define GNN_TN_X6 1
+#endif
 
 static int64_t tn_blocks(int64_t n) {
   const int64_t by_rows = (n + 4 * kTnRows - 1) / (4 * kTnRows);  // >= 4 tiles per block
@@ -345,12 +505,20 @@ static int launch_tn(const float* a, int64_t lda, const float* b, int64_t ldb, c
   constexpr bool mfma = false;
 #endif
   if constexpr (mfma) {
-    if (d)
+    if (GNN_TN_X6 != 0 && g_tf_x6 != 0) {  // the transforms' arithmetic mode (set_precision)
+      if (d)
+        hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, true>), dim3(static_cast<unsigned>(blocks)),
+                           dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+      else
+        hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, false>), dim3(static_cast<unsigned>(blocks)),
+                           dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+    } else if (d) {
       hipLaunchKernelGGL((gemm_tn_mfma_kernel<M, K, true>), dim3(static_cast<unsigned>(blocks)),
                          dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
-    else
+    } else {
       hipLaunchKernelGGL((gemm_tn_mfma_kernel<M, K, false>), dim3(static_cast<unsigned>(blocks)),
                          dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+    }
   } else if (d) {
     hipLaunchKernelGGL((gemm_tn_partial_kernel<M, K, true>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);

@@ -26,10 +26,13 @@ At inference on graphs whose Wh is hub-staged, the layer runs over the column-de
 graph A P^T (``_AttentionBase._ordered``): the projection writes Wh / er in that column order
 and the aggregation reads their hub rows in place (no per-call staging copies).
 
-Training: the aggregation is an autograd Function whose backward is three
-more HIP passes (gat_bwd.hip: ELU/softmax backward, SDDMM edge gradients,
-transposed aggregation), with the forward's per-row log-sum-exp and dropout
-seed saved instead of the attention matrix; dropout masks are recomputed.
+Training: the aggregation is an autograd Function whose backward is two more
+HIP passes (gat_bwd.hip: a row pass -- ELU / softmax backward and the SDDMM
+edge gradients summed per row -- and a node pass that recomputes the edge
+weights over A^T), with the forward's per-row log-sum-exp and dropout seed
+saved instead of the attention matrix; dropout masks are recomputed. On large
+symmetric graphs the model trains over the degree-ordered graph P A P^T
+(``GATBase.forward``).
 """
 from __future__ import annotations
 
@@ -39,7 +42,7 @@ from torch import nn
 
 from .graph import as_csr
 from .ops import (GAT_DENSE, GAT_SPARSE, _transform_or_mm, gat_aggregate, gat_backward,
-                  gat_column_order, gat_logits, gat_project, gemm_tn)
+                  gat_column_order, gat_logits, gat_project, gat_train_order, gemm_tn)
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
@@ -249,8 +252,27 @@ class SpGraphAttentionLayer(_AttentionBase):
         return float(self.dropout.p)
 
 
+class _PermuteRows(torch.autograd.Function):
+    """y = x[perm] with the gradient gathered back through inv (a permutation: no index_add)."""
+
+    @staticmethod
+    def forward(ctx, x, perm, inv):
+        ctx.inv = inv
+        return x.index_select(0, perm)
+
+    @staticmethod
+    def backward(ctx, gy):
+        return gy.index_select(0, ctx.inv), None, None
+
+
 class GATBase(nn.Module):
-    """GAT/models/GAT.py:7-18: dropout -> concat(heads) -> dropout -> ELU(out_att)."""
+    """GAT/models/GAT.py:7-18: dropout -> concat(heads) -> dropout -> ELU(out_att).
+
+    Training on a large symmetric graph runs the whole model over P A P^T (``gat_train_order``:
+    nodes relabelled once by degree): x is permuted once on entry and the logits once on exit,
+    so every attention layer's forward and both backward passes read their hub rows at the top
+    of Wh / er / dout. Same function; the dropout draws (F.dropout's and the attention's
+    (seed, edge, head) hash) fall on the relabelled rows / edges."""
 
     def __init__(self, dropout, **kwargs):
         super().__init__(**kwargs)
@@ -280,11 +302,30 @@ class GATBase(nn.Module):
         return first._aggregate(Wh, adj, len(heads), fh, a_src, a_dst, "elu", first._drop_p(),
                                 logits)
 
+    def _train_order(self, x, adj):
+        """The node order training runs in (None: the graph's own, e.g. at inference, where
+        ``_ordered`` takes the column order instead)."""
+        if not (x.is_cuda and torch.is_grad_enabled()
+                and (x.requires_grad or any(p.requires_grad for p in self.parameters()))):
+            return None
+        g = as_csr(adj, self.attentions[0].PREDICATE)
+        if g.n_rows != x.shape[0]:
+            return None
+        first = self.attentions[0]
+        return gat_train_order(g, len(self.attentions), first.out_features)
+
     def forward(self, x, adj):
+        order = self._train_order(x, adj)
+        if order is not None:
+            x = _PermuteRows.apply(x, order.perm, order.inv)
+            adj = order.graph
         x = F.dropout(x, self.dropout, training=self.training)
         x = self._heads(x, adj)
         x = F.dropout(x, self.dropout, training=self.training)
-        return self.out_att(x, adj, activation="elu")  # F.elu(out_att(x)) fused (concat=False)
+        out = self.out_att(x, adj, activation="elu")  # F.elu(out_att(x)) fused (concat=False)
+        if order is not None:
+            out = _PermuteRows.apply(out, order.inv, order.perm)
+        return out
 
 
 class GAT(GATBase):

@@ -296,6 +296,34 @@ def gat_column_order(g: CsrGraph, heads: int, fh: int):
     return _cached_column_order(g)
 
 
+# GAT training (forward + both backward passes) over P A P^T: every node relabelled once by
+# degree, so the hub rows of Wh / er / dout are the first rows of each table for the forward,
+# the row pass and the node pass alike. cfg3 8-head block: 3.89 -> 3.41 ms, node pass 1.16 ->
+# 0.84 ms (profiles/r06c_gat_order_ab.log). GATBase.forward permutes x once on entry and the
+# logits once on exit (tools/gat_order_ab.py).
+GAT_TRAIN_ORDER = True
+
+
+def gat_train_order(g: CsrGraph, heads: int, fh: int):
+    """The cached ``DegreeOrder(rows=True)`` of a symmetric square ``g`` -- P A P^T, itself
+    symmetric (marked so: the node pass walks it as its own transpose) -- when the GAT
+    aggregation over it reads a table large enough to stage hub rows (else None). Each row's
+    edges keep their CSR order, renamed: the forward's row sums run in the same order as
+    over A."""
+    if not (DEGREE_ORDER and GAT_TRAIN_ORDER) or g.nnz == 0 or not g.symmetric \
+            or g.n_rows != g.n_cols or not g.col.is_cuda:
+        return None
+    if hub_rows_for(g.n_cols, heads * fh + heads) == 0:
+        return None
+    o = g._plans.get(("_nodeorder",))
+    if o is None:
+        from .graph import degree_order
+        o = degree_order(g, rows=True)
+        o.graph.symmetric = True  # P A P^T of a symmetric A
+        g._plans[("_nodeorder",)] = o
+    return o
+
+
 def _spmm_xcd_direct(lib, xp, x, feat, bias, out, seg, skip_empty, flags, stream):
     """The XCD-sliced SpMM of a degree-ordered graph (graph.degree_order): the hub rows are
     X's first k rows, so there is no staging copy. Pass 1 (plain kernel) reads the items'

@@ -355,9 +355,10 @@ def test_bench_variant_graphsage_cfg4_degree_ordered():
         assert np.isin(nb[r], c1[rp1[fr[r]]:rp1[fr[r] + 1]]).all()
 
 
+@pytest.mark.parametrize("order", ["degree", "natural"])
 @pytest.mark.parametrize("model,drop", [("GAT", 0.0), ("GAT", 0.3), ("SpGAT", 0.0),
                                         ("SpGAT", 0.3)])
-def test_gat_training_block_cfg3_vs_oracle(model, drop, monkeypatch):
+def test_gat_training_block_cfg3_vs_oracle(model, drop, order, monkeypatch):
     """bench.py's cfg3 training step at full size: the 8-head attention
     block of GAT / SpGAT(64, 8, ., 8) in train mode (GATBase._heads: _ProjectFn on the MFMA
     transform, _GatLayerFn's fused forward with per-row LSE stats, the two-pass HIP backward:
@@ -367,7 +368,9 @@ def test_gat_training_block_cfg3_vs_oracle(model, drop, monkeypatch):
     autograd in tests/test_oracle_golden.py): the block output, every head's dW and da, and dX
     on every row (the 32 hottest rows included), with and without dropout (the oracle re-derives
     the kernels' (seed, edge, head) masks). Replaces the HIP-vs-HIP check
-    (test_gat_gpu.py::test_gat_backward_two_pass_matches_three_pass_cfg3).
+    (test_gat_gpu.py::test_gat_backward_two_pass_matches_three_pass_cfg3). order "degree": the
+    block over P A P^T with X in that order, as GATBase.forward trains (ops.gat_train_order);
+    "natural": over A itself.
     Reference: GAT/models/layers.py:22-37, :54-64, :94-131. Tolerance 1e-4 relative."""
     from graphneuralnetwork_amd import gat as gat_mod
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
@@ -377,6 +380,11 @@ def test_gat_training_block_cfg3_vs_oracle(model, drop, monkeypatch):
     s, d = rmat_edges(n, 10_000_000, 0)
     g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n)
     del s, d
+    if order == "degree":
+        from graphneuralnetwork_amd.ops import gat_train_order
+        o = gat_train_order(g, H, fh)
+        assert o is not None and o.graph.symmetric
+        g = o.graph
     torch.manual_seed(1)
     net = getattr(gat_mod, model)(Fin, fh, 7, drop, 0.2, H).to(dev).train()
     monkeypatch.setattr(gat_mod, "_dropout_seed", lambda: seed)
@@ -422,6 +430,6 @@ def test_gat_training_block_cfg3_vs_oracle(model, drop, monkeypatch):
             report.append(f"{k}[no kink] {float(np.abs(hip - ref)[clean].max()) / scale:.2e}")
         if excess.max() > 0:
             bad.append((k, float(excess.max()), np.unravel_index(excess.argmax(), excess.shape)))
-    print(f"{model} dropout {drop}: kink (row, head) pairs {kinks}; max |hip - oracle| / "
+    print(f"{model} {order} order, dropout {drop}: kink (row, head) pairs {kinks}; max |hip - oracle| / "
           "max |oracle|: " + ", ".join(report))
     assert not bad, bad

@@ -637,3 +637,44 @@ def test_gat_er_recomputed_from_rows(dev, heads, fh, mode, hubs, monkeypatch):
         sf = torch.isfinite(s0)
         assert torch.equal(sf, torch.isfinite(s1))
         close(s1[sf].cpu().numpy(), s0[sf].cpu().numpy(), rtol=1e-5)
+
+
+@pytest.mark.parametrize("kind", ["GAT", "SpGAT"])
+def test_gat_training_in_degree_order_equals_natural(dev, kind, monkeypatch):
+    """GATBase.forward in training runs the model over P A P^T (ops.gat_train_order: x permuted
+    on entry, the logits on exit): logits and every parameter's gradient equal the
+    natural-order training step within fp32 rounding (dropout 0: the relabelled edges would
+    draw other masks), and x's gradient comes back in the original row order."""
+    from graphneuralnetwork_amd import gat as gat_mod
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.graph import CsrGraph
+    monkeypatch.setattr(ops, "HUB_MIN_X_BYTES", 0)
+    n, nfeat = 3000, 64
+    rowptr, col = _rand_csr(n, 8 * n, 23, hub=2200)
+    rows = np.repeat(np.arange(n), np.diff(rowptr))
+    key = np.unique(np.concatenate([rows * n + col, col.astype(np.int64) * n + rows,
+                                    np.arange(n) * (n + 1)]))  # symmetric, self-loops
+    r, c = key // n, (key % n).astype(np.int32)
+    rp = np.concatenate([[0], np.cumsum(np.bincount(r, minlength=n))]).astype(np.int64)
+
+    def graph():
+        return CsrGraph(torch.from_numpy(rp).to(dev), torch.from_numpy(c).to(dev),
+                        torch.ones(c.size, device=dev), n, n, symmetric=True)
+
+    torch.manual_seed(0)
+    model = getattr(gat_mod, kind)(nfeat, 8, 5, 0.0, 0.2, 8).to(dev).train()
+    x = torch.randn(n, nfeat, device=dev)
+    lab = torch.randint(0, 5, (n,), device=dev)
+    res = {}
+    for use in (True, False):
+        monkeypatch.setattr(ops, "GAT_TRAIN_ORDER", use)
+        g = graph()
+        xx = x.clone().requires_grad_(True)
+        model.zero_grad(set_to_none=True)
+        y = model(xx, g)
+        torch.nn.functional.nll_loss(torch.nn.functional.log_softmax(y, 1), lab).backward()
+        assert (("_nodeorder",) in g._plans) == use
+        res[use] = [y.detach(), xx.grad] + [p.grad.clone() for p in model.parameters()]
+    for a, b in zip(res[True], res[False]):
+        err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+        assert err < 1e-5, err

@@ -124,9 +124,20 @@ def test_gcn_layer_training_cfg2_full_size(dev):
 
 @pytest.mark.parametrize("m,k", [(128, 128), (64, 64), (128, 64), (64, 128), (8, 64)])
 @pytest.mark.parametrize("n", [1, 37, 20000, 300001])
-def test_gemm_tn_vs_float64(dev, m, k, n):
+@pytest.mark.parametrize("prec", ["split-bf16", "fp32-mfma"])
+def test_gemm_tn_vs_float64(dev, m, k, n, prec):
     """gnn_gemm_tn_f32 (the weight / bias gradients): A^T B and the column sums of D against
-    float64, plain and transposed output, strided rows, an empty row range; deterministic."""
+    float64, plain and transposed output, strided rows, an empty row range; deterministic. In
+    both arithmetic modes (split-bf16: gemm_tn_x6_kernel, the default; fp32-mfma)."""
+    from graphneuralnetwork_amd.ops import gemm_tn, set_transform_precision
+    prev = set_transform_precision(prec)
+    try:
+        _gemm_tn_case(dev, m, k, n)
+    finally:
+        set_transform_precision(prev)
+
+
+def _gemm_tn_case(dev, m, k, n):
     from graphneuralnetwork_amd.ops import gemm_tn
     gen = torch.Generator(device=dev).manual_seed(m + k + n)
     a = torch.randn(n, m + 4, device=dev, generator=gen)[:, :m]   # row stride m + 4

@@ -1,6 +1,8 @@
-"""A/B of the weight-gradient kernel (gnn_gemm_tn_f32) at the training shapes: the fp32-MFMA
-partials (main library) against the FMA partials (variant library ``tnfma``, -DGNN_TN_FMA) and
-hipBLASLt's torch.mm, HIP-event medians, interleaved in one process.
+"""A/B of the weight-gradient kernel (gnn_gemm_tn_f32) at the training shapes: the split-bf16
+MFMA partials (main library, the default arithmetic), the fp32-MFMA partials (main library under
+ops.set_transform_precision("fp32-mfma")), the FMA partials (variant library ``tnfma``,
+-DGNN_TN_FMA, when built) and hipBLASLt's torch.mm, HIP-event medians, interleaved in one
+process.
 
     python tools/gemm_tn_ab.py --build           (CPU side: the variant library)
     python tools/gemm_tn_ab.py [--reps 30]
@@ -31,9 +33,11 @@ def main():
     import torch
     from graphneuralnetwork_amd import _lib
     from graphneuralnetwork_amd.build import LIB_DIR
-    from graphneuralnetwork_amd.ops import gemm_tn
+    from graphneuralnetwork_amd.ops import gemm_tn, set_transform_precision
     dev = torch.device("cuda:0")
-    libs = {"mfma": None, "fma": LIB_DIR / "variants" / "libgnn_tnfma.so"}
+    libs = {"x6": (None, "split-bf16"), "f32mfma": (None, "fp32-mfma")}
+    if (LIB_DIR / "variants" / "libgnn_tnfma.so").exists():
+        libs["fma"] = (LIB_DIR / "variants" / "libgnn_tnfma.so", "split-bf16")
     out = {}
     for n, m, k, dsum in SHAPES:
         gen = torch.Generator(device=dev).manual_seed(n + m)
@@ -43,8 +47,9 @@ def main():
         ref = None
         times = {name: [] for name in list(libs) + ["torch_mm"]}
         diffs = {}
-        for name, lib in libs.items():
+        for name, (lib, prec) in libs.items():
             _lib.use_variant(lib)
+            set_transform_precision(prec)
             c = gemm_tn(x, y, d, trans=True)[0]
             torch.cuda.synchronize()
             if ref is None:
@@ -53,7 +58,8 @@ def main():
         for _ in range(a.reps):
             for name in times:
                 if name != "torch_mm":
-                    _lib.use_variant(libs[name])
+                    _lib.use_variant(libs[name][0])
+                    set_transform_precision(libs[name][1])
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -65,6 +71,7 @@ def main():
                 torch.cuda.synchronize()
                 times[name].append(e0.elapsed_time(e1))
         _lib.use_variant(None)
+        set_transform_precision("split-bf16")
         nbytes = 4 * n * (m + k + (k if dsum else 0))
         out[f"n{n}_m{m}_k{k}_dsum{int(dsum)}"] = {
             nm: {"median_ms": round(statistics.median(t), 4),
