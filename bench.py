@@ -1230,13 +1230,24 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
     same pass; hipBLASLt's torch.mm timed beside it). Each backward component is
     also timed alone; the backward SpMM carries its own roofline (compulsory bytes, as the
     forward's)."""
-    from graphneuralnetwork_amd.gcn import Graph_conv_layer
-    from graphneuralnetwork_amd.ops import gcn_transform, gemm_tn, spmm_forward
+    from graphneuralnetwork_amd.gcn import GCN_Model, Graph_conv_layer
+    from graphneuralnetwork_amd.ops import gcn_train_order, gcn_transform, gemm_tn, spmm_forward
     gen = torch.Generator(device=dev).manual_seed(1)
     layer = Graph_conv_layer(F, F).to(dev)
     X = torch.randn(g.n_cols, F, device=dev, generator=gen).requires_grad_(True)
     gy = torch.randn(g.n_rows, F, device=dev, generator=gen)
     steps = max(3, min(args.steps, 10))
+    # a hidden layer of GCN_Model in training runs over P A P^T (gcn_train_order: nodes in
+    # degree order, the model's input permuted once on entry): X, dY in that order
+    t0 = time.perf_counter()
+    order = gcn_train_order(g, F)
+    torch.cuda.synchronize(dev)
+    order_s = time.perf_counter() - t0
+    g_nat, X_nat, gy_nat = g, X, gy
+    if order is not None:
+        g = order.graph
+        X = order.permute_rows(X.detach()).requires_grad_(True)
+        gy = order.permute_rows(gy)
 
     def step():
         X.grad = None
@@ -1244,6 +1255,26 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
         layer(X, g).backward(gy)
 
     step_ms = time_steps(step, steps, 2, dev)[0]
+
+    def step_nat():
+        X_nat.grad = None
+        layer.zero_grad(set_to_none=True)
+        layer(X_nat, g_nat).backward(gy_nat)
+
+    nat_ms = time_steps(step_nat, steps, 2, dev)[0] if order is not None else step_ms
+    # the two-layer model, input and logits in the original order (GCN_Model.forward's two
+    # permutes inside the step), NLL loss (GCN/train_eval.py:43-48)
+    model = GCN_Model(F, F, 8, 2, 0.5).to(dev).train()
+    labels = torch.randint(0, 8, (g.n_rows,), device=dev, generator=gen)
+    Xm = X_nat.detach()
+
+    def model_step():
+        model.zero_grad(set_to_none=True)
+        torch.nn.functional.nll_loss(torch.nn.functional.log_softmax(model(Xm, g_nat), 1),
+                                     labels).backward()
+
+    model_ms = time_steps(model_step, steps, 2, dev)[0]
+    del model
     fwd_ms = time_steps(lambda: layer(X, g), steps, 2, dev)[0]
     keep = {"y": layer(X, g)}
     bwd_ms = time_steps(lambda: keep["y"].backward(gy, retain_graph=True), steps, 2, dev)[0]
@@ -1270,6 +1301,14 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
         "backward_ms": statistics.median(bwd_ms),
         "edges_per_s": 2 * g.nnz / (statistics.median(step_ms) / 1e3),
         "edges_note": "two SpMM passes per step (forward A S, backward A^T dY)",
+        "node_order": ("P A P^T (gcn_train_order: nodes relabelled by degree once per graph, "
+                       "%.2f s outside the timed region; X, dY in that order as GCN_Model's "
+                       "hidden layers see them)" % order_s) if order is not None else "natural",
+        "natural_order_step_ms": statistics.median(nat_ms),
+        "model_step_ms": statistics.median(model_ms),
+        "model_step_what": "GCN_Model(%d, %d, 8, num_layers=2, dropout=0.5).train() forward + "
+                           "NLL loss backward (x in and logits out in the original order)"
+                           % (F, F),
         "backward_components_ms": {
             "spmm_dS_AT_dY": statistics.median(spmm_ms),
             "transform_dX_dS_W": statistics.median(dx_ms),
@@ -1282,8 +1321,10 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
             "bound": "hbm", "achieved": comp / t_sp / 1e9, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": comp / t_sp / 1e9 / HBM_PEAK_GBPS, "compulsory_bytes": comp,
             "avg_launch_ms": t_sp * 1e3,
-            "kernel": "spmm_csr_kernel pass 1 + pass 2 (XCD-sliced hub staging of the natural-"
-                      "order graph: dY is not in the column order) + fix-up"},
+            "kernel": ("spmm_csr_kernel pass 1 + pass 2 over P A P^T (XCD-direct: dY's hub rows "
+                       "read in place) + fix-up") if order is not None else
+                      ("spmm_csr_kernel pass 1 + pass 2 (XCD-sliced hub staging of the natural-"
+                       "order graph: dY is not in the column order) + fix-up")},
         "roofline_backward_gemm_dW": {
             "bound": "hbm", "achieved": dw_bytes / (statistics.mean(dw_ms) / 1e3) / 1e9,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -1305,7 +1346,7 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
             res["cpu_reference_ops"] = cpu_gcn_train_ops(g, F)
         except Exception as e:  # reported, never the target
             res["cpu_reference_ops"] = {"error": repr(e)}
-    del X, gy, ds, layer
+    del X, gy, ds, layer, X_nat, gy_nat, Xm
     torch.cuda.empty_cache()
     return res
 
@@ -1766,7 +1807,9 @@ def compact_line(res: dict, detail: str | None = None) -> dict:
         t = res["train_step"]
         line["train_gcn_cfg2"] = {"step_ms": t.get("step_ms"), "forward_ms": t.get("forward_ms"),
                                   "backward_ms": t.get("backward_ms"),
-                                  "edges_per_s": t.get("edges_per_s")}
+                                  "edges_per_s": t.get("edges_per_s"),
+                                  "natural_order_step_ms": t.get("natural_order_step_ms"),
+                                  "model_step_ms": t.get("model_step_ms")}
     if isinstance(res.get("phases_ms"), dict):  # N > 1: the per-phase max over ranks
         line["phases_ms_max"] = res["phases_ms"].get("max_over_ranks")
         line["exchange_MB_rank0"] = res["phases_ms"].get("exchange_MB_rank0")

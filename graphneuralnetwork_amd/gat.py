@@ -41,8 +41,9 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
-from .ops import (GAT_DENSE, GAT_SPARSE, _transform_or_mm, gat_aggregate, gat_backward,
-                  gat_column_order, gat_logits, gat_project, gat_train_order, gemm_tn)
+from .ops import (GAT_DENSE, GAT_SPARSE, PermuteRows, _transform_or_mm, gat_aggregate,
+                  gat_backward, gat_column_order, gat_logits, gat_project, gat_train_order,
+                  gemm_tn)
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
@@ -252,19 +253,6 @@ class SpGraphAttentionLayer(_AttentionBase):
         return float(self.dropout.p)
 
 
-class _PermuteRows(torch.autograd.Function):
-    """y = x[perm] with the gradient gathered back through inv (a permutation: no index_add)."""
-
-    @staticmethod
-    def forward(ctx, x, perm, inv):
-        ctx.inv = inv
-        return x.index_select(0, perm)
-
-    @staticmethod
-    def backward(ctx, gy):
-        return gy.index_select(0, ctx.inv), None, None
-
-
 class GATBase(nn.Module):
     """GAT/models/GAT.py:7-18: dropout -> concat(heads) -> dropout -> ELU(out_att).
 
@@ -308,23 +296,25 @@ class GATBase(nn.Module):
         if not (x.is_cuda and torch.is_grad_enabled()
                 and (x.requires_grad or any(p.requires_grad for p in self.parameters()))):
             return None
-        g = as_csr(adj, self.attentions[0].PREDICATE)
+        heads = list(self.attentions)  # keys AttentionHead{i}: no integer indexing
+        if not heads:
+            return None
+        g = as_csr(adj, heads[0].PREDICATE)
         if g.n_rows != x.shape[0]:
             return None
-        first = self.attentions[0]
-        return gat_train_order(g, len(self.attentions), first.out_features)
+        return gat_train_order(g, len(heads), heads[0].out_features)
 
     def forward(self, x, adj):
         order = self._train_order(x, adj)
         if order is not None:
-            x = _PermuteRows.apply(x, order.perm, order.inv)
+            x = PermuteRows.apply(x, order.perm, order.inv)
             adj = order.graph
         x = F.dropout(x, self.dropout, training=self.training)
         x = self._heads(x, adj)
         x = F.dropout(x, self.dropout, training=self.training)
         out = self.out_att(x, adj, activation="elu")  # F.elu(out_att(x)) fused (concat=False)
         if order is not None:
-            out = _PermuteRows.apply(out, order.inv, order.perm)
+            out = PermuteRows.apply(out, order.inv, order.perm)
         return out
 
 

@@ -13,13 +13,17 @@ the feature transform ``support = dense(X)`` is an fp32 MFMA GEMM: the hand-writ
 ``gnn_gcn_transform_f32`` for the shapes it covers (F_in/F_out 64-256), otherwise nn.Linear
 on hipBLASLt. Under autograd the layer is one differentiable op (``ops.gcn_layer``): the same
 forward, and a backward of the SpMM over A^T (A itself: the normalised adjacency is
-symmetric), the MFMA transform for dX and a hipBLASLt GEMM for dW. ``adj`` may be the
+symmetric), the MFMA transform for dX and the tall-skinny A^T B kernel (gnn_gemm_tn_f32) for
+dW and d bias in one pass. ``adj`` may be the
 reference's sparse COO tensor, a sparse CSR tensor, a dense tensor or a prebuilt ``CsrGraph``;
 the CSR form is cached on the adjacency tensor.
 
 On graphs large enough for the XCD-sliced hub staging, the inference layer runs over the
 column-degree-ordered graph A P^T (``ops.column_order``): the transform writes the support
 rows in that order and the SpMM reads the hub rows in place, with no per-call staging copy.
+Training ``GCN_Model`` on such a (symmetric) graph runs every layer over P A P^T
+(``ops.gcn_train_order``: X permuted once on entry, the logits once on exit), so the backward
+SpMM dS = A dY reads its hub rows in place too.
 """
 from __future__ import annotations
 
@@ -28,7 +32,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
-from .ops import column_order, gcn_layer, gcn_transform, spmm, spmm_forward
+from .ops import (PermuteRows, column_order, gcn_layer, gcn_train_order, gcn_transform, spmm,
+                  spmm_forward)
 
 
 class GCN_Model(nn.Module):
@@ -49,7 +54,34 @@ class GCN_Model(nn.Module):
                 self.gcn_blocks.add_module(f'relu{i}', nn.ReLU())
                 self.gcn_blocks.add_module(f'dropout{i}', nn.Dropout(dropout))
 
+    def _train_order(self, X, adj):
+        """The degree-ordered graph P A P^T training runs over (ops.gcn_train_order), or None
+        (inference -- the layers take the column order there -- or a graph it does not pay
+        for)."""
+        if not (isinstance(X, torch.Tensor) and X.is_cuda and torch.is_grad_enabled()
+                and (X.requires_grad or any(p.requires_grad for p in self.parameters()))):
+            return None
+        layers = [m for m in self.gcn_blocks if isinstance(m, Graph_conv_layer)]
+        if not layers:
+            return None
+        g = as_csr(adj)
+        if g.n_cols != X.shape[0]:
+            return None
+        return gcn_train_order(g, layers[0].out_features)
+
     def forward(self, X, adj):
+        order = self._train_order(X, adj)
+        if order is not None:
+            # training over P A P^T: X in on its rows once, the logits back out once; every
+            # layer's SpMM (forward, and dS = A dY in backward) reads its hub rows in place
+            X = PermuteRows.apply(X, order.perm, order.inv)
+            adj = order.graph
+        X = self._blocks(X, adj)
+        if order is not None:
+            X = PermuteRows.apply(X, order.inv, order.perm)
+        return X
+
+    def _blocks(self, X, adj):
         blocks = list(self.gcn_blocks)
         i = 0
         while i < len(blocks):

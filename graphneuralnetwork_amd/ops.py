@@ -278,7 +278,7 @@ def _cached_column_order(g: CsrGraph):
 def column_order(g: CsrGraph, feat: int):
     """The cached ``DegreeOrder(rows=False)`` of ``g`` when a feat-wide SpMM over it would
     take the XCD-sliced hub path (else None)."""
-    if not (DEGREE_ORDER and XCD_DIRECT) or g.nnz < XCD_MIN_NNZ:
+    if not (DEGREE_ORDER and XCD_DIRECT) or g.nnz < XCD_MIN_NNZ or g._plans.get("_degree_ordered"):
         return None
     if xcd_hub_rows_for(g.n_cols, feat) < 8 * XCD_PHASES:
         return None
@@ -289,39 +289,72 @@ def gat_column_order(g: CsrGraph, heads: int, fh: int):
     """The cached ``DegreeOrder(rows=False)`` of ``g`` when the GAT aggregation over it would
     stage hub rows of Wh / er (``hub_rows_for``; else None): over A P^T those rows are the
     first rows of the projection's column-ordered output, read in place."""
-    if not (DEGREE_ORDER and XCD_DIRECT) or g.nnz == 0:
+    if not (DEGREE_ORDER and XCD_DIRECT) or g.nnz == 0 or g._plans.get("_degree_ordered"):
         return None
     if hub_rows_for(g.n_cols, heads * fh + heads) == 0:
         return None
     return _cached_column_order(g)
 
 
-# GAT training (forward + both backward passes) over P A P^T: every node relabelled once by
-# degree, so the hub rows of Wh / er / dout are the first rows of each table for the forward,
-# the row pass and the node pass alike. cfg3 8-head block: 3.89 -> 3.41 ms, node pass 1.16 ->
-# 0.84 ms (profiles/r06c_gat_order_ab.log). GATBase.forward permutes x once on entry and the
-# logits once on exit (tools/gat_order_ab.py).
+# Training (forward + backward) over P A P^T: every node relabelled once by degree, so the hub
+# rows of every gathered table (X / S, Wh / er, dY / dout) are its first rows in the forward and
+# in both backward passes, read in place (XCD-direct hub plans, no staging copy). The models
+# (GATBase.forward, GCN_Model.forward) permute their input once on entry and the logits once
+# on exit. cfg3 8-head GAT block: 3.89 -> 3.41 ms, node pass 1.16 -> 0.84 ms
+# (profiles/r06c_gat_order_ab.log, tools/gat_order_ab.py).
 GAT_TRAIN_ORDER = True
+GCN_TRAIN_ORDER = True
 
 
-def gat_train_order(g: CsrGraph, heads: int, fh: int):
-    """The cached ``DegreeOrder(rows=True)`` of a symmetric square ``g`` -- P A P^T, itself
-    symmetric (marked so: the node pass walks it as its own transpose) -- when the GAT
-    aggregation over it reads a table large enough to stage hub rows (else None). Each row's
-    edges keep their CSR order, renamed: the forward's row sums run in the same order as
-    over A."""
-    if not (DEGREE_ORDER and GAT_TRAIN_ORDER) or g.nnz == 0 or not g.symmetric \
-            or g.n_rows != g.n_cols or not g.col.is_cuda:
-        return None
-    if hub_rows_for(g.n_cols, heads * fh + heads) == 0:
-        return None
+def node_order(g: CsrGraph):
+    """The cached ``DegreeOrder(rows=True)`` of a symmetric square graph: P A P^T, itself
+    symmetric (marked so: backward passes walk it as its own transpose) and marked
+    ``_degree_ordered`` (column_order / gat_column_order then return None for it: its hub rows
+    already lead every table). Each row's edges keep their CSR order, renamed: the row sums run
+    in the same order as over A."""
     o = g._plans.get(("_nodeorder",))
     if o is None:
         from .graph import degree_order
         o = degree_order(g, rows=True)
         o.graph.symmetric = True  # P A P^T of a symmetric A
+        o.graph._plans["_degree_ordered"] = True
         g._plans[("_nodeorder",)] = o
     return o
+
+
+def _orderable(g: CsrGraph) -> bool:
+    return (DEGREE_ORDER and g.nnz > 0 and g.symmetric and g.n_rows == g.n_cols
+            and g.col.is_cuda and not g._plans.get("_degree_ordered"))
+
+
+def gat_train_order(g: CsrGraph, heads: int, fh: int):
+    """``node_order(g)`` when GAT training over it pays: a symmetric graph whose Wh / er table
+    is large enough to stage hub rows (else None)."""
+    if not (GAT_TRAIN_ORDER and _orderable(g)) or hub_rows_for(g.n_cols, heads * fh + heads) == 0:
+        return None
+    return node_order(g)
+
+
+def gcn_train_order(g: CsrGraph, feat: int):
+    """``node_order(g)`` when GCN training over it pays: a symmetric graph whose feat-wide
+    SpMM takes the XCD-sliced hub path (else None)."""
+    if not (GCN_TRAIN_ORDER and _orderable(g)) or column_order(g, feat) is None:
+        return None
+    return node_order(g)
+
+
+class PermuteRows(torch.autograd.Function):
+    """y = x[perm] with the gradient gathered back through inv (a permutation: no index_add):
+    the models' one relabelling on entry to and exit from the degree-ordered graph."""
+
+    @staticmethod
+    def forward(ctx, x, perm, inv):
+        ctx.inv = inv
+        return x.index_select(0, perm)
+
+    @staticmethod
+    def backward(ctx, gy):
+        return gy.index_select(0, ctx.inv), None, None
 
 
 def _spmm_xcd_direct(lib, xp, x, feat, bias, out, seg, skip_empty, flags, stream):

@@ -83,11 +83,14 @@ def test_symmetric_graph_is_its_own_transpose(dev):
     assert plain.transpose() is plain and plain.symmetric and plain._transpose is None
 
 
-def test_gcn_layer_training_cfg2_full_size(dev):
+@pytest.mark.parametrize("order", ["natural", "degree"])
+def test_gcn_layer_training_cfg2_full_size(dev, order):
     """The benchmarked training step at BASELINE cfg2 size (R-MAT 1M / 20.1M nnz, 128 -> 128):
-    the forward takes the column-ordered path and equals the inference layer bit for bit; the
-    gradients equal float64 references built from the C oracle's SpMM (dS = A dY, A
-    symmetric) and numpy products (dX = dS W, dW = dS^T X, db = sum dY) on every row."""
+    the forward takes the column-ordered path (natural) or the degree-ordered graph P A P^T
+    GCN_Model trains over (degree: ops.gcn_train_order, XCD-direct hub plans in both
+    directions) and equals the inference layer bit for bit; the gradients equal float64
+    references built from the C oracle's SpMM (dS = A dY, A symmetric) and numpy products
+    (dX = dS W, dW = dS^T X, db = sum dY) on every row."""
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.gcn import Graph_conv_layer
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
@@ -97,6 +100,9 @@ def test_gcn_layer_training_cfg2_full_size(dev):
     g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
     assert g.nnz == 20_073_500 and g.symmetric
     assert ops.column_order(g, 128) is not None
+    if order == "degree":
+        g = ops.gcn_train_order(g, 128).graph
+        assert g.symmetric and ops.column_order(g, 128) is None
     gen = torch.Generator(device=dev).manual_seed(5)
     layer = Graph_conv_layer(128, 128).to(dev)
     with torch.no_grad():
@@ -200,3 +206,34 @@ def test_gat_training_grads_use_tn_kernel(dev):
     ga_d = torch.cat([m.a.grad.view(-1)[8:] for m in net.attentions]).cpu().numpy()
     close(ga_s, a_s.grad.numpy())
     close(ga_d, a_d.grad.numpy())
+
+
+def test_gcn_model_training_in_degree_order_equals_natural(dev, monkeypatch):
+    """GCN_Model in training runs over P A P^T (ops.gcn_train_order: X permuted on entry, the
+    logits on exit): logits and every gradient equal the natural-order step to fp32 rounding
+    (dropout 0), X's gradient back in the original row order."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.gcn import GCN_Model
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    monkeypatch.setattr(ops, "XCD_MIN_NNZ", 0)
+    monkeypatch.setattr(ops, "HUB_MIN_X_BYTES", 0)
+    n = 60_000
+    s, d = rmat_edges(n, 500_000, 3)
+    torch.manual_seed(0)
+    model = GCN_Model(128, 128, 6, 2, 0.0).to(dev).train()
+    X = torch.randn(n, 128, device=dev)
+    lab = torch.randint(0, 6, (n,), device=dev)
+    res = {}
+    for use in (True, False):
+        monkeypatch.setattr(ops, "GCN_TRAIN_ORDER", use)
+        g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
+        xx = X.clone().requires_grad_(True)
+        model.zero_grad(set_to_none=True)
+        y = model(xx, g)
+        torch.nn.functional.nll_loss(torch.nn.functional.log_softmax(y, 1), lab).backward()
+        assert (("_nodeorder",) in g._plans) == use
+        res[use] = [y.detach(), xx.grad] + [p.grad.clone() for p in model.parameters()]
+    for a, b in zip(res[True], res[False]):
+        err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+        assert err < 1e-5, err
