@@ -427,7 +427,9 @@ def test_gat_training_block_cfg3_vs_oracle(model, drop, order, monkeypatch):
         report.append(f"{k} {float(np.abs(hip - ref).max()) / scale:.2e}")
         if not normwise and np.ndim(slack) == 2:  # rows no kink edge reaches
             clean = np.abs(slack).max(1) == 0
-            report.append(f"{k}[no kink] {float(np.abs(hip - ref)[clean].max()) / scale:.2e}")
+            if clean.any():
+                report.append(f"{k}[no kink] "
+                              f"{float(np.abs(hip - ref)[clean].max()) / scale:.2e}")
         if excess.max() > 0:
             bad.append((k, float(excess.max()), np.unravel_index(excess.argmax(), excess.shape)))
     print(f"{model} {order} order, dropout {drop}: kink (row, head) pairs {kinks}; max |hip - oracle| / "

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--workload", default="cfg2", choices=("cfg2", "ns"))
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--table-rows", type=int, default=2048)
+    ap.add_argument("--only", default=None,
+                    help="one variant (a_as_built, b_hub_to_L2_table, ...): per-kernel traces")
     a = ap.parse_args()
     import bench
     from graphneuralnetwork_amd.graph import XcdHubPlan
@@ -68,6 +70,8 @@ def main():
                                                                 r0)),
         "d_all_to_L2_table": (i0 % T, torch.where(r0 >= 0, r0 % T, r0)),
     }
+    if a.only:
+        variants = {a.only: variants[a.only]}
     times = {v: [] for v in variants}
     for _ in range(a.reps):
         for v, (ic, rc) in variants.items():
@@ -86,8 +90,9 @@ def main():
     res = {v: {"median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
                "compulsory_frac": round(comp / (statistics.median(t) / 1e3) / 8e12, 4)}
            for v, t in times.items()}
-    a_ms = res["a_as_built"]["median_ms"]
-    res["a_over_b"] = round(a_ms / res["b_hub_to_L2_table"]["median_ms"], 3)
+    if "a_as_built" in res and "b_hub_to_L2_table" in res:
+        res["a_over_b"] = round(res["a_as_built"]["median_ms"] /
+                                res["b_hub_to_L2_table"]["median_ms"], 3)
     res["workload"] = a.workload
     res.update(counts)
     print(json.dumps(res, indent=1), flush=True)
