@@ -538,7 +538,7 @@ using namespace gnn;
 
 extern "C" int gnn_gemm_tn_supported(int64_t m, int64_t k) {
   return (m == 128 && k == 128) || (m == 64 && k == 64) || (m == 128 && k == 64) ||
-         (m == 64 && k == 128) || (m == 8 && k == 64);
+         (m == 64 && k == 128) || (m == 8 && k == 64) || (m == 16 && k == 64);
 }
 
 extern "C" int64_t gnn_gemm_tn_workspace_bytes(int64_t n, int64_t m, int64_t k) {
@@ -573,5 +573,7 @@ extern "C" int gnn_gemm_tn_f32(const float* a, int64_t lda, const float* b, int6
     return launch_tn<128, 64>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
   if (m == 64 && k == 128)
     return launch_tn<64, 128>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
+  if (m == 16 && k == 64)  // [del | der] against Wh: both GAT a-vector gradients in one pass
+    return launch_tn<16, 64>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
   return launch_tn<8, 64>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
 }

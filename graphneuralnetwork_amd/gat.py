@@ -81,8 +81,14 @@ class _GatLayerFn(torch.autograd.Function):
 
 def _attention_vector_grads(Wh, dl, der, heads, fh):
     """d a_src[h, f] = sum_n dl[n, h] Wh[n, h, f] (el = a_src . Wh) and likewise d a_dst with der:
-    the diagonal [h, h*fh:(h+1)*fh] blocks of dl^T Wh, one pass over Wh each (gnn_gemm_tn_f32)
-    where the shape is covered, else the torch reduction."""
+    the diagonal [h, h*fh:(h+1)*fh] blocks of dl^T Wh and der^T Wh -- both from ONE pass over
+    Wh ([dl | der]^T Wh, gnn_gemm_tn_f32) where the shape is covered, else one pass each, else
+    the torch reduction."""
+    both = gemm_tn(torch.cat([dl, der], 1), Wh)
+    if both is not None:
+        c = both[0].view(2, heads, heads, fh)
+        idx = torch.arange(heads, device=Wh.device)
+        return c[0, idx, idx].reshape(-1), c[1, idx, idx].reshape(-1)
     out = []
     for g in (dl, der):
         r = gemm_tn(g, Wh)
@@ -253,6 +259,32 @@ class SpGraphAttentionLayer(_AttentionBase):
         return float(self.dropout.p)
 
 
+class _HeadParams(torch.autograd.Function):
+    """The H heads' parameters side by side: W = [W_1 | ... | W_H] ([in, H fh]), a_src / a_dst
+    = the heads' a[:fh] / a[fh:] concatenated (GAT.py:16 runs the heads as one layer here).
+    Backward hands every head its gradients as contiguous views of two buffers -- dW
+    regrouped per head by one copy, [da_src | da_dst] per head by one -- which AccumulateGrad
+    takes as they are: two kernels per step where torch.cat / slicing autograd took ~40 tiny
+    copies, fills and adds (~0.2 ms at cfg3, profiles/r06f_*)."""
+
+    @staticmethod
+    def forward(ctx, n_heads, *params):
+        Ws, As = params[:n_heads], params[n_heads:]
+        fh = Ws[0].shape[1]
+        ctx.shapes = (n_heads, Ws[0].shape[0], fh, [a.shape for a in As])
+        a = torch.stack([t.reshape(-1) for t in As])  # [H, 2 fh]
+        return (torch.cat(Ws, dim=1), a[:, :fh].reshape(-1).contiguous(),
+                a[:, fh:].reshape(-1).contiguous())
+
+    @staticmethod
+    def backward(ctx, dW, da_src, da_dst):
+        H, fin, fh, a_shapes = ctx.shapes
+        dWs = dW.reshape(fin, H, fh).permute(1, 0, 2).contiguous()          # [H, in, fh]
+        da = torch.cat([da_src.reshape(H, fh), da_dst.reshape(H, fh)], dim=1)  # [H, 2 fh]
+        return (None, *[dWs[h] for h in range(H)],
+                *[da[h].view(a_shapes[h]) for h in range(H)])
+
+
 class GATBase(nn.Module):
     """GAT/models/GAT.py:7-18: dropout -> concat(heads) -> dropout -> ELU(out_att).
 
@@ -277,10 +309,8 @@ class GATBase(nn.Module):
         if not uniform:
             return torch.cat([att(x, adj) for att in heads], dim=1)
         fh = first.out_features
-        W = torch.cat([m.W for m in heads], dim=1)          # [in, H*fh]
-        parts = [m._a_parts() for m in heads]
-        a_src = torch.cat([p[0] for p in parts])
-        a_dst = torch.cat([p[1] for p in parts])
+        W, a_src, a_dst = _HeadParams.apply(len(heads), *[m.W for m in heads],
+                                            *[m.a for m in heads])  # [in, H*fh], [H*fh] x 2
         out = first._ordered(x, W, len(heads), fh, a_src, a_dst, adj, "elu")
         if out is not None:
             return out

@@ -128,7 +128,8 @@ def test_gcn_layer_training_cfg2_full_size(dev, order):
     close(X.grad.cpu().numpy(), dS @ W)
 
 
-@pytest.mark.parametrize("m,k", [(128, 128), (64, 64), (128, 64), (64, 128), (8, 64)])
+@pytest.mark.parametrize("m,k", [(128, 128), (64, 64), (128, 64), (64, 128), (8, 64),
+                                 (16, 64)])
 @pytest.mark.parametrize("n", [1, 37, 20000, 300001])
 @pytest.mark.parametrize("prec", ["split-bf16", "fp32-mfma"])
 def test_gemm_tn_vs_float64(dev, m, k, n, prec):

@@ -1,7 +1,8 @@
 """The benchmarked training steps alone, for a kernel trace (rocprofv3 --kernel-trace --stats):
 the cfg2 Graph_conv_layer(128, 128) step (X requiring grad) or the cfg3 8 x 8-head GAT block
-step (W, a_src, a_dst requiring grad), as bench.py's gcn_train_step / gat_train_step; prints the
-HIP-event median step time.
+step (W, a_src, a_dst requiring grad), as bench.py's gcn_train_step / gat_train_step (over the
+degree-ordered graph P A P^T the models train on, unless --natural); prints the HIP-event
+median step time.
 
     python tools/train_step_probe.py --model gcn|gat [--steps 10] [--er-gather]
 """
@@ -24,6 +25,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--er-gather", action="store_true",
                     help="GAT: er loaded, not recomputed from the gathered rows")
+    ap.add_argument("--natural", action="store_true",
+                    help="the natural-order graph (default: P A P^T, as the models train)")
     a = ap.parse_args()
     if a.er_gather:
         from graphneuralnetwork_amd import ops
@@ -35,6 +38,10 @@ def main():
     s, d = rmat_edges(n, m, 0)
     g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
     gen = torch.Generator(device=dev).manual_seed(1)
+    from graphneuralnetwork_amd.ops import gat_train_order, gcn_train_order
+    if not a.natural:
+        o = gcn_train_order(g, 128) if a.model == "gcn" else gat_train_order(g, 8, 8)
+        g = o.graph if o is not None else g
     if a.model == "gcn":
         from graphneuralnetwork_amd.gcn import Graph_conv_layer
         net = Graph_conv_layer(128, 128).to(dev)
