@@ -441,6 +441,155 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
   }
 }
 
+// Narrow outputs (K <= 16, M <= 128: the classifier layers' weight gradients, e.g.
+// GCN_Model's last Graph_conv_layer(128, 7) dW = dS^T X, or a 1-head out_att with 7 classes),
+// where a library GEMM took 1.4-2.1 ms at 1M rows. No LDS tiles: each wave walks chunks of 64
+// rows; lane l holds row l's B (and D) values in registers (K scalar loads), and for each row of
+// the chunk the wave reads A's row coalesced (lane = column m, MP = 1 or 2 columns per lane) and
+// takes that row's K B values by v_readlane, so every product is one v_fma with a uniform
+// operand. The 4 waves of a workgroup are summed in wave order through LDS (deterministic),
+// the workgroup partials by gemm_tn_reduce_kernel.
+constexpr int kNarrowK = 16, kNarrowM = 128;
+constexpr int kNarrowRowsInFlight = 16;
+
+template <bool DSUM, int MP>
+__global__ __launch_bounds__(kTnThreads) void gemm_tn_narrow_kernel(
+    const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb,
+    const float* __restrict__ d, int64_t ldd, int64_t n, int64_t rows_per_block, int M, int K,
+    float* __restrict__ part) {
+  __shared__ float red[kTnThreads / kWave][kNarrowM * kNarrowK + kNarrowK];
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+  constexpr int W = kTnThreads / kWave;
+  const int MK = M * K;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  float acc[MP][kNarrowK];
+#pragma unroll
+  for (int p = 0; p < MP; ++p)
+#pragma unroll
+    for (int k = 0; k < kNarrowK; ++k) acc[p][k] = 0.f;
+  float dacc[DSUM ? kNarrowK : 1];
+#pragma unroll
+  for (int k = 0; k < (DSUM ? kNarrowK : 1); ++k) dacc[k] = 0.f;
+  for (int64_t base = r0 + static_cast<int64_t>(w) * kWave; base < r1; base += W * kWave) {
+    const int64_t row = base + lane;
+    const bool ok = row < r1;
+    float brow[kNarrowK];
+#pragma unroll
+    for (int k = 0; k < kNarrowK; ++k) {
+      brow[k] = (ok && k < K) ? b[row * ldb + k] : 0.f;
+      if constexpr (DSUM) dacc[k] += (ok && k < K) ? d[row * ldd + k] : 0.f;
+    }
+    const int nr = static_cast<int>(min(static_cast<int64_t>(kWave), r1 - base));
+    for (int rr = 0; rr < nr; rr += kNarrowRowsInFlight) {
+      float av[kNarrowRowsInFlight][MP];
+#pragma unroll
+      for (int u = 0; u < kNarrowRowsInFlight; ++u)
+#pragma unroll
+        for (int p = 0; p < MP; ++p) {
+          const int m = lane + kWave * p;
+          av[u][p] = (rr + u < nr && m < M) ? a[(base + rr + u) * lda + m] : 0.f;
+        }
+#pragma unroll
+      for (int u = 0; u < kNarrowRowsInFlight; ++u) {
+        const int src = (rr + u) & (kWave - 1);  // wave-uniform
+#pragma unroll
+        for (int k = 0; k < kNarrowK; ++k) {
+          if (k < K) {  // uniform
+            const float bk =
+                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(brow[k]), src));
+#pragma unroll
+            for (int p = 0; p < MP; ++p) acc[p][k] = fmaf(av[u][p], bk, acc[p][k]);
+          }
+        }
+      }
+    }
+  }
+  // this wave's partial -> LDS; workgroup sum in wave order
+#pragma unroll
+  for (int p = 0; p < MP; ++p) {
+    const int m = lane + kWave * p;
+    if (m < M)
+#pragma unroll
+      for (int k = 0; k < kNarrowK; ++k)
+        if (k < K) red[w][m * K + k] = acc[p][k];
+  }
+  if constexpr (DSUM) {
+#pragma unroll
+    for (int k = 0; k < kNarrowK; ++k) {
+      float v = dacc[k];
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) v += __shfl_xor(v, o, kWave);
+      if (lane == 0 && k < K) red[w][MK + k] = v;
+    }
+  }
+  __syncthreads();
+  float* pc = part + static_cast<int64_t>(blockIdx.x) * (MK + (DSUM ? K : 0));
+  for (int e = threadIdx.x; e < MK + (DSUM ? K : 0); e += kTnThreads) {
+    float v = red[0][e];
+#pragma unroll
+    for (int q = 1; q < W; ++q) v += red[q][e];
+    pc[e] = v;
+  }
+}
+
+// Tiny outputs (M * K <= 32: the a-vector gradients of a 1-head out_att, [del | der]^T Wh with
+// M = 2): lane = row, every lane accumulates all M x K products of its rows in registers, the
+// wave's lanes are summed by an xor tree and the 4 waves in order through LDS.
+constexpr int kTinyOut = 32;
+
+template <bool DSUM>
+__global__ __launch_bounds__(kTnThreads) void gemm_tn_tiny_kernel(
+    const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb,
+    const float* __restrict__ d, int64_t ldd, int64_t n, int64_t rows_per_block, int M, int K,
+    float* __restrict__ part) {
+  __shared__ float red[kTnThreads / kWave][kTinyOut + kNarrowK];
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+  const int MK = M * K;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  float acc[kTinyOut], dacc[DSUM ? kNarrowK : 1];
+#pragma unroll
+  for (int o = 0; o < kTinyOut; ++o) acc[o] = 0.f;
+#pragma unroll
+  for (int k = 0; k < (DSUM ? kNarrowK : 1); ++k) dacc[k] = 0.f;
+  for (int64_t row = r0 + threadIdx.x; row < r1; row += kTnThreads) {
+    float av[kTinyOut], bv[kNarrowK];
+#pragma unroll
+    for (int m = 0; m < kTinyOut; ++m) av[m] = m < M ? a[row * lda + m] : 0.f;
+#pragma unroll
+    for (int k = 0; k < kNarrowK; ++k) {
+      bv[k] = k < K ? b[row * ldb + k] : 0.f;
+      if constexpr (DSUM) dacc[k] += k < K ? d[row * ldd + k] : 0.f;
+    }
+#pragma unroll
+    for (int o = 0; o < kTinyOut; ++o)
+      if (o < MK) acc[o] = fmaf(av[o / K < kTinyOut ? o / K : 0], bv[(o % K) & (kNarrowK - 1)],
+                                acc[o]);
+  }
+#pragma unroll
+  for (int o = 0; o < kTinyOut + (DSUM ? kNarrowK : 0); ++o) {
+    if (o >= kTinyOut && o - kTinyOut >= K) continue;
+    if (o < kTinyOut && o >= MK) continue;
+    float v = o < kTinyOut ? acc[o] : (DSUM ? dacc[(o - kTinyOut) & (kNarrowK - 1)] : 0.f);
+#pragma unroll
+    for (int q = 1; q < kWave; q <<= 1) v += __shfl_xor(v, q, kWave);
+    if (lane == 0) red[w][o < kTinyOut ? o : MK + (o - kTinyOut)] = v;
+  }
+  __syncthreads();
+  float* pc = part + static_cast<int64_t>(blockIdx.x) * (MK + (DSUM ? K : 0));
+  for (int e = threadIdx.x; e < MK + (DSUM ? K : 0); e += kTnThreads) {
+    float v = red[0][e];
+#pragma unroll
+    for (int q = 1; q < kTnThreads / kWave; ++q) v += red[q][e];
+    pc[e] = v;
+  }
+}
+
+static bool tn_narrow(int64_t m, int64_t k) {
+  return m >= 1 && k >= 1 && m <= kNarrowM && k <= kNarrowK;
+}
+
 // out[e] = the sum over the blocks' partials in a fixed order (e < M*K: C, then dsum). A
 // workgroup takes 64 consecutive elements; its 4 waves sum the partials g, g + 4, g + 8, ...
 // (coalesced 256-B rows of the partial array, 8 loads in flight per lane) and the 4 wave sums
@@ -536,14 +685,27 @@ static int launch_tn(const float* a, int64_t lda, const float* b, int64_t ldb, c
 
 using namespace gnn;
 
-extern "C" int gnn_gemm_tn_supported(int64_t m, int64_t k) {
+static bool tn_wide(int64_t m, int64_t k) {
   return (m == 128 && k == 128) || (m == 64 && k == 64) || (m == 128 && k == 64) ||
          (m == 64 && k == 128) || (m == 8 && k == 64) || (m == 16 && k == 64);
 }
 
+// 1: a wide shape (16-B aligned rows, strides multiples of 4 floats); 2: a narrow one (K <= 16,
+// M <= 128; any row stride, 4-B aligned); 0: not covered
+extern "C" int gnn_gemm_tn_supported(int64_t m, int64_t k) {
+  return tn_wide(m, k) ? 1 : (tn_narrow(m, k) ? 2 : 0);
+}
+
+// the narrow / tiny kernels are latency-bound row walks: 4x the workgroups (32 waves per CU)
+static int64_t tn_blocks_for(int64_t n, int64_t m, int64_t k) {
+  if (tn_wide(m, k)) return tn_blocks(n);
+  const int64_t by_rows = (n + 2 * kTnRows - 1) / (2 * kTnRows);
+  return by_rows < 4 * kTnBlocks ? (by_rows < 1 ? 1 : by_rows) : 4 * kTnBlocks;
+}
+
 extern "C" int64_t gnn_gemm_tn_workspace_bytes(int64_t n, int64_t m, int64_t k) {
   if (n < 0 || m < 1 || k < 1) return GNN_E_ARG;
-  return tn_blocks(n) * (m * k + k) * static_cast<int64_t>(sizeof(float));
+  return tn_blocks_for(n, m, k) * (m * k + k) * static_cast<int64_t>(sizeof(float));
 }
 
 // C[m, k] = A^T B = sum_i A[i, :]^T B[i, :] (A [n, m], B [n, k], row strides lda / ldb), stored
@@ -559,12 +721,46 @@ extern "C" int gnn_gemm_tn_f32(const float* a, int64_t lda, const float* b, int6
   if (d && (!dsum || ldd < k)) return GNN_E_ARG;
   if (!gnn_gemm_tn_supported(m, k)) return GNN_E_UNSUPPORTED;
   if (workspace_bytes < gnn_gemm_tn_workspace_bytes(n, m, k)) return GNN_E_ARG;
-  if (!aligned_to(a, 16) || !aligned_to(b, 16) || (d && !aligned_to(d, 16)) || lda % 4 ||
-      ldb % 4 || (d && ldd % 4))
-    return GNN_E_ALIGN;
   hipStream_t s = static_cast<hipStream_t>(stream);
   float* part = static_cast<float*>(workspace);
   const int tc = trans_c ? 1 : 0;
+  if (!tn_wide(m, k)) {  // narrow: any row stride
+    if (!aligned_to(a, 4) || !aligned_to(b, 4) || (d && !aligned_to(d, 4))) return GNN_E_ALIGN;
+    const int64_t blocks = tn_blocks_for(n, m, k);
+    int64_t rpb = (n + blocks - 1) / blocks;
+    rpb = (rpb + kTnRows - 1) / kTnRows * kTnRows;
+    const int M = static_cast<int>(m), K = static_cast<int>(k);
+    const dim3 grid(static_cast<unsigned>(blocks)), blk(kTnThreads);
+    if (m * k <= kTinyOut) {
+      if (d)
+        hipLaunchKernelGGL((gemm_tn_tiny_kernel<true>), grid, blk, 0, s, a, lda, b, ldb, d, ldd,
+                           n, rpb, M, K, part);
+      else
+        hipLaunchKernelGGL((gemm_tn_tiny_kernel<false>), grid, blk, 0, s, a, lda, b, ldb, d, ldd,
+                           n, rpb, M, K, part);
+    } else if (m > kWave) {
+      if (d)
+        hipLaunchKernelGGL((gemm_tn_narrow_kernel<true, 2>), grid, blk, 0, s, a, lda, b, ldb, d,
+                           ldd, n, rpb, M, K, part);
+      else
+        hipLaunchKernelGGL((gemm_tn_narrow_kernel<false, 2>), grid, blk, 0, s, a, lda, b, ldb, d,
+                           ldd, n, rpb, M, K, part);
+    } else {
+      if (d)
+        hipLaunchKernelGGL((gemm_tn_narrow_kernel<true, 1>), grid, blk, 0, s, a, lda, b, ldb, d,
+                           ldd, n, rpb, M, K, part);
+      else
+        hipLaunchKernelGGL((gemm_tn_narrow_kernel<false, 1>), grid, blk, 0, s, a, lda, b, ldb, d,
+                           ldd, n, rpb, M, K, part);
+    }
+    const int64_t stride = m * k + (d ? k : 0);
+    hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3(static_cast<unsigned>((stride + 63) / 64)),
+                       dim3(256), 0, s, part, blocks, stride, m * k, k, c, ldc, tc, dsum);
+    return launch_status();
+  }
+  if (!aligned_to(a, 16) || !aligned_to(b, 16) || (d && !aligned_to(d, 16)) || lda % 4 ||
+      ldb % 4 || (d && ldd % 4))
+    return GNN_E_ALIGN;
   if (m == 128 && k == 128)
     return launch_tn<128, 128>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
   if (m == 64 && k == 64)

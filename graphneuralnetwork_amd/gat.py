@@ -41,9 +41,9 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
-from .ops import (GAT_DENSE, GAT_SPARSE, PermuteRows, _transform_or_mm, gat_aggregate,
-                  gat_backward, gat_column_order, gat_logits, gat_project, gat_train_order,
-                  gemm_tn)
+from .ops import (GAT_DENSE, GAT_SPARSE, PermuteRows, _bwd_recompute_ok, _transform_or_mm,
+                  gat_aggregate, gat_backward, gat_column_order, gat_logits, gat_project,
+                  gat_train_order, gemm_tn)
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
@@ -77,6 +77,15 @@ class _GatLayerFn(torch.autograd.Function):
             empty = (g.rowptr[1:] - g.rowptr[:-1]) == 0
             dwh = dwh + dout[empty].sum(0) / n
         return dwh, da_src, da_dst, None, None, None, None, None, None, None, None
+
+
+def _padded_fh(heads: int, fh: int, Wh) -> int:
+    """fh, or the head width to zero-pad to when the two-pass backward refuses fh but takes the
+    next power of two (>= 4: 16-B rows): 3 -> 4, 7 -> 8, 12 -> 16."""
+    if not Wh.is_cuda or _bwd_recompute_ok(heads, fh, Wh.stride(0)):
+        return fh
+    fp = max(4, 1 << (fh - 1).bit_length())
+    return fp if _bwd_recompute_ok(heads, fp, heads * fp) else fh
 
 
 def _attention_vector_grads(Wh, dl, der, heads, fh):
@@ -161,8 +170,21 @@ class _AttentionBase(nn.Module):
         seed = _dropout_seed() if p > 0 else 0
         if torch.is_grad_enabled() and (Wh.requires_grad or a_src.requires_grad
                                         or a_dst.requires_grad):
-            out = _GatLayerFn.apply(Wh, a_src, a_dst, g, heads, fh, self.alpha, self.MODE,
-                                    activation, p, seed)
+            fp = _padded_fh(heads, fh, Wh)
+            if fp != fh:
+                # head width the two-pass backward cannot lay out (e.g. a 7-class out_att):
+                # zero-pad each head to fp features -- zero a-weights, so the logits and the
+                # first fh output columns are unchanged -- and slice the output back
+                n = Wh.shape[0]
+                whp = F.pad(Wh.reshape(n, heads, fh), (0, fp - fh)).reshape(n, heads * fp)
+                asp = F.pad(a_src.reshape(heads, fh), (0, fp - fh)).reshape(-1)
+                adp = F.pad(a_dst.reshape(heads, fh), (0, fp - fh)).reshape(-1)
+                out = _GatLayerFn.apply(whp, asp, adp, g, heads, fp, self.alpha, self.MODE,
+                                        activation, p, seed)
+                out = out.view(n, heads, fp)[:, :, :fh].reshape(n, heads * fh)
+            else:
+                out = _GatLayerFn.apply(Wh, a_src, a_dst, g, heads, fh, self.alpha, self.MODE,
+                                        activation, p, seed)
         else:
             el, er = logits if logits is not None else gat_logits(Wh, heads, fh, a_src, a_dst)
             out = gat_aggregate(g, Wh, el, er, heads, fh, self.alpha, self.MODE, activation,

@@ -343,6 +343,24 @@ def gcn_train_order(g: CsrGraph, feat: int):
     return node_order(g)
 
 
+def gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """x[idx] for a 2-D fp32 device tensor and int64 row ids (gnn_gather_rows_f32: 16-B row
+    pieces per lane; torch's index_select moved the 1M x 128 permutation at ~1.7 TB/s,
+    profiles/r06i_*); other inputs take index_select."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1
+            and idx.dtype == torch.int64 and idx.is_cuda and idx.dim() == 1):
+        return x.index_select(0, idx)
+    idx = idx.contiguous()
+    out = torch.empty((idx.numel(), x.shape[1]), dtype=torch.float32, device=x.device)
+    err = torch.zeros(1, dtype=torch.int32, device=x.device)  # ids come from a permutation
+    _lib.check(_lib.load().gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0],
+                                               idx.data_ptr(), idx.numel(), x.shape[1],
+                                               out.data_ptr(), out.stride(0), err.data_ptr(),
+                                               _lib.stream_handle(x.device)),
+               "gnn_gather_rows_f32")
+    return out
+
+
 class PermuteRows(torch.autograd.Function):
     """y = x[perm] with the gradient gathered back through inv (a permutation: no index_add):
     the models' one relabelling on entry to and exit from the degree-ordered graph."""
@@ -350,11 +368,11 @@ class PermuteRows(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, perm, inv):
         ctx.inv = inv
-        return x.index_select(0, perm)
+        return gather_rows(x, perm)
 
     @staticmethod
     def backward(ctx, gy):
-        return gy.index_select(0, ctx.inv), None, None
+        return gather_rows(gy.contiguous(), ctx.inv), None, None
 
 
 def _spmm_xcd_direct(lib, xp, x, feat, bias, out, seg, skip_empty, flags, stream):
@@ -428,9 +446,13 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, d: torch.Tensor | None = None,
     n, m = a.shape
     k = b.shape[1]
     lib = _lib.load()
-    if not lib.gnn_gemm_tn_supported(m, k):
+    kind = lib.gnn_gemm_tn_supported(m, k)  # 1 wide, 2 narrow (k <= 16: classifier layers)
+    if not kind:
         return None
+
     def fits(t):
+        if kind == 2:  # narrow shapes: any row stride, unit column stride
+            return (t.stride(1) == 1 or t.shape[1] == 1) and t.data_ptr() % 4 == 0
         return t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
 
     # a copy for an operand the kernel cannot read in place: clone, not .contiguous(), which
@@ -445,9 +467,10 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, d: torch.Tensor | None = None,
     dsum = torch.empty(k, dtype=torch.float32, device=a.device) if d is not None else None
     ws = torch.empty(int(lib.gnn_gemm_tn_workspace_bytes(n, m, k)), dtype=torch.uint8,
                      device=a.device)
-    _lib.check(lib.gnn_gemm_tn_f32(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), n, m, k,
-                                   c.data_ptr(), c.stride(0), 1 if trans else 0, _lib.ptr(d),
-                                   d.stride(0) if d is not None else 0, _lib.ptr(dsum),
+    _lib.check(lib.gnn_gemm_tn_f32(a.data_ptr(), max(a.stride(0), m), b.data_ptr(),
+                                   max(b.stride(0), k), n, m, k, c.data_ptr(), c.stride(0),
+                                   1 if trans else 0, _lib.ptr(d),
+                                   max(d.stride(0), k) if d is not None else 0, _lib.ptr(dsum),
                                    ws.data_ptr(), ws.numel(), _lib.stream_handle(a.device)),
                "gnn_gemm_tn_f32")
     return c, dsum

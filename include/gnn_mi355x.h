@@ -533,10 +533,14 @@ int gnn_gat_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, int64_t n_r
  * GAT/train_eval.py:75-76 through GAT/models/layers.py:23): C = A^T B summed over the n rows
  * (A [n, m], B [n, k], row strides lda / ldb), written as C [m, k] (trans_c = 0, row stride
  * ldc >= k) or C^T [k, m] (trans_c = 1, ldc >= m); with d != NULL also dsum[k] = the column sums
- * of D [n, k] (the bias gradient, read in the same pass). fp32 FMAs in row order per block of
- * rows, the block partials summed in block order (deterministic). (m, k) as
- * gnn_gemm_tn_supported; 16-B aligned rows (GNN_E_ALIGN). workspace:
- * gnn_gemm_tn_workspace_bytes(n, m, k) bytes of device memory.
+ * of D [n, k] (the bias gradient, read in the same pass). Per block of rows the products are
+ * accumulated in row order (fp32 FMAs; fp32 or split-bf16 MFMAs at the wide shapes, per
+ * gnn_transform_set_precision), the block partials summed in block order (deterministic).
+ * gnn_gemm_tn_supported(m, k): 1 = a wide shape (m, k) in {(128,128), (64,64), (128,64),
+ * (64,128), (8,64), (16,64)}: 16-B aligned rows, strides multiples of 4 (GNN_E_ALIGN); 2 = a
+ * narrow one (k <= 16, m <= 128: a classifier layer's dW, e.g. k = 7 for 7 classes): any row
+ * stride, 4-B aligned; 0 = not covered. workspace: gnn_gemm_tn_workspace_bytes(n, m, k) bytes
+ * of device memory.
  */
 int gnn_gemm_tn_supported(int64_t m, int64_t k);
 int64_t gnn_gemm_tn_workspace_bytes(int64_t n, int64_t m, int64_t k);

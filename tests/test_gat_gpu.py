@@ -678,3 +678,39 @@ def test_gat_training_in_degree_order_equals_natural(dev, kind, monkeypatch):
     for a, b in zip(res[True], res[False]):
         err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
         assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("kind", ["GAT", "SpGAT"])
+@pytest.mark.parametrize("nclass", [3, 7])
+def test_gat_narrow_out_att_padded_backward(dev, kind, nclass, monkeypatch):
+    """A classifier attention layer whose width the two-pass backward cannot lay out (3 or 7
+    classes: GAT/run.py's out_att) trains zero-padded to 4 / 8 features: the logits and every
+    gradient equal the unpadded three-pass backward's, and its dW / da come from the narrow
+    gemm_tn kernel."""
+    from graphneuralnetwork_amd import gat as gat_mod
+    from graphneuralnetwork_amd.graph import CsrGraph
+    n = 2000
+    rowptr, col = _rand_csr(n, 12 * n, 31, hub=900)
+    rows = np.repeat(np.arange(n), np.diff(rowptr))
+    key = np.unique(np.concatenate([rows * n + col, np.arange(n) * (n + 1)]))  # self-loops
+    r, c = key // n, (key % n).astype(np.int32)
+    rp = np.concatenate([[0], np.cumsum(np.bincount(r, minlength=n))]).astype(np.int64)
+    g = CsrGraph(torch.from_numpy(rp).to(dev), torch.from_numpy(c).to(dev),
+                 torch.ones(c.size, device=dev), n, n)
+    torch.manual_seed(0)
+    model = getattr(gat_mod, kind)(64, 8, nclass, 0.0, 0.2, 8).to(dev).train()
+    x = torch.randn(n, 64, device=dev)
+    lab = torch.randint(0, nclass, (n,), device=dev)
+    assert gat_mod._padded_fh(1, nclass, torch.empty(1, nclass, device=dev)) in (4, 8)
+    res = {}
+    for pad in (True, False):
+        if not pad:
+            monkeypatch.setattr(gat_mod, "_padded_fh", lambda heads, fh, Wh: fh)
+        xx = x.clone().requires_grad_(True)
+        model.zero_grad(set_to_none=True)
+        y = model(xx, g)
+        torch.nn.functional.nll_loss(torch.nn.functional.log_softmax(y, 1), lab).backward()
+        res[pad] = [y.detach(), xx.grad] + [p.grad.clone() for p in model.parameters()]
+    for a, b in zip(res[True], res[False]):
+        err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+        assert err < 1e-5, err

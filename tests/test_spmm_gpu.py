@@ -778,3 +778,25 @@ def test_gcn_model_relu_epilogue_equals_separate_relu(dev):
     assert torch.isnan(y).any() and seen == [1]
     assert torch.equal(torch.nan_to_num(y, nan=7.0), torch.nan_to_num(ref, nan=7.0))
     assert torch.equal(torch.nan_to_num(y2, nan=7.0), torch.nan_to_num(ref, nan=7.0))
+
+
+def test_spmm_replay_restores_the_plan(dev):
+    """bench.spmm_replay (the measured SpMM ceiling: the product kernels with their gathered
+    ids rewritten in place) leaves the plan as it found it: the step after the replay equals
+    the step before it bit for bit, and the variants are timed in the expected order."""
+    import bench
+    from graphneuralnetwork_amd.ops import column_order, spmm_forward
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    n = 1_000_000
+    s, d = rmat_edges(n, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
+    ga = column_order(g, 128).graph
+    X = torch.randn(n, 128, device=dev)
+    b = torch.randn(128, device=dev)
+    Y0 = spmm_forward(ga, X, b)
+    Y = torch.empty_like(Y0)
+    r = bench.spmm_replay(ga, X, b, Y, reps=2)
+    assert r is not None and r["hub_rows"] > 0 and r["pass1_hub_gathers"] > 0
+    assert r["all_gathers_in_L2_ms"] < r["as_built_ms"]
+    assert torch.equal(spmm_forward(ga, X, b), Y0)

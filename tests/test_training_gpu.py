@@ -129,7 +129,8 @@ def test_gcn_layer_training_cfg2_full_size(dev, order):
 
 
 @pytest.mark.parametrize("m,k", [(128, 128), (64, 64), (128, 64), (64, 128), (8, 64),
-                                 (16, 64)])
+                                 (16, 64), (128, 7), (64, 8), (128, 16), (2, 8), (2, 3), (1, 1),
+                                 (33, 5)])
 @pytest.mark.parametrize("n", [1, 37, 20000, 300001])
 @pytest.mark.parametrize("prec", ["split-bf16", "fp32-mfma"])
 def test_gemm_tn_vs_float64(dev, m, k, n, prec):
@@ -159,7 +160,7 @@ def _gemm_tn_case(dev, m, k, n):
     assert torch.equal(ct, c.t())
     c2, ds2 = gemm_tn(a, b, d)
     assert torch.equal(c2, c) and torch.equal(ds2, ds)
-    assert gemm_tn(torch.randn(n, 96, device=dev), b) is None  # uncovered shape: caller's torch.mm
+    assert gemm_tn(torch.randn(n, 200, device=dev), b) is None  # uncovered: the caller's torch.mm
 
 
 def test_gat_training_grads_use_tn_kernel(dev):

@@ -21,7 +21,7 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", choices=("gcn", "gat"), default="gcn")
+    ap.add_argument("--model", choices=("gcn", "gat", "gcn_model", "gat_model"), default="gcn")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--er-gather", action="store_true",
                     help="GAT: er loaded, not recomputed from the gathered rows")
@@ -39,10 +39,31 @@ def main():
     g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
     gen = torch.Generator(device=dev).manual_seed(1)
     from graphneuralnetwork_amd.ops import gat_train_order, gcn_train_order
-    if not a.natural:
+    if a.model.endswith("_model"):  # the whole model, x and the logits in the original order
+        if a.natural:
+            from graphneuralnetwork_amd import ops
+            ops.GCN_TRAIN_ORDER = ops.GAT_TRAIN_ORDER = False
+        if a.model == "gcn_model":
+            from graphneuralnetwork_amd.gcn import GCN_Model
+            net = GCN_Model(128, 128, 7, 2, 0.5).to(dev).train()
+            X = torch.randn(n, 128, device=dev, generator=gen)
+        else:
+            from graphneuralnetwork_amd.gat import GAT
+            net = GAT(64, 8, 7, dropout=0.6, alpha=0.2, nheads=8).to(dev).train()
+            X = torch.randn(n, 64, device=dev, generator=gen)
+        labels = torch.randint(0, 7, (n,), device=dev, generator=gen)
+        idx_train = torch.arange(0, n, 10, device=dev)
+        ce = torch.nn.CrossEntropyLoss()
+
+        def step():  # the reference loops: CE on output[idx_train] (GCN/train_eval.py:43-46)
+            net.zero_grad(set_to_none=True)
+            ce(net(X, g)[idx_train], labels[idx_train]).backward()
+    elif not a.natural:
         o = gcn_train_order(g, 128) if a.model == "gcn" else gat_train_order(g, 8, 8)
         g = o.graph if o is not None else g
-    if a.model == "gcn":
+    if a.model.endswith("_model"):
+        pass
+    elif a.model == "gcn":
         from graphneuralnetwork_amd.gcn import Graph_conv_layer
         net = Graph_conv_layer(128, 128).to(dev)
         X = torch.randn(n, 128, device=dev, generator=gen).requires_grad_(True)
