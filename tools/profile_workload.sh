@@ -16,7 +16,7 @@ shift
 out=gpurun_out/prof
 mkdir -p "$out"
 export TMPDIR=/tmp
-bench=(python3 -u bench.py --steps 5 --warmup 2 --no-extras --no-cold --no-cpu-baseline --no-cpu-reference --no-layer --no-train --no-variants "$@")
+bench=(python3 -u bench.py --steps 5 --warmup 2 --no-extras --no-cold --no-cpu-baseline --no-cpu-reference --no-layer --no-train --no-variants --no-replay "$@")
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/${tag}_stats" -o run -- "${bench[@]}" \
   > "$out/${tag}_stats.log" 2>&1
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/${tag}_fetch" -o run -- "${bench[@]}" \
