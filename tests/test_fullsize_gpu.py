@@ -435,3 +435,78 @@ def test_gat_training_block_cfg3_vs_oracle(model, drop, order, monkeypatch):
     print(f"{model} {order} order, dropout {drop}: kink (row, head) pairs {kinks}; max |hip - oracle| / "
           "max |oracle|: " + ", ".join(report))
     assert not bad, bad
+
+
+def _check_layer(name, hip):
+    """hip: {name: (fp32 result, float64 oracle, kink slack, normwise)}: elementwise 1e-4 relative
+    (+1e-5 of the max) or normwise 1e-4 of the max, plus the oracle's LeakyReLU-kink slack."""
+    report, bad = [], []
+    for k, (h, ref, slack, normwise) in hip.items():
+        scale = float(np.abs(ref).max())
+        tol = (1e-4 * scale if normwise else 1e-4 * np.abs(ref) + 1e-5 * max(1.0, scale)) + slack
+        excess = np.abs(h - ref) - tol
+        report.append(f"{k} {float(np.abs(h - ref).max()) / scale:.2e}")
+        if excess.max() > 0:
+            bad.append((k, float(excess.max())))
+    print(f"{name}: " + ", ".join(report))
+    assert not bad, (name, bad)
+
+
+@pytest.mark.parametrize("model", ["GAT", "SpGAT"])
+def test_gat_model_training_cfg3_vs_oracle(model):
+    """The whole GAT model's training step at cfg3 size (GAT/SpGAT(64, 8, 7, ., 8); GAT.py:14-18,
+    train_eval.py:72-76), as GATBase.forward runs it: over P A P^T, the 8-head block, then the
+    7-class out_att (zero-padded to 8 features for the two-pass backward, its dW / da on the
+    narrow / tiny gemm_tn kernels), ELU. Each layer against the float64 oracle given the same
+    inputs: out_att with the block's fp32 output as its input and the loss gradient, the block
+    with the gradient out_att handed back. Dropout 0 (F.dropout's torch RNG is not restated;
+    the block's dropout is pinned by test_gat_training_block_cfg3_vs_oracle)."""
+    from graphneuralnetwork_amd import gat as gat_mod
+    from graphneuralnetwork_amd.ops import gat_train_order
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    dev = torch.device("cuda:0")
+    n, H, fh, Fin, C = 1_000_000, 8, 8, 64, 7
+    s, d = rmat_edges(n, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n)
+    del s, d
+    g = gat_train_order(g, H, fh).graph
+    torch.manual_seed(2)
+    net = getattr(gat_mod, model)(Fin, fh, C, 0.0, 0.2, H).to(dev).train()
+    gen = torch.Generator(dev).manual_seed(6)
+    X = torch.randn(n, Fin, device=dev, generator=gen).requires_grad_(True)
+    gy = torch.randn(n, C, device=dev, generator=gen)
+    x1 = net._heads(X, g)
+    x1.retain_grad()
+    out = net.out_att(x1, g, activation="elu")
+    out.backward(gy)
+    rowptr, col = g.rowptr.cpu().numpy(), g.col.cpu().numpy()
+    sparse = model == "SpGAT"
+    # out_att: 1 head x 7, input the block's fp32 output
+    W2 = net.out_att.W.detach().cpu().numpy()
+    a2 = net.out_att.a.detach().reshape(-1).cpu().numpy()
+    r2 = c_oracle.gat_block_grad(rowptr, col, x1.detach().cpu().numpy(), W2, a2[:C], a2[C:],
+                                 gy.cpu().numpy(), 1, C, 0.2, sparse)
+    da2 = net.out_att.a.grad.reshape(-1).cpu().numpy()
+    _check_layer(f"{model} out_att", {
+        "out": (out.detach().cpu().numpy(), r2["out"], 0.0, False),
+        "dx": (x1.grad.cpu().numpy(), r2["dx"], r2["slack_dx"], False),
+        "dW": (net.out_att.W.grad.cpu().numpy(), r2["dW"], r2["slack_dW"], True),
+        "da": (da2, np.concatenate([r2["da_src"], r2["da_dst"]]),
+               np.concatenate([r2["slack_da_src"], r2["slack_da_dst"]]), True)})
+    # the 8-head block with the gradient out_att handed back
+    W1 = torch.cat([m.W for m in net.attentions], 1).detach().cpu().numpy()
+    a1 = [m.a.detach().reshape(-1).cpu().numpy() for m in net.attentions]
+    r1 = c_oracle.gat_block_grad(rowptr, col, X.detach().cpu().numpy(), W1,
+                                 np.concatenate([x[:fh] for x in a1]),
+                                 np.concatenate([x[fh:] for x in a1]), x1.grad.cpu().numpy(), H,
+                                 fh, 0.2, sparse)
+    da1 = np.stack([m.a.grad.reshape(-1).cpu().numpy() for m in net.attentions])
+    _check_layer(f"{model} heads", {
+        "out": (x1.detach().cpu().numpy(), r1["out"], 0.0, False),
+        "dx": (X.grad.cpu().numpy(), r1["dx"], r1["slack_dx"], False),
+        "dW": (torch.cat([m.W.grad for m in net.attentions], 1).cpu().numpy(), r1["dW"],
+               r1["slack_dW"], True),
+        "da": (da1, np.concatenate([r1["da_src"].reshape(H, fh), r1["da_dst"].reshape(H, fh)], 1),
+               np.concatenate([r1["slack_da_src"].reshape(H, fh),
+                               r1["slack_da_dst"].reshape(H, fh)], 1), True)})
