@@ -128,6 +128,70 @@ def test_gcn_layer_training_cfg2_full_size(dev, order):
     close(X.grad.cpu().numpy(), dS @ W)
 
 
+def test_gcn_model_training_cfg2_full_size(dev):
+    """The whole benchmarked model's training step at cfg2 size: GCN_Model(128, 128, 7, 2, 0)
+    (GCN/GCN.py:5-27, GCN/train_eval.py:43-48) as its forward runs it -- rows permuted onto
+    P A P^T (PermuteRows), layer 1 128 -> 128 + ReLU, layer 2 128 -> 7 (its weight gradient on
+    the narrow gemm_tn kernel), logits permuted back. Each layer against float64 references
+    (the C oracle's SpMM, numpy products) given the tensors the model handed it, captured in
+    the permuted frame by module hooks: the ReLU mask is the model's own, so no element near
+    the kink can flip between fp32 and float64. Dropout 0 (nn.Dropout's torch RNG)."""
+    from graphneuralnetwork_amd.gcn import GCN_Model
+    from graphneuralnetwork_amd.ops import gcn_train_order
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    n, C = 1_000_000, 7
+    s, d = rmat_edges(n, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
+    del s, d
+    torch.manual_seed(3)
+    net = GCN_Model(128, 128, C, 2, 0.0).to(dev).train()
+    gen = torch.Generator(device=dev).manual_seed(7)
+    with torch.no_grad():
+        for m in (net.gcn_blocks.gcn0, net.gcn_blocks.gcn1):
+            m.bias.normal_(generator=gen)
+    seen = {}
+
+    def keep(name):
+        def hook(mod, inp, out=None):
+            t = inp[0] if out is None else out
+            t.retain_grad()
+            seen[name] = t
+        return hook
+
+    net.gcn_blocks.gcn0.register_forward_pre_hook(keep("x"))
+    net.gcn_blocks.relu0.register_forward_hook(keep("h"))
+    net.gcn_blocks.gcn1.register_forward_hook(keep("y"))
+    X = torch.randn(n, 128, device=dev, generator=gen).requires_grad_(True)
+    gy = torch.randn(n, C, device=dev, generator=gen)
+    Y = net(X, g)
+    Y.backward(gy)
+    gp = gcn_train_order(g, 128).graph
+    assert seen["x"].shape == (n, 128) and seen["y"].shape == (n, C)
+    rp, col, val = (t.cpu().numpy() for t in (gp.rowptr, gp.col, gp.val))
+    A = lambda v: c_oracle.spmm_csr(rp, col, val, v.astype(np.float32)).astype(np.float64)
+    f64 = lambda t: t.detach().cpu().numpy().astype(np.float64)
+    Xp, H, Hg, Yp, gyp = f64(seen["x"]), f64(seen["h"]), f64(seen["h"].grad), f64(seen["y"]), \
+        f64(seen["y"].grad)
+    W1, b1 = f64(net.gcn_blocks.gcn0.dense.weight), f64(net.gcn_blocks.gcn0.bias)
+    W2, b2 = f64(net.gcn_blocks.gcn1.dense.weight), f64(net.gcn_blocks.gcn1.bias)
+    # layer 2 (128 -> 7) given the model's H and the logits' gradient
+    close(Yp, A(H @ W2.T) + b2)
+    dS2 = A(gyp)
+    close(f64(net.gcn_blocks.gcn1.dense.weight.grad), dS2.T @ H)
+    close(f64(net.gcn_blocks.gcn1.bias.grad), gyp.sum(0))
+    close(Hg, dS2 @ W2)
+    # layer 1 (128 -> 128, ReLU) given the model's input rows and the gradient layer 2 handed back
+    close(H, np.maximum(A(Xp @ W1.T) + b1, 0.0))
+    dZ1 = Hg * (H > 0)
+    dS1 = A(dZ1)
+    close(f64(net.gcn_blocks.gcn0.dense.weight.grad), dS1.T @ Xp)
+    close(f64(net.gcn_blocks.gcn0.bias.grad), dZ1.sum(0))
+    close(f64(seen["x"].grad), dS1 @ W1)
+    # the permutation at both ends: the natural-frame gradient is the permuted one moved back
+    assert torch.equal(torch.sort(X.grad.reshape(-1))[0], torch.sort(seen["x"].grad.reshape(-1))[0])
+
+
 @pytest.mark.parametrize("m,k", [(128, 128), (64, 64), (128, 64), (64, 128), (8, 64),
                                  (16, 64), (128, 7), (64, 8), (128, 16), (2, 8), (2, 3), (1, 1),
                                  (33, 5)])
