@@ -1225,9 +1225,15 @@ def gcn_roofline(nnz: int, n_rows: int, n_cols: int, feat: int, step_ms: list, t
             "min_launch_ms": min(step_ms)}
 
 
-def tn_kernel_name(m: int, k: int) -> str:
-    """The gemm_tn kernel launch_tn picks for an (M, K) shape (csrc/gemm_tn.hip)."""
-    return "gemm_tn_mfma_kernel" if m >= 64 and k >= 32 else "gemm_tn_partial_kernel"
+def tn_kernel_name(m: int, k: int, d_is_b: bool = False) -> str:
+    """The gemm_tn kernel launch_tn picks for an (M, K) shape (csrc/gemm_tn.hip) in the
+    transforms' arithmetic mode."""
+    from graphneuralnetwork_amd.ops import transform_precision
+    if not (m >= 64 and k >= 32):
+        return "gemm_tn_partial_kernel"
+    if transform_precision() == "split-bf16":
+        return "gemm_tn_x6_kernel" + ("<DB: dsum from B's loads>" if d_is_b else "")
+    return "gemm_tn_mfma_kernel"
 
 
 def _ms_stats(ms: list) -> dict:
@@ -1236,13 +1242,15 @@ def _ms_stats(ms: list) -> dict:
 
 def gcn_train_step(g, F: int, args, dev) -> dict:
     """One training step of the drop-in Graph_conv_layer(F, F) at cfg2 (GCN/GCN.py:41-47 under
-    GCN/train_eval.py:43-48's loss.backward()), as a hidden layer (dX needed too): forward =
-    MFMA transform into the column-degree order + XCD-sliced SpMM with the bias epilogue;
-    backward = SpMM over A^T (A itself: the normalised adjacency is symmetric) + MFMA transform
-    (dX = dS W) + the tall-skinny A^T B kernel (dW = dS^T X with db = column sums of dY in the
-    same pass; hipBLASLt's torch.mm timed beside it). Each backward component is
-    also timed alone; the backward SpMM carries its own roofline (compulsory bytes, as the
-    forward's)."""
+    GCN/train_eval.py:43-48's loss.backward()), as a hidden layer (dX needed too), over P A P^T.
+    F -> F trains as (A X) W^T + b (ops._GcnLayerFn, GCN_REASSOC): forward = SpMM Z = A X +
+    MFMA transform with the bias epilogue; backward = the tall-skinny A^T B kernel (dW = dY^T Z
+    with db = column sums of dY from the same loads; hipBLASLt's torch.mm timed beside it) +
+    MFMA transform (dZ = dY W) + SpMM over A^T (A itself: the normalised adjacency is
+    symmetric). The A (X W^T) form (GCN_REASSOC off) is timed beside it. Each backward
+    component is also timed alone; the backward SpMM carries its own roofline (compulsory
+    bytes, as the forward's)."""
+    from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.gcn import GCN_Model, Graph_conv_layer
     from graphneuralnetwork_amd.ops import gcn_train_order, gcn_transform, gemm_tn, spmm_forward
     gen = torch.Generator(device=dev).manual_seed(1)
@@ -1275,6 +1283,13 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
         layer(X_nat, g_nat).backward(gy_nat)
 
     nat_ms = time_steps(step_nat, steps, 2, dev)[0] if order is not None else step_ms
+    reassoc = ops._reassociate(X, layer.dense.weight, g)
+    prev_reassoc = ops.GCN_REASSOC
+    ops.GCN_REASSOC = False
+    try:
+        plain_ms = time_steps(step, steps, 2, dev)[0] if reassoc else step_ms
+    finally:
+        ops.GCN_REASSOC = prev_reassoc
     # the two-layer model, input and logits in the original order (GCN_Model.forward's two
     # permutes inside the step), NLL loss (GCN/train_eval.py:43-48)
     model = GCN_Model(F, F, 7, 2, 0.5).to(dev).train()
@@ -1294,27 +1309,41 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
     bwd_ms = time_steps(lambda: keep["y"].backward(gy, retain_graph=True), steps, 2, dev)[0]
     del keep
     gt = g.transpose()
-    ds = torch.empty(g.n_rows, F, device=dev)
-    spmm_ms = time_steps(lambda: spmm_forward(gt, gy, out=ds), steps, 2, dev)[0]
     Wt = layer.dense.weight.detach().t().contiguous()
     Xd = X.detach()
-    dx_ms = time_steps(lambda: gcn_transform(ds, Wt), steps, 2, dev)[0]
-    tn = gemm_tn(Xd, ds, gy, trans=True) is not None
-    dw_ms = (time_steps(lambda: gemm_tn(Xd, ds, gy, trans=True), steps, 2, dev)[0] if tn else
-             time_steps(lambda: torch.mm(ds.t(), Xd), steps, 2, dev)[0])
-    mm_ms = time_steps(lambda: torch.mm(ds.t(), Xd), steps, 2, dev)[0]
+    ds = torch.empty(g.n_rows, F, device=dev)
+    if reassoc:  # (A X) W^T + b: dW = dY^T Z, db from dY's own loads; dZ = dY W; dX = A^T dZ
+        Z = spmm_forward(g, Xd)
+        dz = gcn_transform(gy, Wt)
+        spmm_ms = time_steps(lambda: spmm_forward(gt, dz, out=ds), steps, 2, dev)[0]
+        dx_ms = time_steps(lambda: gcn_transform(gy, Wt), steps, 2, dev)[0]
+        tn_args = (Z, gy, gy)
+    else:  # A (X W^T) + b: dS = A^T dY; dX = dS W; dW = dS^T X, db = colsum dY
+        spmm_ms = time_steps(lambda: spmm_forward(gt, gy, out=ds), steps, 2, dev)[0]
+        dx_ms = time_steps(lambda: gcn_transform(ds, Wt), steps, 2, dev)[0]
+        tn_args = (Xd, ds, gy)
+    ta, tb, td = tn_args
+    tn = gemm_tn(ta, tb, td, trans=True) is not None
+    dw_ms = (time_steps(lambda: gemm_tn(ta, tb, td, trans=True), steps, 2, dev)[0] if tn else
+             time_steps(lambda: torch.mm(tb.t(), ta), steps, 2, dev)[0])
+    mm_ms = time_steps(lambda: torch.mm(tb.t(), ta), steps, 2, dev)[0]
     db_ms = time_steps(lambda: gy.sum(0), steps, 2, dev)[0]
     comp = compulsory_bytes(g.nnz, g.n_rows, g.n_cols, F)
     t_sp = statistics.mean(spmm_ms) / 1e3
     nbytes_rows = g.n_rows * 4 * F
-    dw_bytes = (3 if tn else 2) * nbytes_rows  # X, dS (+ dY, the db operand, in gemm_tn)
+    # operands read: (Z, dY) with db from dY's own loads, or (X, dS) + dY for db
+    dw_bytes = (2 if reassoc or not tn else 3) * nbytes_rows
     res = {
         "what": "Graph_conv_layer(%d, %d) forward + loss.backward() at cfg2, X requiring grad "
                 "(a hidden layer: dX, dW, db)" % (F, F),
         "step_ms": statistics.median(step_ms), "forward_ms": statistics.median(fwd_ms),
         "backward_ms": statistics.median(bwd_ms),
         "edges_per_s": 2 * g.nnz / (statistics.median(step_ms) / 1e3),
-        "edges_note": "two SpMM passes per step (forward A S, backward A^T dY)",
+        "edges_note": ("two SpMM passes per step (forward A X, backward A^T dZ)" if reassoc else
+                       "two SpMM passes per step (forward A S, backward A^T dY)"),
+        "layer_form": ("(A X) W^T + b (ops.GCN_REASSOC: in_features <= out_features)" if reassoc
+                       else "A (X W^T) + b"),
+        "a_xwt_form_step_ms": statistics.median(plain_ms),
         "node_order": ("P A P^T (gcn_train_order: nodes relabelled by degree once per graph, "
                        "%.2f s outside the timed region; X, dY in that order as GCN_Model's "
                        "hidden layers see them)" % order_s) if order is not None else "natural",
@@ -1325,9 +1354,9 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
                            "node (GCN/train_eval.py:43-46; x in and logits out in the original "
                            "order)" % (F, F),
         "backward_components_ms": {
-            "spmm_dS_AT_dY": statistics.median(spmm_ms),
-            "transform_dX_dS_W": statistics.median(dx_ms),
-            ("gemm_tn_dW_db" if tn else "gemm_dW_dST_X_hipblaslt"): statistics.median(dw_ms),
+            ("spmm_dX_AT_dZ" if reassoc else "spmm_dS_AT_dY"): statistics.median(spmm_ms),
+            ("transform_dZ_dY_W" if reassoc else "transform_dX_dS_W"): statistics.median(dx_ms),
+            ("gemm_tn_dW_db" if tn else "gemm_dW_hipblaslt"): statistics.median(dw_ms),
             "colsum_db" + ("_in_gemm_tn" if tn else ""): (0.0 if tn else statistics.median(db_ms))},
         "hipblaslt_mm_dW_for_comparison_ms": statistics.median(mm_ms),
         "backward_spmm_graph": "A itself (symmetric: no transposed copy)" if gt is g else
@@ -1345,23 +1374,29 @@ def gcn_train_step(g, F: int, args, dev) -> dict:
             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": dw_bytes / (statistics.mean(dw_ms) / 1e3) / 1e9 / HBM_PEAK_GBPS,
             "bytes": dw_bytes,
-            "kernel": ("%s + gemm_tn_reduce_kernel (dW^T = X^T dS and db = colsum dY in one "
-                       "pass)" % tn_kernel_name(F, F)) if tn else "hipBLASLt (torch.mm)",
-            "note": "X, dS and dY (the db operand) read once (K = n_rows reduction, %.1f GFLOP)"
-                    % (2 * g.n_rows * F * F / 1e9) if tn else
-                    "X and dS read once (%.1f GFLOP)" % (2 * g.n_rows * F * F / 1e9)},
+            "kernel": ("%s + gemm_tn_reduce_kernel (%s in one pass)"
+                       % (tn_kernel_name(F, F, reassoc),
+                          "dW = dY^T Z and db = colsum dY" if reassoc else
+                          "dW^T = X^T dS and db = colsum dY")) if tn else "hipBLASLt (torch.mm)",
+            "note": ("Z and dY read once, db from dY's loads" if reassoc and tn else
+                     "X, dS and dY (the db operand) read once" if tn else
+                     "two operands read once") + " (K = n_rows reduction, %.1f GFLOP)"
+                    % (2 * g.n_rows * F * F / 1e9)},
         "roofline_backward_transform_dX": {
             "bound": "hbm", "achieved": 2 * nbytes_rows / (statistics.mean(dx_ms) / 1e3) / 1e9,
             "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": 2 * nbytes_rows / (statistics.mean(dx_ms) / 1e3) / 1e9 / HBM_PEAK_GBPS,
-            "bytes": 2 * nbytes_rows, "note": "dS read, dX written"},
+            "bytes": 2 * nbytes_rows,
+            "note": "dY read, dZ written" if reassoc else "dS read, dX written"},
     }
     if not args.no_cpu_baseline:
         try:
             res["cpu_reference_ops"] = cpu_gcn_train_ops(g, F)
         except Exception as e:  # reported, never the target
             res["cpu_reference_ops"] = {"error": repr(e)}
-    del X, gy, ds, layer, X_nat, gy_nat, Xm
+    del X, gy, ds, layer, X_nat, gy_nat, Xm, ta, tb, td, tn_args
+    if reassoc:
+        del Z, dz
     torch.cuda.empty_cache()
     return res
 

@@ -97,6 +97,8 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_transform_set_precision": (ctypes.c_int, [ctypes.c_int]),
     "gnn_transform_get_precision": (ctypes.c_int, []),
     "gnn_gcn_transform_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
+    "gnn_gcn_transform_bias_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp,
+                                                  _i64, _vp]),
     "gnn_linear_relu_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnn_linear_relu_live_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                                                 _vp]),

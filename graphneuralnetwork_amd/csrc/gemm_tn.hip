@@ -293,7 +293,9 @@ __global__ __launch_bounds__(kTnThreads) void gemm_tn_mfma_kernel(
 // (8 rows apart = 32 banks apart) keeps conflict-free for the two lane halves; the strips are
 // split in registers. 6 x 32 cycles per 16 rows x 32 x 32 outputs against 8 x 64 on the f32
 // MFMA: the kernel is left paced by its HBM reads. C/D lane map as the f32 form's.
-template <int M, int K, bool DSUM>
+// DB: D is B (dsum = the column sums of B, taken from B's own staged loads: no third read --
+// the bias gradient next to dW = dY^T Z of a layer trained as (A X) W^T + b).
+template <int M, int K, bool DSUM, bool DB = false>
 __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
     const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb,
     const float* __restrict__ d, int64_t ldd, int64_t n, int64_t rows_per_block,
@@ -320,7 +322,8 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
 #pragma unroll
   for (int q = 0; q < NB; ++q) ds[q] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  auto load = [&](int64_t row0, float4 (&va)[NA], float4 (&vb)[NB], float4 (&vd)[NB]) {
+  constexpr int ND = DB ? 1 : NB;  // D's float4s in flight (none of its own when D is B)
+  auto load = [&](int64_t row0, float4 (&va)[NA], float4 (&vb)[NB], float4 (&vd)[ND]) {
 #pragma unroll
     for (int q = 0; q < NA; ++q) {
       const int e = t + q * kTnThreads;
@@ -336,13 +339,13 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
       const bool ok = e < kTnRows * B4 && row < r1;
       vb[q] = ok ? *reinterpret_cast<const float4*>(b + row * ldb + 4 * (e % B4))
                  : make_float4(0.f, 0.f, 0.f, 0.f);
-      if constexpr (DSUM)
+      if constexpr (DSUM && !DB)
         vd[q] = ok ? *reinterpret_cast<const float4*>(d + row * ldd + 4 * (e % B4))
                    : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
 
-  float4 va[NA], vb[NB], vd[NB];
+  float4 va[NA], vb[NB], vd[ND];
   load(r0, va, vb, vd);
   const float* saf = reinterpret_cast<const float*>(sa);
   const float* sbf = reinterpret_cast<const float*>(sb);
@@ -358,10 +361,11 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
       const int e = t + q * kTnThreads;
       if (e < kTnRows * B4) sb[(e / B4) * (PB / 4) + e % B4] = vb[q];
       if constexpr (DSUM) {
-        ds[q].x += vd[q].x;
-        ds[q].y += vd[q].y;
-        ds[q].z += vd[q].z;
-        ds[q].w += vd[q].w;
+        const float4 dv = DB ? vb[q] : vd[DB ? 0 : q];
+        ds[q].x += dv.x;
+        ds[q].y += dv.y;
+        ds[q].z += dv.z;
+        ds[q].w += dv.w;
       }
     }
     __syncthreads();
@@ -655,7 +659,11 @@ static int launch_tn(const float* a, int64_t lda, const float* b, int64_t ldb, c
 #endif
   if constexpr (mfma) {
     if (GNN_TN_X6 != 0 && g_tf_x6 != 0) {  // the transforms' arithmetic mode (set_precision)
-      if (d)
+      if (d && d == b && ldd == ldb)  // dsum of B itself: B's loads serve both
+        hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, true, true>),
+                           dim3(static_cast<unsigned>(blocks)), dim3(kTnThreads), 0, s, a, lda, b,
+                           ldb, d, ldd, n, rpb, part);
+      else if (d)
         hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, true>), dim3(static_cast<unsigned>(blocks)),
                            dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
       else

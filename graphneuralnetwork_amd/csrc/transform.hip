@@ -1,7 +1,8 @@
 // transform.hip -- the GCN feature transform on the matrix cores: Y = X W^T (fp32).
 //
 // Replaces `support = self.dense(X_input)` (nn.Linear, no bias) at GCN/GCN.py:42, the
-// dense half of Graph_conv_layer.forward, for the inference path (no autograd); with the
+// dense half of Graph_conv_layer.forward (with the layer's bias in the store epilogue,
+// gnn_gcn_transform_bias_f32, when training runs the layer as (A X) W^T + b); with the
 // ReLU epilogue (gnn_linear_relu_f32) the SageLayer's relu(weight(cat[self, agg])) at
 // GraphSAGE/GraphSAGE.py:18-20.
 // Shapes: X [n, K] row-major, W [FO, K] (nn.Linear's [out, in]), Y [n, FO].
@@ -84,7 +85,8 @@ template <int K, int CB, int NW, bool RELU, int TR, int MODE, bool X6 = false>
 __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
     float* __restrict__ y, int64_t ldy, const int64_t* __restrict__ y_row, int64_t n_y,
-    int32_t* __restrict__ err, Classifier cls, const int64_t* __restrict__ live) {
+    int32_t* __restrict__ err, Classifier cls, const int64_t* __restrict__ live,
+    const float* __restrict__ bias) {
   if (live != nullptr) {  // uniform: every wave reads the same count
     const int64_t l = *live;
     n_rows = l < n_rows ? (l > 0 ? l : 0) : n_rows;
@@ -328,6 +330,14 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
           float4 o = make_float4(acc[j][cb][0], acc[j][cb][1], acc[j][cb][2], acc[j][cb][3]);
+          if (bias != nullptr) {  // uniform: the Linear's bias (gnn_gcn_transform_bias_f32)
+            const float4 bv =
+                *reinterpret_cast<const float4*>(bias + (wv * CB + cb) * 16 + 4 * q);
+            o.x += bv.x;
+            o.y += bv.y;
+            o.z += bv.z;
+            o.w += bv.w;
+          }
           if constexpr (RELU) {
             o.x = fmaxf(o.x, 0.f);
             o.y = fmaxf(o.y, 0.f);
@@ -410,26 +420,26 @@ int g_tf_x6 = 1;
 template <int K, int CB, int NW, bool RELU, int TR, bool X6>
 static void launch_transform_kernel(dim3 grid, const float* x, int64_t ldx, int64_t n_rows,
                                     const float* w, float* y, int64_t ldy, const RowIdx& ri,
-                                    const Classifier& cls, hipStream_t s) {
+                                    const Classifier& cls, const float* bias, hipStream_t s) {
   if (ri.row != nullptr)  // a template flag: no index loads in the in-order kernel
     hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfScatter, X6>), grid,
                        dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err,
-                       cls, ri.live);
+                       cls, ri.live, bias);
   else if (RELU && cls.logits != nullptr)  // the classifier epilogue: SageLayer GEMMs only
     hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, RELU ? kTfClassify : kTfPlain,
                                              X6>),
                        grid, dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y,
-                       ri.err, cls, ri.live);
+                       ri.err, cls, ri.live, bias);
   else
     hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfPlain, X6>), grid,
                        dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err,
-                       cls, ri.live);
+                       cls, ri.live, bias);
 }
 
 template <int K, int CB, int NW, bool RELU, int TR>
 static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, const float* w,
                                float* y, int64_t ldy, const RowIdx& ri, const Classifier& cls,
-                               hipStream_t s) {
+                               const float* bias, hipStream_t s) {
   const int64_t tiles = (n_rows + TR - 1) / TR;
 #ifndef GNN_TF_GRID
 #define GNN_TF_GRID 512  // persistent grid: 2 workgroups per CU
@@ -440,11 +450,11 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
   // X6 tiles: 3 bf16 planes, at most 32 rows; 2 blocks of K = 256 pieces (192 VGPRs) spill
   if constexpr (K >= 128 && TR <= 32 && !(K == 256 && CB == 2)) {
     if (g_tf_x6) {
-      launch_transform_kernel<K, CB, NW, RELU, TR, true>(g, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+      launch_transform_kernel<K, CB, NW, RELU, TR, true>(g, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
       return launch_status();
     }
   }
-  launch_transform_kernel<K, CB, NW, RELU, TR, false>(g, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+  launch_transform_kernel<K, CB, NW, RELU, TR, false>(g, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
   return launch_status();
 }
 
@@ -462,60 +472,62 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
 // 2891 vs 307 / 2932 us; K = 64 -> 64 keeps 64 rows (95 vs 113 us at 1M).
 template <int K, int CB, int NW, bool RELU>
 static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const float* w,
-                            float* y, int64_t ldy, const RowIdx& ri, const Classifier& cls, hipStream_t s) {
+                            float* y, int64_t ldy, const RowIdx& ri, const Classifier& cls, const float* bias, hipStream_t s) {
   constexpr int64_t slots = GNN_TF_GRID * kTfWaves / NW;
 #ifdef GNN_TF_TR32_ROWS  // A/B: 16-row tiles below GNN_TF_TR16_ROWS, 32-row below this
 #ifndef GNN_TF_TR16_ROWS
 #define GNN_TF_TR16_ROWS (32 * 2 * slots)
 #endif
-  if (n_rows < GNN_TF_TR16_ROWS) return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
-  if (n_rows < GNN_TF_TR32_ROWS) return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+  if (n_rows < GNN_TF_TR16_ROWS) return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+  if (n_rows < GNN_TF_TR32_ROWS) return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
 #endif
   // X6 at K = 256: 16-row tiles at every size (in one process, tools/transform_x6_ab.py,
   // profiles/r03x_transform_x6_ab.log: 62K / 200K x 256 -> 128 30.9 / 79.9 vs 32.9 / 89.7 us
   // with 32-row tiles; K = 128 keeps 32: 1M x 128 -> 128 205 vs 211 us)
   if (GNN_TF_MIN_TR <= 16 &&
       (n_rows < 32 * 2 * slots || (K == 256 && g_tf_x6 && !(CB == 2 && K == 256))))
-    return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+    return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
   if (GNN_TF_MIN_TR <= 32 && (K > GNN_TF_TR64_MAX_K || n_rows < 64 * 2 * slots))
-    return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+    return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
   if constexpr (K <= GNN_TF_TR64_MAX_K || GNN_TF_MIN_TR > 32)
-    return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
-  return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+    return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+  return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
 }
 
 template <int K, bool RELU>
 static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t n_rows,
                               const float* w, float* y, int64_t ldy, const RowIdx& ri,
-                              const Classifier& cls, hipStream_t s) {
-  if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+                              const Classifier& cls, const float* bias, hipStream_t s) {
+  if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
   if (fout == 128) {
     if constexpr (K <= 128 || GNN_TF_K256_CB2)
-      return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+      return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
     else
-      return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+      return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
   }
   if (fout == 256) {
     if constexpr (K <= 64) {
-      return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+      return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
     } else if (K == 256 && g_tf_x6 && cls.logits == nullptr) {
       // X6 at K = 256: the 2-block tile does not fit the registers, so two launches of the
       // 1-block kernel, one per half of W's rows (X read twice; memory-bound either way)
-      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
       if (rc != GNN_OK) return rc;
-      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, cls, s);
+      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, cls,
+                                        bias ? bias + 128 : nullptr, s);
     } else if constexpr (GNN_TF_ONE256) {
       // one launch, 8 waves x 2 column blocks (128 W values per lane resident, 200 VGPRs):
       // X read and staged once for all 256 columns. In one process (tools/transform_tile_ab.py,
       // profiles/r03o_transform_one256_ab.log): 10M x 256 -> 256 9.63 ms (136 TF/s) vs 10.57
       // as two launches vs 9.95 hipBLASLt; 1M x 128 -> 256 0.545 vs 0.618 vs 0.628 ms
-      return launch_transform<K, 2, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, s);
+      return launch_transform<K, 2, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
     } else {
       // A/B: two launches of the 128-column kernel, one per half of W's rows (X read twice)
       if (cls.logits != nullptr) return GNN_E_UNSUPPORTED;
-      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
       if (rc != GNN_OK) return rc;
-      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, cls, s);
+      return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, cls,
+                                        bias ? bias + 128 : nullptr, s);
     }
   }
   return GNN_E_UNSUPPORTED;
@@ -525,7 +537,8 @@ template <bool RELU>
 static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
                            const float* w, int64_t fout, float* y, int64_t ldy,
                            void* stream, const RowIdx& ri = RowIdx{nullptr, 0, nullptr},
-                           const Classifier& cls = Classifier{nullptr, nullptr, nullptr, 0, 0}) {
+                           const Classifier& cls = Classifier{nullptr, nullptr, nullptr, 0, 0},
+                           const float* bias = nullptr) {
   if (n_rows < 0 || ldx < k || ldy < fout) return GNN_E_ARG;
   if (ri.row != nullptr && (ri.err == nullptr || ri.n_y < 0)) return GNN_E_ARG;
   if (!gnn_gcn_transform_supported(k, fout)) return GNN_E_UNSUPPORTED;
@@ -535,11 +548,11 @@ static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t 
     return GNN_E_ALIGN;
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (k) {
-    case 16: return dispatch_transform<16, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
-    case 32: return dispatch_transform<32, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
-    case 64: return dispatch_transform<64, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
-    case 128: return dispatch_transform<128, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
-    default: return dispatch_transform<256, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, s);
+    case 16: return dispatch_transform<16, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+    case 32: return dispatch_transform<32, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+    case 64: return dispatch_transform<64, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+    case 128: return dispatch_transform<128, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+    default: return dispatch_transform<256, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
   }
 }
 
@@ -566,6 +579,17 @@ extern "C" int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows
                                      const float* w, int64_t fout, float* y, int64_t ldy,
                                      void* stream) {
   return transform_entry<false>(x, ldx, n_rows, k, w, fout, y, ldy, stream);
+}
+
+// y = x w^T + bias (bias [fout], 16-B aligned): the transform of a GCN layer trained as
+// (A X) W^T + b (graphneuralnetwork_amd/ops.py _GcnLayerFn), the bias in the store epilogue
+extern "C" int gnn_gcn_transform_bias_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                                          const float* w, int64_t fout, const float* bias,
+                                          float* y, int64_t ldy, void* stream) {
+  if (n_rows > 0 && (!bias || !aligned_to(bias, 16))) return bias ? GNN_E_ALIGN : GNN_E_ARG;
+  return transform_entry<false>(x, ldx, n_rows, k, w, fout, y, ldy, stream,
+                                RowIdx{nullptr, 0, nullptr},
+                                Classifier{nullptr, nullptr, nullptr, 0, 0}, bias);
 }
 
 extern "C" int gnn_gcn_transform_rows_f32(const float* x, int64_t ldx, int64_t n_rows,

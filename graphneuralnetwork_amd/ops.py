@@ -482,21 +482,52 @@ def _transform_or_mm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return y if y is not None else torch.mm(x, w.t())
 
 
+# A layer with in_features <= out_features trains as (A X) W^T + b: the same product as the
+# reference's A (X W^T) + b (GCN/GCN.py:42-45), reassociated. The SpMM then gathers rows of X
+# instead of the support (no wider), and the backward needs dY and Z = A X only: dW = dY^T Z
+# and db = sum dY come out of ONE gemm_tn pass over (Z, dY) (dY read once, not next to dS and
+# X), and where X needs no gradient -- a first layer over the input features -- the backward
+# runs no SpMM at all (the A (X W^T) form needs dS = A^T dY for dW regardless).
+GCN_REASSOC = True
+
+
+def _reassociate(x, weight, g) -> bool:
+    fout, fin = weight.shape
+    return GCN_REASSOC and fin <= fout and x.shape[0] == g.n_cols
+
+
 class _GcnLayerFn(torch.autograd.Function):
     """Graph_conv_layer (GCN/GCN.py:41-47) as one differentiable op, trained the way the
-    reference's loop runs it (GCN/train_eval.py:43-48: forward, loss.backward()):
+    reference's loop runs it (GCN/train_eval.py:43-48: forward, loss.backward()). Two forms:
 
-    forward   S = X W^T on the MFMA transform -- scattered into the column-degree order of
-              A P^T when the graph takes that path (``column_order``), as at inference --
-              then Y = A S + b (the forward SpMM path, bias in its epilogue);
-    backward  dS = A^T dY (the same SpMM kernels; A itself when it is symmetric, as the GCN
-              normalisation is: no transposed copy), dX = dS W on the MFMA transform,
-              dW = dS^T X and db = the column sums of dY in one pass (gnn_gemm_tn_f32, a
-              K = n_rows reduction: 1.81 ms on hipBLASLt at cfg2).
-    The support S is not kept for backward (dW needs X and dS only)."""
+    A (X W^T) + b (in_features > out_features: the narrower SpMM)
+      forward   S = X W^T on the MFMA transform -- scattered into the column-degree order of
+                A P^T when the graph takes that path (``column_order``), as at inference --
+                then Y = A S + b (the forward SpMM path, bias in its epilogue);
+      backward  dS = A^T dY (the same SpMM kernels; A itself when it is symmetric, as the GCN
+                normalisation is: no transposed copy), dX = dS W on the MFMA transform,
+                dW = dS^T X and db = the column sums of dY in one pass (gnn_gemm_tn_f32, a
+                K = n_rows reduction: 1.81 ms on hipBLASLt at cfg2). S is not kept.
+    (A X) W^T + b (in_features <= out_features, ``GCN_REASSOC``)
+      forward   Z = A X (the SpMM over X), Y = Z W^T + b (the transform, bias in its store
+                epilogue: gnn_gcn_transform_bias_f32); Z is kept for backward;
+      backward  dW = dY^T Z and db = the column sums of dY in one gemm_tn pass that reads dY
+                once (d = b), and only when X needs a gradient dZ = dY W (transform) and
+                dX = A^T dZ (SpMM).
+    The two forms agree to fp32 rounding (a sum of products regrouped)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, g):
+        ctx.g = g
+        ctx.has_bias = bias is not None
+        ctx.reassoc = _reassociate(x, weight, g)
+        if ctx.reassoc:
+            z = spmm_forward(g, x)
+            y = gcn_transform(z, weight, bias=bias)
+            if y is None:
+                y = torch.mm(z, weight.t()) if bias is None else torch.addmm(bias, z, weight.t())
+            ctx.save_for_backward(z, weight)
+            return y
         order = column_order(g, weight.shape[0]) if x.shape[0] == g.n_cols else None
         s = None
         if order is not None:
@@ -506,19 +537,30 @@ class _GcnLayerFn(torch.autograd.Function):
         else:
             y = spmm_forward(g, _transform_or_mm(x, weight), bias)
         ctx.save_for_backward(x, weight)
-        ctx.g = g
-        ctx.has_bias = bias is not None
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, weight = ctx.saved_tensors
+        x, weight = ctx.saved_tensors  # Z = A X in the reassociated form
         gy = gy.contiguous()
-        ds = spmm_forward(ctx.g.transpose(), gy)
         gx = gw = gb = None
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.reassoc:
+            if ctx.needs_input_grad[1]:
+                # dW = dY^T Z as (Z^T dY)^T; db = the column sums of dY from the same loads
+                r = gemm_tn(x, gy, gy if want_b else None, trans=True)
+                if r is not None:
+                    gw, gb = r
+                else:
+                    gw = torch.mm(gy.t(), x)
+            if want_b and gb is None:
+                gb = gy.sum(0)
+            if ctx.needs_input_grad[0]:
+                gx = spmm_forward(ctx.g.transpose(), _transform_or_mm(gy, weight.t().contiguous()))
+            return gx, gw, gb, None
+        ds = spmm_forward(ctx.g.transpose(), gy)
         if ctx.needs_input_grad[0]:
             gx = _transform_or_mm(ds, weight.t().contiguous())
-        want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             # dW = dS^T X as (X^T dS)^T, with db = the column sums of dY read in the same pass
             r = gemm_tn(x, ds, gy if want_b else None, trans=True)
@@ -650,7 +692,8 @@ def set_transform_precision(mode: str) -> str:
 
 def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
                   out: torch.Tensor | None = None, out_rows: torch.Tensor | None = None,
-                  check_rows: bool = True, live: torch.Tensor | None = None) -> torch.Tensor | None:
+                  check_rows: bool = True, live: torch.Tensor | None = None,
+                  bias: torch.Tensor | None = None) -> torch.Tensor | None:
     """support = x @ weight^T on fp32 MFMA (gnn_gcn_transform_f32), the dense half of
     Graph_conv_layer.forward (GCN/GCN.py:42); ``relu=True``: max(x @ weight^T, 0)
     (gnn_linear_relu_f32, the SageLayer at GraphSAGE/GraphSAGE.py:18-20). Inference only
@@ -666,7 +709,10 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
 
     ``live`` (with ``relu=True``): a device int64 scalar; only rows [0, min(live, rows of x))
     are computed (gnn_linear_relu_live_f32) -- a sampled batch's frontier whose size the host
-    never read; the other output rows are left as they were."""
+    never read; the other output rows are left as they were.
+
+    ``bias`` (fp32 [fout], without relu / out_rows / live): x @ weight^T + bias, the add in
+    the store epilogue (gnn_gcn_transform_bias_f32)."""
     _require_device(x, weight)
     if (x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 2
             or weight.dim() != 2 or x.shape[1] != weight.shape[1]):
@@ -679,6 +725,15 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
         return None
     if out_rows is not None and relu:
         raise ValueError("out_rows= is supported without the ReLU epilogue only")
+    if bias is not None:
+        _require_device(bias)
+        if relu or out_rows is not None or live is not None:
+            raise ValueError("bias= is supported without relu / out_rows / live only")
+        if bias.dtype != torch.float32 or bias.numel() != fout:
+            raise ValueError("bias must be float32 [fout]")
+        bias = bias.contiguous()
+        if bias.data_ptr() % 16:
+            bias = bias.clone()
     if live is not None:
         _require_device(live)
         if not relu or out_rows is not None:
@@ -715,6 +770,12 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
             x.data_ptr(), x.stride(0), x.shape[0], live.data_ptr(), k, w.data_ptr(), fout,
             out.data_ptr(), out.stride(0), _lib.stream_handle(x.device)),
             "gnn_linear_relu_live_f32")
+        return out
+    if bias is not None:
+        _lib.check(lib.gnn_gcn_transform_bias_f32(
+            x.data_ptr(), x.stride(0), x.shape[0], k, w.data_ptr(), fout, bias.data_ptr(),
+            out.data_ptr(), out.stride(0), _lib.stream_handle(x.device)),
+            "gnn_gcn_transform_bias_f32")
         return out
     fn, name = ((lib.gnn_linear_relu_f32, "gnn_linear_relu_f32") if relu else
                 (lib.gnn_gcn_transform_f32, "gnn_gcn_transform_f32"))

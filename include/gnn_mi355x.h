@@ -344,6 +344,18 @@ int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k
                           int64_t fout, float* y, int64_t ldy, void* stream);
 
 /*
+ * y = x @ w^T + bias (bias [fout] fp32, 16-B aligned; the add in the store epilogue): the
+ * dense half of a Graph_conv_layer trained as (A X) W^T + b -- the same layer as
+ * GCN/GCN.py:42-45's A (X W^T) + b, reassociated where in_features <= out_features so that
+ * the backward's dW = dY^T (A X) and db = sum dY read dY once (graphneuralnetwork_amd/ops.py
+ * _GcnLayerFn). Shapes, alignment, arithmetic and return codes as gnn_gcn_transform_f32;
+ * GNN_E_ARG for a null bias with n_rows > 0, GNN_E_ALIGN for a misaligned one.
+ */
+int gnn_gcn_transform_bias_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                               const float* w, int64_t fout, const float* bias, float* y,
+                               int64_t ldy, void* stream);
+
+/*
  * The same product with the output rows scattered: y[y_row[i], :fout] = x[i, :k] @ w^T for
  * i < n_rows (y has n_y rows; x is read in order). With y_row = a degree order's inv (old ->
  * new id) it writes the support of GCN/GCN.py:42 directly in the row order the
@@ -533,7 +545,8 @@ int gnn_gat_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, int64_t n_r
  * GAT/train_eval.py:75-76 through GAT/models/layers.py:23): C = A^T B summed over the n rows
  * (A [n, m], B [n, k], row strides lda / ldb), written as C [m, k] (trans_c = 0, row stride
  * ldc >= k) or C^T [k, m] (trans_c = 1, ldc >= m); with d != NULL also dsum[k] = the column sums
- * of D [n, k] (the bias gradient, read in the same pass). Per block of rows the products are
+ * of D [n, k] (the bias gradient, read in the same pass; d == b with ldd == ldb sums B's own
+ * loads, no third read, at the split-bf16 wide shapes). Per block of rows the products are
  * accumulated in row order (fp32 FMAs; fp32 or split-bf16 MFMAs at the wide shapes, per
  * gnn_transform_set_precision), the block partials summed in block order (deterministic).
  * gnn_gemm_tn_supported(m, k): 1 = a wide shape (m, k) in {(128,128), (64,64), (128,64),

@@ -31,10 +31,12 @@ def _rand_graph(n, m, seed):
     return np.cumsum(rowptr), c.astype(np.int32), rng.standard_normal(m).astype(np.float32)
 
 
+@pytest.mark.parametrize("fout", [64, 128])
 @pytest.mark.parametrize("bias", [True, False])
-def test_gcn_layer_grads_vs_float64(dev, bias):
+def test_gcn_layer_grads_vs_float64(dev, bias, fout):
     """A non-symmetric graph (transposed CSR built for dX): Y, dX, dW, db against float64
-    dense autograd of A (X W^T) + b."""
+    dense autograd of A (X W^T) + b, in both of _GcnLayerFn's forms (128 -> 64: A (X W^T);
+    128 -> 128: (A X) W^T, ops.GCN_REASSOC)."""
     from graphneuralnetwork_amd.gcn import Graph_conv_layer
     from graphneuralnetwork_amd.graph import CsrGraph
     n = 400
@@ -45,7 +47,7 @@ def test_gcn_layer_grads_vs_float64(dev, bias):
     rows = np.repeat(np.arange(n), np.diff(rowptr))
     A.index_put_((torch.from_numpy(rows), torch.from_numpy(col.astype(np.int64))),
                  torch.from_numpy(val.astype(np.float64)), accumulate=True)
-    layer = Graph_conv_layer(128, 64, is_bias=bias).to(dev)
+    layer = Graph_conv_layer(128, fout, is_bias=bias).to(dev)
     if bias:
         torch.nn.init.normal_(layer.bias)
     X = torch.randn(n, 128, device=dev, requires_grad=True)
@@ -63,6 +65,74 @@ def test_gcn_layer_grads_vs_float64(dev, bias):
     close(layer.dense.weight.grad.cpu().numpy(), Wd.grad.numpy())
     if bias:
         close(layer.bias.grad.cpu().numpy(), bd.grad.numpy())
+
+
+@pytest.mark.parametrize("fin,fout", [(128, 128), (64, 128), (128, 64), (128, 256)])
+@pytest.mark.parametrize("x_grad", [True, False])
+def test_gcn_layer_forms_agree(dev, fin, fout, x_grad, monkeypatch):
+    """_GcnLayerFn's two forms of one layer -- A (X W^T) + b and (A X) W^T + b (GCN_REASSOC,
+    taken when in_features <= out_features) -- give the same output and gradients to fp32
+    rounding, with and without dX; the reassociated backward with X needing no gradient runs
+    no SpMM (its dW = dY^T Z needs Z = A X from the forward only)."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.gcn import Graph_conv_layer
+    from graphneuralnetwork_amd.graph import CsrGraph
+    rp, col, val = _rand_graph(3000, 30000, 4)
+    g = CsrGraph(torch.from_numpy(rp).to(dev), torch.from_numpy(col).to(dev),
+                 torch.from_numpy(val).to(dev), 3000, 3000)
+    torch.manual_seed(fin + fout)
+    layer = Graph_conv_layer(fin, fout).to(dev)
+    with torch.no_grad():
+        layer.bias.normal_()
+    X = torch.randn(3000, fin, device=dev)
+    gy = torch.randn(3000, fout, device=dev)
+    calls = []
+    real = ops.spmm_forward
+    monkeypatch.setattr(ops, "spmm_forward", lambda *a, **k: calls.append(1) or real(*a, **k))
+    res = {}
+    for re in (True, False):
+        monkeypatch.setattr(ops, "GCN_REASSOC", re)
+        assert ops._reassociate(X, layer.dense.weight, g) == (re and fin <= fout)
+        xx = X.clone().requires_grad_(x_grad)
+        layer.zero_grad(set_to_none=True)
+        calls.clear()
+        y = layer(xx, g)
+        n_fwd = len(calls)
+        y.backward(gy)
+        n_bwd = len(calls) - n_fwd
+        if re and fin <= fout and not x_grad:
+            assert n_bwd == 0  # dW = dY^T Z, db = colsum dY: no SpMM
+        else:
+            assert n_bwd == 1
+        res[re] = [y.detach(), layer.dense.weight.grad, layer.bias.grad] + (
+            [xx.grad] if x_grad else [])
+    for a, b in zip(res[True], res[False]):
+        close(a.cpu().numpy(), b.cpu().numpy())
+
+
+def test_transform_bias_and_tn_dsum_of_b(dev):
+    """gnn_gcn_transform_bias_f32: x W^T + b equals the transform plus b to fp32 rounding of
+    the one add (bit for bit), at 128 -> 128 and the split 256 -> 256; gnn_gemm_tn_f32 with
+    d == b (the x6 kernel's DB form: dsum from B's own loads) equals the three-operand call
+    with a copy of B as D, bit for bit."""
+    from graphneuralnetwork_amd.ops import gcn_transform, gemm_tn
+    gen = torch.Generator(device=dev).manual_seed(9)
+    for k, fo, n in ((128, 128, 50001), (256, 256, 7000), (64, 64, 333)):
+        x = torch.randn(n, k, device=dev, generator=gen)
+        w = torch.randn(fo, k, device=dev, generator=gen)
+        b = torch.randn(fo, device=dev, generator=gen)
+        y0 = gcn_transform(x, w)
+        y1 = gcn_transform(x, w, bias=b)
+        assert torch.equal(y1, y0 + b)
+    with pytest.raises(ValueError):
+        gcn_transform(x, w, bias=b, relu=True)
+    for n in (1, 37, 20000, 300001):
+        a = torch.randn(n, 128, device=dev, generator=gen)
+        bb = torch.randn(n, 128, device=dev, generator=gen)
+        c1, s1 = gemm_tn(a, bb, bb, trans=True)
+        c2, s2 = gemm_tn(a, bb, bb.clone(), trans=True)
+        assert torch.equal(c1, c2) and torch.equal(s1, s2)
+        close(s1.cpu().numpy(), bb.double().sum(0).cpu().numpy(), rtol=1e-5)
 
 
 def test_symmetric_graph_is_its_own_transpose(dev):
@@ -85,10 +155,11 @@ def test_symmetric_graph_is_its_own_transpose(dev):
 
 @pytest.mark.parametrize("order", ["natural", "degree"])
 def test_gcn_layer_training_cfg2_full_size(dev, order):
-    """The benchmarked training step at BASELINE cfg2 size (R-MAT 1M / 20.1M nnz, 128 -> 128):
-    the forward takes the column-ordered path (natural) or the degree-ordered graph P A P^T
-    GCN_Model trains over (degree: ops.gcn_train_order, XCD-direct hub plans in both
-    directions) and equals the inference layer bit for bit; the gradients equal float64
+    """The benchmarked training step at BASELINE cfg2 size (R-MAT 1M / 20.1M nnz, 128 -> 128)
+    over the natural graph or the degree-ordered graph P A P^T GCN_Model trains over (degree:
+    ops.gcn_train_order, XCD-direct hub plans in both directions), as (A X) W^T + b
+    (ops.GCN_REASSOC): the forward equals the inference layer to fp32 rounding; the gradients
+    equal float64
     references built from the C oracle's SpMM (dS = A dY, A symmetric) and numpy products
     (dX = dS W, dW = dS^T X, db = sum dY) on every row."""
     from graphneuralnetwork_amd import ops
@@ -111,7 +182,9 @@ def test_gcn_layer_training_cfg2_full_size(dev, order):
     with torch.no_grad():
         y_inf = layer(X, g)
     y = layer(X, g)
-    assert torch.equal(y.detach(), y_inf)
+    # training runs the 128 -> 128 layer as (A X) W^T + b (ops.GCN_REASSOC): the inference
+    # layer's A (X W^T) + b regrouped
+    close(y.detach().cpu().numpy(), y_inf.cpu().numpy())
     gy = torch.randn(n, 128, device=dev, generator=gen)
     y.backward(gy)
     assert g._transpose is None  # the symmetric graph served the backward itself
