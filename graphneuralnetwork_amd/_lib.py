@@ -97,8 +97,8 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_transform_set_precision": (ctypes.c_int, [ctypes.c_int]),
     "gnn_transform_get_precision": (ctypes.c_int, []),
     "gnn_gcn_transform_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
-    "gnn_gcn_transform_bias_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp,
-                                                  _i64, _vp]),
+    "gnn_gcn_transform_epi_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i32,
+                                                 ctypes.c_float, ctypes.c_uint64, _vp, _i64, _vp]),
     "gnn_linear_relu_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnn_linear_relu_live_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
                                                 _vp]),
@@ -219,8 +219,14 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_frontier_emit": (ctypes.c_int, [_i64, _vp, _vp, _vp]),
     "gnn_frontier_rank": (ctypes.c_int, [_vp, _i64, _i64, _vp, _vp, _vp]),
     "gnn_sample_layers_workspace_bytes": (ctypes.c_int64, [_i64]),
+    "gnn_linear_small_supported": (ctypes.c_int, [_i64, _i64]),
+    "gnn_linear_small_f32": (ctypes.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gnn_gemm_tn_supported": (ctypes.c_int, [_i64, _i64]),
     "gnn_gemm_tn_workspace_bytes": (_i64, [_i64, _i64, _i64]),
+    "gnn_gemm_tn_masked_supported": (ctypes.c_int, [_i64, _i64]),
+    "gnn_gemm_tn_masked_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, ctypes.c_float,
+                                              _i64, _i64, _i64, _vp, _i64, _i32, _vp, _vp, _i64,
+                                              _vp]),
     "gnn_gemm_tn_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _i64, _i32,
                                        _vp, _i64, _vp, _vp, _i64, _vp]),
     "gnn_sample_layers": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp, _i32, _vp,

@@ -138,6 +138,24 @@ template <int K> __device__ __forceinline__ int swz6(int rr) {
   return K >= 256 ? (rr >> 2) & 1 : K >= 128 ? (rr >> 1) & 1 : rr & 1;
 }
 template <int K> constexpr int x6_pitch() { return 2 * K + 32; }  // bytes per LDS row
+// One 32-bit hash of (seed, a, b): the dropout stream of the HIP kernels (the same function as
+// gat.hip's hash3 over (edge, head); restated by oracle/spmm_oracle.c oracle_hash3). An item is
+// kept when (h >> 8) / 2^24 >= p.
+__device__ __forceinline__ uint32_t dropout_hash(uint64_t seed, int64_t a, int b) {
+  uint32_t h = static_cast<uint32_t>(seed) ^ (static_cast<uint32_t>(seed >> 32) * 0x27d4eb2fu);
+  h ^= static_cast<uint32_t>(a) * 0x9e3779b9u;
+  h ^= static_cast<uint32_t>(static_cast<uint64_t>(a) >> 32) * 0x85ebca6bu;
+  h ^= static_cast<uint32_t>(b) * 0xc2b2ae35u;
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, int64_t a, int b, float p) {
+  return static_cast<float>(dropout_hash(seed, a, b) >> 8) * (1.0f / 16777216.0f) >= p;
+}
 // the transforms' arithmetic at K >= 128 and the GAT projection's at K in {64, 128}
 // (gnn_transform_set_precision, defined in transform.hip): 1 = X6 split bf16, 0 = fp32 MFMA
 extern int g_tf_x6;

@@ -295,11 +295,14 @@ __global__ __launch_bounds__(kTnThreads) void gemm_tn_mfma_kernel(
 // MFMA: the kernel is left paced by its HBM reads. C/D lane map as the f32 form's.
 // DB: D is B (dsum = the column sums of B, taken from B's own staged loads: no third read --
 // the bias gradient next to dW = dY^T Z of a layer trained as (A X) W^T + b).
-template <int M, int K, bool DSUM, bool DB = false>
+// MB: D is a mask H and the kernel multiplies B' = B . [H > 0] * mscale (elementwise, at
+// staging), dsum from B' -- dW, db of that layer when its ReLU and Dropout ran in the
+// transform's epilogue (H = their output: H > 0 exactly where the gradient passes).
+template <int M, int K, bool DSUM, bool DB = false, bool MB = false>
 __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
     const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb,
     const float* __restrict__ d, int64_t ldd, int64_t n, int64_t rows_per_block,
-    float* __restrict__ part) {
+    float* __restrict__ part, float mscale) {
   constexpr int A4 = M / 4, B4 = K / 4;
   constexpr int PA = M + 4, PB = K + 4;  // padded LDS row pitches (floats)
   constexpr int NA = (kTnRows * A4 + kTnThreads - 1) / kTnThreads;
@@ -322,7 +325,7 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
 #pragma unroll
   for (int q = 0; q < NB; ++q) ds[q] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  constexpr int ND = DB ? 1 : NB;  // D's float4s in flight (none of its own when D is B)
+  constexpr int ND = DB || (!DSUM && !MB) ? 1 : NB;  // D's float4s in flight (none when D is B)
   auto load = [&](int64_t row0, float4 (&va)[NA], float4 (&vb)[NB], float4 (&vd)[ND]) {
 #pragma unroll
     for (int q = 0; q < NA; ++q) {
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
       const bool ok = e < kTnRows * B4 && row < r1;
       vb[q] = ok ? *reinterpret_cast<const float4*>(b + row * ldb + 4 * (e % B4))
                  : make_float4(0.f, 0.f, 0.f, 0.f);
-      if constexpr (DSUM && !DB)
+      if constexpr ((DSUM || MB) && !DB)
         vd[q] = ok ? *reinterpret_cast<const float4*>(d + row * ldd + 4 * (e % B4))
                    : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -359,9 +362,16 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       const int e = t + q * kTnThreads;
+      if constexpr (MB) {  // after the wait for the tile: no stall on the prefetch
+        const float4 h = vd[q];
+        vb[q].x = h.x > 0.f ? vb[q].x * mscale : 0.f;
+        vb[q].y = h.y > 0.f ? vb[q].y * mscale : 0.f;
+        vb[q].z = h.z > 0.f ? vb[q].z * mscale : 0.f;
+        vb[q].w = h.w > 0.f ? vb[q].w * mscale : 0.f;
+      }
       if (e < kTnRows * B4) sb[(e / B4) * (PB / 4) + e % B4] = vb[q];
       if constexpr (DSUM) {
-        const float4 dv = DB ? vb[q] : vd[DB ? 0 : q];
+        const float4 dv = DB || MB ? vb[q] : vd[ND == 1 ? 0 : q];
         ds[q].x += dv.x;
         ds[q].y += dv.y;
         ds[q].z += dv.z;
@@ -647,11 +657,12 @@ static int64_t tn_blocks(int64_t n) {
 template <int M, int K>
 static int launch_tn(const float* a, int64_t lda, const float* b, int64_t ldb, const float* d,
                      int64_t ldd, int64_t n, float* c, int64_t ldc, int trans_c, float* dsum,
-                     float* part, hipStream_t s) {
+                     float* part, hipStream_t s, const float* mask = nullptr, int64_t ldm = 0,
+                     float mscale = 1.f) {
   const int64_t blocks = tn_blocks(n);
   int64_t rpb = (n + blocks - 1) / blocks;
   rpb = (rpb + kTnRows - 1) / kTnRows * kTnRows;
-  const int64_t stride = M * K + (d ? K : 0);
+  const int64_t stride = M * K + (d || (mask && dsum) ? K : 0);
 #ifndef GNN_TN_FMA  // A/B: the FMA kernel at every shape
   constexpr bool mfma = M >= 64 && K >= 32;
 #else
@@ -659,16 +670,23 @@ static int launch_tn(const float* a, int64_t lda, const float* b, int64_t ldb, c
 #endif
   if constexpr (mfma) {
     if (GNN_TN_X6 != 0 && g_tf_x6 != 0) {  // the transforms' arithmetic mode (set_precision)
-      if (d && d == b && ldd == ldb)  // dsum of B itself: B's loads serve both
-        hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, true, true>),
-                           dim3(static_cast<unsigned>(blocks)), dim3(kTnThreads), 0, s, a, lda, b,
-                           ldb, d, ldd, n, rpb, part);
+      const dim3 grid(static_cast<unsigned>(blocks)), blk(kTnThreads);
+      if (mask)  // B' = B . [mask > 0] * mscale (gnn_gemm_tn_masked_f32)
+        if (dsum)
+          hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, true, false, true>), grid, blk, 0, s, a,
+                             lda, b, ldb, mask, ldm, n, rpb, part, mscale);
+        else
+          hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, false, false, true>), grid, blk, 0, s, a,
+                             lda, b, ldb, mask, ldm, n, rpb, part, mscale);
+      else if (d && d == b && ldd == ldb)  // dsum of B itself: B's loads serve both
+        hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, true, true>), grid, blk, 0, s, a, lda, b, ldb,
+                           d, ldd, n, rpb, part, 1.f);
       else if (d)
-        hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, true>), dim3(static_cast<unsigned>(blocks)),
-                           dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+        hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, true>), grid, blk, 0, s, a, lda, b, ldb, d,
+                           ldd, n, rpb, part, 1.f);
       else
-        hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, false>), dim3(static_cast<unsigned>(blocks)),
-                           dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
+        hipLaunchKernelGGL((gemm_tn_x6_kernel<M, K, false>), grid, blk, 0, s, a, lda, b, ldb, d,
+                           ldd, n, rpb, part, 1.f);
     } else if (d) {
       hipLaunchKernelGGL((gemm_tn_mfma_kernel<M, K, true>), dim3(static_cast<unsigned>(blocks)),
                          dim3(kTnThreads), 0, s, a, lda, b, ldb, d, ldd, n, rpb, part);
@@ -780,4 +798,42 @@ extern "C" int gnn_gemm_tn_f32(const float* a, int64_t lda, const float* b, int6
   if (m == 16 && k == 64)  // [del | der] against Wh: both GAT a-vector gradients in one pass
     return launch_tn<16, 64>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
   return launch_tn<8, 64>(a, lda, b, ldb, d, ldd, n, c, ldc, tc, dsum, part, s);
+}
+
+// C = A^T B' with B' = B . [H > 0] * scale elementwise (H [n, k], row stride ldh), and dsum = the
+// column sums of B' when dsum != NULL: dW and db of a GCN layer whose ReLU and Dropout ran in its
+// transform's store epilogue (gnn_gcn_transform_epi_f32), H being that output -- the gradient
+// passes exactly where H > 0, scaled by 1 / (1 - p). Wide shapes with m, k >= 64 in the
+// split-bf16 arithmetic only (gnn_gemm_tn_masked_supported); the workspace as gnn_gemm_tn_f32's.
+extern "C" int gnn_gemm_tn_masked_supported(int64_t m, int64_t k) {
+  return GNN_TN_X6 != 0 && g_tf_x6 != 0 && tn_wide(m, k) && m >= 64 && k >= 64;
+}
+
+extern "C" int gnn_gemm_tn_masked_f32(const float* a, int64_t lda, const float* b, int64_t ldb,
+                                      const float* h, int64_t ldh, float scale, int64_t n,
+                                      int64_t m, int64_t k, float* c, int64_t ldc, int32_t trans_c,
+                                      float* dsum, void* workspace, int64_t workspace_bytes,
+                                      void* stream) {
+  if (n < 0 || !a || !b || !h || !c || !workspace || lda < m || ldb < k || ldh < k)
+    return GNN_E_ARG;
+  if (trans_c ? ldc < m : ldc < k) return GNN_E_ARG;
+  if (!gnn_gemm_tn_masked_supported(m, k)) return GNN_E_UNSUPPORTED;
+  if (workspace_bytes < gnn_gemm_tn_workspace_bytes(n, m, k)) return GNN_E_ARG;
+  if (!aligned_to(a, 16) || !aligned_to(b, 16) || !aligned_to(h, 16) || lda % 4 || ldb % 4 ||
+      ldh % 4)
+    return GNN_E_ALIGN;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(workspace);
+  const int tc = trans_c ? 1 : 0;
+  if (m == 128 && k == 128)
+    return launch_tn<128, 128>(a, lda, b, ldb, nullptr, 0, n, c, ldc, tc, dsum, part, s, h, ldh,
+                               scale);
+  if (m == 64 && k == 64)
+    return launch_tn<64, 64>(a, lda, b, ldb, nullptr, 0, n, c, ldc, tc, dsum, part, s, h, ldh,
+                             scale);
+  if (m == 128 && k == 64)
+    return launch_tn<128, 64>(a, lda, b, ldb, nullptr, 0, n, c, ldc, tc, dsum, part, s, h, ldh,
+                              scale);
+  return launch_tn<64, 128>(a, lda, b, ldb, nullptr, 0, n, c, ldc, tc, dsum, part, s, h, ldh,
+                            scale);
 }

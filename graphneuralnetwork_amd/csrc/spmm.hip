@@ -554,9 +554,12 @@ static int launch_spmm_t(const SpmmLaunch& L) {
   SpmmParams p = L.p;
   const int64_t seg_blocks = (p.n_seg + kWavesPerBlock - 1) / kWavesPerBlock;
   const int64_t mid_blocks = (p.n_mid + kWavesPerBlock - 1) / kWavesPerBlock;
-  if constexpr (VW == 4 && LPR >= 16 && !STAGE) {
+  if constexpr (VW == 4 && !STAGE) {
     if (p.task_row != nullptr) {  // packed row tasks in place of the small-row class
-      constexpr int UT = (GNN_SPMM_TASK_U > 0 && NCH == 1) ? GNN_SPMM_TASK_U : (U > 1 ? U : 2);
+      // neighbour rows in flight per slot: at most LPR (a batch never straddles a chunk of LPR
+      // edges), so the narrow rows (LPR = 2: feat 5-8, 32 slots per wave) take 2
+      constexpr int UT0 = (GNN_SPMM_TASK_U > 0 && NCH == 1) ? GNN_SPMM_TASK_U : (U > 1 ? U : 2);
+      constexpr int UT = UT0 < LPR ? UT0 : LPR;
       const int64_t task_blocks = (p.n_task + kWavesPerBlock - 1) / kWavesPerBlock;
       p.seg_waves = seg_blocks * kWavesPerBlock;
       p.mid_waves = mid_blocks * kWavesPerBlock;

@@ -1,10 +1,10 @@
 // transform.hip -- the GCN feature transform on the matrix cores: Y = X W^T (fp32).
 //
 // Replaces `support = self.dense(X_input)` (nn.Linear, no bias) at GCN/GCN.py:42, the
-// dense half of Graph_conv_layer.forward (with the layer's bias in the store epilogue,
-// gnn_gcn_transform_bias_f32, when training runs the layer as (A X) W^T + b); with the
-// ReLU epilogue (gnn_linear_relu_f32) the SageLayer's relu(weight(cat[self, agg])) at
-// GraphSAGE/GraphSAGE.py:18-20.
+// dense half of Graph_conv_layer.forward (with the layer's bias, and GCN_Model's ReLU and
+// Dropout, in the store epilogue -- gnn_gcn_transform_epi_f32 -- when training runs the layer
+// as (A X) W^T + b); with the ReLU epilogue (gnn_linear_relu_f32) the SageLayer's
+// relu(weight(cat[self, agg])) at GraphSAGE/GraphSAGE.py:18-20.
 // Shapes: X [n, K] row-major, W [FO, K] (nn.Linear's [out, in]), Y [n, FO].
 //
 // One workgroup = 4 waves; the X tile (64 rows x K) is staged in LDS once by all four
@@ -42,6 +42,21 @@ struct Classifier {
   float* logits;    // [n_rows, ldl]
   int64_t ldl;
   int n_cls;
+};
+// the optional store epilogue of the plain mode: y = dropout(act(x w^T + bias)) -- a GCN layer
+// trained as (A X) W^T + b with GCN_Model's ReLU and Dropout after it (gnn_gcn_transform_epi_f32)
+struct TfEpi {
+  const float* bias = nullptr;  // [fout] or null
+  float drop_p = 0.f;           // element (row, col) kept iff dropout_keep(seed, row, col0 + col, p)
+  float drop_scale = 1.f;       // 1 / (1 - p)
+  uint64_t seed = 0;
+  int col0 = 0;                 // column offset of this launch (the two-launch 256 split)
+  TfEpi shifted(int c) const {
+    TfEpi e = *this;
+    if (e.bias) e.bias += c;
+    e.col0 += c;
+    return e;
+  }
 };
 // kernel epilogue modes
 constexpr int kTfPlain = 0, kTfScatter = 1, kTfClassify = 2;
@@ -86,7 +101,7 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
     const float* __restrict__ x, int64_t ldx, int64_t n_rows, const float* __restrict__ w,
     float* __restrict__ y, int64_t ldy, const int64_t* __restrict__ y_row, int64_t n_y,
     int32_t* __restrict__ err, Classifier cls, const int64_t* __restrict__ live,
-    const float* __restrict__ bias) {
+    TfEpi epi) {
   if (live != nullptr) {  // uniform: every wave reads the same count
     const int64_t l = *live;
     n_rows = l < n_rows ? (l > 0 ? l : 0) : n_rows;
@@ -330,9 +345,9 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
           float4 o = make_float4(acc[j][cb][0], acc[j][cb][1], acc[j][cb][2], acc[j][cb][3]);
-          if (bias != nullptr) {  // uniform: the Linear's bias (gnn_gcn_transform_bias_f32)
-            const float4 bv =
-                *reinterpret_cast<const float4*>(bias + (wv * CB + cb) * 16 + 4 * q);
+          const int col = (wv * CB + cb) * 16 + 4 * q;
+          if (epi.bias != nullptr) {  // uniform: the layer's bias (gnn_gcn_transform_epi_f32)
+            const float4 bv = *reinterpret_cast<const float4*>(epi.bias + col);
             o.x += bv.x;
             o.y += bv.y;
             o.z += bv.z;
@@ -343,6 +358,13 @@ __global__ __launch_bounds__(NW * kWave) void gcn_transform_kernel(
             o.y = fmaxf(o.y, 0.f);
             o.z = fmaxf(o.z, 0.f);
             o.w = fmaxf(o.w, 0.f);
+          }
+          if (epi.drop_p > 0.f) {  // uniform: inverted dropout, one hash per element
+            const int c = epi.col0 + col;
+            o.x = dropout_keep(epi.seed, orow, c, epi.drop_p) ? o.x * epi.drop_scale : 0.f;
+            o.y = dropout_keep(epi.seed, orow, c + 1, epi.drop_p) ? o.y * epi.drop_scale : 0.f;
+            o.z = dropout_keep(epi.seed, orow, c + 2, epi.drop_p) ? o.z * epi.drop_scale : 0.f;
+            o.w = dropout_keep(epi.seed, orow, c + 3, epi.drop_p) ? o.w * epi.drop_scale : 0.f;
           }
           *reinterpret_cast<float4*>(y + orow * ldy + (wv * CB + cb) * 16 + 4 * q) = o;
         }
@@ -420,26 +442,26 @@ int g_tf_x6 = 1;
 template <int K, int CB, int NW, bool RELU, int TR, bool X6>
 static void launch_transform_kernel(dim3 grid, const float* x, int64_t ldx, int64_t n_rows,
                                     const float* w, float* y, int64_t ldy, const RowIdx& ri,
-                                    const Classifier& cls, const float* bias, hipStream_t s) {
+                                    const Classifier& cls, const TfEpi& epi, hipStream_t s) {
   if (ri.row != nullptr)  // a template flag: no index loads in the in-order kernel
     hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfScatter, X6>), grid,
                        dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err,
-                       cls, ri.live, bias);
+                       cls, ri.live, epi);
   else if (RELU && cls.logits != nullptr)  // the classifier epilogue: SageLayer GEMMs only
     hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, RELU ? kTfClassify : kTfPlain,
                                              X6>),
                        grid, dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y,
-                       ri.err, cls, ri.live, bias);
+                       ri.err, cls, ri.live, epi);
   else
     hipLaunchKernelGGL((gcn_transform_kernel<K, CB, NW, RELU, TR, kTfPlain, X6>), grid,
                        dim3(NW * kWave), 0, s, x, ldx, n_rows, w, y, ldy, ri.row, ri.n_y, ri.err,
-                       cls, ri.live, bias);
+                       cls, ri.live, epi);
 }
 
 template <int K, int CB, int NW, bool RELU, int TR>
 static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, const float* w,
                                float* y, int64_t ldy, const RowIdx& ri, const Classifier& cls,
-                               const float* bias, hipStream_t s) {
+                               const TfEpi& epi, hipStream_t s) {
   const int64_t tiles = (n_rows + TR - 1) / TR;
 #ifndef GNN_TF_GRID
 #define GNN_TF_GRID 512  // persistent grid: 2 workgroups per CU
@@ -450,11 +472,11 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
   // X6 tiles: 3 bf16 planes, at most 32 rows; 2 blocks of K = 256 pieces (192 VGPRs) spill
   if constexpr (K >= 128 && TR <= 32 && !(K == 256 && CB == 2)) {
     if (g_tf_x6) {
-      launch_transform_kernel<K, CB, NW, RELU, TR, true>(g, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+      launch_transform_kernel<K, CB, NW, RELU, TR, true>(g, x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
       return launch_status();
     }
   }
-  launch_transform_kernel<K, CB, NW, RELU, TR, false>(g, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+  launch_transform_kernel<K, CB, NW, RELU, TR, false>(g, x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
   return launch_status();
 }
 
@@ -472,62 +494,62 @@ static int launch_transform_tr(const float* x, int64_t ldx, int64_t n_rows, cons
 // 2891 vs 307 / 2932 us; K = 64 -> 64 keeps 64 rows (95 vs 113 us at 1M).
 template <int K, int CB, int NW, bool RELU>
 static int launch_transform(const float* x, int64_t ldx, int64_t n_rows, const float* w,
-                            float* y, int64_t ldy, const RowIdx& ri, const Classifier& cls, const float* bias, hipStream_t s) {
+                            float* y, int64_t ldy, const RowIdx& ri, const Classifier& cls, const TfEpi& epi, hipStream_t s) {
   constexpr int64_t slots = GNN_TF_GRID * kTfWaves / NW;
 #ifdef GNN_TF_TR32_ROWS  // A/B: 16-row tiles below GNN_TF_TR16_ROWS, 32-row below this
 #ifndef GNN_TF_TR16_ROWS
 #define GNN_TF_TR16_ROWS (32 * 2 * slots)
 #endif
-  if (n_rows < GNN_TF_TR16_ROWS) return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
-  if (n_rows < GNN_TF_TR32_ROWS) return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+  if (n_rows < GNN_TF_TR16_ROWS) return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
+  if (n_rows < GNN_TF_TR32_ROWS) return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
 #endif
   // X6 at K = 256: 16-row tiles at every size (in one process, tools/transform_x6_ab.py,
   // profiles/r03x_transform_x6_ab.log: 62K / 200K x 256 -> 128 30.9 / 79.9 vs 32.9 / 89.7 us
   // with 32-row tiles; K = 128 keeps 32: 1M x 128 -> 128 205 vs 211 us)
   if (GNN_TF_MIN_TR <= 16 &&
       (n_rows < 32 * 2 * slots || (K == 256 && g_tf_x6 && !(CB == 2 && K == 256))))
-    return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+    return launch_transform_tr<K, CB, NW, RELU, 16>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
   if (GNN_TF_MIN_TR <= 32 && (K > GNN_TF_TR64_MAX_K || n_rows < 64 * 2 * slots))
-    return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+    return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
   if constexpr (K <= GNN_TF_TR64_MAX_K || GNN_TF_MIN_TR > 32)
-    return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
-  return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+    return launch_transform_tr<K, CB, NW, RELU, 64>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
+  return launch_transform_tr<K, CB, NW, RELU, 32>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
 }
 
 template <int K, bool RELU>
 static int dispatch_transform(int64_t fout, const float* x, int64_t ldx, int64_t n_rows,
                               const float* w, float* y, int64_t ldy, const RowIdx& ri,
-                              const Classifier& cls, const float* bias, hipStream_t s) {
-  if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+                              const Classifier& cls, const TfEpi& epi, hipStream_t s) {
+  if (fout == 64) return launch_transform<K, 1, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
   if (fout == 128) {
     if constexpr (K <= 128 || GNN_TF_K256_CB2)
-      return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+      return launch_transform<K, 2, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
     else
-      return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+      return launch_transform<K, 1, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
   }
   if (fout == 256) {
     if constexpr (K <= 64) {
-      return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+      return launch_transform<K, 4, kTfWaves, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
     } else if (K == 256 && g_tf_x6 && cls.logits == nullptr) {
       // X6 at K = 256: the 2-block tile does not fit the registers, so two launches of the
       // 1-block kernel, one per half of W's rows (X read twice; memory-bound either way)
-      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
       if (rc != GNN_OK) return rc;
       return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, cls,
-                                        bias ? bias + 128 : nullptr, s);
+                                        epi.shifted(128), s);
     } else if constexpr (GNN_TF_ONE256) {
       // one launch, 8 waves x 2 column blocks (128 W values per lane resident, 200 VGPRs):
       // X read and staged once for all 256 columns. In one process (tools/transform_tile_ab.py,
       // profiles/r03o_transform_one256_ab.log): 10M x 256 -> 256 9.63 ms (136 TF/s) vs 10.57
       // as two launches vs 9.95 hipBLASLt; 1M x 128 -> 256 0.545 vs 0.618 vs 0.628 ms
-      return launch_transform<K, 2, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+      return launch_transform<K, 2, 8, RELU>(x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
     } else {
       // A/B: two launches of the 128-column kernel, one per half of W's rows (X read twice)
       if (cls.logits != nullptr) return GNN_E_UNSUPPORTED;
-      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+      const int rc = dispatch_transform<K, RELU>(128, x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
       if (rc != GNN_OK) return rc;
       return dispatch_transform<K, RELU>(128, x, ldx, n_rows, w + 128 * K, y + 128, ldy, ri, cls,
-                                        bias ? bias + 128 : nullptr, s);
+                                        epi.shifted(128), s);
     }
   }
   return GNN_E_UNSUPPORTED;
@@ -538,7 +560,7 @@ static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t 
                            const float* w, int64_t fout, float* y, int64_t ldy,
                            void* stream, const RowIdx& ri = RowIdx{nullptr, 0, nullptr},
                            const Classifier& cls = Classifier{nullptr, nullptr, nullptr, 0, 0},
-                           const float* bias = nullptr) {
+                           const TfEpi& epi = TfEpi{}) {
   if (n_rows < 0 || ldx < k || ldy < fout) return GNN_E_ARG;
   if (ri.row != nullptr && (ri.err == nullptr || ri.n_y < 0)) return GNN_E_ARG;
   if (!gnn_gcn_transform_supported(k, fout)) return GNN_E_UNSUPPORTED;
@@ -548,11 +570,11 @@ static int transform_entry(const float* x, int64_t ldx, int64_t n_rows, int64_t 
     return GNN_E_ALIGN;
   hipStream_t s = static_cast<hipStream_t>(stream);
   switch (k) {
-    case 16: return dispatch_transform<16, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
-    case 32: return dispatch_transform<32, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
-    case 64: return dispatch_transform<64, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
-    case 128: return dispatch_transform<128, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
-    default: return dispatch_transform<256, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, bias, s);
+    case 16: return dispatch_transform<16, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
+    case 32: return dispatch_transform<32, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
+    case 64: return dispatch_transform<64, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
+    case 128: return dispatch_transform<128, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
+    default: return dispatch_transform<256, RELU>(fout, x, ldx, n_rows, w, y, ldy, ri, cls, epi, s);
   }
 }
 
@@ -581,15 +603,25 @@ extern "C" int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows
   return transform_entry<false>(x, ldx, n_rows, k, w, fout, y, ldy, stream);
 }
 
-// y = x w^T + bias (bias [fout], 16-B aligned): the transform of a GCN layer trained as
-// (A X) W^T + b (graphneuralnetwork_amd/ops.py _GcnLayerFn), the bias in the store epilogue
-extern "C" int gnn_gcn_transform_bias_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
-                                          const float* w, int64_t fout, const float* bias,
-                                          float* y, int64_t ldy, void* stream) {
-  if (n_rows > 0 && (!bias || !aligned_to(bias, 16))) return bias ? GNN_E_ALIGN : GNN_E_ARG;
-  return transform_entry<false>(x, ldx, n_rows, k, w, fout, y, ldy, stream,
-                                RowIdx{nullptr, 0, nullptr},
-                                Classifier{nullptr, nullptr, nullptr, 0, 0}, bias);
+// y = dropout(act(x w^T + bias)) (bias [fout] 16-B aligned or null; act = ReLU if relu;
+// element (i, c) kept iff dropout_keep(seed, i, c, drop_p), kept values scaled by 1/(1 - p)):
+// the transform of a GCN layer trained as (A X) W^T + b with GCN_Model's ReLU and Dropout in
+// its store epilogue (graphneuralnetwork_amd/ops.py _GcnLayerFn)
+extern "C" int gnn_gcn_transform_epi_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                                         const float* w, int64_t fout, const float* bias,
+                                         int32_t relu, float drop_p, uint64_t drop_seed, float* y,
+                                         int64_t ldy, void* stream) {
+  if (!(drop_p >= 0.f && drop_p < 1.f)) return GNN_E_ARG;
+  if (bias && !aligned_to(bias, 16)) return GNN_E_ALIGN;
+  TfEpi epi;
+  epi.bias = bias;
+  epi.drop_p = drop_p;
+  epi.drop_scale = 1.f / (1.f - drop_p);
+  epi.seed = drop_seed;
+  const RowIdx ri{nullptr, 0, nullptr};
+  const Classifier cls{nullptr, nullptr, nullptr, 0, 0};
+  return relu ? transform_entry<true>(x, ldx, n_rows, k, w, fout, y, ldy, stream, ri, cls, epi)
+              : transform_entry<false>(x, ldx, n_rows, k, w, fout, y, ldy, stream, ri, cls, epi);
 }
 
 extern "C" int gnn_gcn_transform_rows_f32(const float* x, int64_t ldx, int64_t n_rows,

@@ -23,7 +23,10 @@ column-degree-ordered graph A P^T (``ops.column_order``): the transform writes t
 rows in that order and the SpMM reads the hub rows in place, with no per-call staging copy.
 Training ``GCN_Model`` on such a (symmetric) graph runs every layer over P A P^T
 (``ops.gcn_train_order``: X permuted once on entry, the logits once on exit), so the backward
-SpMM dS = A dY reads its hub rows in place too.
+SpMM dS = A dY reads its hub rows in place too. In training, a layer with in_features <=
+out_features runs as (A X) W^T + b (ops._GcnLayerFn), and a Graph_conv_layer -> ReLU ->
+Dropout triple of such a layer as one op: ReLU and (hashed) dropout in the transform's store
+epilogue, their backward folded into the weight-gradient pass (``_fuse_train``).
 """
 from __future__ import annotations
 
@@ -32,8 +35,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
-from .ops import (PermuteRows, column_order, gcn_layer, gcn_train_order, gcn_transform, spmm,
-                  spmm_forward)
+from .ops import (PermuteRows, column_order, dropout_seed, fuses_relu_dropout, gcn_layer,
+                  gcn_train_order, gcn_transform, spmm, spmm_forward)
 
 
 class GCN_Model(nn.Module):
@@ -88,6 +91,17 @@ class GCN_Model(nn.Module):
             gcn_block = blocks[i]
             if gcn_block._get_name() == 'Graph_conv_layer':
                 nxt = blocks[i + 1] if i + 1 < len(blocks) else None
+                span = _fuse_train(gcn_block, nxt, blocks[i + 2] if i + 2 < len(blocks) else None,
+                                   X, adj)
+                if span:
+                    # Graph_conv_layer -> ReLU (-> Dropout) in training: one op, ReLU and dropout
+                    # in the transform's epilogue (GCN/GCN.py:12-14)
+                    drop = blocks[i + 2] if span == 3 else None
+                    p = drop.p if drop is not None and drop.training else 0.0
+                    X = gcn_layer(as_csr(adj), X, gcn_block.dense.weight, gcn_block.bias,
+                                  relu_dropout=(p, dropout_seed() if p > 0 else 0))
+                    i += span
+                    continue
                 if _fuse_relu(gcn_block, nxt, X):
                     # the ReLU in the SpMM's store epilogue (GNN_EPI_RELU): one pass over the
                     # [n, hidden] activations fewer at inference
@@ -99,6 +113,29 @@ class GCN_Model(nn.Module):
                 X = gcn_block(X)
             i += 1
         return X
+
+
+def _no_hooks(*mods) -> bool:
+    return not any(m._forward_hooks or m._forward_pre_hooks for m in mods)
+
+
+def _fuse_train(block, nxt, nxt2, X, adj) -> int:
+    """How many modules from ``block`` run as one training op (0: none): 3 for
+    Graph_conv_layer -> nn.ReLU -> nn.Dropout, 2 for Graph_conv_layer -> nn.ReLU (a Dropout
+    with hooks runs on its own), when the layer trains in the reassociated form on a transform
+    shape (ops.fuses_relu_dropout) and none of the fused modules has hooks (they would not run).
+    """
+    if not (isinstance(block, Graph_conv_layer) and type(nxt) is nn.ReLU
+            and isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.float32
+            and torch.is_grad_enabled() and _no_hooks(block, nxt)):
+        return 0
+    if not (X.requires_grad or any(p.requires_grad for p in block.parameters())):
+        return 0
+    g = as_csr(adj)
+    if X.dim() != 2 or X.shape[1] != block.in_features or not fuses_relu_dropout(
+            X, block.dense.weight, g):
+        return 0
+    return 3 if type(nxt2) is nn.Dropout and _no_hooks(nxt2) else 2
 
 
 def _fuse_relu(block, nxt, X) -> bool:

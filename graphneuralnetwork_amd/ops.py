@@ -84,15 +84,25 @@ def xcd_hub_rows_for(n_cols: int, feat: int) -> int:
 # Packed row tasks (gnn_spmm_csr_tasks_f32, spmm.hip packed_rows): rows of degree <=
 # TASK_MAX_DEG are streamed a task (<= 63 consecutive rows, ~TASK_COST edges + rows) per wave
 # instead of one wave per row, so the rowptr -> col -> X chain of short rows is paid once per
-# task. Needs the 16-B vector path and feat > 32 (two or fewer edge slots per 16 lanes).
+# task. Needs the 16-B vector path. Narrow rows (feat <= 32: LPR <= 8 lanes per row, 8 or more
+# edge slots per wave) take tasks of up to TASK_COST_NARROW edges + rows, so that every slot of
+# the wave gets rows (one wave per row left most of its lanes idle at feat 8).
 SPMM_TASKS = True
+SPMM_TASKS_NARROW = True
 TASK_MAX_DEG = 128
 TASK_COST = 128  # 256 until late round 4: 128 is 0.7 % faster with the slice groups (cfg2, north star)
+TASK_COST_NARROW = 2048
+
+
+def _task_cost(feat: int) -> int:
+    return TASK_COST_NARROW if feat <= 32 else TASK_COST
 
 
 def _tasks_ok(feat: int, *ts) -> bool:
-    # every column block of the launch (<= 2048 wide) must be a vector block wider than 32
-    if not SPMM_TASKS or feat % 4 or feat <= 32 or 0 < feat % 2048 <= 32:
+    # every column block of the launch (<= 2048 wide) must be a vector block; one of 32 or
+    # fewer columns only with the narrow tasks
+    if not SPMM_TASKS or feat % 4 or (not SPMM_TASKS_NARROW and (feat <= 32
+                                                                  or 0 < feat % 2048 <= 32)):
         return False
     return all(t is None or (t.data_ptr() % 16 == 0 and (t.dim() == 1 or t.stride(0) % 4 == 0))
                for t in ts)
@@ -188,7 +198,8 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
                        "gnn_gather_rows_f32")
         if tasks:
             gh = CsrGraph(g.rowptr, hp.col_hub, g.val, g.n_rows, g.n_cols)
-            _spmm_tasks_call(lib, gh, hp.col_hub, g.task_plan(seg, TASK_MAX_DEG, TASK_COST), x,
+            _spmm_tasks_call(lib, gh, hp.col_hub,
+                             g.task_plan(seg, TASK_MAX_DEG, _task_cost(feat)), x,
                              xh, feat, bias, out, out.stride(0), partial,
                              flags | (_lib.EPI_SKIP_EMPTY if skip_empty else 0), stream,
                              "gnn_spmm_csr_tasks_f32 (hub)")
@@ -200,7 +211,8 @@ def spmm_forward(g: CsrGraph, x: torch.Tensor, bias: torch.Tensor | None = None,
         _lib.check(rc, "gnn_spmm_csr_hub_f32")
         return out
     if tasks and g.nnz:
-        _spmm_tasks_call(lib, g, g.col, g.task_plan(seg, TASK_MAX_DEG, TASK_COST), x, None, feat,
+        _spmm_tasks_call(lib, g, g.col, g.task_plan(seg, TASK_MAX_DEG, _task_cost(feat)), x,
+                         None, feat,
                          bias, out, out.stride(0), partial,
                          flags | (_lib.EPI_SKIP_EMPTY if skip_empty else 0), stream,
                          "gnn_spmm_csr_tasks_f32")
@@ -232,7 +244,7 @@ def _spmm_xcd(lib, g: CsrGraph, xp, x, feat, bias, out, seg, skip_empty, flags, 
     _spmm_hub_call(lib, xp.items, xp.items.col, p1, p1.args(), x, buf, feat, None, buf[k:], feat,
                    None, 0, stream, "gnn_spmm_csr_hub_f32 (xcd items)")
     if _tasks_ok(feat, x, out, bias, buf):
-        tp = xp.rest.task_plan(seg, TASK_MAX_DEG, TASK_COST)
+        tp = xp.rest.task_plan(seg, TASK_MAX_DEG, _task_cost(feat))
         partial = None
         if tp.base.n_seg:
             partial = torch.empty((tp.base.n_seg, feat), dtype=torch.float32, device=x.device)
@@ -390,7 +402,7 @@ def _spmm_xcd_direct(lib, xp, x, feat, bias, out, seg, skip_empty, flags, stream
         x.data_ptr(), x.stride(0), feat, None, part.data_ptr(), feat, p1.seg_len, *p1.args(),
         None, 0, stream), "gnn_spmm_csr_f32 (xcd direct items)")
     if _tasks_ok(feat, x, out, bias, part):
-        tp = rest.task_plan(seg, TASK_MAX_DEG, TASK_COST)
+        tp = rest.task_plan(seg, TASK_MAX_DEG, _task_cost(feat))
         partial = None
         if tp.base.n_seg:
             partial = torch.empty((tp.base.n_seg, feat), dtype=torch.float32, device=x.device)
@@ -476,9 +488,63 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, d: torch.Tensor | None = None,
     return c, dsum
 
 
+def gemm_tn_masked(a: torch.Tensor, b: torch.Tensor, h: torch.Tensor, scale: float,
+                   want_dsum: bool, trans: bool = False):
+    """(A^T B', column sums of B' if want_dsum) for B' = B . [H > 0] * scale
+    (gnn_gemm_tn_masked_f32): the weight / bias gradients behind a fused ReLU + dropout epilogue
+    whose output is H. Where the kernel does not take the shape, B' is formed with torch and
+    handed to ``gemm_tn`` (None if that does not take it either)."""
+    _require_device(a, b, h)
+    lib = _lib.load()
+    n, m = a.shape
+    k = b.shape[1]
+    ok = (a.dtype == b.dtype == h.dtype == torch.float32 and h.shape == b.shape
+          and lib.gnn_gemm_tn_masked_supported(m, k)
+          and all(t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+                  for t in (a, b, h)))
+    if not ok:
+        bm = torch.where(h > 0, b * scale, torch.zeros((), dtype=b.dtype, device=b.device))
+        return gemm_tn(a, bm, bm if want_dsum else None, trans=trans)
+    c = torch.empty((k, m) if trans else (m, k), dtype=torch.float32, device=a.device)
+    dsum = torch.empty(k, dtype=torch.float32, device=a.device) if want_dsum else None
+    ws = torch.empty(int(lib.gnn_gemm_tn_workspace_bytes(n, m, k)), dtype=torch.uint8,
+                     device=a.device)
+    _lib.check(lib.gnn_gemm_tn_masked_f32(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                                          h.data_ptr(), h.stride(0), float(scale), n, m, k,
+                                          c.data_ptr(), c.stride(0), 1 if trans else 0,
+                                          _lib.ptr(dsum), ws.data_ptr(), ws.numel(),
+                                          _lib.stream_handle(a.device)), "gnn_gemm_tn_masked_f32")
+    return c, dsum
+
+
+def linear_small(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor | None:
+    """x @ w^T with one narrow side (gnn_linear_small_f32: fout <= 16 on fp32 MFMA rows, or
+    k <= 16 on a broadcast kernel) -- the classifier layer's support and its dX; None when the
+    shape is not covered."""
+    _require_device(x, w)
+    if (x.dtype != torch.float32 or w.dtype != torch.float32 or x.dim() != 2 or w.dim() != 2
+            or x.shape[1] != w.shape[1]):
+        return None
+    lib = _lib.load()
+    fout, k = w.shape
+    if not lib.gnn_linear_small_supported(k, fout):
+        return None
+    if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
+        x = x.clone(memory_format=torch.contiguous_format)
+    w = w.contiguous()
+    y = torch.empty((x.shape[0], fout + (-fout) % 4), dtype=torch.float32, device=x.device)
+    _lib.check(lib.gnn_linear_small_f32(x.data_ptr(), x.stride(0), x.shape[0], k, w.data_ptr(),
+                                        fout, y.data_ptr(), y.stride(0),
+                                        _lib.stream_handle(x.device)), "gnn_linear_small_f32")
+    return y[:, :fout] if y.shape[1] != fout else y
+
+
 def _transform_or_mm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """x @ w^T: the MFMA transform where it covers the shape, else torch.mm (hipBLASLt)."""
+    """x @ w^T: the MFMA transform where it covers the shape, the narrow kernels where one side
+    is narrow (linear_small), else torch.mm (hipBLASLt)."""
     y = gcn_transform(x, w)
+    if y is None:
+        y = linear_small(x, w)
     return y if y is not None else torch.mm(x, w.t())
 
 
@@ -489,11 +555,34 @@ def _transform_or_mm(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 # X), and where X needs no gradient -- a first layer over the input features -- the backward
 # runs no SpMM at all (the A (X W^T) form needs dS = A^T dY for dW regardless).
 GCN_REASSOC = True
+# the A (X W^T) form zero-pads an output width below 64 to a multiple of 4 (see _GcnLayerFn)
+GCN_PAD_NARROW = True
 
 
 def _reassociate(x, weight, g) -> bool:
     fout, fin = weight.shape
     return GCN_REASSOC and fin <= fout and x.shape[0] == g.n_cols
+
+
+# GCN_Model's Graph_conv_layer -> ReLU -> Dropout run in training as ONE op when the layer takes
+# the (A X) W^T + b form: ReLU and dropout in the transform's store epilogue, their backward
+# folded into the weight-gradient pass (gemm_tn_masked) -- two elementwise passes forward and
+# two backward fewer over the [n, hidden] activations
+GCN_FUSE_RELU_DROPOUT = True
+
+
+def fuses_relu_dropout(x, weight, g) -> bool:
+    """Whether ``gcn_layer(..., relu_dropout=...)`` applies to this layer: the reassociated form
+    (``_reassociate``) on a shape the MFMA transform takes."""
+    fout, fin = weight.shape
+    return (GCN_FUSE_RELU_DROPOUT and _reassociate(x, weight, g)
+            and bool(_lib.load().gnn_gcn_transform_supported(fin, fout)))
+
+
+def dropout_seed() -> int:
+    """A 62-bit seed for the HIP kernels' hashed dropout, drawn from torch's CPU generator (so
+    torch.manual_seed fixes it)."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
 class _GcnLayerFn(torch.autograd.Function):
@@ -510,17 +599,33 @@ class _GcnLayerFn(torch.autograd.Function):
                 K = n_rows reduction: 1.81 ms on hipBLASLt at cfg2). S is not kept.
     (A X) W^T + b (in_features <= out_features, ``GCN_REASSOC``)
       forward   Z = A X (the SpMM over X), Y = Z W^T + b (the transform, bias in its store
-                epilogue: gnn_gcn_transform_bias_f32); Z is kept for backward;
+                epilogue: gnn_gcn_transform_epi_f32); Z is kept for backward;
       backward  dW = dY^T Z and db = the column sums of dY in one gemm_tn pass that reads dY
                 once (d = b), and only when X needs a gradient dZ = dY W (transform) and
                 dX = A^T dZ (SpMM).
-    The two forms agree to fp32 rounding (a sum of products regrouped)."""
+    The two forms agree to fp32 rounding (a sum of products regrouped).
+
+    ``relu_dropout`` = (p, seed), reassociated form only (``fuses_relu_dropout``): the output
+    is H = dropout_p(ReLU(Y)) -- GCN_Model's ReLU and Dropout after the layer (GCN/GCN.py:12-14)
+    -- from the transform's epilogue (hashed dropout: element (i, c) kept iff the (seed, i, c)
+    hash clears p); H is kept, and the backward's upstream gradient passes exactly where
+    H > 0, scaled by 1 / (1 - p): folded into the dW / db pass (gemm_tn_masked), formed
+    explicitly only when X needs a gradient."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, g):
+    def forward(ctx, x, weight, bias, g, relu_dropout=None):
         ctx.g = g
         ctx.has_bias = bias is not None
         ctx.reassoc = _reassociate(x, weight, g)
+        ctx.relu_dropout = relu_dropout
+        if relu_dropout is not None:
+            if not fuses_relu_dropout(x, weight, g):
+                raise ValueError("relu_dropout= needs the reassociated form on a transform shape")
+            p, seed = relu_dropout
+            z = spmm_forward(g, x)
+            h = gcn_transform(z, weight, relu=True, bias=bias, dropout_p=p, seed=seed)
+            ctx.save_for_backward(z, weight, h)
+            return h
         if ctx.reassoc:
             z = spmm_forward(g, x)
             y = gcn_transform(z, weight, bias=bias)
@@ -528,6 +633,14 @@ class _GcnLayerFn(torch.autograd.Function):
                 y = torch.mm(z, weight.t()) if bias is None else torch.addmm(bias, z, weight.t())
             ctx.save_for_backward(z, weight)
             return y
+        # an output width that is not a multiple of 4 (a classifier layer: 7 classes) is
+        # zero-padded to one: the SpMMs then gather 16-B pieces of the support / dY rows instead
+        # of scalars (7 -> 8 at cfg2: 0.30 -> 0.15 ms per SpMM pass)
+        fout = weight.shape[0]
+        ctx.pad = (-fout) % 4 if GCN_PAD_NARROW and fout < 64 else 0
+        if ctx.pad:
+            weight = torch.nn.functional.pad(weight, (0, 0, 0, ctx.pad))
+            bias = torch.nn.functional.pad(bias, (0, ctx.pad)) if bias is not None else None
         order = column_order(g, weight.shape[0]) if x.shape[0] == g.n_cols else None
         s = None
         if order is not None:
@@ -537,14 +650,33 @@ class _GcnLayerFn(torch.autograd.Function):
         else:
             y = spmm_forward(g, _transform_or_mm(x, weight), bias)
         ctx.save_for_backward(x, weight)
-        return y
+        return y[:, :fout] if ctx.pad else y
 
     @staticmethod
     def backward(ctx, gy):
-        x, weight = ctx.saved_tensors  # Z = A X in the reassociated form
         gy = gy.contiguous()
         gx = gw = gb = None
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.relu_dropout is not None:
+            z, weight, h = ctx.saved_tensors
+            scale = 1.0 / (1.0 - ctx.relu_dropout[0])
+            if ctx.needs_input_grad[1]:
+                r = gemm_tn_masked(z, gy, h, scale, want_b, trans=True)
+                if r is not None:
+                    gw, gb = r
+            dy = None
+            if (ctx.needs_input_grad[1] and gw is None) or (want_b and gb is None) \
+                    or ctx.needs_input_grad[0]:
+                dy = torch.where(h > 0, gy * scale, torch.zeros((), dtype=gy.dtype,
+                                                                device=gy.device))
+            if ctx.needs_input_grad[1] and gw is None:
+                gw = torch.mm(dy.t(), z)
+            if want_b and gb is None:
+                gb = dy.sum(0)
+            if ctx.needs_input_grad[0]:
+                gx = spmm_forward(ctx.g.transpose(), _transform_or_mm(dy, weight.t().contiguous()))
+            return gx, gw, gb, None, None
+        x, weight = ctx.saved_tensors  # Z = A X in the reassociated form
         if ctx.reassoc:
             if ctx.needs_input_grad[1]:
                 # dW = dY^T Z as (Z^T dY)^T; db = the column sums of dY from the same loads
@@ -557,7 +689,9 @@ class _GcnLayerFn(torch.autograd.Function):
                 gb = gy.sum(0)
             if ctx.needs_input_grad[0]:
                 gx = spmm_forward(ctx.g.transpose(), _transform_or_mm(gy, weight.t().contiguous()))
-            return gx, gw, gb, None
+            return gx, gw, gb, None, None
+        if ctx.pad:
+            gy = torch.nn.functional.pad(gy, (0, ctx.pad))
         ds = spmm_forward(ctx.g.transpose(), gy)
         if ctx.needs_input_grad[0]:
             gx = _transform_or_mm(ds, weight.t().contiguous())
@@ -570,19 +704,25 @@ class _GcnLayerFn(torch.autograd.Function):
                 gw = torch.mm(ds.t(), x)
         if want_b and gb is None:
             gb = gy.sum(0)
-        return gx, gw, gb, None
+        if ctx.pad:
+            fout = weight.shape[0] - ctx.pad
+            gw = gw[:fout] if gw is not None else None
+            gb = gb[:fout] if gb is not None else None
+        return gx, gw, gb, None, None
 
 
 def gcn_layer(g: CsrGraph, x: torch.Tensor, weight: torch.Tensor,
-              bias: torch.Tensor | None = None) -> torch.Tensor:
-    """A_hat (x W^T) + b, differentiable w.r.t. x, W and b (``_GcnLayerFn``)."""
+              bias: torch.Tensor | None = None, relu_dropout=None) -> torch.Tensor:
+    """A_hat (x W^T) + b, differentiable w.r.t. x, W and b (``_GcnLayerFn``); with
+    ``relu_dropout`` = (p, seed): dropout_p(ReLU(A_hat x W^T + b)) as one op (see
+    _GcnLayerFn; requires ``fuses_relu_dropout``)."""
     _require_device(g.rowptr, x, weight, bias)
     if x.dtype != torch.float32 or weight.dtype != torch.float32:
         raise TypeError("gcn_layer runs in float32")
     if x.dim() != 2 or weight.dim() != 2 or x.shape[1] != weight.shape[1] \
             or x.shape[0] != g.n_cols:
         raise ValueError("x must be [n_cols, F_in] and weight [F_out, F_in]")
-    return _GcnLayerFn.apply(x, weight, bias, g)
+    return _GcnLayerFn.apply(x, weight, bias, g, relu_dropout)
 
 
 # ---------------------------------------------------------------------- GAT
@@ -693,7 +833,8 @@ def set_transform_precision(mode: str) -> str:
 def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
                   out: torch.Tensor | None = None, out_rows: torch.Tensor | None = None,
                   check_rows: bool = True, live: torch.Tensor | None = None,
-                  bias: torch.Tensor | None = None) -> torch.Tensor | None:
+                  bias: torch.Tensor | None = None, dropout_p: float = 0.0,
+                  seed: int = 0) -> torch.Tensor | None:
     """support = x @ weight^T on fp32 MFMA (gnn_gcn_transform_f32), the dense half of
     Graph_conv_layer.forward (GCN/GCN.py:42); ``relu=True``: max(x @ weight^T, 0)
     (gnn_linear_relu_f32, the SageLayer at GraphSAGE/GraphSAGE.py:18-20). Inference only
@@ -711,8 +852,10 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
     are computed (gnn_linear_relu_live_f32) -- a sampled batch's frontier whose size the host
     never read; the other output rows are left as they were.
 
-    ``bias`` (fp32 [fout], without relu / out_rows / live): x @ weight^T + bias, the add in
-    the store epilogue (gnn_gcn_transform_bias_f32)."""
+    ``bias`` (fp32 [fout]) and ``dropout_p`` / ``seed`` (without out_rows / live):
+    dropout(act(x @ weight^T + bias)) in the store epilogue (gnn_gcn_transform_epi_f32; act =
+    ReLU if ``relu``; element (i, c) kept iff the (seed, i, c) hash clears p, kept values scaled
+    by 1 / (1 - p))."""
     _require_device(x, weight)
     if (x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 2
             or weight.dim() != 2 or x.shape[1] != weight.shape[1]):
@@ -725,10 +868,13 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
         return None
     if out_rows is not None and relu:
         raise ValueError("out_rows= is supported without the ReLU epilogue only")
+    epi = bias is not None or dropout_p > 0
+    if epi and (out_rows is not None or live is not None):
+        raise ValueError("bias= / dropout_p= are supported without out_rows / live only")
+    if not 0.0 <= dropout_p < 1.0:
+        raise ValueError("dropout_p must be in [0, 1)")
     if bias is not None:
         _require_device(bias)
-        if relu or out_rows is not None or live is not None:
-            raise ValueError("bias= is supported without relu / out_rows / live only")
         if bias.dtype != torch.float32 or bias.numel() != fout:
             raise ValueError("bias must be float32 [fout]")
         bias = bias.contiguous()
@@ -771,11 +917,11 @@ def gcn_transform(x: torch.Tensor, weight: torch.Tensor, relu: bool = False,
             out.data_ptr(), out.stride(0), _lib.stream_handle(x.device)),
             "gnn_linear_relu_live_f32")
         return out
-    if bias is not None:
-        _lib.check(lib.gnn_gcn_transform_bias_f32(
-            x.data_ptr(), x.stride(0), x.shape[0], k, w.data_ptr(), fout, bias.data_ptr(),
-            out.data_ptr(), out.stride(0), _lib.stream_handle(x.device)),
-            "gnn_gcn_transform_bias_f32")
+    if epi:
+        _lib.check(lib.gnn_gcn_transform_epi_f32(
+            x.data_ptr(), x.stride(0), x.shape[0], k, w.data_ptr(), fout, _lib.ptr(bias),
+            1 if relu else 0, float(dropout_p), int(seed) & (2 ** 64 - 1), out.data_ptr(),
+            out.stride(0), _lib.stream_handle(x.device)), "gnn_gcn_transform_epi_f32")
         return out
     fn, name = ((lib.gnn_linear_relu_f32, "gnn_linear_relu_f32") if relu else
                 (lib.gnn_gcn_transform_f32, "gnn_gcn_transform_f32"))

@@ -124,8 +124,9 @@ int gnn_spmm_csr_hub_f32(const int64_t* rowptr, const int32_t* col_hub, const fl
  * task instead of once per row. mid_row lists the other rows of degree <= seg_len (one
  * wavefront each), seg_* / long_* the long rows as in gnn_spmm_csr_f32. xh / ldh: the
  * optional hub table (col < 0 names row -1-col of xh, as gnn_spmm_csr_hub_f32; NULL: none).
- * flags: GNN_EPI_* including GNN_EPI_SKIP_EMPTY. Needs feat % 4 == 0, 32 < feat,
- * 16-B aligned x / xh / y / bias / partial and ldx, ldh, ldy multiples of 4
+ * flags: GNN_EPI_* including GNN_EPI_SKIP_EMPTY. Needs feat % 4 == 0 (a row of feat <= 32
+ * is held by feat / 4 lanes, 64 / (feat / 4) edge slots per wavefront: the narrow classifier
+ * widths), 16-B aligned x / xh / y / bias / partial and ldx, ldh, ldy multiples of 4
  * (else GNN_E_UNSUPPORTED). Each row's sum runs in edge order: deterministic. A task
  * outside the contract (no row, more than 63 rows, rows outside [0, n_rows)) is skipped by
  * the kernel (its rows are left unwritten, nothing is read out of bounds): validate a task
@@ -344,16 +345,20 @@ int gnn_gcn_transform_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k
                           int64_t fout, float* y, int64_t ldy, void* stream);
 
 /*
- * y = x @ w^T + bias (bias [fout] fp32, 16-B aligned; the add in the store epilogue): the
- * dense half of a Graph_conv_layer trained as (A X) W^T + b -- the same layer as
- * GCN/GCN.py:42-45's A (X W^T) + b, reassociated where in_features <= out_features so that
- * the backward's dW = dY^T (A X) and db = sum dY read dY once (graphneuralnetwork_amd/ops.py
- * _GcnLayerFn). Shapes, alignment, arithmetic and return codes as gnn_gcn_transform_f32;
- * GNN_E_ARG for a null bias with n_rows > 0, GNN_E_ALIGN for a misaligned one.
+ * y = dropout(act(x @ w^T + bias)): the dense half of a Graph_conv_layer trained as
+ * (A X) W^T + b -- the same layer as GCN/GCN.py:42-45's A (X W^T) + b, reassociated where
+ * in_features <= out_features (graphneuralnetwork_amd/ops.py _GcnLayerFn) -- with the ReLU
+ * and Dropout that follow it in GCN_Model (GCN/GCN.py:12-14) in the store epilogue. bias: fp32
+ * [fout], 16-B aligned (GNN_E_ALIGN), or NULL; act = ReLU when relu != 0; dropout: element
+ * (i, c) is kept iff (h >> 8) / 2^24 >= drop_p for h = the 32-bit hash of (drop_seed, i, c)
+ * (oracle/spmm_oracle.c oracle_hash3 restates it), kept values scaled by 1 / (1 - drop_p)
+ * (inverted dropout, as F.dropout); drop_p in [0, 1) (GNN_E_ARG), 0 = no dropout. Shapes,
+ * alignment, arithmetic and return codes as gnn_gcn_transform_f32.
  */
-int gnn_gcn_transform_bias_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
-                               const float* w, int64_t fout, const float* bias, float* y,
-                               int64_t ldy, void* stream);
+int gnn_gcn_transform_epi_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k,
+                              const float* w, int64_t fout, const float* bias, int32_t relu,
+                              float drop_p, uint64_t drop_seed, float* y, int64_t ldy,
+                              void* stream);
 
 /*
  * The same product with the output rows scattered: y[y_row[i], :fout] = x[i, :k] @ w^T for
@@ -541,6 +546,19 @@ int gnn_gat_csr_tasks_f32(const int64_t* rowptr, const int32_t* col, int64_t n_r
                           int64_t ldwh, const float* erh, int64_t ldeh);
 
 /*
+ * y[n, fout] = x[n, k] w^T (w [fout, k], nn.Linear's layout), fp32, with one side narrow: the
+ * classifier layer of GCN_Model in training (GCN/GCN.py:16-17, 42: support = H W^T with 7
+ * classes padded to 8, and its backward dH = dS W), where a library GEMM spends 1.6x the HBM
+ * time. gnn_linear_small_supported(k, fout): 1 = fout <= 16 and k in {16, 32, 64, 128, 256}
+ * (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation); 2 = k <= 16 and fout in
+ * {64, 128, 256} (fp32 FMAs in k order); 0 = not covered (GNN_E_UNSUPPORTED). x, y 16-B
+ * aligned, ldx and ldy multiples of 4 (GNN_E_ALIGN).
+ */
+int gnn_linear_small_supported(int64_t k, int64_t fout);
+int gnn_linear_small_f32(const float* x, int64_t ldx, int64_t n_rows, int64_t k, const float* w,
+                         int64_t fout, float* y, int64_t ldy, void* stream);
+
+/*
  * Weight gradients of the training step (GCN/train_eval.py:43-48 through GCN/GCN.py:42,
  * GAT/train_eval.py:75-76 through GAT/models/layers.py:23): C = A^T B summed over the n rows
  * (A [n, m], B [n, k], row strides lda / ldb), written as C [m, k] (trans_c = 0, row stride
@@ -561,6 +579,23 @@ int gnn_gemm_tn_f32(const float* a, int64_t lda, const float* b, int64_t ldb, in
                     int64_t m, int64_t k, float* c, int64_t ldc, int32_t trans_c, const float* d,
                     int64_t ldd, float* dsum, void* workspace, int64_t workspace_bytes,
                     void* stream);
+
+/*
+ * The same reduction over B' = B . [H > 0] * scale (elementwise; H [n, k], row stride ldh,
+ * 16-B aligned): C = A^T B' (or its transpose) and, when dsum != NULL, dsum = the column sums
+ * of B'. The weight and bias gradients of a Graph_conv_layer whose ReLU and Dropout
+ * (GCN/GCN.py:12-14) ran in its transform's epilogue (gnn_gcn_transform_epi_f32) with output
+ * H: the upstream gradient B passes exactly where H > 0, scaled by 1 / (1 - p) -- no separate
+ * ReLU / dropout backward pass. gnn_gemm_tn_masked_supported(m, k): 1 for (m, k) in {(128,128),
+ * (64,64), (128,64), (64,128)} in the split-bf16 arithmetic (gnn_transform_set_precision 1),
+ * else 0 (GNN_E_UNSUPPORTED: the caller masks B itself and calls gnn_gemm_tn_f32). Workspace,
+ * alignment and determinism as gnn_gemm_tn_f32.
+ */
+int gnn_gemm_tn_masked_supported(int64_t m, int64_t k);
+int gnn_gemm_tn_masked_f32(const float* a, int64_t lda, const float* b, int64_t ldb,
+                           const float* h, int64_t ldh, float scale, int64_t n, int64_t m,
+                           int64_t k, float* c, int64_t ldc, int32_t trans_c, float* dsum,
+                           void* workspace, int64_t workspace_bytes, void* stream);
 
 /*
  * Column mean of x[n_rows, feat] (double accumulation, deterministic): the dense

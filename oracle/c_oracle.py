@@ -46,6 +46,8 @@ def load():
                                               ctypes.c_double, ctypes.c_uint64, vp, vp, vp, vp,
                                               vp, vp]
         lib.oracle_gat_block_grad.restype = ctypes.c_int
+        lib.oracle_dropout_keep.argtypes = [ctypes.c_uint64, vp, vp, i64, ctypes.c_float, vp]
+        lib.oracle_dropout_keep.restype = None
         _lib = lib
     return _lib
 
@@ -180,3 +182,18 @@ def gat_block_grad(rowptr, col, x, W, a_src, a_dst, gy, heads: int, fh: int, slo
              slack_da_src=np.einsum("nh,nhf->hf", kdl, awh).reshape(-1),
              slack_da_dst=np.einsum("nh,nhf->hf", kdr, awh).reshape(-1))
     return r
+
+
+def dropout_keep(seed: int, rows, cols, p: float):
+    """bool keep mask of the hashed element dropout (oracle_dropout_keep: csrc/common.hpp
+    dropout_hash) for broadcastable int64 row / column ids -- GCN_Model's Dropout (GCN/GCN.py:14)
+    as the fused training layer draws it."""
+    lib = load()
+    r, c = np.broadcast_arrays(np.asarray(rows, np.int64), np.asarray(cols, np.int64))
+    r = np.ascontiguousarray(r)
+    c = np.ascontiguousarray(c)
+    out = np.empty(r.shape, np.uint8)
+    lib.oracle_dropout_keep(int(seed) & (2 ** 64 - 1), r.ctypes.data, c.ctypes.data, r.size,
+                            float(p), out.ctypes.data)
+    return out.astype(bool)
+

@@ -187,6 +187,17 @@ static uint32_t oracle_hash3(uint64_t seed, int64_t edge, int64_t head) {
   return h;
 }
 
+/* The same hash over (seed, a[i], b[i]) for i < n: the element dropout of a GCN layer trained
+ * with its ReLU and Dropout (GCN/GCN.py:12-14) in the transform epilogue (csrc/common.hpp
+ * dropout_hash over (row, column)); keep[i] = 1 iff (h >> 8) / 2^24 >= p. */
+void oracle_dropout_keep(uint64_t seed, const int64_t* a, const int64_t* b, int64_t n, float p,
+                         uint8_t* keep) {
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t h = oracle_hash3(seed, a[i], b[i]);
+        keep[i] = (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
+    }
+}
+
 /*
  * Forward + backward of the H-head attention block of GATBase (GAT/models/GAT.py:16, each head
  * GAT/models/layers.py:22-37 dense or :94-131 sparse, concat=True: ELU applied) in float64,

@@ -583,8 +583,10 @@ def test_packed_tasks_check(dev):
 
 
 def test_packed_tasks_c_abi_contract(dev):
-    """gnn_spmm_csr_tasks_f32 rejects what it does not cover (feat <= 32, misaligned
-    vectors) with GNN_E_UNSUPPORTED and unknown flags with GNN_E_ARG."""
+    """gnn_spmm_csr_tasks_f32 rejects what it does not cover (feat not a multiple of 4,
+    misaligned vectors) with GNN_E_UNSUPPORTED and unknown flags with GNN_E_ARG; narrow rows
+    (feat 4 / 8 / 32: 1 / 2 / 8 lanes per row, 64 / 32 / 8 edge slots per wave) are
+    covered."""
     from graphneuralnetwork_amd import _lib
     from graphneuralnetwork_amd.graph import CsrGraph
     lib = _lib.load()
@@ -595,8 +597,9 @@ def test_packed_tasks_c_abi_contract(dev):
     g = CsrGraph(rowptr, col, val, n, n)
     tp = g.task_plan(256, 64, 128)
     s = torch.cuda.current_stream().cuda_stream
-    for F, off, flags, want in ((32, 0, 0, _lib.E_UNSUPPORTED), (64, 1, 0, _lib.E_UNSUPPORTED),
-                                (64, 0, 64, _lib.E_ARG), (64, 0, 0, 0)):
+    for F, off, flags, want in ((6, 0, 0, _lib.E_UNSUPPORTED), (64, 1, 0, _lib.E_UNSUPPORTED),
+                                (64, 0, 64, _lib.E_ARG), (64, 0, 0, 0), (32, 0, 0, 0),
+                                (8, 0, 0, 0), (4, 0, 0, 0)):
         X = torch.randn(n, F + 4, device=dev)[:, off:off + F]
         y = torch.empty(n, F, device=dev)
         rc = lib.gnn_spmm_csr_tasks_f32(rowptr.data_ptr(), col.data_ptr(), val.data_ptr(), n,

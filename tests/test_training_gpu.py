@@ -31,12 +31,13 @@ def _rand_graph(n, m, seed):
     return np.cumsum(rowptr), c.astype(np.int32), rng.standard_normal(m).astype(np.float32)
 
 
-@pytest.mark.parametrize("fout", [64, 128])
+@pytest.mark.parametrize("fout", [7, 64, 128])
 @pytest.mark.parametrize("bias", [True, False])
 def test_gcn_layer_grads_vs_float64(dev, bias, fout):
     """A non-symmetric graph (transposed CSR built for dX): Y, dX, dW, db against float64
     dense autograd of A (X W^T) + b, in both of _GcnLayerFn's forms (128 -> 64: A (X W^T);
-    128 -> 128: (A X) W^T, ops.GCN_REASSOC)."""
+    128 -> 128: (A X) W^T, ops.GCN_REASSOC; 128 -> 7: A (X W^T) zero-padded to 8 columns,
+    ops.GCN_PAD_NARROW)."""
     from graphneuralnetwork_amd.gcn import Graph_conv_layer
     from graphneuralnetwork_amd.graph import CsrGraph
     n = 400
@@ -125,7 +126,9 @@ def test_transform_bias_and_tn_dsum_of_b(dev):
         y1 = gcn_transform(x, w, bias=b)
         assert torch.equal(y1, y0 + b)
     with pytest.raises(ValueError):
-        gcn_transform(x, w, bias=b, relu=True)
+        gcn_transform(x, w, bias=b, dropout_p=1.0)
+    with pytest.raises(ValueError):
+        gcn_transform(x, w, bias=b, out_rows=torch.arange(x.shape[0], device=dev))
     for n in (1, 37, 20000, 300001):
         a = torch.randn(n, 128, device=dev, generator=gen)
         bb = torch.randn(n, 128, device=dev, generator=gen)
@@ -133,6 +136,145 @@ def test_transform_bias_and_tn_dsum_of_b(dev):
         c2, s2 = gemm_tn(a, bb, bb.clone(), trans=True)
         assert torch.equal(c1, c2) and torch.equal(s1, s2)
         close(s1.cpu().numpy(), bb.double().sum(0).cpu().numpy(), rtol=1e-5)
+
+
+@pytest.mark.parametrize("k,fo", [(128, 128), (64, 128), (256, 256)])
+def test_transform_relu_dropout_epilogue(dev, k, fo):
+    """gnn_gcn_transform_epi_f32: dropout_p(ReLU(x W^T + b)) equals the plain transform + b,
+    ReLU and the oracle's hashed keep mask (oracle_dropout_keep over (row, column)) times
+    1 / (1 - p), bit for bit at p = 0.5 (a power-of-two scale), to one rounding at p = 0.3;
+    about 1 - p of the positive entries survive."""
+    from graphneuralnetwork_amd.ops import gcn_transform
+    gen = torch.Generator(device=dev).manual_seed(k + fo)
+    n = 20011
+    x = torch.randn(n, k, device=dev, generator=gen)
+    w = torch.randn(fo, k, device=dev, generator=gen)
+    b = torch.randn(fo, device=dev, generator=gen)
+    base = torch.relu(gcn_transform(x, w) + b)
+    for p, seed in ((0.5, 77), (0.3, 2 ** 61 + 5), (0.0, 0)):
+        y = gcn_transform(x, w, relu=True, bias=b, dropout_p=p, seed=seed)
+        keep = torch.from_numpy(c_oracle.dropout_keep(seed, np.arange(n)[:, None],
+                                                      np.arange(fo)[None, :], p)).to(dev)
+        ref = torch.where(keep, base * (1.0 / (1.0 - p)), torch.zeros((), device=dev))
+        if p in (0.5, 0.0):
+            assert torch.equal(y, ref)
+        else:
+            close(y.cpu().numpy(), ref.cpu().numpy(), rtol=1e-6)
+        pos = base > 0
+        frac = float((y[pos] > 0).float().mean())
+        assert abs(frac - (1 - p)) < 0.01, frac
+    y = gcn_transform(x, w, bias=b)  # bias only, no ReLU
+    assert torch.equal(y, gcn_transform(x, w) + b)
+
+
+@pytest.mark.parametrize("m,k", [(128, 128), (64, 128), (128, 64), (64, 64)])
+@pytest.mark.parametrize("n", [1, 37, 20000, 300001])
+def test_gemm_tn_masked(dev, m, k, n):
+    """gnn_gemm_tn_masked_f32 (B' = B . [H > 0] * scale): equals gemm_tn over a B' formed in
+    torch (with its column sums) bit for bit, and float64."""
+    from graphneuralnetwork_amd.ops import gemm_tn, gemm_tn_masked
+    gen = torch.Generator(device=dev).manual_seed(m + k + n)
+    a = torch.randn(n, m, device=dev, generator=gen)
+    b = torch.randn(n, k, device=dev, generator=gen)
+    h = torch.relu(torch.randn(n, k, device=dev, generator=gen))
+    bm = torch.where(h > 0, b * 2.0, torch.zeros((), device=dev))
+    c, ds = gemm_tn_masked(a, b, h, 2.0, True, trans=True)
+    c0, ds0 = gemm_tn(a, bm, bm, trans=True)
+    assert torch.equal(c, c0) and torch.equal(ds, ds0)
+    close(c.cpu().numpy(), (bm.double().t() @ a.double()).cpu().numpy(), rtol=1e-5)
+    c1, none = gemm_tn_masked(a, b, h, 2.0, False)
+    assert none is None and torch.equal(c1, c0.t())
+
+
+@pytest.mark.parametrize("p", [0.0, 0.5])
+@pytest.mark.parametrize("x_grad", [True, False])
+def test_gcn_relu_dropout_fused_layer(dev, p, x_grad, monkeypatch):
+    """Graph_conv_layer -> ReLU -> Dropout as one training op (ops.gcn_layer relu_dropout=):
+    output and gradients (dW, db, and dX when X needs it) against the unfused layer followed by
+    ReLU and the oracle's hashed keep mask times 1 / (1 - p) under torch autograd."""
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.gcn import Graph_conv_layer
+    from graphneuralnetwork_amd.graph import CsrGraph
+    rp, col, val = _rand_graph(3000, 30000, 6)
+    g = CsrGraph(torch.from_numpy(rp).to(dev), torch.from_numpy(col).to(dev),
+                 torch.from_numpy(val).to(dev), 3000, 3000)
+    torch.manual_seed(1)
+    layer = Graph_conv_layer(128, 128).to(dev)
+    with torch.no_grad():
+        layer.bias.normal_()
+    X = torch.randn(3000, 128, device=dev)
+    gy = torch.randn(3000, 128, device=dev)
+    seed = 4242
+    assert ops.fuses_relu_dropout(X, layer.dense.weight, g)
+    xx = X.clone().requires_grad_(x_grad)
+    h = ops.gcn_layer(g, xx, layer.dense.weight, layer.bias, relu_dropout=(p, seed))
+    h.backward(gy)
+    got = [h.detach(), layer.dense.weight.grad.clone(), layer.bias.grad.clone()] + (
+        [xx.grad] if x_grad else [])
+    layer.zero_grad(set_to_none=True)
+    keep = torch.from_numpy(c_oracle.dropout_keep(seed, np.arange(3000)[:, None],
+                                                  np.arange(128)[None, :], p)).to(dev)
+    xr = X.clone().requires_grad_(x_grad)
+    y = ops.gcn_layer(g, xr, layer.dense.weight, layer.bias)
+    hr = torch.where(keep, torch.relu(y) * (1.0 / (1.0 - p)), torch.zeros((), device=dev))
+    hr.backward(gy)
+    ref = [hr.detach(), layer.dense.weight.grad, layer.bias.grad] + ([xr.grad] if x_grad else [])
+    assert torch.equal(got[0], ref[0])
+    for a, b in zip(got[1:], ref[1:]):
+        close(a.cpu().numpy(), b.cpu().numpy())
+
+
+def test_gcn_model_fused_training_equals_unfused(dev, monkeypatch):
+    """GCN_Model(128, 128, 6, 3, 0).train(): the Graph_conv_layer -> ReLU -> Dropout triples run
+    fused (gcn._fuse_train) and unfused (ops.GCN_FUSE_RELU_DROPOUT off) give the same logits and
+    gradients to fp32 rounding; a forward hook on a ReLU turns the fusion off for its triple."""
+    from graphneuralnetwork_amd import gcn as gcn_mod
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.gcn import GCN_Model
+    from graphneuralnetwork_amd.graph import CsrGraph
+    rp, col, val = _rand_graph(5000, 60000, 8)
+    g = CsrGraph(torch.from_numpy(rp).to(dev), torch.from_numpy(col).to(dev),
+                 torch.from_numpy(val).to(dev), 5000, 5000)
+    torch.manual_seed(3)
+    model = GCN_Model(128, 128, 6, 3, 0.0).to(dev).train()
+    X = torch.randn(5000, 128, device=dev)
+    lab = torch.randint(0, 6, (5000,), device=dev)
+    spans = []
+    real = gcn_mod._fuse_train
+    monkeypatch.setattr(gcn_mod, "_fuse_train", lambda *a: spans.append(real(*a)) or spans[-1])
+    res = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(ops, "GCN_FUSE_RELU_DROPOUT", fuse)
+        spans.clear()
+        model.zero_grad(set_to_none=True)
+        y = model(X, g)
+        torch.nn.functional.cross_entropy(y, lab).backward()
+        assert spans == ([3, 3, 0] if fuse else [0, 0, 0])
+        res[fuse] = [y.detach()] + [p.grad.clone() for p in model.parameters()]
+    for a, b in zip(res[True], res[False]):
+        close(a.cpu().numpy(), b.cpu().numpy())
+    monkeypatch.setattr(ops, "GCN_FUSE_RELU_DROPOUT", True)
+    hk = model.gcn_blocks.relu0.register_forward_hook(lambda *a: None)
+    spans.clear()
+    model(X, g)
+    hk.remove()
+    assert spans[0] == 0 and spans[1] == 3
+
+
+@pytest.mark.parametrize("k,fo", [(128, 8), (64, 7), (256, 16), (16, 1), (8, 128), (7, 64),
+                                  (16, 256), (1, 128)])
+@pytest.mark.parametrize("n", [1, 37, 20000, 300001])
+def test_linear_small_vs_float64(dev, k, fo, n):
+    """gnn_linear_small_f32 (ops.linear_small, the classifier layer's support H W^T and its
+    dX = dS W): x W^T against float64 with strided rows of x; uncovered shapes return None."""
+    from graphneuralnetwork_amd.ops import linear_small
+    gen = torch.Generator(device=dev).manual_seed(k * 7 + fo + n)
+    x = torch.randn(n, k + 4 + (-k) % 4, device=dev, generator=gen)[:, :k]
+    w = torch.randn(fo, k, device=dev, generator=gen)
+    y = linear_small(x, w)
+    assert y is not None and y.shape == (n, fo)
+    close(y.cpu().numpy(), (x.double() @ w.double().t()).cpu().numpy(), rtol=1e-5)
+    assert linear_small(x, torch.randn(24, k, device=dev)) is None
 
 
 def test_symmetric_graph_is_its_own_transpose(dev):
@@ -201,28 +343,36 @@ def test_gcn_layer_training_cfg2_full_size(dev, order):
     close(X.grad.cpu().numpy(), dS @ W)
 
 
-def test_gcn_model_training_cfg2_full_size(dev):
-    """The whole benchmarked model's training step at cfg2 size: GCN_Model(128, 128, 7, 2, 0)
+def test_gcn_model_training_cfg2_full_size(dev, monkeypatch):
+    """The whole benchmarked model's training step at cfg2 size: GCN_Model(128, 128, 7, 2, 0.5)
     (GCN/GCN.py:5-27, GCN/train_eval.py:43-48) as its forward runs it -- rows permuted onto
-    P A P^T (PermuteRows), layer 1 128 -> 128 + ReLU, layer 2 128 -> 7 (its weight gradient on
-    the narrow gemm_tn kernel), logits permuted back. Each layer against float64 references
-    (the C oracle's SpMM, numpy products) given the tensors the model handed it, captured in
-    the permuted frame by module hooks: the ReLU mask is the model's own, so no element near
-    the kink can flip between fp32 and float64. Dropout 0 (nn.Dropout's torch RNG)."""
+    P A P^T (PermuteRows); layer 1 128 -> 128 as (A X) W^T + b with ReLU and Dropout(0.5) in the
+    transform's epilogue (one op: gcn._fuse_train), its dW / db on the masked gemm_tn; layer 2
+    128 -> 7 (its weight gradient on the narrow gemm_tn kernel); logits permuted back. Each
+    layer against float64 references (the C oracle's SpMM, numpy products, the oracle's hashed
+    keep mask for the dropout seed the model drew) given the tensors the model handed it,
+    captured in the permuted frame: layer 2's input and output by hooks on that layer, X's
+    rows through the order's permutation. The ReLU mask is the model's own (H > 0), so no
+    element near the kink can flip between fp32 and float64."""
+    from graphneuralnetwork_amd import gcn as gcn_mod
     from graphneuralnetwork_amd.gcn import GCN_Model
     from graphneuralnetwork_amd.ops import gcn_train_order
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     from graphneuralnetwork_amd.rmat import rmat_edges
-    n, C = 1_000_000, 7
+    n, C, seed = 1_000_000, 7, 987654321
     s, d = rmat_edges(n, 10_000_000, 0)
     g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
     del s, d
     torch.manual_seed(3)
-    net = GCN_Model(128, 128, C, 2, 0.0).to(dev).train()
+    net = GCN_Model(128, 128, C, 2, 0.5).to(dev).train()
     gen = torch.Generator(device=dev).manual_seed(7)
     with torch.no_grad():
         for m in (net.gcn_blocks.gcn0, net.gcn_blocks.gcn1):
             m.bias.normal_(generator=gen)
+    monkeypatch.setattr(gcn_mod, "dropout_seed", lambda: seed)
+    spans = []
+    real = gcn_mod._fuse_train
+    monkeypatch.setattr(gcn_mod, "_fuse_train", lambda *a: spans.append(real(*a)) or spans[-1])
     seen = {}
 
     def keep(name):
@@ -232,20 +382,21 @@ def test_gcn_model_training_cfg2_full_size(dev):
             seen[name] = t
         return hook
 
-    net.gcn_blocks.gcn0.register_forward_pre_hook(keep("x"))
-    net.gcn_blocks.relu0.register_forward_hook(keep("h"))
+    net.gcn_blocks.gcn1.register_forward_pre_hook(keep("h"))
     net.gcn_blocks.gcn1.register_forward_hook(keep("y"))
     X = torch.randn(n, 128, device=dev, generator=gen).requires_grad_(True)
     gy = torch.randn(n, C, device=dev, generator=gen)
     Y = net(X, g)
     Y.backward(gy)
-    gp = gcn_train_order(g, 128).graph
-    assert seen["x"].shape == (n, 128) and seen["y"].shape == (n, C)
+    assert spans == [3, 0]  # layer 1 + ReLU + Dropout fused; layer 2 alone
+    order = gcn_train_order(g, 128)
+    gp = order.graph
+    perm = order.perm
     rp, col, val = (t.cpu().numpy() for t in (gp.rowptr, gp.col, gp.val))
     A = lambda v: c_oracle.spmm_csr(rp, col, val, v.astype(np.float32)).astype(np.float64)
     f64 = lambda t: t.detach().cpu().numpy().astype(np.float64)
-    Xp, H, Hg, Yp, gyp = f64(seen["x"]), f64(seen["h"]), f64(seen["h"].grad), f64(seen["y"]), \
-        f64(seen["y"].grad)
+    Xp, dXp = f64(X[perm]), f64(X.grad[perm])
+    H, Hg, Yp, gyp = f64(seen["h"]), f64(seen["h"].grad), f64(seen["y"]), f64(seen["y"].grad)
     W1, b1 = f64(net.gcn_blocks.gcn0.dense.weight), f64(net.gcn_blocks.gcn0.bias)
     W2, b2 = f64(net.gcn_blocks.gcn1.dense.weight), f64(net.gcn_blocks.gcn1.bias)
     # layer 2 (128 -> 7) given the model's H and the logits' gradient
@@ -254,15 +405,16 @@ def test_gcn_model_training_cfg2_full_size(dev):
     close(f64(net.gcn_blocks.gcn1.dense.weight.grad), dS2.T @ H)
     close(f64(net.gcn_blocks.gcn1.bias.grad), gyp.sum(0))
     close(Hg, dS2 @ W2)
-    # layer 1 (128 -> 128, ReLU) given the model's input rows and the gradient layer 2 handed back
-    close(H, np.maximum(A(Xp @ W1.T) + b1, 0.0))
-    dZ1 = Hg * (H > 0)
+    # layer 1 (128 -> 128, ReLU, Dropout 0.5 on the (seed, row, column) hash of the permuted
+    # frame) given the model's input rows and the gradient layer 2 handed back
+    kp = c_oracle.dropout_keep(seed, np.arange(n)[:, None], np.arange(128)[None, :], 0.5)
+    assert abs(kp.mean() - 0.5) < 1e-3
+    close(H, np.where(kp, np.maximum(A(Xp @ W1.T) + b1, 0.0) * 2.0, 0.0))
+    dZ1 = Hg * (H > 0) * 2.0
     dS1 = A(dZ1)
     close(f64(net.gcn_blocks.gcn0.dense.weight.grad), dS1.T @ Xp)
     close(f64(net.gcn_blocks.gcn0.bias.grad), dZ1.sum(0))
-    close(f64(seen["x"].grad), dS1 @ W1)
-    # the permutation at both ends: the natural-frame gradient is the permuted one moved back
-    assert torch.equal(torch.sort(X.grad.reshape(-1))[0], torch.sort(seen["x"].grad.reshape(-1))[0])
+    close(dXp, dS1 @ W1)
 
 
 @pytest.mark.parametrize("m,k", [(128, 128), (64, 64), (128, 64), (64, 128), (8, 64),
