@@ -293,6 +293,11 @@ __global__ __launch_bounds__(kTnThreads) void gemm_tn_mfma_kernel(
 // (8 rows apart = 32 banks apart) keeps conflict-free for the two lane halves; the strips are
 // split in registers. 6 x 32 cycles per 16 rows x 32 x 32 outputs against 8 x 64 on the f32
 // MFMA: the kernel is left paced by its HBM reads. C/D lane map as the f32 form's.
+#ifndef GNN_TN_X6_2X2
+#define GNN_TN_X6_2X2 1  // 128 x 128 outputs as 2 x 2 blocks of 32 x 32 per wave (0: 1 x 4;
+                         // tools/tn_ab.py, profiles/r06v_tn_ab.log: DB 0.282 vs 0.325 ms,
+                         // masked 0.331 vs 0.352 at 1M rows)
+#endif
 // DB: D is B (dsum = the column sums of B, taken from B's own staged loads: no third read --
 // the bias gradient next to dW = dY^T Z of a layer trained as (A X) W^T + b).
 // MB: D is a mask H and the kernel multiplies B' = B . [H > 0] * mscale (elementwise, at
@@ -309,18 +314,26 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
   constexpr int NB = (kTnRows * B4 + kTnThreads - 1) / kTnThreads;
   constexpr int QA = M / 32, QB = K / 32;
   constexpr int S = 4 / QA;  // k-step streams per tile
+  // the 4 waves' share of the QA x QB output blocks: one A block x all B blocks each, or (T22,
+  // M = K = 128) 2 x 2 blocks each -- every wave then splits 2 + 2 strips per step, not 1 + 4
+  constexpr bool T22 = GNN_TN_X6_2X2 != 0 && QA == 4 && QB == 4;
+  constexpr int WH = T22 ? 2 : 1, WQ = T22 ? 2 : QB;
   __shared__ float4 sa[kTnRows * PA / 4];
   __shared__ float4 sb[kTnRows * PB / 4];
   __shared__ float red[S > 1 ? M * K : 1];
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
-  const int h = w % QA, s = w / QA;
+  const int s = T22 ? 0 : w / QA;
+  const int hb = T22 ? 2 * (w & 1) : w % QA;  // this wave's first A block
+  const int qb = T22 ? 2 * (w >> 1) : 0;      // and first B block
   const int i = lane & 31, kh = lane >> 5;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = min(n, r0 + rows_per_block);
-  f16x acc[QB];
+  f16x acc[WH][WQ];
 #pragma unroll
-  for (int q = 0; q < QB; ++q) acc[q] = f16x(0.f);
+  for (int hi = 0; hi < WH; ++hi)
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) acc[hi][q] = f16x(0.f);
   float4 ds[NB];
 #pragma unroll
   for (int q = 0; q < NB; ++q) ds[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -383,33 +396,39 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
     const int nsteps = static_cast<int>((min(static_cast<int64_t>(kTnRows), r1 - row0) + 15) / 16);
     for (int st = s; st < nsteps; st += S) {  // rows past r1 were staged as zeros
       const int rb = 16 * st + 8 * kh;
-      bf16x8 a0, a1, a2;
+      bf16x8 ap[WH][3];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        __bf16 x0, x1, x2;
-        split3(saf[(rb + j) * PA + 32 * h + i], x0, x1, x2);
-        a0[j] = x0;
-        a1[j] = x1;
-        a2[j] = x2;
-      }
+      for (int hi = 0; hi < WH; ++hi)
 #pragma unroll
-      for (int q = 0; q < QB; ++q) {
+        for (int j = 0; j < 8; ++j) {
+          __bf16 x0, x1, x2;
+          split3(saf[(rb + j) * PA + 32 * (hb + hi) + i], x0, x1, x2);
+          ap[hi][0][j] = x0;
+          ap[hi][1][j] = x1;
+          ap[hi][2][j] = x2;
+        }
+#pragma unroll
+      for (int q = 0; q < WQ; ++q) {
         bf16x8 b0, b1, b2;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           __bf16 y0, y1, y2;
-          split3(sbf[(rb + j) * PB + 32 * q + i], y0, y1, y2);
+          split3(sbf[(rb + j) * PB + 32 * (qb + q) + i], y0, y1, y2);
           b0[j] = y0;
           b1[j] = y1;
           b2[j] = y2;
         }
-        f16x c = acc[q];  // smallest terms first
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
-        acc[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c, 0, 0, 0);
+#pragma unroll
+        for (int hi = 0; hi < WH; ++hi) {
+          const bf16x8 a0 = ap[hi][0], a1 = ap[hi][1], a2 = ap[hi][2];
+          f16x c = acc[hi][q];  // smallest terms first
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
+          acc[hi][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c, 0, 0, 0);
+        }
       }
     }
   }
@@ -417,18 +436,21 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
   for (int tt = S - 1; tt >= 0; --tt) {  // the S streams' partials, summed in s order
     if (s == tt) {
 #pragma unroll
-      for (int q = 0; q < QB; ++q) {
+      for (int hi = 0; hi < WH; ++hi)
 #pragma unroll
-        for (int rg = 0; rg < 16; ++rg) {
-          const int m = 32 * h + (rg & 3) + 8 * (rg >> 2) + 4 * kh, nn = 32 * q + i;
-          float v = acc[q][rg];
-          if (tt < S - 1) v += red[m * K + nn];
-          if (tt > 0)
-            red[m * K + nn] = v;
-          else
-            pc[m * K + nn] = v;
+        for (int q = 0; q < WQ; ++q) {
+#pragma unroll
+          for (int rg = 0; rg < 16; ++rg) {
+            const int m = 32 * (hb + hi) + (rg & 3) + 8 * (rg >> 2) + 4 * kh;
+            const int nn = 32 * (qb + q) + i;
+            float v = acc[hi][q][rg];
+            if (tt < S - 1) v += red[m * K + nn];
+            if (tt > 0)
+              red[m * K + nn] = v;
+            else
+              pc[m * K + nn] = v;
+          }
         }
-      }
     }
     __syncthreads();
   }

@@ -5,6 +5,8 @@ library must be loadable, otherwise a RuntimeError is raised.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 
 from . import _lib
@@ -559,6 +561,21 @@ GCN_REASSOC = True
 GCN_PAD_NARROW = True
 
 
+# The reassociated backward's dW / db pass (gemm_tn over Z and dY) and its dX chain (transform
+# dZ = dY W, then the SpMM A^T dZ) read the same dY and nothing of each other: when X needs a
+# gradient the weight pass runs on a side stream beside the chain (the SpMM is bound by gather
+# latency and leaves the matrix cores and VALUs idle).
+GCN_OVERLAP_DW = True  # tools/train_step_probe.py --set: 2.49-2.53 vs 2.51-2.64 ms at cfg2
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _SIDE_STREAMS.get(dev.index)
+    if s is None:
+        s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
 def _reassociate(x, weight, g) -> bool:
     fout, fin = weight.shape
     return GCN_REASSOC and fin <= fout and x.shape[0] == g.n_cols
@@ -634,8 +651,9 @@ class _GcnLayerFn(torch.autograd.Function):
             ctx.save_for_backward(z, weight)
             return y
         # an output width that is not a multiple of 4 (a classifier layer: 7 classes) is
-        # zero-padded to one: the SpMMs then gather 16-B pieces of the support / dY rows instead
-        # of scalars (7 -> 8 at cfg2: 0.30 -> 0.15 ms per SpMM pass)
+        # zero-padded to one: the SpMMs then gather 16-B pieces of the support / dY rows in
+        # packed row tasks (7 -> 8 at cfg2: 0.30 -> 0.27 ms per SpMM pass), the support and dX
+        # products take the narrow kernels (linear_small)
         fout = weight.shape[0]
         ctx.pad = (-fout) % 4 if GCN_PAD_NARROW and fout < 64 else 0
         if ctx.pad:
@@ -678,17 +696,33 @@ class _GcnLayerFn(torch.autograd.Function):
             return gx, gw, gb, None, None
         x, weight = ctx.saved_tensors  # Z = A X in the reassociated form
         if ctx.reassoc:
+            main = side = None
+            if GCN_OVERLAP_DW and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]:
+                main = torch.cuda.current_stream(gy.device)
+                side = _side_stream(gy.device)
+                side.wait_stream(main)
             if ctx.needs_input_grad[1]:
-                # dW = dY^T Z as (Z^T dY)^T; db = the column sums of dY from the same loads
-                r = gemm_tn(x, gy, gy if want_b else None, trans=True)
-                if r is not None:
-                    gw, gb = r
-                else:
-                    gw = torch.mm(gy.t(), x)
+                with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                    # dW = dY^T Z as (Z^T dY)^T; db = the column sums of dY from the same loads
+                    r = gemm_tn(x, gy, gy if want_b else None, trans=True)
+                    if r is not None:
+                        gw, gb = r
+                    else:
+                        gw = torch.mm(gy.t(), x)
+                    if want_b and gb is None:
+                        gb = gy.sum(0)
+                if side is not None:  # read there: not recycled before the side work is done
+                    x.record_stream(side)
+                    gy.record_stream(side)
             if want_b and gb is None:
                 gb = gy.sum(0)
             if ctx.needs_input_grad[0]:
                 gx = spmm_forward(ctx.g.transpose(), _transform_or_mm(gy, weight.t().contiguous()))
+            if side is not None:
+                main.wait_stream(side)
+                for t in (gw, gb):
+                    if t is not None:
+                        t.record_stream(main)
             return gx, gw, gb, None, None
         if ctx.pad:
             gy = torch.nn.functional.pad(gy, (0, ctx.pad))

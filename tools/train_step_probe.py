@@ -27,7 +27,14 @@ def main():
                     help="GAT: er loaded, not recomputed from the gathered rows")
     ap.add_argument("--natural", action="store_true",
                     help="the natural-order graph (default: P A P^T, as the models train)")
+    ap.add_argument("--set", action="append", default=[],
+                    help="NAME=0|1: an ops switch (e.g. GCN_OVERLAP_DW=0)")
     a = ap.parse_args()
+    for kv in a.set:
+        from graphneuralnetwork_amd import ops
+        k, v = kv.split("=")
+        assert hasattr(ops, k), k
+        setattr(ops, k, bool(int(v)))
     if a.er_gather:
         from graphneuralnetwork_amd import ops
         ops.GAT_ER_RECOMPUTE = False
