@@ -486,6 +486,9 @@ __global__ __launch_bounds__(kTnThreads, 2) void gemm_tn_x6_kernel(
 // operand. The 4 waves of a workgroup are summed in wave order through LDS (deterministic),
 // the workgroup partials by gemm_tn_reduce_kernel.
 constexpr int kNarrowK = 16, kNarrowM = 128;
+#ifndef GNN_TN_NARROW_MFMA
+#define GNN_TN_NARROW_MFMA 1  // A/B: 0 = the FMA row walk for M in {64, 128} too
+#endif
 constexpr int kNarrowRowsInFlight = 16;
 
 template <bool DSUM, int MP>
@@ -573,6 +576,80 @@ __global__ __launch_bounds__(kTnThreads) void gemm_tn_narrow_kernel(
 // M = 2): lane = row, every lane accumulates all M x K products of its rows in registers, the
 // wave's lanes are summed by an xor tree and the 4 waves in order through LDS.
 constexpr int kTinyOut = 32;
+
+// The same narrow partials on the matrix cores for M in {64, 128} with 16-B aligned A rows
+// (GCN_Model's classifier layer: dW = dS^T H, M = 128, K = 8): v_mfma_f32_16x16x4_f32 contracts
+// 4 rows per instruction. Lane (i, q) = (l & 15, l >> 4) loads A[row0 + q][64 h + 4 i .. + 3]
+// (a row's 256 B per 16 lanes) and B[row0 + q][i] (i < K); MFMA (h, c) takes component c of
+// A's float4 h as its A operand, so its output rows are m = 64 h + 4 i' + c. G row groups of 4
+// per wave step are loaded before their MFMAs. fp32 products, fp32 accumulation.
+constexpr int kNarrowGroups = 4;
+template <int M, bool DSUM>
+__global__ __launch_bounds__(kTnThreads) void gemm_tn_narrow_mfma_kernel(
+    const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb,
+    const float* __restrict__ d, int64_t ldd, int64_t n, int64_t rows_per_block, int K,
+    float* __restrict__ part) {
+  constexpr int H = M / 64, G = kNarrowGroups, W = kTnThreads / kWave;
+  using fx4 = __attribute__((ext_vector_type(4))) float;
+  __shared__ float red[W][M * kNarrowK + kNarrowK];
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x >> 6;
+  const int i = lane & 15, q = lane >> 4;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(n, r0 + rows_per_block);
+  fx4 acc[H][4];
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[h][c] = fx4{0.f, 0.f, 0.f, 0.f};
+  float dacc = 0.f;
+  for (int64_t base = r0 + static_cast<int64_t>(w) * (4 * G); base < r1; base += W * 4 * G) {
+    float4 av[G][H];
+    float bv[G];
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi) {
+      const int64_t row = base + 4 * gi + q;
+      const bool ok = row < r1;
+#pragma unroll
+      for (int h = 0; h < H; ++h)
+        av[gi][h] = ok ? *reinterpret_cast<const float4*>(a + row * lda + 64 * h + 4 * i)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      bv[gi] = (ok && i < K) ? b[row * ldb + i] : 0.f;
+      if constexpr (DSUM) dacc += (ok && i < K) ? d[row * ldd + i] : 0.f;
+    }
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi)
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        acc[h][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[gi][h].x, bv[gi], acc[h][0], 0, 0, 0);
+        acc[h][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[gi][h].y, bv[gi], acc[h][1], 0, 0, 0);
+        acc[h][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[gi][h].z, bv[gi], acc[h][2], 0, 0, 0);
+        acc[h][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[gi][h].w, bv[gi], acc[h][3], 0, 0, 0);
+      }
+  }
+  // D of MFMA (h, c): lane (j = l & 15, q) holds rows 4 q + r, i.e. m = 64 h + 4 (4 q + r) + c
+  const int MK = M * K;
+  if (i < K) {
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[w][(64 * h + 4 * (4 * q + r) + c) * K + i] = acc[h][c][r];
+  }
+  if constexpr (DSUM) {  // the 4 row lanes of column i, in lane order
+    dacc += __shfl_xor(dacc, 16, kWave);
+    dacc += __shfl_xor(dacc, 32, kWave);
+    if (q == 0 && i < K) red[w][MK + i] = dacc;
+  }
+  __syncthreads();
+  float* pc = part + static_cast<int64_t>(blockIdx.x) * (MK + (DSUM ? K : 0));
+  for (int e = threadIdx.x; e < MK + (DSUM ? K : 0); e += kTnThreads) {
+    float v = red[0][e];
+#pragma unroll
+    for (int ww = 1; ww < W; ++ww) v += red[ww][e];
+    pc[e] = v;
+  }
+}
 
 template <bool DSUM>
 __global__ __launch_bounds__(kTnThreads) void gemm_tn_tiny_kernel(
@@ -786,6 +863,19 @@ extern "C" int gnn_gemm_tn_f32(const float* a, int64_t lda, const float* b, int6
       else
         hipLaunchKernelGGL((gemm_tn_tiny_kernel<false>), grid, blk, 0, s, a, lda, b, ldb, d, ldd,
                            n, rpb, M, K, part);
+    } else if (GNN_TN_NARROW_MFMA && (m == 64 || m == 128) && aligned_to(a, 16) && lda % 4 == 0) {
+      if (m == 128 && d)
+        hipLaunchKernelGGL((gemm_tn_narrow_mfma_kernel<128, true>), grid, blk, 0, s, a, lda, b,
+                           ldb, d, ldd, n, rpb, K, part);
+      else if (m == 128)
+        hipLaunchKernelGGL((gemm_tn_narrow_mfma_kernel<128, false>), grid, blk, 0, s, a, lda, b,
+                           ldb, d, ldd, n, rpb, K, part);
+      else if (d)
+        hipLaunchKernelGGL((gemm_tn_narrow_mfma_kernel<64, true>), grid, blk, 0, s, a, lda, b,
+                           ldb, d, ldd, n, rpb, K, part);
+      else
+        hipLaunchKernelGGL((gemm_tn_narrow_mfma_kernel<64, false>), grid, blk, 0, s, a, lda, b,
+                           ldb, d, ldd, n, rpb, K, part);
     } else if (m > kWave) {
       if (d)
         hipLaunchKernelGGL((gemm_tn_narrow_kernel<true, 2>), grid, blk, 0, s, a, lda, b, ldb, d,

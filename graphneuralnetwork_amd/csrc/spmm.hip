@@ -47,6 +47,9 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 #ifndef GNN_SPMM_SMALL_SPLIT
 #define GNN_SPMM_SMALL_SPLIT 0
 #endif
+#ifndef GNN_SPMM_NARROW_CH
+#define GNN_SPMM_NARROW_CH 8  // edges per slot chunk in packed tasks of narrow rows (1 = LPR)
+#endif
 #ifndef GNN_SPMM_TASK_U
 #define GNN_SPMM_TASK_U 0  // neighbour rows in flight per slot in packed tasks (0: as GNN_SPMM_U)
 #endif
@@ -301,10 +304,14 @@ __device__ __forceinline__ void small_rows(const SpmmParams& P, int64_t swave, i
 // rowptr -> col -> X dependency chain is paid once per task instead of once per row, and the
 // gathers of a row overlap the bookkeeping of the next one. Each row's sum runs in edge order
 // in one slot: deterministic, no shuffle reduction.
-template <int VW, int LPR, int NCH, int U, bool NT, bool HUB>
+// CPL: edges per lane per chunk (a chunk = LPR * CPL edges of the slot, lane `sub` holding edges
+// sub, sub + LPR, ...): narrow rows (LPR = 2 at feat 8) take several, so that a slot keeps more
+// than LPR neighbour rows in flight.
+template <int VW, int LPR, int NCH, int U, bool NT, bool HUB, int CPL = 1>
 __device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int lane) {
   constexpr int EPI = kWave / LPR;
-  static_assert(LPR % U == 0, "a batch of U edges never straddles a chunk of LPR edges");
+  constexpr int CH = LPR * CPL;  // edges per slot chunk
+  static_assert(CH % U == 0, "a batch of U edges never straddles a chunk");
   const int sub = lane & (LPR - 1);
   const int grp = lane / LPR;
   const int32_t rb = P.task_row[2 * t];
@@ -373,28 +380,42 @@ __device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int 
 #pragma unroll
   for (int m = 1; m < kWave; m <<= 1) len = max(len, __shfl_xor(len, m, kWave));
   flush_upto(es);  // leading rows without edges
-  for (int off = 0; off < len; off += LPR) {
-    const int cb = es + off;  // this slot's chunk: lane `sub` holds edge cb + sub
-    int c = 0;
-    float v = 0.f;
-    if (cb + sub < ee) {
-      c = __builtin_nontemporal_load(P.col + e0 + cb + sub);
-      v = __builtin_nontemporal_load(P.val + e0 + cb + sub);
+  for (int off = 0; off < len; off += CH) {
+    const int cb = es + off;  // this slot's chunk: lane `sub` holds edges cb + sub + j * LPR
+    int c[CPL];
+    float v[CPL];
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      c[j] = 0;
+      v[j] = 0.f;
+      if (cb + sub + j * LPR < ee) {
+        c[j] = __builtin_nontemporal_load(P.col + e0 + cb + sub + j * LPR);
+        v[j] = __builtin_nontemporal_load(P.val + e0 + cb + sub + j * LPR);
+      }
     }
-    const int n = min(LPR, len - off);  // wave-uniform
-    for (int k = 0; k < n; k += U) {
+    const int n = min(CH, len - off);  // wave-uniform
+    auto batch = [&](int k, auto kc) {  // edges k .. k + U - 1 of the chunk (kc: k when constant)
       typename Vec<VW>::T xv[U][NCH];
       float w[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        int ce;
+        float we;
+        if constexpr (CPL == 1) {
 #if GNN_SPMM_READLANE
-        const int ce = slot_lane_i<LPR>(c, (k + u) & (LPR - 1), LPR, grp);
-        const float we = slot_lane_f<LPR>(v, (k + u) & (LPR - 1), LPR, grp);
+          ce = slot_lane_i<LPR>(c[0], (k + u) & (LPR - 1), LPR, grp);
+          we = slot_lane_f<LPR>(v[0], (k + u) & (LPR - 1), LPR, grp);
 #else
-        const int src = grp * LPR + ((k + u) & (LPR - 1));
-        const int ce = __shfl(c, src, kWave);
-        const float we = __shfl(v, src, kWave);
+          const int src = grp * LPR + ((k + u) & (LPR - 1));
+          ce = __shfl(c[0], src, kWave);
+          we = __shfl(v[0], src, kWave);
 #endif
+        } else {  // k is a constant here: the register of edge k + u is known
+          constexpr int K0 = decltype(kc)::value;
+          const int src = grp * LPR + ((K0 + u) % LPR);
+          ce = __shfl(c[(K0 + u) / LPR], src, kWave);
+          we = __shfl(v[(K0 + u) / LPR], src, kWave);
+        }
         const bool ok = cb + k + u < ee;
         w[u] = ok ? we : 0.f;
         const float* xr = (HUB && ce < 0) ? P.xh + static_cast<int64_t>(-1 - ce) * P.ldh
@@ -411,13 +432,28 @@ __device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int 
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) acc[ch] += w[u] * xv[u][ch];
       }
+    };
+    if constexpr (CPL == 1) {
+      for (int k = 0; k < n; k += U) batch(k, std::integral_constant<int, 0>{});
+    } else {  // CH / U batches, unrolled (the register index of each edge is a constant)
+      static_assert(CH / U <= 4, "at most 4 batches per chunk");
+      batch(0, std::integral_constant<int, 0>{});
+      if constexpr (CH / U > 1) {
+        if (U < n) batch(U, std::integral_constant<int, U>{});
+      }
+      if constexpr (CH / U > 2) {
+        if (2 * U < n) batch(2 * U, std::integral_constant<int, 2 * U>{});
+      }
+      if constexpr (CH / U > 3) {
+        if (3 * U < n) batch(3 * U, std::integral_constant<int, 3 * U>{});
+      }
     }
   }
   flush_upto(0x7fffffff);  // the last row and trailing rows without edges
 }
 
 template <int VW, int LPR, int NCH, int U, bool NT, bool STAGE = false, bool HUB = false,
-          bool TASKS = false>
+          bool TASKS = false, int CPL = 1>
 __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
   constexpr int EPI = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
@@ -462,7 +498,7 @@ __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
   }
   if constexpr (TASKS) {  // ---- packed row tasks
     const int64_t t = wave - P.seg_waves - P.mid_waves;
-    if (t < P.n_task) packed_rows<VW, LPR, NCH, U, NT, HUB>(P, t, lane);
+    if (t < P.n_task) packed_rows<VW, LPR, NCH, U, NT, HUB, CPL>(P, t, lane);
   } else if constexpr (!kSmallSplit) {
     // ---- packed small rows (unless they have their own launch, spmm_small_kernel)
     small_rows<VW, LPR, NCH, NT, small_unroll<NCH>()>(P, wave - P.seg_waves - P.mid_waves, lane);
@@ -559,14 +595,17 @@ static int launch_spmm_t(const SpmmLaunch& L) {
       // neighbour rows in flight per slot: at most LPR (a batch never straddles a chunk of LPR
       // edges), so the narrow rows (LPR = 2: feat 5-8, 32 slots per wave) take 2
       constexpr int UT0 = (GNN_SPMM_TASK_U > 0 && NCH == 1) ? GNN_SPMM_TASK_U : (U > 1 ? U : 2);
-      constexpr int UT = UT0 < LPR ? UT0 : LPR;
+      // rows of LPR < GNN_SPMM_NARROW_CH lanes: chunks of GNN_SPMM_NARROW_CH edges per slot,
+      // all in flight at once
+      constexpr int CPL = LPR < GNN_SPMM_NARROW_CH ? GNN_SPMM_NARROW_CH / LPR : 1;
+      constexpr int UT = CPL > 1 ? (LPR * CPL > 8 ? 8 : LPR * CPL) : (UT0 < LPR ? UT0 : LPR);
       const int64_t task_blocks = (p.n_task + kWavesPerBlock - 1) / kWavesPerBlock;
       p.seg_waves = seg_blocks * kWavesPerBlock;
       p.mid_waves = mid_blocks * kWavesPerBlock;
       const int64_t blocks = seg_blocks + mid_blocks + task_blocks;
       if (blocks > 0x7fffffffLL) return GNN_E_UNSUPPORTED;
       if (blocks > 0)
-        hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, UT, NT, false, HUB, true>),
+        hipLaunchKernelGGL((spmm_csr_kernel<VW, LPR, NCH, UT, NT, false, HUB, true, CPL>),
                            dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, L.stream, p);
       if (L.n_long > 0)
         hipLaunchKernelGGL((spmm_fixup_kernel<VW, LPR, NCH, NT>), dim3(static_cast<unsigned>(L.n_long)),

@@ -532,7 +532,10 @@ def linear_small(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor | None:
     if not lib.gnn_linear_small_supported(k, fout):
         return None
     if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
-        x = x.clone(memory_format=torch.contiguous_format)
+        # rows copied to a 16-B aligned pitch (a multiple of 4 floats >= k)
+        xp = torch.empty((x.shape[0], k + (-k) % 4), dtype=torch.float32, device=x.device)
+        xp[:, :k] = x
+        x = xp[:, :k]
     w = w.contiguous()
     y = torch.empty((x.shape[0], fout + (-fout) % 4), dtype=torch.float32, device=x.device)
     _lib.check(lib.gnn_linear_small_f32(x.data_ptr(), x.stride(0), x.shape[0], k, w.data_ptr(),

@@ -269,11 +269,12 @@ def test_linear_small_vs_float64(dev, k, fo, n):
     dX = dS W): x W^T against float64 with strided rows of x; uncovered shapes return None."""
     from graphneuralnetwork_amd.ops import linear_small
     gen = torch.Generator(device=dev).manual_seed(k * 7 + fo + n)
-    x = torch.randn(n, k + 4 + (-k) % 4, device=dev, generator=gen)[:, :k]
     w = torch.randn(fo, k, device=dev, generator=gen)
-    y = linear_small(x, w)
-    assert y is not None and y.shape == (n, fo)
-    close(y.cpu().numpy(), (x.double() @ w.double().t()).cpu().numpy(), rtol=1e-5)
+    for x in (torch.randn(n, k + 4 + (-k) % 4, device=dev, generator=gen)[:, :k],
+              torch.randn(n, k, device=dev, generator=gen)):  # an aligned pitch; rows of k
+        y = linear_small(x, w)
+        assert y is not None and y.shape == (n, fo)
+        close(y.cpu().numpy(), (x.double() @ w.double().t()).cpu().numpy(), rtol=1e-5)
     assert linear_small(x, torch.randn(24, k, device=dev)) is None
 
 
