@@ -519,6 +519,9 @@ def gemm_tn_masked(a: torch.Tensor, b: torch.Tensor, h: torch.Tensor, scale: flo
     return c, dsum
 
 
+LINEAR_SMALL_MAX_FOUT = 64  # widest output the k <= 16 kernel takes by default
+
+
 def linear_small(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor | None:
     """x @ w^T with one narrow side (gnn_linear_small_f32: fout <= 16 on fp32 MFMA rows, or
     k <= 16 on a broadcast kernel) -- the classifier layer's support and its dX; None when the
@@ -529,7 +532,11 @@ def linear_small(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor | None:
         return None
     lib = _lib.load()
     fout, k = w.shape
-    if not lib.gnn_linear_small_supported(k, fout):
+    kind = lib.gnn_linear_small_supported(k, fout)
+    # the broadcast kernel (k <= 16) beat hipBLASLt at fout 64 (GAT out_att dX: 0.055 vs 0.120
+    # ms) but not at 128 inside the GCN_Model step (0.189 vs 0.146 ms,
+    # profiles/r06y_gcn_model_train_step_kernel_stats.csv): 128 and 256 stay on torch.mm
+    if not kind or (kind == 2 and fout > LINEAR_SMALL_MAX_FOUT):
         return None
     if x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
         # rows copied to a 16-B aligned pitch (a multiple of 4 floats >= k)

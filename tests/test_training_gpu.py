@@ -264,10 +264,12 @@ def test_gcn_model_fused_training_equals_unfused(dev, monkeypatch):
 @pytest.mark.parametrize("k,fo", [(128, 8), (64, 7), (256, 16), (16, 1), (8, 128), (7, 64),
                                   (16, 256), (1, 128)])
 @pytest.mark.parametrize("n", [1, 37, 20000, 300001])
-def test_linear_small_vs_float64(dev, k, fo, n):
+def test_linear_small_vs_float64(dev, k, fo, n, monkeypatch):
     """gnn_linear_small_f32 (ops.linear_small, the classifier layer's support H W^T and its
     dX = dS W): x W^T against float64 with strided rows of x; uncovered shapes return None."""
+    from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.ops import linear_small
+    monkeypatch.setattr(ops, "LINEAR_SMALL_MAX_FOUT", 256)  # every shape the kernels take
     gen = torch.Generator(device=dev).manual_seed(k * 7 + fo + n)
     w = torch.randn(fo, k, device=dev, generator=gen)
     for x in (torch.randn(n, k + 4 + (-k) % 4, device=dev, generator=gen)[:, :k],
