@@ -714,3 +714,34 @@ def test_gat_narrow_out_att_padded_backward(dev, kind, nclass, monkeypatch):
     for a, b in zip(res[True], res[False]):
         err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
         assert err < 1e-5, err
+
+
+def test_gat_replay_restores_the_plan(dev):
+    """bench.gat_replay (the GAT aggregation's measured ceiling, gathered ids rewritten in place
+    in the hub plan's column array) leaves the plan as it found it: the aggregation after the
+    replay equals the one before it bit for bit; every gather from an L2-sized table is faster
+    than the step as built."""
+    import bench
+    from graphneuralnetwork_amd.ops import (GAT_DENSE, gat_aggregate, gat_column_order,
+                                            gat_project, hub_rows_for)
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    n, H, Fh = 1_000_000, 8, 8
+    s, d = rmat_edges(n, 10_000_000, 0)
+    g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
+    order = gat_column_order(g, H, Fh)
+    assert order is not None
+    ga = order.graph
+    gen = torch.Generator(device=dev).manual_seed(3)
+    X = torch.randn(n, 64, device=dev, generator=gen)
+    W = torch.randn(64, H * Fh, device=dev, generator=gen) * 0.2
+    a_s = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
+    a_d = torch.randn(H * Fh, device=dev, generator=gen) * 0.3
+    wh, el, er = gat_project(X, W, H, Fh, a_s, a_d, col_rows=order.inv)
+    out = torch.empty_like(wh)
+    fn = lambda: gat_aggregate(ga, wh, el, er, H, Fh, 0.2, GAT_DENSE, "elu", out=out, a_dst=a_d)
+    y0 = fn().clone()
+    r = bench.gat_replay(ga, hub_rows_for(ga.n_cols, H * Fh + H), fn, reps=2)
+    assert r is not None and r["hub_gathers"] > 0 and r["nonhub_gathers"] > 0
+    assert r["all_gathers_in_L2_ms"] < r["as_built_ms"]
+    assert torch.equal(fn(), y0)
