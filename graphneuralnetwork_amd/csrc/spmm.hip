@@ -455,13 +455,11 @@ __device__ __forceinline__ void packed_rows(const SpmmParams& P, int64_t t, int 
 template <int VW, int LPR, int NCH, int U, bool NT, bool STAGE = false, bool HUB = false,
           bool TASKS = false, int CPL = 1>
 __global__ __launch_bounds__(kBlock) void spmm_csr_kernel(SpmmParams P) {
-  constexpr int EPI = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
   __shared__ f4 stage_all[STAGE ? kWavesPerBlock * U * kWave : 1];
   f4* stage = stage_all + (STAGE ? (threadIdx.x >> 6) * U * kWave : 0);
   const int sub = lane & (LPR - 1);
-  const int grp = lane / LPR;
   typename Vec<VW>::T acc[NCH];
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) acc[ch] = vzero<VW>();

@@ -35,8 +35,9 @@ import torch.nn.functional as F
 from torch import nn
 
 from .graph import as_csr
+from . import ops
 from .ops import (PermuteRows, column_order, dropout_seed, fuses_relu_dropout, gcn_layer,
-                  gcn_train_order, gcn_transform, spmm, spmm_forward)
+                  gcn_train_order, gcn_transform, row_order_graph, spmm, spmm_forward)
 
 
 class GCN_Model(nn.Module):
@@ -74,41 +75,57 @@ class GCN_Model(nn.Module):
 
     def forward(self, X, adj):
         order = self._train_order(X, adj)
+        first = None
         if order is not None:
             # training over P A P^T: X in on its rows once, the logits back out once; every
-            # layer's SpMM (forward, and dS = A dY in backward) reads its hub rows in place
-            X = PermuteRows.apply(X, order.perm, order.inv)
+            # layer's SpMM (forward, and dS = A dY in backward) reads its hub rows in place. A
+            # first layer over features without gradient reads X as it is through P A instead
+            # (its output rows land in the degree order all the same)
+            if self._first_rows(X, order.graph):
+                first = row_order_graph(as_csr(adj))
+            else:
+                X = PermuteRows.apply(X, order.perm, order.inv)
             adj = order.graph
-        X = self._blocks(X, adj)
+        X = self._blocks(X, adj, first)
         if order is not None:
             X = PermuteRows.apply(X, order.inv, order.perm)
         return X
 
-    def _blocks(self, X, adj):
+    def _first_rows(self, X, g) -> bool:
+        blocks = list(self.gcn_blocks)
+        b = blocks[0] if blocks else None
+        return (ops.GCN_FIRST_ROWS and not X.requires_grad and isinstance(b, Graph_conv_layer)
+                and not (b._forward_hooks or b._forward_pre_hooks)
+                and ops._reassociate(X, b.dense.weight, g))
+
+    def _blocks(self, X, adj, first=None):
+        """The Sequential's modules in order (GCN/GCN.py:22-27), with the fusions above; the
+        first Graph_conv_layer runs over ``first`` when given (P A, see forward)."""
         blocks = list(self.gcn_blocks)
         i = 0
         while i < len(blocks):
             gcn_block = blocks[i]
             if gcn_block._get_name() == 'Graph_conv_layer':
+                g_i = first if (i == 0 and first is not None) else adj
                 nxt = blocks[i + 1] if i + 1 < len(blocks) else None
                 span = _fuse_train(gcn_block, nxt, blocks[i + 2] if i + 2 < len(blocks) else None,
-                                   X, adj)
+                                   X, g_i)
                 if span:
                     # Graph_conv_layer -> ReLU (-> Dropout) in training: one op, ReLU and dropout
                     # in the transform's epilogue (GCN/GCN.py:12-14)
                     drop = blocks[i + 2] if span == 3 else None
                     p = drop.p if drop is not None and drop.training else 0.0
-                    X = gcn_layer(as_csr(adj), X, gcn_block.dense.weight, gcn_block.bias,
+                    X = gcn_layer(as_csr(g_i), X, gcn_block.dense.weight, gcn_block.bias,
                                   relu_dropout=(p, dropout_seed() if p > 0 else 0))
                     i += span
                     continue
                 if _fuse_relu(gcn_block, nxt, X):
                     # the ReLU in the SpMM's store epilogue (GNN_EPI_RELU): one pass over the
                     # [n, hidden] activations fewer at inference
-                    X = gcn_block._forward(X, adj, 'relu')
+                    X = gcn_block._forward(X, g_i, 'relu')
                     i += 2
                     continue
-                X = gcn_block(X, adj)
+                X = gcn_block(X, g_i)
             else:
                 X = gcn_block(X)
             i += 1

@@ -336,6 +336,34 @@ def node_order(g: CsrGraph):
     return o
 
 
+# GCN_Model in training: a first layer over input features that need no gradient reads X in
+# its original row order through P A (rows relabelled, column ids as in A) instead of
+# permuting X onto P A P^T first (one [n, F] gather pass fewer; its SpMM stages the hub rows)
+GCN_FIRST_ROWS = True
+
+
+def row_order_graph(g: CsrGraph) -> CsrGraph:
+    """P A for ``node_order(g)``'s P: row i is A's row perm[i] with its edges as in A (column ids
+    not renamed), cached on g. A layer over it maps X in the original order to output rows in
+    the degree order."""
+    rg = g._plans.get(("_nodeorder_rows",))
+    if rg is None:
+        o = node_order(g)
+        n = g.n_rows
+        deg = g.rowptr[1:] - g.rowptr[:-1]
+        nd = deg.index_select(0, o.perm)
+        rp = torch.zeros(n + 1, dtype=torch.int64, device=g.rowptr.device)
+        torch.cumsum(nd, 0, out=rp[1:])
+        src = torch.repeat_interleave(g.rowptr[:-1].index_select(0, o.perm) - rp[:-1], nd,
+                                      output_size=g.nnz)
+        src += torch.arange(g.nnz, dtype=torch.int64, device=src.device)
+        rg = CsrGraph(rp, g.col.index_select(0, src).contiguous(),
+                      g.val.index_select(0, src).contiguous(), n, g.n_cols)
+        del src
+        g._plans[("_nodeorder_rows",)] = rg
+    return rg
+
+
 def _orderable(g: CsrGraph) -> bool:
     return (DEGREE_ORDER and g.nnz > 0 and g.symmetric and g.n_rows == g.n_cols
             and g.col.is_cuda and not g._plans.get("_degree_ordered"))

@@ -502,6 +502,48 @@ def test_gat_training_grads_use_tn_kernel(dev):
     close(ga_d, a_d.grad.numpy())
 
 
+@pytest.mark.parametrize("drop", [0.0, 0.5])
+def test_gcn_model_first_layer_over_row_order(dev, monkeypatch, drop):
+    """GCN_Model in training with input features that need no gradient: the first layer reads
+    X in its original order through P A (ops.row_order_graph: rows relabelled, column ids as in
+    A) instead of permuting X onto P A P^T -- logits and every parameter gradient equal the
+    permuting path to fp32 rounding; P A is A's rows in the order's permutation, edges intact."""
+    from graphneuralnetwork_amd import gcn as gcn_mod
+    from graphneuralnetwork_amd import ops
+    from graphneuralnetwork_amd.gcn import GCN_Model
+    from graphneuralnetwork_amd.preprocess import gcn_adjacency
+    from graphneuralnetwork_amd.rmat import rmat_edges
+    monkeypatch.setattr(ops, "XCD_MIN_NNZ", 0)
+    monkeypatch.setattr(ops, "HUB_MIN_X_BYTES", 0)
+    monkeypatch.setattr(gcn_mod, "dropout_seed", lambda: 12345)
+    n = 60_000
+    s, d = rmat_edges(n, 500_000, 5)
+    g = gcn_adjacency(torch.from_numpy(s), torch.from_numpy(d), n, device=dev)
+    torch.manual_seed(0)
+    model = GCN_Model(128, 128, 7, 2, drop).to(dev).train()
+    X = torch.randn(n, 128, device=dev)
+    lab = torch.randint(0, 7, (n,), device=dev)
+    res, used = {}, {}
+    for rows in (True, False):
+        monkeypatch.setattr(ops, "GCN_FIRST_ROWS", rows)
+        model.zero_grad(set_to_none=True)
+        y = model(X, g)
+        torch.nn.functional.cross_entropy(y, lab).backward()
+        used[rows] = ("_nodeorder_rows",) in g._plans
+        res[rows] = [y.detach()] + [p.grad.clone() for p in model.parameters()]
+    assert used[True]
+    for a, b in zip(res[True], res[False]):
+        err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+        assert err < 1e-5, err
+    o = ops.node_order(g)
+    rg = ops.row_order_graph(g)
+    deg = (g.rowptr[1:] - g.rowptr[:-1])[o.perm]
+    assert torch.equal(rg.rowptr[1:] - rg.rowptr[:-1], deg)
+    r = int(o.perm[7])
+    a, b = int(rg.rowptr[7]), int(rg.rowptr[8])
+    assert torch.equal(rg.col[a:b], g.col[int(g.rowptr[r]):int(g.rowptr[r + 1])])
+
+
 def test_gcn_model_training_in_degree_order_equals_natural(dev, monkeypatch):
     """GCN_Model in training runs over P A P^T (ops.gcn_train_order: X permuted on entry, the
     logits on exit): logits and every gradient equal the natural-order step to fp32 rounding
