@@ -202,6 +202,8 @@ SIGNATURES: dict[str, tuple] = {
     "gnn_sage_gather_aggregate_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64,
                                                      _i32, _vp, _i64, _vp, _vp]),
     "gnn_gather_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _vp]),
+    "gnn_dropout_rows_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, ctypes.c_int32, _i64, _i64,
+                                            ctypes.c_float, ctypes.c_uint64, _vp, _i64, _vp, _vp]),
     "gnn_sage_layer_supported": (ctypes.c_int, [_i64, _i64]),
     "gnn_sage_layer_f32": (ctypes.c_int, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _i64,
                                           _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp]),

@@ -219,6 +219,36 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
   }
 }
 
+// out[i, c] = keep(seed, key, c) ? x[r, c] / (1 - p) : 0 with r = idx ? idx[i] : i and key = r
+// (KEY_SRC) or i: F.dropout (GAT/models/GAT.py:15,17) as a hashed element mask, fused with the
+// models' relabelling gather. The mask is never stored: the backward re-derives it from the
+// seed (the same launch with key = the source row through the inverse permutation).
+template <int VW, bool KEY_SRC>
+__global__ __launch_bounds__(256) void dropout_rows_kernel(
+    const float* __restrict__ x, int64_t ldx, int64_t n_x, const int64_t* __restrict__ idx,
+    int64_t n, int64_t feat, float p, float scale, uint64_t seed, float* __restrict__ out,
+    int64_t ldo, int32_t* __restrict__ err) {
+  const int64_t nv = feat / VW;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t total = n * nv;
+  for (int64_t q = t; q < total; q += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t i = q / nv, v = q % nv;
+    const int64_t r = idx ? idx[i] : i;
+    if (r < 0 || r >= n_x) {
+      if (v == 0) atomicOr(err, 1);
+      continue;
+    }
+    const int64_t key = KEY_SRC ? r : i;
+    typename Vec<VW>::T a = vload<VW>(x + r * ldx + v * VW);
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const int c = static_cast<int>(v * VW + j);
+      vset(a, j, dropout_keep(seed, key, c, p) ? vget(a, j) * scale : 0.f);
+    }
+    vstore<VW>(out + i * ldo + v * VW, a);
+  }
+}
+
 struct SageArgs {
   const float* src;
   int64_t ld_row, ld_m, n_table;
@@ -353,6 +383,39 @@ extern "C" int gnn_gather_rows_f32(const float* x, int64_t ldx, int64_t n_x, con
   else
     hipLaunchKernelGGL(gather_rows_kernel<1>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
                        x, ldx, n_x, idx, n, feat, out, ldo, err_flag);
+  return launch_status();
+}
+
+extern "C" int gnn_dropout_rows_f32(const float* x, int64_t ldx, int64_t n_x, const int64_t* idx,
+                                    int32_t key_by_source, int64_t n, int64_t feat, float p,
+                                    uint64_t seed, float* out, int64_t ldo, int32_t* err_flag,
+                                    void* stream) {
+  if (n < 0 || feat < 0 || n_x < 0 || !(p >= 0.f && p < 1.f)) return GNN_E_ARG;
+  if (feat > 0x7fffffff) return GNN_E_ARG;  // the hash takes the column as an int
+  if (n == 0 || feat == 0) return GNN_OK;
+  if (!x || !out || !err_flag || ldx < feat || ldo < feat) return GNN_E_ARG;
+  if (!idx && n > n_x) return GNN_E_ARG;
+  if (x == out && idx) return GNN_E_ARG;  // in place only without a gather
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool vec4 = feat % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && aligned_to(x, 16) &&
+                    aligned_to(out, 16);
+  const float scale = 1.0f / (1.0f - p);
+  const int64_t total = n * (vec4 ? feat / 4 : feat);
+  const int64_t blocks = total / 256 + 1 < 65536 ? total / 256 + 1 : 65536;
+  const dim3 grid(static_cast<unsigned>(blocks));
+  const bool ks = key_by_source != 0;
+  if (vec4 && ks)
+    hipLaunchKernelGGL((dropout_rows_kernel<4, true>), grid, dim3(256), 0, s, x, ldx, n_x, idx, n,
+                       feat, p, scale, seed, out, ldo, err_flag);
+  else if (vec4)
+    hipLaunchKernelGGL((dropout_rows_kernel<4, false>), grid, dim3(256), 0, s, x, ldx, n_x, idx, n,
+                       feat, p, scale, seed, out, ldo, err_flag);
+  else if (ks)
+    hipLaunchKernelGGL((dropout_rows_kernel<1, true>), grid, dim3(256), 0, s, x, ldx, n_x, idx, n,
+                       feat, p, scale, seed, out, ldo, err_flag);
+  else
+    hipLaunchKernelGGL((dropout_rows_kernel<1, false>), grid, dim3(256), 0, s, x, ldx, n_x, idx, n,
+                       feat, p, scale, seed, out, ldo, err_flag);
   return launch_status();
 }
 

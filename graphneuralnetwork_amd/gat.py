@@ -43,7 +43,7 @@ from torch import nn
 from .graph import as_csr
 from .ops import (GAT_DENSE, GAT_SPARSE, PermuteRows, _bwd_recompute_ok, _transform_or_mm,
                   gat_aggregate, gat_backward, gat_column_order, gat_logits, gat_project,
-                  gat_train_order, gemm_tn)
+                  gat_train_order, gemm_tn, model_dropout)
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
@@ -313,8 +313,9 @@ class GATBase(nn.Module):
     Training on a large symmetric graph runs the whole model over P A P^T (``gat_train_order``:
     nodes relabelled once by degree): x is permuted once on entry and the logits once on exit,
     so every attention layer's forward and both backward passes read their hub rows at the top
-    of Wh / er / dout. Same function; the dropout draws (F.dropout's and the attention's
-    (seed, edge, head) hash) fall on the relabelled rows / edges."""
+    of Wh / er / dout. Same function; the dropout draws fall on the relabelled rows / edges.
+    In training the two F.dropout calls run as hashed element masks that are never stored
+    (``ops.model_dropout``: (seed, row, column) hash, the first fused with the relabelling)."""
 
     def __init__(self, dropout, **kwargs):
         super().__init__(**kwargs)
@@ -358,12 +359,13 @@ class GATBase(nn.Module):
 
     def forward(self, x, adj):
         order = self._train_order(x, adj)
-        if order is not None:
-            x = PermuteRows.apply(x, order.perm, order.inv)
+        if order is not None:  # relabel and drop out in one pass
+            x = model_dropout(x, self.dropout, self.training, order.perm, order.inv)
             adj = order.graph
-        x = F.dropout(x, self.dropout, training=self.training)
+        else:
+            x = model_dropout(x, self.dropout, self.training)
         x = self._heads(x, adj)
-        x = F.dropout(x, self.dropout, training=self.training)
+        x = model_dropout(x, self.dropout, self.training)
         out = self.out_att(x, adj, activation="elu")  # F.elu(out_att(x)) fused (concat=False)
         if order is not None:
             out = PermuteRows.apply(out, order.inv, order.perm)

@@ -385,8 +385,10 @@ def gcn_train_order(g: CsrGraph, feat: int):
     return node_order(g)
 
 
-def gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
-    """x[idx] for a 2-D fp32 device tensor and int64 row ids (gnn_gather_rows_f32: 16-B row
+def permute_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """x[idx] for a 2-D fp32 device tensor and int64 row ids from a permutation, unchecked (no
+    host read of the error flag: the training steps run it 2-4 times per step; the checked
+    ``gather_rows`` below synced the host each time) (gnn_gather_rows_f32: 16-B row
     pieces per lane; torch's index_select moved the 1M x 128 permutation at ~1.7 TB/s,
     profiles/r06i_*); other inputs take index_select."""
     if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1
@@ -394,7 +396,7 @@ def gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
         return x.index_select(0, idx)
     idx = idx.contiguous()
     out = torch.empty((idx.numel(), x.shape[1]), dtype=torch.float32, device=x.device)
-    err = torch.zeros(1, dtype=torch.int32, device=x.device)  # ids come from a permutation
+    err = _err_flag(x.device, False)  # ids come from a permutation: the flag is never read
     _lib.check(_lib.load().gnn_gather_rows_f32(x.data_ptr(), x.stride(0), x.shape[0],
                                                idx.data_ptr(), idx.numel(), x.shape[1],
                                                out.data_ptr(), out.stride(0), err.data_ptr(),
@@ -410,11 +412,63 @@ class PermuteRows(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, perm, inv):
         ctx.inv = inv
-        return gather_rows(x, perm)
+        return permute_rows(x, perm)
 
     @staticmethod
     def backward(ctx, gy):
-        return gather_rows(gy.contiguous(), ctx.inv), None, None
+        return permute_rows(gy.contiguous(), ctx.inv), None, None
+
+
+# F.dropout (GAT/models/GAT.py:15,17) in training as gnn_dropout_rows_f32: a hashed element mask
+# that is never stored, fused with the entry relabelling where there is one. torch's dropout
+# wrote a byte mask beside its output and read it back in the backward (~0.1 ms forward +
+# ~0.08 ms backward per [1M, 64] at cfg3, profiles/r06y_*).
+HASHED_DROPOUT = True
+
+
+def dropout_rows(x: torch.Tensor, p: float, seed: int, idx: torch.Tensor | None = None,
+                 key_by_source: bool = False) -> torch.Tensor:
+    """out[i] = x[r] with r = idx[i] (or i), element (i, c) kept iff the (seed, key, c) hash clears
+    p (key = r when ``key_by_source``, else i), kept values scaled by 1 / (1 - p). Unchecked ids
+    (they come from a permutation)."""
+    n = idx.numel() if idx is not None else x.shape[0]
+    out = torch.empty((n, x.shape[1]), dtype=torch.float32, device=x.device)
+    if idx is not None:
+        idx = idx.contiguous()
+    _lib.check(_lib.load().gnn_dropout_rows_f32(
+        x.data_ptr(), x.stride(0), x.shape[0], idx.data_ptr() if idx is not None else None,
+        int(key_by_source), n, x.shape[1], float(p), int(seed) & (2 ** 64 - 1), out.data_ptr(),
+        out.stride(0), _err_flag(x.device, False).data_ptr(), _lib.stream_handle(x.device)),
+        "gnn_dropout_rows_f32")
+    return out
+
+
+class DropoutRows(torch.autograd.Function):
+    """y = dropout(x[perm]) (perm None: y = dropout(x)) with the hashed mask keyed by y's row; the
+    gradient dx[j] = mask(inv[j]) dy[inv[j]] / (1 - p) re-derives the mask through inv."""
+
+    @staticmethod
+    def forward(ctx, x, p, seed, perm, inv):
+        ctx.cfg = (p, seed, inv)
+        return dropout_rows(x, p, seed, perm)
+
+    @staticmethod
+    def backward(ctx, gy):
+        p, seed, inv = ctx.cfg
+        gx = dropout_rows(gy.contiguous(), p, seed, inv, key_by_source=inv is not None)
+        return gx, None, None, None, None
+
+
+def model_dropout(x: torch.Tensor, p: float, training: bool, perm=None, inv=None):
+    """F.dropout(x[perm] or x, p, training) on the hashed kernel where it applies (2-D fp32 device
+    rows with unit column stride, 0 < p < 1), else PermuteRows + torch's dropout."""
+    ok = (training and 0.0 < p < 1.0 and HASHED_DROPOUT and x.dim() == 2 and x.is_cuda
+          and x.dtype == torch.float32 and x.stride(1) == 1 and x.stride(0) >= x.shape[1])
+    if not ok:
+        if perm is not None:
+            x = PermuteRows.apply(x, perm, inv)
+        return torch.nn.functional.dropout(x, p, training=training)
+    return DropoutRows.apply(x, p, dropout_seed(), perm, inv)
 
 
 def _spmm_xcd_direct(lib, xp, x, feat, bias, out, seg, skip_empty, flags, stream):

@@ -769,6 +769,18 @@ int gnn_gather_rows_f32(const float* x, int64_t ldx, int64_t n_x, const int64_t*
                         int64_t feat, float* out, int64_t ldo, int32_t* err_flag, void* stream);
 
 /*
+ * Hashed element dropout fused with a row gather, replacing F.dropout(x, p, training) at
+ * GAT/models/GAT.py:15,17 in training (and its backward): r = idx ? idx[i] : i,
+ * out[i, c] = x[r, c] / (1 - p) when the (seed, key, c) hash clears p (common.hpp
+ * dropout_keep; key = r if key_by_source else i), else 0. No mask is stored: the backward
+ * re-derives it from the seed. 0 <= p < 1; x == out only without idx. Out-of-range index ->
+ * *err_flag |= 1, row skipped.
+ */
+int gnn_dropout_rows_f32(const float* x, int64_t ldx, int64_t n_x, const int64_t* idx,
+                         int32_t key_by_source, int64_t n, int64_t feat, float p, uint64_t seed,
+                         float* out, int64_t ldo, int32_t* err_flag, void* stream);
+
+/*
  * GraphSAGE neighbour sampling for a frontier (GraphSAGE/data_utils.py:89-94):
  *   out[i, 0..k) = k neighbours of nodes[i] in the CSR (rowptr, col):
  *     deg >  k: k distinct neighbours (random.sample), Floyd's algorithm;
