@@ -188,6 +188,14 @@ SIGNATURES: dict[str, tuple] = {
         _i64, _vp, _vp, _i64, _vp, _vp, _i64,       # plan
         _vp, _i64, _vp, _i64, _vp, _vp, _vp]),      # rows, n, short_rows, n, del_part, a_dst,
                                                     # stream
+    "gnn_gat_backward_rows_ex_f32": (ctypes.c_int, [
+        _vp, _vp, _i64, _vp, _i64, _i64, _i64,
+        _vp, _vp, _vp, _vp, _vp, _i64, _i32,
+        ctypes.c_float, _i32, ctypes.c_float, ctypes.c_uint64,
+        _vp, _vp, _vp,
+        _i64, _vp, _vp, _i64, _vp, _vp, _i64,
+        _vp, _i64, _vp, _i64, _vp, _vp,
+        ctypes.c_float, ctypes.c_uint64, _vp]),     # ... a_dst, dy_drop_p, dy_drop_seed, stream
     "gnn_gat_backward_nodes_recompute_f32": (ctypes.c_int, [
         _vp, _vp, _vp, _i64, _i64, _i64,            # rowptr_t, src_t, eid_t, n, heads, fh
         _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,    # dout, nstat, wh, ldw, er, del, a_src, a_dst

@@ -118,7 +118,9 @@ __global__ __launch_bounds__(256) void gat_bwd_prep_rec_kernel(const float* __re
                                                                const float* __restrict__ el,
                                                                const float* __restrict__ lse,
                                                                float* __restrict__ dout,
-                                                               float* __restrict__ nstat) {
+                                                               float* __restrict__ nstat,
+                                                               float dyp, float dyscale,
+                                                               uint64_t dyseed) {
   const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t per_row = heads * G;  // float4s per row
   const bool live = t < n_rows * per_row;
@@ -129,6 +131,12 @@ __global__ __launch_bounds__(256) void gat_bwd_prep_rec_kernel(const float* __re
     gv = *reinterpret_cast<const float4*>(dy + r * ldo + 4 * c);
   }
   float yy[4] = {yv.x, yv.y, yv.z, yv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w}, dd[4];
+  if (dyp > 0.f) {  // dy is the gradient of dropout(y): the mask of gnn_dropout_rows_f32 (key r)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      gg[i] = dropout_keep(dyseed, r, static_cast<int>(4 * c + i), dyp) ? gg[i] * dyscale
+                                                                         : gg[i] * 0.f;
+  }
   float acc = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1145,6 +1153,16 @@ extern "C" int gnn_gat_backward_nodes_f32(
 
 static int hp_for(int64_t heads) { return heads <= 1 ? 1 : heads <= 2 ? 2 : heads <= 4 ? 4 : 8; }
 
+extern "C" int gnn_gat_backward_rows_ex_f32(
+    const int64_t* rowptr, const int32_t* col, int64_t n_rows, const float* wh, int64_t ldw,
+    int64_t heads, int64_t fh, const float* el, const float* er, const float* lse, const float* dy,
+    const float* y, int64_t ldo, int32_t elu, float negative_slope, int32_t mode, float dropout_p,
+    uint64_t dropout_seed, float* dout, float* nstat, float* del, int64_t seg_len,
+    const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
+    const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows, int64_t n_rows_list,
+    const int32_t* short_rows, int64_t n_short, float* del_part, const float* a_dst,
+    float dy_dropout_p, uint64_t dy_dropout_seed, void* stream);
+
 extern "C" int gnn_gat_backward_rows_f32(
     const int64_t* rowptr, const int32_t* col, int64_t n_rows, const float* wh, int64_t ldw,
     int64_t heads, int64_t fh, const float* el, const float* er, const float* lse, const float* dy,
@@ -1154,11 +1172,28 @@ extern "C" int gnn_gat_backward_rows_f32(
     const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows, int64_t n_rows_list,
     const int32_t* short_rows, int64_t n_short, float* del_part, const float* a_dst,
     void* stream) {
+  return gnn_gat_backward_rows_ex_f32(rowptr, col, n_rows, wh, ldw, heads, fh, el, er, lse, dy, y,
+                                      ldo, elu, negative_slope, mode, dropout_p, dropout_seed,
+                                      dout, nstat, del, seg_len, seg_row, seg_begin, n_seg,
+                                      long_row, long_seg_ptr, n_long, rows, n_rows_list,
+                                      short_rows, n_short, del_part, a_dst, 0.f, 0, stream);
+}
+
+extern "C" int gnn_gat_backward_rows_ex_f32(
+    const int64_t* rowptr, const int32_t* col, int64_t n_rows, const float* wh, int64_t ldw,
+    int64_t heads, int64_t fh, const float* el, const float* er, const float* lse, const float* dy,
+    const float* y, int64_t ldo, int32_t elu, float negative_slope, int32_t mode, float dropout_p,
+    uint64_t dropout_seed, float* dout, float* nstat, float* del, int64_t seg_len,
+    const int32_t* seg_row, const int64_t* seg_begin, int64_t n_seg, const int32_t* long_row,
+    const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows, int64_t n_rows_list,
+    const int32_t* short_rows, int64_t n_short, float* del_part, const float* a_dst,
+    float dy_dropout_p, uint64_t dy_dropout_seed, void* stream) {
   const int64_t feat = heads * fh;
   if (n_rows < 0 || heads < 1 || fh < 1 || ldw < feat || ldo < feat || n_seg < 0 || n_long < 0 ||
       n_rows_list < 0 || n_short < 0 || seg_len < 1 || (mode != 0 && mode != 1))
     return GNN_E_ARG;
   if (!(dropout_p >= 0.f && dropout_p < 1.f)) return GNN_E_ARG;
+  if (!(dy_dropout_p >= 0.f && dy_dropout_p < 1.f)) return GNN_E_ARG;
   if (n_rows == 0) return GNN_OK;
   if (!rowptr || !wh || !el || !er || !lse || !dy || !y || !dout || !nstat || !del) return GNN_E_ARG;
   if (!aligned_to(nstat, 16)) return GNN_E_ALIGN;
@@ -1220,10 +1255,14 @@ extern "C" int gnn_gat_backward_rows_f32(
   const int64_t g4 = fh / 4;
   const bool split = GNN_BWD_SPLIT_PREP && vec4 && (g4 & (g4 - 1)) == 0 && g4 <= 64 &&
                      aligned_to(nstat, 16);
+  // the upstream dropout mask is applied by the coalesced prep only (the caller masks dy itself
+  // for the shapes that fuse the prep into the row pass)
+  if (dy_dropout_p > 0.f && (!split || ldo != feat)) return GNN_E_UNSUPPORTED;
+  const float dy_scale = dy_dropout_p > 0.f ? 1.f / (1.f - dy_dropout_p) : 1.f;
   if (split) {
     const int64_t tv = n_rows * heads * g4;
     const dim3 pg(static_cast<unsigned>((tv + 255) / 256));
-#define GNN_PREP(G) hipLaunchKernelGGL(gat_bwd_prep_rec_kernel<G>, pg, dim3(256), 0, s, dy, y, ldo, n_rows, heads, static_cast<int>(elu != 0), el, lse, dout, nstat)
+#define GNN_PREP(G) hipLaunchKernelGGL(gat_bwd_prep_rec_kernel<G>, pg, dim3(256), 0, s, dy, y, ldo, n_rows, heads, static_cast<int>(elu != 0), el, lse, dout, nstat, dy_dropout_p, dy_scale, dy_dropout_seed)
     switch (g4) {
       case 1: GNN_PREP(1); break;
       case 2: GNN_PREP(2); break;

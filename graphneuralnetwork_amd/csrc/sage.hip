@@ -219,7 +219,8 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
   }
 }
 
-// out[i, c] = keep(seed, key, c) ? x[r, c] / (1 - p) : 0 with r = idx ? idx[i] : i and key = r
+// out[i, c] = keep(seed, key, c) ? x[r, c] / (1 - p) : x[r, c] * 0 (torch's x * mask * scale:
+// NaN stays NaN) with r = idx ? idx[i] : i and key = r
 // (KEY_SRC) or i: F.dropout (GAT/models/GAT.py:15,17) as a hashed element mask, fused with the
 // models' relabelling gather. The mask is never stored: the backward re-derives it from the
 // seed (the same launch with key = the source row through the inverse permutation).
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(256) void dropout_rows_kernel(
 #pragma unroll
     for (int j = 0; j < VW; ++j) {
       const int c = static_cast<int>(v * VW + j);
-      vset(a, j, dropout_keep(seed, key, c, p) ? vget(a, j) * scale : 0.f);
+      vset(a, j, dropout_keep(seed, key, c, p) ? vget(a, j) * scale : vget(a, j) * 0.f);
     }
     vstore<VW>(out + i * ldo + v * VW, a);
   }

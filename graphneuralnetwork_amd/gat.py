@@ -40,43 +40,55 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from . import ops as _ops
 from .graph import as_csr
 from .ops import (GAT_DENSE, GAT_SPARSE, PermuteRows, _bwd_recompute_ok, _transform_or_mm,
                   gat_aggregate, gat_backward, gat_column_order, gat_logits, gat_project,
-                  gat_train_order, gemm_tn, model_dropout)
+                  gat_train_order, gemm_tn, model_dropout, dropout_rows,
+                  hashed_dropout_ok as HASHED_DROPOUT_OK)
 
 # The reference asserts ``not torch.isnan(...).any()`` in the sparse layer
 # (layers.py:102,109,119,124).  Kept on by default for identical error
 # behaviour; each check is one device reduction + host sync.
 SPARSE_NAN_CHECK = True
+# the GAT model's hidden dropout (GAT.py:17) inside the heads' autograd op: the forward applies
+# the hashed mask to the layer's output, the backward prep applies it to the upstream gradient
+# (no separate dropout backward pass)
+GAT_FUSE_OUT_DROPOUT = True
 
 
 class _GatLayerFn(torch.autograd.Function):
     """Fused attention layer: Wh, a_src, a_dst -> act(edge-softmax aggregation)."""
 
     @staticmethod
-    def forward(ctx, Wh, a_src, a_dst, g, heads, fh, slope, mode, activation, drop_p, seed):
+    def forward(ctx, Wh, a_src, a_dst, g, heads, fh, slope, mode, activation, drop_p, seed,
+                out_drop=None):
         el, er = gat_logits(Wh, heads, fh, a_src, a_dst)
         stats = torch.empty((g.n_rows, heads), dtype=torch.float32, device=Wh.device)
         out = gat_aggregate(g, Wh, el, er, heads, fh, slope, mode, activation,
                             dropout_p=drop_p, seed=seed, stats=stats, a_dst=a_dst)
         ctx.save_for_backward(Wh, a_src, a_dst, el, er, stats, out)
-        ctx.cfg = (g, heads, fh, slope, mode, activation, drop_p, seed)
+        ctx.cfg = (g, heads, fh, slope, mode, activation, drop_p, seed, out_drop)
+        if out_drop is not None:
+            # the model's hidden F.dropout (GAT.py:17) on the layer's output; its backward runs
+            # inside this layer's backward prep (gat_backward dy_dropout)
+            return dropout_rows(out, out_drop[0], out_drop[1])
         return out
 
     @staticmethod
     def backward(ctx, dy):
         Wh, a_src, a_dst, el, er, stats, out = ctx.saved_tensors
-        g, heads, fh, slope, mode, activation, drop_p, seed = ctx.cfg
+        g, heads, fh, slope, mode, activation, drop_p, seed, out_drop = ctx.cfg
         dwh, dout, dl, der = gat_backward(g, Wh, el, er, stats, out, dy, a_src, a_dst, heads, fh,
-                                          slope, mode, activation == "elu", drop_p, seed)
+                                          slope, mode, activation == "elu", drop_p, seed,
+                                          dy_dropout=out_drop)
         n = Wh.shape[0]
         da_src, da_dst = _attention_vector_grads(Wh.detach(), dl, der, heads, fh)
         if mode == GAT_DENSE and g.has_empty_rows():
             # an edgeless row is the uniform average of every row (layers.py:29-32)
             empty = (g.rowptr[1:] - g.rowptr[:-1]) == 0
             dwh = dwh + dout[empty].sum(0) / n
-        return dwh, da_src, da_dst, None, None, None, None, None, None, None, None
+        return dwh, da_src, da_dst, None, None, None, None, None, None, None, None, None
 
 
 def _padded_fh(heads: int, fh: int, Wh) -> int:
@@ -164,7 +176,11 @@ class _AttentionBase(nn.Module):
         F_ = self.out_features
         return a[:F_], a[F_:]
 
-    def _aggregate(self, Wh, adj, heads, fh, a_src, a_dst, activation, dropout_p, logits=None):
+    def _aggregate(self, Wh, adj, heads, fh, a_src, a_dst, activation, dropout_p, logits=None,
+                   out_drop=0.0):
+        """The layer's output, followed by F.dropout(., out_drop) when out_drop > 0 (the GAT
+        model's hidden dropout: fused into the layer's autograd op on the hashed kernel, whose
+        mask the backward prep applies; else model_dropout on the output)."""
         g = as_csr(adj, self.PREDICATE)
         p = dropout_p if self.training else 0.0
         seed = _dropout_seed() if p > 0 else 0
@@ -183,14 +199,21 @@ class _AttentionBase(nn.Module):
                                         activation, p, seed)
                 out = out.view(n, heads, fp)[:, :, :fh].reshape(n, heads * fh)
             else:
+                od = None
+                if out_drop > 0 and GAT_FUSE_OUT_DROPOUT and HASHED_DROPOUT_OK(Wh, out_drop):
+                    od = (float(out_drop), _ops.dropout_seed())  # after the attention's seed
                 out = _GatLayerFn.apply(Wh, a_src, a_dst, g, heads, fh, self.alpha, self.MODE,
-                                        activation, p, seed)
+                                        activation, p, seed, od)
+                if od is not None:
+                    out_drop = 0.0  # applied
         else:
             el, er = logits if logits is not None else gat_logits(Wh, heads, fh, a_src, a_dst)
             out = gat_aggregate(g, Wh, el, er, heads, fh, self.alpha, self.MODE, activation,
                                 dropout_p=p, seed=seed, a_dst=a_dst)
         if self.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
-            assert not torch.isnan(out).any()
+            assert not torch.isnan(out).any()  # dropout keeps NaNs (x * 0): same verdict
+        if out_drop > 0:
+            out = model_dropout(out, out_drop, True)
         return out
 
     def _ordered(self, x, W, heads, fh, a_src, a_dst, adj, activation):
@@ -323,25 +346,27 @@ class GATBase(nn.Module):
         self.attentions = nn.ModuleList()
         self.out_att = None
 
-    def _heads(self, x, adj):
+    def _heads(self, x, adj, out_drop: float = 0.0):
+        """concat(heads) (GAT.py:16) followed by F.dropout(., out_drop) (GAT.py:17; 0 = none)."""
         heads = list(self.attentions)
         first = heads[0]
         uniform = all(type(m) is type(first) and m.concat and m.alpha == first.alpha
                       and m.out_features == first.out_features
                       and m._drop_p() == first._drop_p() for m in heads)
         if not uniform:
-            return torch.cat([att(x, adj) for att in heads], dim=1)
+            return model_dropout(torch.cat([att(x, adj) for att in heads], dim=1), out_drop,
+                                 out_drop > 0)
         fh = first.out_features
         W, a_src, a_dst = _HeadParams.apply(len(heads), *[m.W for m in heads],
                                             *[m.a for m in heads])  # [in, H*fh], [H*fh] x 2
         out = first._ordered(x, W, len(heads), fh, a_src, a_dst, adj, "elu")
         if out is not None:
-            return out
+            return model_dropout(out, out_drop, out_drop > 0)
         Wh, logits = _project(x, W, len(heads), fh, a_src, a_dst)  # one MFMA pass, all heads
         if first.MODE == GAT_SPARSE and SPARSE_NAN_CHECK:
             assert not torch.isnan(Wh).any()
         return first._aggregate(Wh, adj, len(heads), fh, a_src, a_dst, "elu", first._drop_p(),
-                                logits)
+                                logits, out_drop=out_drop)
 
     def _train_order(self, x, adj):
         """The node order training runs in (None: the graph's own, e.g. at inference, where
@@ -364,8 +389,7 @@ class GATBase(nn.Module):
             adj = order.graph
         else:
             x = model_dropout(x, self.dropout, self.training)
-        x = self._heads(x, adj)
-        x = model_dropout(x, self.dropout, self.training)
+        x = self._heads(x, adj, self.dropout if self.training else 0.0)  # + F.dropout (GAT.py:17)
         out = self.out_att(x, adj, activation="elu")  # F.elu(out_att(x)) fused (concat=False)
         if order is not None:
             out = PermuteRows.apply(out, order.inv, order.perm)

@@ -459,11 +459,17 @@ class DropoutRows(torch.autograd.Function):
         return gx, None, None, None, None
 
 
+def hashed_dropout_ok(x: torch.Tensor, p: float) -> bool:
+    """The hashed kernel takes F.dropout(x, p) in training: 2-D fp32 device rows with unit column
+    stride, 0 < p < 1."""
+    return (0.0 < p < 1.0 and HASHED_DROPOUT and x.dim() == 2 and x.is_cuda
+            and x.dtype == torch.float32 and x.stride(1) == 1 and x.stride(0) >= x.shape[1])
+
+
 def model_dropout(x: torch.Tensor, p: float, training: bool, perm=None, inv=None):
-    """F.dropout(x[perm] or x, p, training) on the hashed kernel where it applies (2-D fp32 device
-    rows with unit column stride, 0 < p < 1), else PermuteRows + torch's dropout."""
-    ok = (training and 0.0 < p < 1.0 and HASHED_DROPOUT and x.dim() == 2 and x.is_cuda
-          and x.dtype == torch.float32 and x.stride(1) == 1 and x.stride(0) >= x.shape[1])
+    """F.dropout(x[perm] or x, p, training) on the hashed kernel where it applies
+    (``hashed_dropout_ok``), else PermuteRows + torch's dropout."""
+    ok = training and hashed_dropout_ok(x, p)
     if not ok:
         if perm is not None:
             x = PermuteRows.apply(x, perm, inv)
@@ -1649,7 +1655,8 @@ def _bwd_recompute_ok(heads: int, fh: int, ldw: int) -> bool:
 
 
 def _gat_backward_recompute(g, wh, el, er, stats, y, dy, a_src, a_dst, heads, fh,
-                            negative_slope, mode, elu, dropout_p, seed, seg_len, mark):
+                            negative_slope, mode, elu, dropout_p, seed, seg_len, mark,
+                            dy_dropout=None):
     """The two-pass backward; None when the kernels refuse the shape (GNN_E_UNSUPPORTED)."""
     n = g.n_rows
     feat = heads * fh
@@ -1672,19 +1679,29 @@ def _gat_backward_recompute(g, wh, el, er, stats, y, dy, a_src, a_dst, heads, fh
     del_part = torch.empty((max(plan.n_seg, 1), heads), **f32)
     seed64 = int(seed) & 0xFFFFFFFFFFFFFFFF
     mark("rows")
-    rc = lib.gnn_gat_backward_rows_f32(
-        g.rowptr.data_ptr(), g.col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
-        el.data_ptr(), er.data_ptr(), stats.data_ptr(), dy.data_ptr(), y.data_ptr(), feat,
-        int(elu), float(negative_slope), int(mode), float(dropout_p), seed64,
-        dout.data_ptr(), nstat.data_ptr(), dl.data_ptr(), plan.seg_len,
-        _lib.ptr(plan.seg_row), _lib.ptr(plan.seg_begin), plan.n_seg, _lib.ptr(plan.long_row),
-        plan.long_seg_ptr.data_ptr(), plan.n_long, _lib.ptr(rows), rows.numel(),
-        _lib.ptr(short), short.numel(), del_part.data_ptr(),
-        a_dst.data_ptr() if GAT_ER_RECOMPUTE else None, stream)
+
+    def rows_pass(dy, dp, ds):
+        return lib.gnn_gat_backward_rows_ex_f32(
+            g.rowptr.data_ptr(), g.col.data_ptr(), n, wh.data_ptr(), wh.stride(0), heads, fh,
+            el.data_ptr(), er.data_ptr(), stats.data_ptr(), dy.data_ptr(), y.data_ptr(), feat,
+            int(elu), float(negative_slope), int(mode), float(dropout_p), seed64,
+            dout.data_ptr(), nstat.data_ptr(), dl.data_ptr(), plan.seg_len,
+            _lib.ptr(plan.seg_row), _lib.ptr(plan.seg_begin), plan.n_seg,
+            _lib.ptr(plan.long_row), plan.long_seg_ptr.data_ptr(), plan.n_long, _lib.ptr(rows),
+            rows.numel(), _lib.ptr(short), short.numel(), del_part.data_ptr(),
+            a_dst.data_ptr() if GAT_ER_RECOMPUTE else None, float(dp),
+            int(ds) & 0xFFFFFFFFFFFFFFFF, stream)
+
+    if dy_dropout is not None:  # the upstream mask inside the prep where it takes the shape
+        rc = rows_pass(dy, dy_dropout[0], dy_dropout[1])
+        if rc == _lib.E_UNSUPPORTED:
+            rc = rows_pass(dropout_rows(dy, dy_dropout[0], dy_dropout[1]), 0.0, 0)
+    else:
+        rc = rows_pass(dy, 0.0, 0)
     if rc == _lib.E_UNSUPPORTED:  # (_bwd_recompute_ok passed: an unaligned view)
         mark(None)
         return None
-    _lib.check(rc, "gnn_gat_backward_rows_f32")
+    _lib.check(rc, "gnn_gat_backward_rows_ex_f32")
     if g.symmetric and dropout_p == 0.0:
         # A^T = A: node j's in-edges are row j's (ascending sources); no edge ids needed
         rowptr_t, src_t, eid_t, gt = g.rowptr, g.col, None, g
@@ -1718,13 +1735,16 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
                  stats: torch.Tensor, y: torch.Tensor, dy: torch.Tensor, a_src: torch.Tensor,
                  a_dst: torch.Tensor, heads: int, fh: int, negative_slope: float, mode: int,
                  elu: bool, dropout_p: float = 0.0, seed: int = 0,
-                 seg_len: int | None = None, timings: list | None = None):
+                 seg_len: int | None = None, timings: list | None = None,
+                 dy_dropout: tuple | None = None):
     """dWh (incl. the el/er terms), del, der for one GAT layer: two HIP passes (row pass,
     recomputing node pass; GAT_BWD_RECOMPUTE) or, for the shapes those refuse, three.
 
     Returns (dwh [N, H*fh], dout [N, H*fh], del [N, H], der [N, H]). ``timings`` (a list):
     (pass name, start event, end event) of each pass on the current stream is appended
-    (bench.py's per-kernel backward times)."""
+    (bench.py's per-kernel backward times). ``dy_dropout`` = (p, seed): dy is the gradient of
+    ``dropout_rows(y, p, seed)`` (the hidden dropout fused into the layer); its mask is applied
+    to dy here -- inside the backward prep where the two-pass kernels take the shape."""
     _require_device(wh, dy)
     n = g.n_rows
     feat = heads * fh
@@ -1745,9 +1765,12 @@ def gat_backward(g: CsrGraph, wh: torch.Tensor, el: torch.Tensor, er: torch.Tens
 
     if GAT_BWD_RECOMPUTE:
         r = _gat_backward_recompute(g, wh, el, er, stats, y, dy, a_src, a_dst, heads, fh,
-                                    negative_slope, mode, elu, dropout_p, seed, seg_len, mark)
+                                    negative_slope, mode, elu, dropout_p, seed, seg_len, mark,
+                                    dy_dropout)
         if r is not None:
             return r
+    if dy_dropout is not None:
+        dy = dropout_rows(dy, dy_dropout[0], dy_dropout[1])
     dout = torch.empty((n, feat), dtype=torch.float32, device=dev)
     D = torch.empty((n, heads), dtype=torch.float32, device=dev)
     mark("prep")

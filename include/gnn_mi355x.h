@@ -669,6 +669,25 @@ int gnn_gat_backward_rows_f32(const int64_t* rowptr, const int32_t* col, int64_t
                               const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows,
                               int64_t n_rows_list, const int32_t* short_rows, int64_t n_short,
                               float* del_part, const float* a_dst, void* stream);
+/*
+ * rows_ex: the same, with dy the gradient of dropout(y) taken by gnn_dropout_rows_f32 (key =
+ * the row, p = dy_dropout_p, seed = dy_dropout_seed; GAT/models/GAT.py:17 after the heads):
+ * the prep applies that mask to dy, so the separate backward of the dropout is not run.
+ * dy_dropout_p > 0 needs ldo == heads*fh and the coalesced prep (fh % 4 == 0, fh / 4 a power of
+ * two <= 64, 16-B aligned operands), else GNN_E_UNSUPPORTED (mask dy first, then call rows).
+ */
+int gnn_gat_backward_rows_ex_f32(const int64_t* rowptr, const int32_t* col, int64_t n_rows,
+                                 const float* wh, int64_t ldw, int64_t heads, int64_t fh,
+                                 const float* el, const float* er, const float* lse,
+                                 const float* dy, const float* y, int64_t ldo, int32_t elu,
+                                 float negative_slope, int32_t mode, float dropout_p,
+                                 uint64_t dropout_seed, float* dout, float* nstat, float* del,
+                                 int64_t seg_len, const int32_t* seg_row, const int64_t* seg_begin,
+                                 int64_t n_seg, const int32_t* long_row,
+                                 const int32_t* long_seg_ptr, int64_t n_long, const int32_t* rows,
+                                 int64_t n_rows_list, const int32_t* short_rows, int64_t n_short,
+                                 float* del_part, const float* a_dst, float dy_dropout_p,
+                                 uint64_t dy_dropout_seed, void* stream);
 int gnn_gat_backward_nodes_recompute_f32(
     const int64_t* rowptr_t, const int32_t* src_t, const int64_t* eid_t, int64_t n_nodes,
     int64_t heads, int64_t fh, const float* dout, const float* nstat, const float* wh,

@@ -67,53 +67,79 @@ def test_dropout_rows_strided_and_in_place_refused(dev):
     assert rc != 0  # p = 1 (torch returns zeros) is left to torch
 
 
-@pytest.mark.parametrize("model", ["GAT", "SpGAT"])
-def test_gat_model_dropouts_vs_oracle_mask(dev, model, monkeypatch):
-    """GATBase.forward in training over P A P^T with dropout 0.5: the heads' input is
-    X[perm] under the oracle mask of the first seed, out_att's input the heads' output under the
-    mask of the second, and X.grad is the heads' input gradient masked and scattered back
-    through the permutation -- all bit-exact."""
+def _gat_setup(dev, model, p, monkeypatch):
     from graphneuralnetwork_amd import gat as gat_mod
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     from graphneuralnetwork_amd.rmat import rmat_edges
-    n, H, fh, Fin, C, p = 20000, 4, 8, 32, 7, 0.5
+    n, H, fh, Fin, C = 20000, 4, 8, 32, 7
     s, d = rmat_edges(n, 150_000, 3)
     g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n)
     order = ops.node_order(g)
     monkeypatch.setattr(gat_mod.GATBase, "_train_order", lambda self, x, adj: order)
-    seeds = []
-    real_seed = ops.dropout_seed
+    torch.manual_seed(0)
+    net = getattr(gat_mod, model)(Fin, fh, C, p, 0.2, H).to(dev).train()
+    # small inputs: SpGAT's exp(-LeakyReLU) weights overflow to inf / inf = NaN on large logits
+    # (the reference's arithmetic and NaN assert, layers.py:102-124)
+    X = (0.1 * torch.randn(n, Fin, device=dev)).requires_grad_(True)
+    return gat_mod, ops, net, X, g, order
+
+
+@pytest.mark.parametrize("model", ["GAT", "SpGAT"])
+def test_gat_model_dropouts_vs_oracle_mask(dev, model, monkeypatch):
+    """GATBase.forward in training over P A P^T with dropout 0.5, the hidden dropout unfused
+    (GAT_FUSE_OUT_DROPOUT off): the heads' input is X[perm] under the oracle mask of the first
+    seed, out_att's input the heads' output under the mask of the second, and X.grad is the
+    heads' input gradient masked and scattered back through the permutation -- all bit-exact."""
+    p = 0.5
+    gat_mod, ops, net, X, g, order = _gat_setup(dev, model, p, monkeypatch)
+    monkeypatch.setattr(gat_mod, "GAT_FUSE_OUT_DROPOUT", False)
+    seeds, calls = [], []
+    real_seed, real_md = ops.dropout_seed, gat_mod.model_dropout
 
     def rec_seed():
         seeds.append(real_seed())
         return seeds[-1]
-    monkeypatch.setattr(ops, "dropout_seed", rec_seed)
-    cap = {}
-    real_heads = gat_mod.GATBase._heads
 
-    def heads(self, x, adj):
-        x.retain_grad()
-        cap["x_in"] = x
-        cap["x_out"] = real_heads(self, x, adj)
-        return cap["x_out"]
-    monkeypatch.setattr(gat_mod.GATBase, "_heads", heads)
-    torch.manual_seed(0)
-    net = getattr(gat_mod, model)(Fin, fh, C, p, 0.2, H).to(dev).train()
-    net.out_att.register_forward_pre_hook(lambda m, args: cap.__setitem__("att_in", args[0]))
-    # small inputs: SpGAT's exp(-LeakyReLU) weights overflow to inf / inf = NaN on large logits
-    # (the reference's arithmetic and NaN assert, layers.py:102-124)
-    X = (0.1 * torch.randn(n, Fin, device=dev)).requires_grad_(True)
+    def rec_md(x, *a, **k):
+        y = real_md(x, *a, **k)
+        y.retain_grad()
+        calls.append((x, y))
+        return y
+    monkeypatch.setattr(ops, "dropout_seed", rec_seed)
+    monkeypatch.setattr(gat_mod, "model_dropout", rec_md)
     out = net(X, g)
     out.sum().backward()
-    assert len(seeds) == 2
+    assert len(seeds) == 2 and len(calls) == 2
+    n, Fin = X.shape
     perm = order.perm.cpu().numpy()
     want, keep = _expect(X.detach().cpu().numpy(), p, seeds[0], perm, np.arange(n))
-    np.testing.assert_array_equal(cap["x_in"].detach().cpu().numpy(), want)
-    want2, _ = _expect(cap["x_out"].detach().cpu().numpy(), p, seeds[1], np.arange(n),
+    np.testing.assert_array_equal(calls[0][1].detach().cpu().numpy(), want)
+    want2, _ = _expect(calls[1][0].detach().cpu().numpy(), p, seeds[1], np.arange(n),
                        np.arange(n))
-    np.testing.assert_array_equal(cap["att_in"].detach().cpu().numpy(), want2)
+    np.testing.assert_array_equal(calls[1][1].detach().cpu().numpy(), want2)
     scale = np.float32(1.0) / (np.float32(1.0) - np.float32(p))
     gx = np.zeros((n, Fin), np.float32)
-    gx[perm] = np.where(keep, cap["x_in"].grad.cpu().numpy() * scale, np.float32(0.0))
+    gx[perm] = np.where(keep, calls[0][1].grad.cpu().numpy() * scale, np.float32(0.0))
     np.testing.assert_array_equal(X.grad.cpu().numpy(), gx)
+
+
+@pytest.mark.parametrize("model", ["GAT", "SpGAT"])
+def test_gat_model_fused_hidden_dropout_bit_identical(dev, model, monkeypatch):
+    """The hidden dropout inside the heads' op (its mask applied to dy by the backward prep,
+    gnn_gat_backward_rows_ex_f32) gives the same bits as the separate pass (pinned above): the
+    logits, X.grad and every parameter gradient, with the same seeds."""
+    p = 0.5
+    gat_mod, ops, net, X, g, order = _gat_setup(dev, model, p, monkeypatch)
+    res = {}
+    for fused in (False, True):
+        monkeypatch.setattr(gat_mod, "GAT_FUSE_OUT_DROPOUT", fused)
+        torch.manual_seed(11)
+        X.grad = None
+        net.zero_grad(set_to_none=True)
+        out = net(X, g)
+        out.backward(torch.ones_like(out) * 0.01)
+        res[fused] = [out.detach().clone(), X.grad.clone()] + [q.grad.clone()
+                                                               for q in net.parameters()]
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
