@@ -67,12 +67,12 @@ def test_dropout_rows_strided_and_in_place_refused(dev):
     assert rc != 0  # p = 1 (torch returns zeros) is left to torch
 
 
-def _gat_setup(dev, model, p, monkeypatch):
+def _gat_setup(dev, model, p, monkeypatch, fh=8):
     from graphneuralnetwork_amd import gat as gat_mod
     from graphneuralnetwork_amd import ops
     from graphneuralnetwork_amd.preprocess import gcn_adjacency
     from graphneuralnetwork_amd.rmat import rmat_edges
-    n, H, fh, Fin, C = 20000, 4, 8, 32, 7
+    n, H, Fin, C = 20000, 4, 32, 7
     s, d = rmat_edges(n, 150_000, 3)
     g = gcn_adjacency(torch.from_numpy(s).to(dev), torch.from_numpy(d).to(dev), n)
     order = ops.node_order(g)
@@ -124,13 +124,19 @@ def test_gat_model_dropouts_vs_oracle_mask(dev, model, monkeypatch):
     np.testing.assert_array_equal(X.grad.cpu().numpy(), gx)
 
 
+@pytest.mark.parametrize("fh", [8, 2])
 @pytest.mark.parametrize("model", ["GAT", "SpGAT"])
-def test_gat_model_fused_hidden_dropout_bit_identical(dev, model, monkeypatch):
+def test_gat_model_fused_hidden_dropout_bit_identical(dev, model, fh, monkeypatch):
     """The hidden dropout inside the heads' op (its mask applied to dy by the backward prep,
     gnn_gat_backward_rows_ex_f32) gives the same bits as the separate pass (pinned above): the
-    logits, X.grad and every parameter gradient, with the same seeds."""
+    logits, X.grad and every parameter gradient, with the same seeds. fh = 2: the prep is fused
+    into the row pass, rows_ex refuses the mask and dy is masked first (the fallback)."""
     p = 0.5
-    gat_mod, ops, net, X, g, order = _gat_setup(dev, model, p, monkeypatch)
+    gat_mod, ops, net, X, g, order = _gat_setup(dev, model, p, monkeypatch, fh)
+    calls = []
+    real = ops._gat_backward_recompute
+    monkeypatch.setattr(ops, "_gat_backward_recompute",
+                        lambda *a: calls.append(a[-1]) or real(*a))
     res = {}
     for fused in (False, True):
         monkeypatch.setattr(gat_mod, "GAT_FUSE_OUT_DROPOUT", fused)
@@ -143,3 +149,4 @@ def test_gat_model_fused_hidden_dropout_bit_identical(dev, model, monkeypatch):
                                                                for q in net.parameters()]
     for a, b in zip(res[False], res[True]):
         assert torch.equal(a, b)
+    assert any(c is not None for c in calls)  # the fused form ran (dy_dropout handed down)
